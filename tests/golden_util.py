@@ -1,0 +1,54 @@
+"""Helpers shared by the golden-vector tests (fixtures from tools/gen_golden.py)."""
+import json
+import os
+
+import numpy as np
+
+from conftest import GOLDEN
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name + '.npz'))
+
+
+def universe(fix):
+    from orbitanalysis_amd.synthetic import PlummerSnapshots
+    meta = json.loads(str(fix['meta_json']))
+    g = dict(meta['gen'])
+    for k in ('dtype', 'centre_dtype'):
+        if k in g:
+            g[k] = np.dtype(g[k])
+    u = PlummerSnapshots(**g)
+    assert u.input_digest() == str(fix['input_sha256']), 'synthetic generator drifted'
+    return u, meta
+
+
+def groups(fix, prefix=''):
+    """{group: {dataset: array}} for keys 'prefix' + 'snapshot_XXX/name'."""
+    out = {}
+    for k in fix.files:
+        if not k.startswith(prefix + 'snapshot_'):
+            continue
+        g, d = k[len(prefix):].split('/')
+        out.setdefault(g, {})[d] = fix[k]
+    return out
+
+
+def assert_same(a, b, what=''):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    assert a.dtype == b.dtype, (what, a.dtype, b.dtype)
+    if a.dtype.kind == 'f':
+        same = (a == b) | (np.isnan(a) & np.isnan(b))
+        assert same.all(), (what, int((~same).sum()), 'mismatches')
+    else:
+        assert np.array_equal(a, b), what
+
+
+def assert_groups_equal(got, want):
+    assert sorted(got) == sorted(want), (sorted(got), sorted(want))
+    for g in want:
+        assert sorted(got[g]) == sorted(want[g]), (g, sorted(got[g]), sorted(want[g]))
+        for d in want[g]:
+            assert_same(got[g][d], want[g][d], g + '/' + d)
