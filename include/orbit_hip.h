@@ -1,0 +1,181 @@
+/*
+ * orbit_hip.h — C ABI of liborbit_hip.so, the MI355X (gfx950) implementation of the
+ * per-snapshot orbit-tagging hot path of s-balu/nbody-orbit-analysis.
+ *
+ * The reference is pure Python/NumPy and has no FFI; every entry point below
+ * replaces a NumPy code path of the reference, cited per function
+ * (paths relative to /root/reference/orbitanalysis/).  Bindings: INTEGRATION.md.
+ *
+ * Conventions
+ *   - all array arguments are DEVICE pointers (HIP global memory) unless noted;
+ *   - sizes are element counts; `stream` is a hipStream_t (NULL = default stream);
+ *   - functions enqueue work on `stream` and return immediately; they never
+ *     allocate, free or synchronise, so they are graph-capturable;
+ *   - return 0 on success, a negative OA_E* code on bad arguments or a launch
+ *     error; oa_last_error() returns the message of the last failure (thread-local);
+ *   - no exception ever crosses the ABI.
+ *
+ * Numerics contract: the frame follows the reference's
+ * NumPy expression tree and dtype promotion, with the reference host's einsum
+ * summation order (f64 (p0+p2)+p1, f32 (p0+p1)+p2), no FMA contraction,
+ * correctly rounded sqrt/div, float16 rounded directly from float64.
+ */
+#ifndef ORBIT_HIP_H
+#define ORBIT_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OA_ABI_VERSION 1
+
+#define OA_OK 0
+#define OA_E_ARG (-1)       /* invalid argument / unsupported dtype plan */
+#define OA_E_LAUNCH (-2)    /* HIP launch error */
+#define OA_E_DEVICE (-3)    /* no HIP device */
+
+/* Run-time flags reported by the step kernel in `status` (bit mask). */
+#define OA_STATUS_BUCKET_OVERFLOW 1u  /* a hash bucket exceeded its LDS capacity:
+                                         re-plan the halo with more buckets */
+
+#define OA_MODE_PERICENTRIC 0
+#define OA_MODE_APOCENTRIC 1
+
+/* One current-snapshot halo (region block).  96 bytes, device array. */
+typedef struct oa_halo {
+    int64_t cur_off, cur_cnt;   /* block [cur_off, cur_off+cur_cnt) of the current arrays
+                                   (region_offsets, track_orbits.py:129-132)            */
+    int64_t prev_off, prev_cnt; /* progenitor block in the previous snapshot's arrays;
+                                   prev_cnt < 0: the halo has no progenitor
+                                   (track_orbits.py:162-165)                             */
+    double centre[3];           /* region_positions[j], exact value of its dtype         */
+    double bulk[3];             /* bulk velocity: catalogue value or oa_bulk_velocity()  */
+    int64_t out_slot;           /* index among halos with a progenitor (apsis offsets),
+                                   -1 if none                                            */
+    int64_t reserved;
+} oa_halo;
+
+/* One work-group's share of a snapshot.  32 bytes, device array.
+ * nbuckets == 1: halos [h0,h1) whose current blocks total <= lds_entries.
+ * nbuckets  > 1: the single halo h0 (= h1-1), restricted to the particles whose ID
+ *                hashes to `bucket` (blocks larger than one work-group's LDS).   */
+typedef struct oa_item {
+    int32_t h0, h1, bucket, nbuckets;
+    int64_t scratch_off;        /* first scratch record of this item (nbuckets == 1) */
+    int64_t reserved;
+} oa_item;
+
+/* Arguments of oa_step (one snapshot of the batch driver's inner loop). */
+typedef struct oa_step_args {
+    /* current snapshot, as returned by load_snapshot_data (track_orbits.py:121) */
+    const void *ids;            /* (n_cur,) int32/int64 (id_bytes)                 */
+    const void *coords;         /* (n_cur,3) row-major, f32 or f64 (coord_f64)     */
+    const void *vels;           /* (n_cur,3) row-major, f32 or f64 (vel_f64)       */
+    int64_t n_cur;
+    /* previous snapshot state (outputs of the previous oa_step) */
+    const void *ids_prev;       /* (n_prev,) same dtype as ids                     */
+    const void *rec_prev;       /* (n_prev,) particle records, see rec_out         */
+    int64_t n_prev;
+    /* outputs */
+    void *rec_out;              /* (n_cur,) records: f32 plan {float rhat[3]; u32 meta}
+                                   16 B; f64 plan {double rhat[3]; u32 meta; u32 pad}
+                                   32 B.  meta = f16 angle bits | sign(v_r) << 16
+                                   (sign: 1 = v_r > 0, 2 = v_r < 0, 0 = neither)    */
+    const uint16_t *angles_in;  /* optional (n_cur,) f16 bits used as angles when
+                                   compare == 0 (checkpoint resume), NULL -> 0     */
+    /* tables: items (nbuckets == 1) and big_items (nbuckets > 1), any order */
+    const oa_halo *halos;
+    int32_t n_halos;
+    const oa_item *items;
+    int32_t n_items;
+    const oa_item *big_items;
+    int32_t n_big_items;
+    /* per-snapshot scalars (hubble_parameter, utils.py:36-39) */
+    double H, one_plus_z;
+    double box[3];
+    int32_t n_box_dims;         /* 0: no periodic wrap */
+    /* dtype plan: 1 = float64, 0 = float32 */
+    int32_t coord_f64, vel_f64, dx_f64, vb_f64, wrap_f64;
+    int32_t id_bytes;           /* 4 or 8 */
+    int32_t mode;               /* OA_MODE_* */
+    int32_t compare;            /* 0: frame only (first processed snapshot)       */
+    int32_t lds_entries;        /* hash-table entries per work-group (items)      */
+    int32_t lds_slots;          /* open-addressing slots per work-group (> entries) */
+    int32_t big_entries;        /* the same for big_items (bucketed halos)        */
+    int32_t big_slots;
+    /* apsis scratch */
+    void *scratch_ids;          /* nbuckets==1 items: ordered records at scratch_off */
+    uint16_t *scratch_ang;
+    uint16_t *dense_code;       /* nbuckets>1 halos: per previous position, f16 angle
+                                   bits of an apsis or 0xFFFF                         */
+    int32_t *halo_count;        /* [n_slots] apsis count per halo with a progenitor;
+                                   must be zero on entry                             */
+    int32_t *item_count;        /* [n_items] */
+    uint32_t *status;           /* device word, OA_STATUS_* bits; zero on entry       */
+} oa_step_args;
+
+/* Arguments of oa_compact: gather the per-item apsis records into the reference's
+ * output layout (track_orbits.py:212-227 -> save_to_file :379-381). */
+typedef struct oa_compact_args {
+    const oa_halo *halos;
+    int32_t n_halos;
+    const oa_item *items;
+    int32_t n_items;
+    const oa_item *big_items;
+    int32_t n_big_items;
+    const void *ids_prev;
+    int32_t id_bytes;
+    const void *scratch_ids;
+    const uint16_t *scratch_ang;
+    const uint16_t *dense_code;
+    const int32_t *halo_count;
+    const int32_t *item_count;
+    int32_t n_slots;
+    int64_t *offsets_out;       /* [n_slots+1] apsis region offsets (cumsum([0]+lens)) */
+    void *out_ids;              /* capacity >= total (<= n_prev) */
+    uint16_t *out_ang;
+    int64_t *total_out;         /* device scalar: number of apsis records */
+} oa_compact_args;
+
+/* ABI version (OA_ABI_VERSION) — lets the host reject a stale library. */
+int oa_abi_version(void);
+
+/* sizeof() of the ABI structs (0 oa_halo, 1 oa_item, 2 oa_step_args,
+ * 3 oa_compact_args) so a binding can verify its layout; -1 otherwise. */
+int64_t oa_struct_size(int32_t which);
+
+/* Message of the last failing call on this thread ("" if none). */
+const char *oa_last_error(void);
+
+/* Bulk velocity of each listed halo block, with NumPy's reduction orders:
+ *   masses == NULL : mean(v, axis=0)          (track_orbits.py:279-280)
+ *   masses != NULL : sum(m[:,None]*v, axis=0) / sum(m)   (:269-272)
+ * axis-0 sums are sequential; sum(m) is NumPy's pairwise sum over 8192-element
+ * chunks.  Writes halos[list[k]].bulk (exact value of the result dtype). */
+int oa_bulk_velocity(const void *vels, int32_t vel_f64, const void *masses, int32_t mass_f64,
+                     oa_halo *halos, const int32_t *halo_list, int32_t n_list, void *stream);
+
+/* Fused per-snapshot kernel: region_frame (track_orbits.py:247-290) for every
+ * particle of every halo, then — when compare != 0 — the ID join against the
+ * progenitor block, the strict sign-flip test, the arccos angle change and the
+ * float16 angle bookkeeping of compare_radial_velocities + calc_angles
+ * (:293-351), emitting apsis records in previous-block order. */
+int oa_step(const oa_step_args *args, void *stream);
+
+/* Dynamic LDS bytes oa_step needs per work-group for the given table sizes
+ * (bucketed != 0: the big_items layout, which also keeps a local index per entry). */
+int64_t oa_step_lds_bytes(int32_t entries, int32_t slots, int32_t bucketed);
+
+/* Largest dynamic LDS allocation a work-group may use on this device (bytes). */
+int64_t oa_max_lds_bytes(void);
+
+/* Scan the per-halo / per-item apsis counts and gather the records in output order. */
+int oa_compact(const oa_compact_args *args, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ORBIT_HIP_H */

@@ -1,0 +1,111 @@
+"""ctypes binding of liborbit_hip.so (C ABI: include/orbit_hip.h).
+
+The library is loaded AFTER ``import torch`` so that its ``libamdhip64.so.7``
+dependency resolves to the HIP runtime torch already loaded (one runtime, one set
+of streams).  There is deliberately no fallback: if the library or a HIP device is
+missing, every device entry point raises ``NativeUnavailable``.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, 'liborbit_hip.so')
+ABI_VERSION = 1
+
+c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
+
+# numpy mirrors of the device tables (little-endian, C layout)
+HALO_DTYPE = np.dtype([('cur_off', '<i8'), ('cur_cnt', '<i8'), ('prev_off', '<i8'),
+                       ('prev_cnt', '<i8'), ('centre', '<f8', (3,)), ('bulk', '<f8', (3,)),
+                       ('out_slot', '<i8'), ('reserved', '<i8')])
+ITEM_DTYPE = np.dtype([('h0', '<i4'), ('h1', '<i4'), ('bucket', '<i4'), ('nbuckets', '<i4'),
+                       ('scratch_off', '<i8'), ('reserved', '<i8')])
+
+MODE = {'pericentric': 0, 'apocentric': 1}
+STATUS_BUCKET_OVERFLOW = 1
+
+
+class StepArgs(ctypes.Structure):
+    _fields_ = [('ids', c_vp), ('coords', c_vp), ('vels', c_vp), ('n_cur', c_i64),
+                ('ids_prev', c_vp), ('rec_prev', c_vp), ('n_prev', c_i64),
+                ('rec_out', c_vp), ('angles_in', c_vp),
+                ('halos', c_vp), ('n_halos', c_i32), ('items', c_vp), ('n_items', c_i32),
+                ('big_items', c_vp), ('n_big_items', c_i32),
+                ('H', c_dbl), ('one_plus_z', c_dbl), ('box', c_dbl * 3), ('n_box_dims', c_i32),
+                ('coord_f64', c_i32), ('vel_f64', c_i32), ('dx_f64', c_i32), ('vb_f64', c_i32),
+                ('wrap_f64', c_i32), ('id_bytes', c_i32), ('mode', c_i32), ('compare', c_i32),
+                ('lds_entries', c_i32), ('lds_slots', c_i32), ('big_entries', c_i32),
+                ('big_slots', c_i32),
+                ('scratch_ids', c_vp), ('scratch_ang', c_vp), ('dense_code', c_vp),
+                ('halo_count', c_vp), ('item_count', c_vp), ('status', c_vp)]
+
+
+class CompactArgs(ctypes.Structure):
+    _fields_ = [('halos', c_vp), ('n_halos', c_i32), ('items', c_vp), ('n_items', c_i32),
+                ('big_items', c_vp), ('n_big_items', c_i32),
+                ('ids_prev', c_vp), ('id_bytes', c_i32),
+                ('scratch_ids', c_vp), ('scratch_ang', c_vp), ('dense_code', c_vp),
+                ('halo_count', c_vp), ('item_count', c_vp), ('n_slots', c_i32),
+                ('offsets_out', c_vp), ('out_ids', c_vp), ('out_ang', c_vp),
+                ('total_out', c_vp)]
+
+
+# every symbol include/orbit_hip.h declares: name -> (restype, argtypes)
+SYMBOLS = {
+    'oa_abi_version': (ctypes.c_int, []),
+    'oa_struct_size': (c_i64, [c_i32]),
+    'oa_last_error': (ctypes.c_char_p, []),
+    'oa_bulk_velocity': (ctypes.c_int, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
+    'oa_step': (ctypes.c_int, [ctypes.POINTER(StepArgs), c_vp]),
+    'oa_step_lds_bytes': (c_i64, [c_i32, c_i32, c_i32]),
+    'oa_max_lds_bytes': (c_i64, []),
+    'oa_compact': (ctypes.c_int, [ctypes.POINTER(CompactArgs), c_vp]),
+}
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_LIB = None
+
+
+def load(require_device=False):
+    """Load (once) and verify the native library; raise loudly if unusable."""
+    global _LIB
+    if _LIB is None:
+        import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
+        if not os.path.exists(LIB_PATH):
+            raise NativeUnavailable(
+                'liborbit_hip.so not built: run `python -c "import __graft_entry__ as g; g.build()"`')
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SYMBOLS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.oa_abi_version() != ABI_VERSION:
+            raise NativeUnavailable('liborbit_hip.so ABI %d != %d (stale build)'
+                                    % (lib.oa_abi_version(), ABI_VERSION))
+        sizes = {0: HALO_DTYPE.itemsize, 1: ITEM_DTYPE.itemsize,
+                 2: ctypes.sizeof(StepArgs), 3: ctypes.sizeof(CompactArgs)}
+        for k, v in sizes.items():
+            if lib.oa_struct_size(k) != v:
+                raise NativeUnavailable('ABI struct %d size mismatch: C %d, Python %d'
+                                        % (k, lib.oa_struct_size(k), v))
+        _LIB = lib
+    if require_device:
+        import torch
+        if not torch.cuda.is_available():
+            raise NativeUnavailable('no HIP device visible: the orbit kernels need an MI355X')
+    return _LIB
+
+
+def check(rc, what):
+    if rc != 0:
+        raise NativeError('%s failed (%d): %s' % (what, rc, _LIB.oa_last_error().decode()))

@@ -1,0 +1,394 @@
+"""Device engine for the per-snapshot orbit-tagging path.
+
+One ``OrbitEngine`` owns the previous snapshot's device state (IDs, particle
+records {r̂, sign(v_r), f16 angle}, block table) and turns each new snapshot into
+exactly three stream-ordered native calls:
+
+    oa_bulk_velocity  (only when the catalogue gives no bulk velocity)
+    oa_step           fused region_frame + ID join + sign flip + angles
+    oa_compact        apsis records in the reference's output order
+
+Host work per snapshot is O(n_halos) table building (no per-particle Python).
+Reference behaviour mirrored: track_orbits.py:104-240 (per-snapshot body),
+:247-290 (frame), :293-327 (compare), :330-351 (angles), :199-227 (assembly).
+"""
+import math
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+F32, F64 = np.dtype(np.float32), np.dtype(np.float64)
+
+_TORCH_FROM_NP = {
+    np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
+    np.dtype(np.int32): torch.int32, np.dtype(np.uint32): torch.int32,
+    np.dtype(np.int64): torch.int64, np.dtype(np.uint64): torch.int64,
+    np.dtype(np.float16): torch.float16, np.dtype(np.int16): torch.int16,
+    np.dtype(np.uint16): torch.int16,
+}
+_NP_FROM_TORCH = {torch.float32: F32, torch.float64: F64, torch.int32: np.dtype(np.int32),
+                  torch.int64: np.dtype(np.int64), torch.float16: np.dtype(np.float16)}
+
+
+def np_dtype(x):
+    if isinstance(x, torch.Tensor):
+        return _NP_FROM_TORCH[x.dtype]
+    if isinstance(x, np.ndarray):
+        return x.dtype
+    return np.asarray(x).dtype
+
+
+def is_array(x):
+    return isinstance(x, (np.ndarray, torch.Tensor))
+
+
+# ---------------------------------------------------------------- dtype plan
+@dataclass
+class DtypePlan:
+    """NumPy's promotion results for the reference expression tree of one snapshot
+    (track_orbits.py:254-288), evaluated on 1-row samples of the real dtypes."""
+    coord: np.dtype
+    vel: np.dtype
+    dx: np.dtype            # x - centre, and r̂
+    vb: np.dtype            # v - bulk
+    wrap_f64: bool          # recenter arithmetic in float64
+    box: tuple = ()         # per-dimension box lengths (float64 values)
+    ids: np.dtype = np.dtype(np.int64)
+    bulk: np.dtype = F64    # bulk-velocity result dtype
+    mass: Optional[np.dtype] = None
+
+    @property
+    def rec_bytes(self):
+        return 32 if self.dx == F64 else 16
+
+
+def plan_dtypes(snapshot, centre, bulk_cat, H, z):
+    coord, vel = np_dtype(snapshot['coordinates']), np_dtype(snapshot['velocities'])
+    for name, dt in (('coordinates', coord), ('velocities', vel)):
+        if dt not in (F32, F64):
+            raise NotImplementedError('%s dtype %s: the device path supports float32/float64'
+                                      % (name, dt))
+    ids = np_dtype(snapshot['ids'])
+    if ids.kind not in 'iu' or ids.itemsize not in (4, 8):
+        raise NotImplementedError('ids dtype %s: the device path supports 32/64-bit integers' % ids)
+    x1 = np.zeros((1, 3), coord)
+    v1 = np.zeros((1, 3), vel)
+    c = np.zeros(3, dtype=np.asarray(centre).dtype)
+    dx = x1 - c
+    if dx.dtype not in (F32, F64):
+        raise NotImplementedError('x - centre dtype %s unsupported' % dx.dtype)
+    wrap_f64, box = dx.dtype == F64, ()
+    if 'box_size' in snapshot:
+        bs = snapshot['box_size']
+        if isinstance(bs, (float, np.floating, int, np.integer)):
+            bs = np.float64(bs) * np.ones(3)          # utils.py:25-26
+        elems = list(bs)
+        if len(elems) > 3:
+            raise ValueError('box_size has more than 3 dimensions')
+        kinds = {(dx[:, 0] - e).dtype for e in elems}
+        if len(kinds) != 1 or next(iter(kinds)) not in (F32, F64):
+            raise NotImplementedError('mixed/unsupported box_size dtypes %s' % kinds)
+        wrap_f64 = next(iter(kinds)) == F64
+        box = tuple(float(e) for e in elems)
+    masses = snapshot['masses']
+    mass = None
+    if bulk_cat is not None:
+        bulk = np.asarray(bulk_cat).dtype
+    elif is_array(masses):
+        mass = np_dtype(masses)
+        if mass not in (F32, F64):
+            raise NotImplementedError('masses dtype %s unsupported' % mass)
+        m1 = np.ones(1, mass)
+        bulk = (np.sum(m1[:, None] * v1, axis=0) / np.sum(m1)).dtype
+    else:
+        bulk = np.mean(v1, axis=0).dtype
+    vb = (v1 - np.zeros(3, bulk)).dtype
+    hterm = (H * dx) / (1 + z)
+    w = vb.type(0) + hterm
+    if hterm.dtype != F64 or w.dtype != F64 or vb not in (F32, F64):
+        raise NotImplementedError('Hubble term dtype %s: the device path needs a float64 H '
+                                  '(hubble_parameter of Python floats)' % hterm.dtype)
+    return DtypePlan(coord=coord, vel=vel, dx=dx.dtype, vb=vb, wrap_f64=bool(wrap_f64),
+                     box=box, ids=ids, bulk=bulk, mass=mass)
+
+
+# ---------------------------------------------------------------- items
+def plan_items(cur_cnt, prev_cnt, entries, big_entries, hmax=128, fill=0.7, min_buckets=None):
+    """Greedy packing of consecutive halos into work-group items.
+
+    Returns (items, big_items) as ITEM_DTYPE arrays.  ``min_buckets`` (per halo)
+    forces more buckets after an overflow."""
+    nh = len(cur_cnt)
+    small, big = [], []
+    scratch = 0
+    j = 0
+    pc = np.maximum(prev_cnt, 0)
+    while j < nh:
+        need_b = 1
+        if cur_cnt[j] > entries:
+            need_b = max(2, int(math.ceil(cur_cnt[j] / (fill * big_entries))))
+        if min_buckets is not None and min_buckets[j] > need_b:
+            need_b = int(min_buckets[j])
+        if need_b > 1:
+            for q in range(need_b):
+                big.append((j, j + 1, q, need_b, 0, 0))
+            j += 1
+            continue
+        start, tot, ptot = j, 0, 0
+        while (j < nh and j - start < hmax and tot + cur_cnt[j] <= entries
+               and (min_buckets is None or min_buckets[j] <= 1)):
+            tot += cur_cnt[j]
+            ptot += pc[j]
+            j += 1
+        small.append((start, j, 0, 1, scratch, 0))
+        scratch += ptot
+    it = np.array(small, dtype=N.ITEM_DTYPE) if small else np.zeros(0, N.ITEM_DTYPE)
+    bt = np.array(big, dtype=N.ITEM_DTYPE) if big else np.zeros(0, N.ITEM_DTYPE)
+    return it, bt, scratch
+
+
+def to_device(x, device, dtype=None):
+    """numpy/torch array -> contiguous device tensor (bit-preserving for uint)."""
+    if isinstance(x, torch.Tensor):
+        t = x
+    else:
+        a = np.ascontiguousarray(x)
+        if dtype is not None:
+            a = a.astype(dtype, copy=False)
+        if a.dtype.kind == 'u':
+            a = a.view(a.dtype.str.replace('u', 'i'))
+        t = torch.from_numpy(a)
+    return t.to(device, non_blocking=False).contiguous()
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+@dataclass
+class SnapshotState:
+    """Device state a snapshot leaves for the next one (track_orbits.py:234-240)."""
+    ids: torch.Tensor
+    rec: torch.Tensor
+    starts: np.ndarray
+    counts: np.ndarray
+    exists: np.ndarray
+    plan: DtypePlan
+
+
+@dataclass
+class StepResult:
+    n_slots: int
+    has_prog: np.ndarray                       # bool per current halo
+    offsets: Optional[torch.Tensor] = None     # device int64 [n_slots+1]
+    apsis_ids: Optional[torch.Tensor] = None   # device, capacity >= total
+    apsis_ang: Optional[torch.Tensor] = None   # device int16 (f16 bits)
+    total: Optional[torch.Tensor] = None       # device int64 scalar
+    halos: Optional[torch.Tensor] = None       # device halo table (bulk written on device)
+    extra: dict = field(default_factory=dict)
+
+
+class OrbitEngine:
+    """Per-snapshot device pipeline with carried state (see module docstring)."""
+
+    def __init__(self, mode='pericentric', device=None, lds_entries=16384, lds_slots=None,
+                 big_entries=12288, big_slots=None, hmax=128):
+        if mode not in N.MODE:
+            raise ValueError("Orbit detection mode not recognized. Please specify either "
+                             "'pericentric' or 'apocentric'.")
+        self.lib = N.load(require_device=True)
+        self.device = torch.device(device if device is not None else 'cuda')
+        self.mode = mode
+        self.entries = int(lds_entries)
+        self.slots = int(lds_slots or 2 * self.entries)
+        self.big_entries = int(big_entries)
+        self.big_slots = int(big_slots or 2 * self.big_entries)
+        self.hmax = int(hmax)
+        max_lds = self.lib.oa_max_lds_bytes()
+        for e, s, b in ((self.entries, self.slots, 0), (self.big_entries, self.big_slots, 1)):
+            need = self.lib.oa_step_lds_bytes(e, s, b)
+            if need > max_lds:
+                raise ValueError('LDS table needs %d bytes > device limit %d' % (need, max_lds))
+        self.prev: Optional[SnapshotState] = None
+
+    def reset(self):
+        self.prev = None
+
+    # ------------------------------------------------------------------ tables
+    def build_tables(self, snapshot, centres, bulk_cat, exists, compare, min_buckets=None):
+        n = len(snapshot['ids'])
+        starts = np.asarray(snapshot['region_offsets'], dtype=np.int64).reshape(-1)
+        ends = np.append(starts[1:], n)
+        counts = ends - starts
+        nh = len(starts)
+        if nh != len(exists):
+            raise ValueError('region_offsets has %d blocks for %d halos' % (nh, len(exists)))
+        if nh and (np.any(counts < 0) or starts[0] < 0 or ends[-1] > n):
+            raise ValueError('region_offsets must be non-decreasing block starts within [0, N]')
+        halos = np.zeros(nh, dtype=N.HALO_DTYPE)
+        halos['cur_off'], halos['cur_cnt'] = starts, counts
+        halos['centre'] = np.asarray(centres, dtype=np.float64).reshape(nh, 3)
+        if bulk_cat is not None:
+            halos['bulk'] = np.asarray(bulk_cat, dtype=np.float64).reshape(nh, 3)
+        halos['prev_cnt'] = -1
+        halos['out_slot'] = -1
+        has_prog = np.zeros(nh, dtype=bool)
+        if compare:
+            pe = self.prev.exists
+            p = np.searchsorted(pe, exists)
+            pc = np.minimum(p, max(len(pe) - 1, 0))
+            has_prog = (p < len(pe)) & (pe[pc] == exists) if len(pe) else has_prog
+            halos['prev_off'][has_prog] = self.prev.starts[p[has_prog]]
+            halos['prev_cnt'][has_prog] = self.prev.counts[p[has_prog]]
+            halos['out_slot'][has_prog] = np.arange(int(has_prog.sum()))
+        items, big, scratch = plan_items(counts, halos['prev_cnt'], self.entries,
+                                         self.big_entries, self.hmax, min_buckets=min_buckets)
+        return halos, items, big, scratch, starts, counts, has_prog
+
+    # ------------------------------------------------------------------ step
+    def step(self, snapshot, centres, bulk_cat, H, z, exists, compare, angles_in=None):
+        """Process one snapshot.  ``compare`` is the reference's ``i > istart``."""
+        exists = np.asarray(exists)
+        if compare and self.prev is None:
+            raise RuntimeError('compare step without a previous snapshot')
+        dev = self.device
+        plan = plan_dtypes(snapshot, centres[0] if len(centres) else np.zeros(3),
+                           None if bulk_cat is None else bulk_cat[0], H, z)
+        if compare and plan.dx != self.prev.plan.dx:
+            raise NotImplementedError('r̂ dtype changed between snapshots (%s -> %s)'
+                                      % (self.prev.plan.dx, plan.dx))
+        if compare and plan.ids.itemsize != self.prev.plan.ids.itemsize:
+            raise NotImplementedError('ids dtype changed between snapshots')
+        ids = to_device(snapshot['ids'], dev)
+        x = to_device(snapshot['coordinates'], dev)
+        v = to_device(snapshot['velocities'], dev)
+        n = ids.numel()
+        if x.numel() != 3 * n or v.numel() != 3 * n:
+            raise ValueError('coordinates/velocities must be (N, 3) with N = len(ids)')
+        min_b = None
+        for attempt in range(8):
+            res, rec, counts_ok = self._run(snapshot, plan, ids, x, v, centres, bulk_cat, H, z,
+                                            exists, compare, angles_in, min_b)
+            if counts_ok is None:
+                break
+            min_b = counts_ok          # bucket overflow: re-plan with more buckets
+        else:
+            raise RuntimeError('hash buckets kept overflowing (adversarial IDs?)')
+        self.prev = SnapshotState(ids=ids, rec=rec, starts=res.extra['starts'],
+                                  counts=res.extra['counts'], exists=exists, plan=plan)
+        return res
+
+    def _run(self, snapshot, plan, ids, x, v, centres, bulk_cat, H, z, exists, compare,
+             angles_in, min_buckets):
+        dev, lib = self.device, self.lib
+        halos, items, big, scratch, starts, counts, has_prog = self.build_tables(
+            snapshot, centres, bulk_cat, exists, compare, min_buckets)
+        n = ids.numel()
+        nh = len(halos)
+        n_slots = int(has_prog.sum())
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        d_halos = torch.from_numpy(halos.view(np.uint8)).to(dev)
+        d_items = torch.from_numpy(items.view(np.uint8)).to(dev)
+        d_big = torch.from_numpy(big.view(np.uint8)).to(dev)
+        if bulk_cat is None and nh:
+            masses = snapshot['masses']
+            m = to_device(masses, dev) if plan.mass is not None else None
+            hl = torch.arange(nh, dtype=torch.int32, device=dev)
+            N.check(lib.oa_bulk_velocity(v.data_ptr(), int(plan.vel == F64), _ptr(m),
+                                         int(plan.mass == F64), d_halos.data_ptr(),
+                                         hl.data_ptr(), nh, stream), 'oa_bulk_velocity')
+        rec = torch.empty(n * plan.rec_bytes, dtype=torch.uint8, device=dev)
+        a = N.StepArgs()
+        a.ids, a.coords, a.vels, a.n_cur = ids.data_ptr(), x.data_ptr(), v.data_ptr(), n
+        a.rec_out = rec.data_ptr()
+        a.halos, a.n_halos = d_halos.data_ptr(), nh
+        a.items, a.n_items = d_items.data_ptr(), len(items)
+        a.big_items, a.n_big_items = d_big.data_ptr(), len(big)
+        a.H, a.one_plus_z = float(H), float(1 + z)
+        a.n_box_dims = len(plan.box)
+        for d, L in enumerate(plan.box):
+            a.box[d] = L
+        a.coord_f64, a.vel_f64 = int(plan.coord == F64), int(plan.vel == F64)
+        a.dx_f64, a.vb_f64, a.wrap_f64 = int(plan.dx == F64), int(plan.vb == F64), int(plan.wrap_f64)
+        a.id_bytes = plan.ids.itemsize
+        a.mode = N.MODE[self.mode]
+        a.compare = int(bool(compare))
+        a.lds_entries, a.lds_slots = self.entries, self.slots
+        a.big_entries, a.big_slots = self.big_entries, self.big_slots
+        keep = [d_halos, d_items, d_big, rec]
+        ain = None
+        if angles_in is not None and not compare:
+            ain = to_device(np.asarray(angles_in, dtype=np.float16).view(np.int16), dev)
+            a.angles_in = ain.data_ptr()
+        res = StepResult(n_slots=n_slots, has_prog=has_prog, halos=d_halos)
+        res.extra.update(starts=starts, counts=counts, items=items, big=big)
+        if compare:
+            prev = self.prev
+            a.ids_prev, a.rec_prev, a.n_prev = prev.ids.data_ptr(), prev.rec.data_ptr(), prev.ids.numel()
+            n_prev = prev.ids.numel()
+            scr_ids = torch.empty(max(scratch, 1), dtype=ids.dtype, device=dev)
+            scr_ang = torch.empty(max(scratch, 1), dtype=torch.int16, device=dev)
+            dense = torch.empty(max(n_prev, 1) if len(big) else 1, dtype=torch.int16, device=dev)
+            halo_count = torch.zeros(max(n_slots, 1), dtype=torch.int32, device=dev)
+            item_count = torch.zeros(max(len(items), 1), dtype=torch.int32, device=dev)
+            status = torch.zeros(1, dtype=torch.int32, device=dev)
+            a.scratch_ids, a.scratch_ang, a.dense_code = (scr_ids.data_ptr(), scr_ang.data_ptr(),
+                                                         dense.data_ptr())
+            a.halo_count, a.item_count, a.status = (halo_count.data_ptr(), item_count.data_ptr(),
+                                                   status.data_ptr())
+            keep += [scr_ids, scr_ang, dense, halo_count, item_count, status]
+        N.check(lib.oa_step(a, stream), 'oa_step')
+        if not compare:
+            return res, rec, None
+        if len(big):
+            st = int(status.item())
+            if st & N.STATUS_BUCKET_OVERFLOW:
+                mb = np.ones(nh, dtype=np.int64)
+                for h0, nb in zip(big['h0'], big['nbuckets']):
+                    mb[h0] = max(mb[h0], 2 * nb)
+                if min_buckets is not None:
+                    mb = np.maximum(mb, 2 * np.asarray(min_buckets))
+                return res, rec, mb
+        offsets = torch.empty(n_slots + 1, dtype=torch.int64, device=dev)
+        out_ids = torch.empty(max(prev.ids.numel(), 1), dtype=ids.dtype, device=dev)
+        out_ang = torch.empty(max(prev.ids.numel(), 1), dtype=torch.int16, device=dev)
+        total = torch.zeros(1, dtype=torch.int64, device=dev)
+        c = N.CompactArgs()
+        c.halos, c.n_halos = d_halos.data_ptr(), nh
+        c.items, c.n_items = d_items.data_ptr(), len(items)
+        c.big_items, c.n_big_items = d_big.data_ptr(), len(big)
+        c.ids_prev, c.id_bytes = prev.ids.data_ptr(), plan.ids.itemsize
+        c.scratch_ids, c.scratch_ang, c.dense_code = a.scratch_ids, a.scratch_ang, a.dense_code
+        c.halo_count, c.item_count, c.n_slots = a.halo_count, a.item_count, n_slots
+        c.offsets_out, c.out_ids, c.out_ang = offsets.data_ptr(), out_ids.data_ptr(), out_ang.data_ptr()
+        c.total_out = total.data_ptr()
+        N.check(lib.oa_compact(c, stream), 'oa_compact')
+        res.offsets, res.apsis_ids, res.apsis_ang, res.total = offsets, out_ids, out_ang, total
+        res.extra['keep'] = keep
+        return res, rec, None
+
+    # ------------------------------------------------------------------ host views
+    def fetch(self, res, ids_dtype):
+        """Device results -> host arrays in the reference's dtypes."""
+        offsets = res.offsets.cpu().numpy()
+        total = int(offsets[-1]) if len(offsets) else 0
+        ids = res.apsis_ids[:total].cpu().numpy().view(ids_dtype) if total else \
+            np.zeros(0, dtype=ids_dtype)
+        ang = res.apsis_ang[:total].cpu().numpy().view(np.float16) if total else \
+            np.zeros(0, dtype=np.float16)
+        return offsets, ids, ang
+
+    def bulk_velocities(self, res, plan):
+        h = res.halos.cpu().numpy().view(N.HALO_DTYPE)
+        return h['bulk'].astype(plan.bulk)
+
+    def angles(self):
+        """Current per-particle float16 angles (checkpoint payload, track_orbits.py:390-394)."""
+        p = self.prev
+        words = p.rec.view(torch.int32).view(-1, p.plan.rec_bytes // 4)
+        meta = words[:, 3] if p.plan.rec_bytes == 16 else words[:, 6]
+        return (meta & 0xFFFF).to(torch.int32).cpu().numpy().astype(np.uint16).view(np.float16)

@@ -100,8 +100,11 @@ class PlummerSnapshots:
             centres = rng.uniform(0.0, span, (self.n_halos, 3))
         self.centres0 = np.asarray(centres, dtype=np.float64).reshape(self.n_halos, 3)
         self.halo_vel = rng.normal(0.0, halo_velocity, (self.n_halos, 3))
-        ids = rng.permutation(self.n_total).astype(np.int64) + int(id_offset)
-        self.ids = ids.astype(id_dtype)
+        perm = rng.permutation(self.n_total)
+        if np.dtype(id_dtype).kind == 'u':
+            self.ids = (perm.astype(np.uint64) + np.uint64(id_offset)).astype(id_dtype)
+        else:
+            self.ids = (perm.astype(np.int64) + np.int64(id_offset)).astype(id_dtype)
         if masses == 'array':
             self.mass_values = (rng.uniform(0.5, 1.5, self.n_total) / self.n_total).astype(self.dtype)
         else:

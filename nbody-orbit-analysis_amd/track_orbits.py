@@ -1,0 +1,155 @@
+"""Drop-in batch driver: ``track_orbits`` with the reference's signature, callbacks,
+errors, verbose messages and savefile layout (orbitanalysis/track_orbits.py:9-244).
+
+What changes is underneath: the per-halo Python loop and the pathos process pool
+(track_orbits.py:147-194) are replaced by one fused HIP kernel launch per snapshot
+over all halos (``engine.OrbitEngine``); the previous snapshot's state stays in
+HBM.  ``npool`` is accepted for signature compatibility and ignored (halo
+parallelism is the GPU grid).
+"""
+import time
+
+import numpy as np
+
+from .engine import OrbitEngine
+from .savefile import open_savefile, group_datasets
+from .utils import hubble_parameter
+
+
+def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
+                 savefile, mode='pericentric', checkpoint=False, resume=False,
+                 npool=1, verbose=True, engine=None):
+    """
+    Track the orbits of particles in gravitating systems (reference docstring:
+    track_orbits.py:13-71).
+
+    Parameters are those of the reference.  ``savefile`` may be a path (HDF5 via
+    h5py) or a savefile object (``savefile.MemorySavefile``).  ``engine`` optionally
+    supplies a configured ``OrbitEngine`` (device, LDS table sizes).
+    """
+    if len(main_branches) != len(snapshot_numbers):
+        raise ValueError(
+            "Number of halo main branch nodes does not equal the number of "
+            "snapshot numbers supplied. Must have len(main_branches) == "
+            "len(snapshot_numbers).")
+    if (mode != 'pericentric') and (mode != 'apocentric'):
+        raise ValueError(
+            "Orbit detection mode not recognized. Please specify either "
+            "'pericentric' or 'apocentric'.")
+
+    tstart = time.time()
+    out = open_savefile(savefile)
+
+    main_branches = np.asarray(main_branches)
+    if main_branches.ndim == 1:
+        main_branches = main_branches[:, np.newaxis]
+    snapshot_numbers = np.asarray(snapshot_numbers)
+    order = np.argsort(snapshot_numbers)
+    snapshot_numbers = snapshot_numbers[order]
+    main_branches = main_branches[order]
+
+    if resume:
+        print('Resuming from file...\n')
+        last = out.last_snapshot_number()
+        sind = np.argwhere(snapshot_numbers == last).flatten()[0]
+        snapshot_numbers = snapshot_numbers[sind:]
+        main_branches = main_branches[sind:]
+
+    eng = engine if engine is not None else OrbitEngine(mode=mode)
+    if eng.mode != mode:
+        raise ValueError('engine mode %r != mode %r' % (eng.mode, mode))
+    eng.reset()
+
+    istart, started = 0, False
+    progen_exists = None
+    for i, (halo_ids, snapshot_number) in enumerate(zip(main_branches, snapshot_numbers)):
+
+        if verbose:
+            print('-' * 30, '\n')
+            print('Snapshot {}\n'.format('%03d' % snapshot_number))
+
+        halo_exists = np.argwhere(halo_ids != -1).flatten()
+        if len(halo_exists) == 0:
+            if started is False:
+                istart = i + 1
+            continue
+        halo_ids_ = halo_ids[halo_exists]
+
+        region_positions, region_radii, region_bulk_vels = regions(snapshot_number, halo_ids_)
+        snapshot = load_snapshot_data(snapshot_number, region_positions, region_radii)
+        if len(snapshot['coordinates']) == 0:
+            if started is False:
+                istart = i + 1
+            continue
+        started = True
+
+        if 'Omega_k' not in snapshot:
+            snapshot['Omega_k'] = 0
+        H = hubble_parameter(snapshot['redshift'], snapshot['H0'], snapshot['Omega_m'],
+                             snapshot['Omega_L'], snapshot['Omega_k'])
+
+        if i == 0 and not resume:
+            box_size = snapshot['box_size'] if 'box_size' in snapshot else None
+            out.initialize(mode, box_size)
+            if verbose:
+                print('Savefile initialized\n')
+
+        compare = i > istart
+        angles_in = out.read_checkpoint() if (resume and not compare) else None
+
+        if verbose:
+            t0 = time.time()
+        res = eng.step(snapshot, region_positions, region_bulk_vels, H, snapshot['redshift'],
+                       halo_exists, compare, angles_in=angles_in)
+        if compare:
+            apsis_offsets, apsis_ids, apsis_angles = eng.fetch(res, eng.prev.plan.ids)
+        if verbose:
+            print('Finished pericenter detection for snapshot {} in {} s\n'.format(
+                '%03d' % snapshot_number, time.time() - t0))
+
+        if compare:
+            if res.n_slots == 0:
+                # the reference concatenates an empty list here (track_orbits.py:216)
+                raise ValueError('need at least one array to concatenate')
+            hinds = np.where(res.has_prog)[0]
+            if region_bulk_vels is None:
+                bulk = eng.bulk_velocities(res, eng.prev.plan)
+            else:
+                bulk = np.array([region_bulk_vels[j] for j in range(len(halo_exists))])
+            halo_ids_final = main_branches[-1][progen_exists] if \
+                snapshot_number != snapshot_numbers[-1] else None
+            save_to_file(out, apsis_ids, apsis_offsets, apsis_angles,
+                         region_positions[hinds], region_radii[hinds], bulk[hinds],
+                         halo_ids_[hinds], halo_ids_final, snapshot_number, mode,
+                         checkpoint, eng.angles() if checkpoint else None, verbose)
+
+        progen_exists = halo_exists
+
+    if verbose:
+        print('Finished pericenter detection for all snapshots in {} s\n'.format(
+            time.time() - tstart))
+
+
+def save_to_file(savefile, apsis_ids, apsis_offsets, apsis_angles, region_positions,
+                 region_radii, bulk_velocities, halo_ids, halo_ids_final, snapshot_number,
+                 mode, checkpoint, angles, verbose):
+    """Write one snapshot group (+ checkpoint) in the reference layout (:366-397)."""
+    out = open_savefile(savefile)
+    if verbose:
+        print('Saving to file...')
+        t0 = time.time()
+    out.write_group('snapshot_{}'.format('%0.3d' % snapshot_number),
+                    group_datasets(mode, apsis_ids, apsis_offsets, apsis_angles,
+                                   region_positions, region_radii, bulk_velocities,
+                                   halo_ids, halo_ids_final))
+    if checkpoint:
+        out.write_checkpoint(angles)
+    if verbose:
+        print('Saved to file ({} s)\n'.format(time.time() - t0))
+
+
+def initialize_savefile(savefile, mode, box_size, verbose):
+    """Create the savefile with its attributes (:354-363)."""
+    open_savefile(savefile).initialize(mode, box_size)
+    if verbose:
+        print('Savefile initialized\n')

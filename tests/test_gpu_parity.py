@@ -1,0 +1,121 @@
+"""HIP path vs the reference's golden vectors and the pinned oracle (needs a GPU).
+
+Bar (BASELINE north star): apsis IDs, offsets, halo tables and bulk
+velocities bit-exact; float16 angles bit-exact or within 1 float16 ulp, with the
+mismatch count reported (numpy's SIMD arccos is not correctly rounded: ~25 % of
+float32 and ~9 % of float64 values differ from a correctly rounded acos by an ulp)."""
+import numpy as np
+import pytest
+
+from golden_util import load, universe, groups
+
+pytestmark = pytest.mark.gpu
+
+BATCH = ['g1_config1', 'g2_overlap_birth_massarray', 'g3_apo_periodic',
+         'g4_hubble_catalogue', 'g5_fp32_centre32', 'g5_fp32_centre64',
+         'g5_fp32_catalogue32', 'g8_many_small_halos']
+
+ANGLE_MISMATCH_MAX = 0.01      # fraction of apsis angles allowed to differ by 1 f16 ulp
+
+
+def compare_groups(got, want, report):
+    assert sorted(got) == sorted(want), (sorted(got), sorted(want))
+    for g in want:
+        assert sorted(got[g]) == sorted(want[g]), g
+        for k, w in want[g].items():
+            v = np.asarray(got[g][k])
+            assert v.dtype == w.dtype and v.shape == w.shape, (g, k, v.dtype, w.dtype, v.shape, w.shape)
+            if k == 'angles':
+                a, b = v.astype(np.float64), w.astype(np.float64)
+                same = (a == b) | (np.isnan(a) & np.isnan(b))
+                ulp = np.spacing(np.maximum(np.abs(a), np.abs(b)).astype(np.float16)).astype(np.float64)
+                near = np.abs(a - b) <= ulp
+                assert np.all(same | near), (g, 'angle off by more than 1 f16 ulp')
+                report['angles'] = report.get('angles', 0) + a.size
+                report['angle_mismatch'] = report.get('angle_mismatch', 0) + int((~same).sum())
+            elif w.dtype.kind == 'f':
+                assert np.array_equal(v, w, equal_nan=True), (g, k)
+            else:
+                assert np.array_equal(v, w), (g, k)
+
+
+def run_driver(u, run, engine=None, savefile=None):
+    from orbitanalysis_amd.track_orbits import track_orbits
+    from orbitanalysis_amd.savefile import MemorySavefile
+    out = savefile if savefile is not None else MemorySavefile()
+    track_orbits(u.snapshot_numbers, u.main_branches(), u.regions, u.load_snapshot_data,
+                 out, verbose=False, engine=engine, **run)
+    return out
+
+
+@pytest.mark.parametrize('name', BATCH)
+def test_driver_matches_reference_golden(name):
+    fix = load(name)
+    u, meta = universe(fix)
+    rep = {}
+    out = run_driver(u, meta['run'])
+    assert out.attrs['mode'] == str(fix['attr/mode'])
+    compare_groups(out.groups, groups(fix), rep)
+    if 'checkpoint/angles' in fix.files:
+        c, w = out.checkpoint, fix['checkpoint/angles']
+        assert c.dtype == w.dtype and c.shape == w.shape
+        frac = float(np.mean((c != w) & ~(np.isnan(c) & np.isnan(w))))
+        assert frac < ANGLE_MISMATCH_MAX, frac
+    if rep.get('angles'):
+        assert rep['angle_mismatch'] / rep['angles'] < ANGLE_MISMATCH_MAX, rep
+    print(name, rep)
+
+
+@pytest.mark.parametrize('name', ['g1_config1', 'g3_apo_periodic'])
+def test_resume_matches_reference_golden(name):
+    from orbitanalysis_amd.savefile import MemorySavefile
+    fix = load(name)
+    u, meta = universe(fix)
+    out = MemorySavefile()
+    k = 3
+    from orbitanalysis_amd.track_orbits import track_orbits
+    track_orbits(u.snapshot_numbers[:k], u.main_branches()[:k], u.regions, u.load_snapshot_data,
+                 out, verbose=False, **meta['run'])
+    track_orbits(u.snapshot_numbers, u.main_branches(), u.regions, u.load_snapshot_data,
+                 out, verbose=False, resume=True, **meta['run'])
+    compare_groups(out.groups, groups(fix, 'resume/'), {})
+
+
+@pytest.mark.parametrize('name', ['g1_config1', 'g2_overlap_birth_massarray', 'g3_apo_periodic',
+                                  'g5_fp32_centre32', 'g8_many_small_halos'])
+def test_bucketed_and_packed_paths_match(name):
+    """Tiny LDS tables force every halo through the hash-bucketed multi-work-group
+    path (and many halos per item through the packed path): same outputs."""
+    from orbitanalysis_amd.engine import OrbitEngine
+    fix = load(name)
+    u, meta = universe(fix)
+    for entries, big in ((256, 200), (700, 128)):
+        eng = OrbitEngine(mode=meta['run']['mode'], lds_entries=entries, big_entries=big, hmax=7)
+        out = run_driver(u, meta['run'], engine=eng)
+        compare_groups(out.groups, groups(fix), {})
+
+
+def _oracle_run(u, mode):
+    from oracle import orbit_oracle as O
+    return O.track_orbits(u.snapshot_numbers, u.main_branches(), u.regions,
+                          u.load_snapshot_data, O.MemoryRecord(), mode=mode).groups
+
+
+@pytest.mark.parametrize('kw', [
+    dict(n_halos=60, n_per_halo=5000, n_snapshots=3, seed=21, dtype=np.float32,
+         centre_dtype=np.float32, bulk='catalogue', box_size=200.0),
+    dict(n_halos=12, n_per_halo=30000, n_snapshots=3, seed=22),
+    dict(n_halos=25, n_per_halo=4000, n_snapshots=3, seed=23, id_offset=2 ** 32 - 40000),
+    dict(n_halos=25, n_per_halo=4000, n_snapshots=3, seed=24, id_dtype=np.int32,
+         masses='array', dtype=np.float32),
+    dict(n_halos=8, n_per_halo=3000, n_snapshots=3, seed=25, id_dtype=np.uint64,
+         id_offset=2 ** 63 + 5, cosmology=dict(redshift=1.0, H0=0.1, Omega_m=0.3, Omega_L=0.7)),
+])
+@pytest.mark.parametrize('mode', ['pericentric', 'apocentric'])
+def test_random_cases_match_oracle(kw, mode):
+    from orbitanalysis_amd.synthetic import PlummerSnapshots
+    u = PlummerSnapshots(**kw)
+    rep = {}
+    compare_groups(run_driver(u, dict(mode=mode)).groups, _oracle_run(u, mode), rep)
+    assert rep['angles'] > 0
+    assert rep['angle_mismatch'] / rep['angles'] < ANGLE_MISMATCH_MAX, rep

@@ -1,0 +1,121 @@
+"""CPU-only checks: the C-ABI library loads and exports every declared symbol, struct
+layouts agree, host-side planning mirrors NumPy's promotion rules, and the device
+path fails loudly without a GPU (no silent CPU fallback)."""
+import os
+import re
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+def test_library_exports_every_declared_symbol():
+    from orbitanalysis_amd import _native as N
+    lib = N.load()
+    hdr = open(os.path.join(ROOT, 'include', 'orbit_hip.h')).read()
+    declared = set(re.findall(r'\b(oa_[a-z_0-9]+)\s*\(', hdr))
+    assert declared, 'no declarations parsed'
+    raw = ctypes.CDLL(N.LIB_PATH)
+    for name in declared:
+        assert hasattr(raw, name), name
+    assert declared == set(N.SYMBOLS), declared ^ set(N.SYMBOLS)
+    assert lib.oa_abi_version() == N.ABI_VERSION
+    assert lib.oa_struct_size(0) == 96 and lib.oa_struct_size(1) == 32
+    assert lib.oa_step_lds_bytes(16384, 32768, 0) < 160 * 1024
+
+
+def test_no_silent_cpu_fallback():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip('GPU present')
+    from orbitanalysis_amd import _native as N
+    from orbitanalysis_amd.engine import OrbitEngine
+    with pytest.raises(N.NativeUnavailable):
+        OrbitEngine()
+
+
+def test_null_args_rejected_without_device():
+    from orbitanalysis_amd import _native as N
+    lib = N.load()
+    a = N.StepArgs()
+    a.id_bytes = 3
+    assert lib.oa_step(a, None) == -1
+    assert b'id_bytes' in lib.oa_last_error()
+
+
+@pytest.mark.parametrize('coord,centre,vel,bulk,box', [
+    (np.float64, np.float64, np.float64, None, None),
+    (np.float32, np.float32, np.float32, None, 50.0),
+    (np.float32, np.float32, np.float32, 'cat32', [60.0, 70.0, 80.0]),
+    (np.float32, np.float64, np.float32, 'cat64', np.array([10.0, 10.0, 10.0], np.float32)),
+    (np.float32, np.float32, np.float32, 'mass64', np.array([10.0], np.float64)),
+])
+def test_dtype_plan_follows_numpy(coord, centre, vel, bulk, box):
+    from orbitanalysis_amd.engine import plan_dtypes
+    from orbitanalysis_amd.utils import hubble_parameter
+    n = 5
+    snap = {'ids': np.arange(n), 'coordinates': np.ones((n, 3), coord),
+            'velocities': np.ones((n, 3), vel), 'masses': 1.0, 'redshift': 0.3}
+    if box is not None:
+        snap['box_size'] = box
+    cat = None
+    if bulk == 'cat32':
+        cat = np.zeros((1, 3), np.float32)
+    elif bulk == 'cat64':
+        cat = np.zeros((1, 3), np.float64)
+    elif bulk == 'mass64':
+        snap['masses'] = np.ones(n, np.float64)
+    H = hubble_parameter(0.3, 70.0, 0.3, 0.7)
+    c = np.zeros(3, centre)
+    p = plan_dtypes(snap, c, None if cat is None else cat[0], H, 0.3)
+    dx = snap['coordinates'] - c
+    assert p.dx == dx.dtype
+    from oracle import orbit_oracle as O
+    if box is not None:
+        ref = O.recenter_coordinates(dx.copy(), box)
+        assert ref.dtype == p.dx
+        assert len(p.box) == (3 if np.ndim(box) == 0 else len(box))
+    b = cat[0] if cat is not None else O.bulk_velocity(snap['velocities'], snap['masses'])
+    assert p.bulk == np.asarray(b).dtype
+    assert p.vb == (snap['velocities'] - b).dtype
+
+
+def test_wrap_dtype_python_list_box_is_weak():
+    from orbitanalysis_amd.engine import plan_dtypes
+    snap = {'ids': np.arange(2), 'coordinates': np.ones((2, 3), np.float32),
+            'velocities': np.ones((2, 3), np.float32), 'masses': 1.0, 'box_size': [5.0, 5.0, 5.0]}
+    p = plan_dtypes(snap, np.zeros(3, np.float32), None, np.float64(0.0), 0.0)
+    assert p.wrap_f64 is False                       # Python floats are weak (NEP 50)
+    snap['box_size'] = 5.0
+    assert plan_dtypes(snap, np.zeros(3, np.float32), None, np.float64(0.0), 0.0).wrap_f64
+
+
+def test_plan_items_invariants():
+    from orbitanalysis_amd.engine import plan_items
+    rng = np.random.default_rng(0)
+    cur = rng.integers(0, 3000, 500)
+    cur[::37] = 50000
+    prev = cur + rng.integers(-10, 10, 500)
+    prev[::11] = -1
+    items, big, scratch = plan_items(cur, prev, 4096, 3000, hmax=16)
+    covered = np.zeros(500, int)
+    for it in items:
+        assert it['nbuckets'] == 1 and it['h1'] - it['h0'] <= 16
+        assert cur[it['h0']:it['h1']].sum() <= 4096
+        covered[it['h0']:it['h1']] += 1
+    for h in np.unique(big['h0']):
+        b = big[big['h0'] == h]
+        assert sorted(b['bucket']) == list(range(b['nbuckets'][0]))
+        assert cur[h] / b['nbuckets'][0] <= 0.7 * 3000
+        covered[h] += 1
+    assert np.all(covered == 1)
+    assert scratch == sum(np.maximum(prev[it['h0']:it['h1']], 0).sum() for it in items)
+
+
+def test_synthetic_generator_is_deterministic():
+    from orbitanalysis_amd.synthetic import PlummerSnapshots
+    a = PlummerSnapshots(n_halos=2, n_per_halo=300, n_snapshots=3, seed=5).input_digest()
+    b = PlummerSnapshots(n_halos=2, n_per_halo=300, n_snapshots=3, seed=5).input_digest()
+    assert a == b

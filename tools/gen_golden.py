@@ -120,12 +120,12 @@ BATCH_CASES = {
     'g4_hubble_catalogue': dict(
         gen=dict(n_halos=3, n_per_halo=[800, 600, 700], n_snapshots=5, seed=4, dt=0.5,
                  bulk='catalogue',
-                 cosmology=dict(redshift=0.5, H0=70.0, Omega_m=0.3, Omega_L=0.7)),
+                 cosmology=dict(redshift=0.5, H0=0.07, Omega_m=0.3, Omega_L=0.7)),
         run=dict(mode='pericentric')),
     'g5_fp32_centre32': dict(
         gen=dict(n_halos=2, n_per_halo=[1500, 1000], n_snapshots=5, seed=5, dt=0.5,
                  dtype='float32', centre_dtype='float32', box_size=[60.0, 70.0, 80.0],
-                 cosmology=dict(redshift=0.2, H0=67.7, Omega_m=0.31, Omega_L=0.69)),
+                 cosmology=dict(redshift=0.2, H0=0.0677, Omega_m=0.31, Omega_L=0.69, Omega_k=0.0)),
         run=dict(mode='pericentric')),
     'g5_fp32_centre64': dict(
         gen=dict(n_halos=2, n_per_halo=[1500, 1000], n_snapshots=5, seed=6, dt=0.5,
