@@ -1,0 +1,258 @@
+#!/usr/bin/env python
+"""bench.py — particle-snapshots/s of the per-snapshot orbit-tagging hot path.
+
+Workload (BASELINE.json configs[2], the metric's 1-GPU configuration): 1e8
+particles per GPU in 1e4 halo region blocks, float32 coordinates/velocities with
+float32 catalogue centres and bulk velocities, int64 IDs, periodic box, Hubble term
+on.  A step = one snapshot of track_orbits' per-snapshot body on device-resident
+inputs: fused frame + ID join + sign flip + angles (oa_step) and the apsis output
+assembly (oa_compact).  Multi-GPU: particles sharded by ID range, weak scaling (1e8
+per GPU), one RCCL all-gather of the halo catalogue rows per snapshot.
+
+Prints ONE JSON line on rank 0 (contract in the task statement): value =
+particle-snapshots/s over all ranks; roofline = algorithmic bytes of the oa_step
+kernel / its HIP-event duration vs 8 TB/s; cpu_baseline = the CPU oracle (NumPy
+restatement of the reference path, 1 core) timed on a bounded sample of the same
+workload, with its apsis IDs checked against the GPU's for that sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = 'particle-snapshots/sec (peri/apo tagging), 1e8 particles, 1/2/4/8 GPUs'
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(*a):
+    print('[bench]', *a, file=sys.stderr, flush=True)
+
+
+def step_bytes(pr, n_prev, n_apsis):
+    """Algorithmic HBM bytes of one oa_step launch: every
+    current particle reads id + x + v and writes its record; every previous
+    particle reads id + record; every apsis writes id + f16 angle."""
+    p = pr.plan
+    cur = p.ids.itemsize + 3 * p.coord.itemsize + 3 * p.vel.itemsize + p.rec_bytes
+    if p.mass is not None:
+        cur += p.mass.itemsize
+    prev = p.ids.itemsize + p.rec_bytes
+    return pr.n * cur + n_prev * prev + n_apsis * (p.ids.itemsize + 2)
+
+
+def cpu_baseline(snap_cur, snap_prev, cat_cur, cat_prev, H, z, gpu_prev_angles,
+                 gpu_ids, gpu_offs, n_halos, mode):
+    """Time the oracle's per-halo path (track_orbits.py:147-185 for a compared
+    snapshot) on the first n_halos blocks; return rate + parity vs the GPU."""
+    from oracle import orbit_oracle as O
+
+    def host(snap, k):
+        offs = snap['region_offsets']
+        end = int(offs[k]) if k < len(offs) else int(snap['ids'].numel())
+        d = {key: snap[key][:end].cpu().numpy() for key in ('ids', 'coordinates', 'velocities')}
+        d.update({key: snap[key] for key in ('masses', 'box_size', 'redshift')})
+        d['region_offsets'] = offs[:k]
+        return d, np.append(offs[:k], end)
+
+    cur, cb = host(snap_cur, n_halos)
+    prv, pb = host(snap_prev, n_halos)
+    ang_prev = gpu_prev_angles[:pb[-1]]
+    # previous-snapshot frame (state input of the step, untimed)
+    prev_rh, prev_vr = [], []
+    for j in range(n_halos):
+        rh, vr, _ = O.region_frame(prv, (pb[j], pb[j + 1]), cat_prev[0][j], cat_prev[2][j], H)
+        prev_rh.append(rh)
+        prev_vr.append(vr)
+    t0 = time.perf_counter()
+    ids_out = []
+    for j in range(n_halos):
+        sl = (cb[j], cb[j + 1])
+        rh, vr, _ = O.region_frame(cur, sl, cat_cur[0][j], cat_cur[2][j], H)
+        d = O.compare_radial_velocities(cur['ids'][sl[0]:sl[1]], prv['ids'][pb[j]:pb[j + 1]],
+                                        vr, prev_vr[j], rh, prev_rh[j], mode)
+        O.calc_angles(sl[1] - sl[0], ang_prev[pb[j]:pb[j + 1]], d)
+        ids_out.append(d['apsis_ids'])
+    dt = time.perf_counter() - t0
+    units = int(cb[-1])
+    want = np.concatenate(ids_out)
+    got = gpu_ids[:int(gpu_offs[n_halos])]
+    return units / dt, dt, units, bool(np.array_equal(want, got))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--particles', type=float, default=1e8, help='per GPU')
+    ap.add_argument('--halos', type=int, default=10000)
+    ap.add_argument('--mode', default='pericentric')
+    ap.add_argument('--max-snapshots', type=int, default=16)
+    ap.add_argument('--cpu-halos', type=int, default=1500)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    import torch
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=dev)
+
+    import orbitanalysis_amd  # noqa: F401
+    from orbitanalysis_amd import _native
+    from orbitanalysis_amd.engine import OrbitEngine, Workspace
+    from orbitanalysis_amd.synthetic_device import DevicePlummer
+    from orbitanalysis_amd.utils import hubble_parameter
+
+    t_setup = time.perf_counter()
+    gen = DevicePlummer(n_halos=args.halos, n_particles=int(args.particles), seed=0,
+                        rank=rank, world=world, device=dev)
+    S = min(args.steps + args.warmup + 1, args.max_snapshots)
+    snaps, cats = [], []
+    for s in range(S):
+        snaps.append(gen.snapshot(s))
+        cats.append(gen.catalogue(s))
+        log('rank %d snapshot %d/%d: %d particles' % (rank, s + 1, S, snaps[-1]['ids'].numel()))
+    cos = gen.cosmology
+    H = hubble_parameter(cos['redshift'], cos['H0'], cos['Omega_m'], cos['Omega_L'])
+    z = cos['redshift']
+    exists = np.arange(args.halos)
+    eng = OrbitEngine(mode=args.mode, device=dev)
+
+    # snapshot 0: frame only (the reference's i == istart), outside the timing
+    prep0 = eng.prepare(snaps[0], cats[0][0], cats[0][2], H, z, exists, False)
+    eng.launch(prep0, None)
+    chain = [(prep0, 0)]
+    layout = (prep0.starts, prep0.counts, exists, prep0.plan, prep0.n)
+    for t in range(1, args.warmup + args.steps + 1):
+        s = t % S
+        pr = eng.prepare(snaps[s], cats[s][0], cats[s][2], H, z, exists, True, prev_layout=layout)
+        chain.append((pr, s))
+        layout = (pr.starts, pr.counts, exists, pr.plan, pr.n)
+    preps = [c[0] for c in chain[1:]]
+    ws = Workspace(dev, torch.int64 if preps[0].plan.ids.itemsize == 8 else torch.int32,
+                   max(p.scratch for p in preps), max(p.n_prev for p in preps),
+                   max(int(p.has_prog.sum()) for p in preps), max(len(p.items) for p in preps),
+                   any(len(p.big) for p in preps))
+    # catalogue exchange (N > 1): rank r holds catalogue rows [r*nl, (r+1)*nl)
+    nl = -(-args.halos // world)
+    cat_local, cat_all = [], None
+    if world > 1:
+        cat_all = torch.empty(nl * world, 6, dtype=torch.float64, device=dev)
+        for pr in preps:
+            hv = pr.halos.view(torch.float64).view(args.halos, 12)
+            rows = torch.zeros(nl, 6, dtype=torch.float64, device=dev)
+            lo, hi = rank * nl, min((rank + 1) * nl, args.halos)
+            if hi > lo:
+                rows[:hi - lo] = hv[lo:hi, 4:10]
+            cat_local.append(rows)
+    log('setup %.1f s; items/step %d, big %d' % (time.perf_counter() - t_setup,
+                                                  len(preps[0].items), len(preps[0].big)))
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+
+    def run(k, events=None):
+        pr, s = chain[k + 1]
+        prev_pr, ps = chain[k]
+        if world > 1:
+            dist.all_gather_into_tensor(cat_all, cat_local[k])
+            pr.halos.view(torch.float64).view(args.halos, 12)[:, 4:10] = cat_all[:args.halos]
+        eng.launch(pr, ws, snaps[ps]['ids'], prev_pr.rec, step_events=events)
+
+    for k in range(args.warmup):
+        run(k)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier(device_ids=[local])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        run(args.warmup + i, evs[i])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier(device_ids=[local])
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    units = sum(chain[args.warmup + i + 1][0].n for i in range(args.steps))
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        u = torch.tensor([units], dtype=torch.float64, device=dev)
+        dist.all_reduce(u, op=dist.ReduceOp.SUM)
+        units = float(u.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    last = chain[-1][0]
+    n_apsis = int(ws.total.item())
+    bytes_launch = float(np.mean([step_bytes(chain[args.warmup + i + 1][0],
+                                             chain[args.warmup + i + 1][0].n_prev, n_apsis)
+                                  for i in range(args.steps)]))
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    log('elapsed %.4f s for %d steps; k_step %.3f ms; %.1f GB/s; apsis %d'
+        % (elapsed, args.steps, kern_ms, achieved, n_apsis))
+
+    traffic = None
+    pmc = os.path.join(ROOT, 'profiles', 'pmc_k_step.json')
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get('hbm_bytes_per_launch')
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        pr_last, s_last = chain[-1]
+        prev_pr, s_prev = chain[-2]
+        words = prev_pr.rec.view(torch.int32).view(-1, prev_pr.plan.rec_bytes // 4)
+        ang_prev = (words[:, 3 if prev_pr.plan.rec_bytes == 16 else 6] & 0xFFFF).to(
+            torch.int32).cpu().numpy().astype(np.uint16).view(np.float16)
+        offs = ws.offsets[:int(last.has_prog.sum()) + 1].cpu().numpy()
+        gids = ws.out_ids[:n_apsis].cpu().numpy()
+        nh = min(args.cpu_halos, args.halos)
+        rate, dt, cu, ok = cpu_baseline(snaps[s_last], snaps[s_prev], cats[s_last], cats[s_prev],
+                                        H, z, ang_prev, gids, offs, nh, args.mode)
+        cpu = {'value': rate, 'unit': 'particle-snapshots/s', 'cores': 1, 'kind': 'port',
+               'sample': '%d of %d halos (%d particles) of the last timed snapshot, oracle '
+                         'region_frame+compare_radial_velocities+calc_angles per halo, %.1f s; '
+                         'apsis IDs identical to the GPU: %s' % (nh, args.halos, cu, dt, ok)}
+        log('cpu baseline %.3e particle-snapshots/s over %.1f s, parity %s' % (rate, dt, ok))
+
+    if rank == 0:
+        out = {
+            'metric': METRIC, 'value': units / elapsed, 'unit': 'particle-snapshots/s',
+            'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': elapsed / args.steps * 1e3, 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None,
+            'dtype': last.plan.coord.name.replace('float', 'f'),
+            'data': 'synthetic: %d Plummer spheres (device-generated, AHW sampling, leapfrog '
+                    'orbits), region cut r<4a, per-snapshot shuffled blocks, int64 randperm IDs'
+                    % args.halos,
+            'config': {'workload': 'BASELINE configs[2]: %.0e particles/GPU, %d halos, f32 '
+                                   'coords/vels/centres, catalogue bulk velocities, periodic '
+                                   'box, Hubble term, %s' % (args.particles, args.halos, args.mode),
+                       'particles_per_step_per_gpu': int(last.n),
+                       'halos': args.halos, 'work_items': int(len(last.items)),
+                       'parallelism': 'id-range shards x%d' % world},
+            'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
+                         'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
+                         'traffic': traffic, 'kernel': 'k_step', 'kernel_ms': kern_ms,
+                         'alg_bytes_per_launch': bytes_launch},
+            'cpu_baseline': cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

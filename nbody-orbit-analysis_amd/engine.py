@@ -192,6 +192,65 @@ class StepResult:
     extra: dict = field(default_factory=dict)
 
 
+@dataclass
+class PreparedStep:
+    """Everything one snapshot step needs on the device, built by OrbitEngine.prepare."""
+    plan: DtypePlan
+    n: int
+    starts: np.ndarray
+    counts: np.ndarray
+    has_prog: np.ndarray
+    items: np.ndarray
+    big: np.ndarray
+    scratch: int
+    compare: bool
+    n_prev: int = 0
+    halos: Optional[torch.Tensor] = None
+    d_items: Optional[torch.Tensor] = None
+    d_big: Optional[torch.Tensor] = None
+    rec: Optional[torch.Tensor] = None
+    angles_in: Optional[torch.Tensor] = None
+    halo_list: Optional[torch.Tensor] = None
+    bulk_computed: bool = False
+    snap: dict = field(default_factory=dict)
+    args: N.StepArgs = field(default_factory=N.StepArgs)
+    cargs: N.CompactArgs = field(default_factory=N.CompactArgs)
+
+    def more_buckets(self):
+        mb = np.ones(len(self.counts), dtype=np.int64)
+        for h0, nb in zip(self.big['h0'], self.big['nbuckets']):
+            mb[h0] = max(mb[h0], 2 * nb)
+        return mb
+
+
+class Workspace:
+    """Reusable scratch for compare steps (sized for the largest step it serves)."""
+
+    def __init__(self, device, id_torch_dtype, scratch, n_prev, n_slots, n_items, dense):
+        def e(n, dt):
+            return torch.empty(max(int(n), 1), dtype=dt, device=device)
+        self.scratch_ids = e(scratch, id_torch_dtype)
+        self.scratch_ang = e(scratch, torch.int16)
+        self.dense = e(n_prev if dense else 1, torch.int16)
+        self.halo_count = e(n_slots, torch.int32)
+        self.item_count = e(n_items, torch.int32)
+        self.status = e(1, torch.int32)
+        self.offsets = e(n_slots + 1, torch.int64)
+        self.out_ids = e(n_prev, id_torch_dtype)
+        self.out_ang = e(n_prev, torch.int16)
+        self.total = e(1, torch.int64)
+
+    @classmethod
+    def for_step(cls, pr, device):
+        dt = torch.int64 if pr.plan.ids.itemsize == 8 else torch.int32
+        return cls(device, dt, pr.scratch, pr.n_prev, int(pr.has_prog.sum()), len(pr.items),
+                   len(pr.big) > 0)
+
+    def reset(self, n_slots):
+        self.halo_count[:max(n_slots, 1)].zero_()
+        self.status.zero_()
+
+
 class OrbitEngine:
     """Per-snapshot device pipeline with carried state (see module docstring)."""
 
@@ -219,8 +278,10 @@ class OrbitEngine:
         self.prev = None
 
     # ------------------------------------------------------------------ tables
-    def build_tables(self, snapshot, centres, bulk_cat, exists, compare, min_buckets=None):
-        n = len(snapshot['ids'])
+    def build_tables(self, snapshot, centres, bulk_cat, exists, compare, min_buckets=None,
+                     prev_layout=None):
+        n = int(snapshot['ids'].numel()) if isinstance(snapshot['ids'], torch.Tensor) \
+            else len(snapshot['ids'])
         starts = np.asarray(snapshot['region_offsets'], dtype=np.int64).reshape(-1)
         ends = np.append(starts[1:], n)
         counts = ends - starts
@@ -238,12 +299,12 @@ class OrbitEngine:
         halos['out_slot'] = -1
         has_prog = np.zeros(nh, dtype=bool)
         if compare:
-            pe = self.prev.exists
+            p_starts, p_counts, pe = prev_layout[0], prev_layout[1], np.asarray(prev_layout[2])
             p = np.searchsorted(pe, exists)
             pc = np.minimum(p, max(len(pe) - 1, 0))
             has_prog = (p < len(pe)) & (pe[pc] == exists) if len(pe) else has_prog
-            halos['prev_off'][has_prog] = self.prev.starts[p[has_prog]]
-            halos['prev_cnt'][has_prog] = self.prev.counts[p[has_prog]]
+            halos['prev_off'][has_prog] = p_starts[p[has_prog]]
+            halos['prev_cnt'][has_prog] = p_counts[p[has_prog]]
             halos['out_slot'][has_prog] = np.arange(int(has_prog.sum()))
         items, big, scratch = plan_items(counts, halos['prev_cnt'], self.entries,
                                          self.big_entries, self.hmax, min_buckets=min_buckets)
@@ -256,58 +317,74 @@ class OrbitEngine:
         if compare and self.prev is None:
             raise RuntimeError('compare step without a previous snapshot')
         dev = self.device
-        plan = plan_dtypes(snapshot, centres[0] if len(centres) else np.zeros(3),
-                           None if bulk_cat is None else bulk_cat[0], H, z)
-        if compare and plan.dx != self.prev.plan.dx:
-            raise NotImplementedError('r̂ dtype changed between snapshots (%s -> %s)'
-                                      % (self.prev.plan.dx, plan.dx))
-        if compare and plan.ids.itemsize != self.prev.plan.ids.itemsize:
-            raise NotImplementedError('ids dtype changed between snapshots')
-        ids = to_device(snapshot['ids'], dev)
-        x = to_device(snapshot['coordinates'], dev)
-        v = to_device(snapshot['velocities'], dev)
-        n = ids.numel()
-        if x.numel() != 3 * n or v.numel() != 3 * n:
-            raise ValueError('coordinates/velocities must be (N, 3) with N = len(ids)')
+        snap = dict(snapshot)
+        for k in ('ids', 'coordinates', 'velocities'):
+            snap[k] = to_device(snapshot[k], dev)
+        if is_array(snapshot['masses']):
+            snap['masses'] = to_device(snapshot['masses'], dev)
         min_b = None
-        for attempt in range(8):
-            res, rec, counts_ok = self._run(snapshot, plan, ids, x, v, centres, bulk_cat, H, z,
-                                            exists, compare, angles_in, min_b)
-            if counts_ok is None:
+        for _ in range(8):
+            prep = self.prepare(snap, centres, bulk_cat, H, z, exists, compare,
+                                angles_in=angles_in, min_buckets=min_b, plan_src=snapshot)
+            ws = Workspace.for_step(prep, dev)
+            res = self.launch(prep, ws)
+            if not compare or not len(prep.big) or not (int(ws.status.item()) &
+                                                        N.STATUS_BUCKET_OVERFLOW):
                 break
-            min_b = counts_ok          # bucket overflow: re-plan with more buckets
+            min_b = prep.more_buckets()      # a hash bucket overflowed: re-plan
         else:
             raise RuntimeError('hash buckets kept overflowing (adversarial IDs?)')
-        self.prev = SnapshotState(ids=ids, rec=rec, starts=res.extra['starts'],
-                                  counts=res.extra['counts'], exists=exists, plan=plan)
+        self.prev = SnapshotState(ids=snap['ids'], rec=prep.rec, starts=prep.starts,
+                                  counts=prep.counts, exists=exists, plan=prep.plan)
         return res
 
-    def _run(self, snapshot, plan, ids, x, v, centres, bulk_cat, H, z, exists, compare,
-             angles_in, min_buckets):
-        dev, lib = self.device, self.lib
+    def prepare(self, snap, centres, bulk_cat, H, z, exists, compare, angles_in=None,
+                min_buckets=None, plan_src=None, prev_layout=None):
+        """Host half of a step: dtype plan, halo/item tables, device uploads.
+
+        ``snap`` holds device tensors for ids/coordinates/velocities(/masses);
+        ``prev_layout`` (starts, counts, exists, plan) defaults to the engine state."""
+        dev = self.device
+        exists = np.asarray(exists)
+        plan = plan_dtypes(plan_src if plan_src is not None else snap,
+                           centres[0] if len(centres) else np.zeros(3),
+                           None if bulk_cat is None else bulk_cat[0], H, z)
+        if prev_layout is None and compare:
+            p = self.prev
+            prev_layout = (p.starts, p.counts, p.exists, p.plan, p.ids.numel())
+        if compare:
+            pplan = prev_layout[3]
+            if plan.dx != pplan.dx:
+                raise NotImplementedError('r̂ dtype changed between snapshots (%s -> %s)'
+                                          % (pplan.dx, plan.dx))
+            if plan.ids.itemsize != pplan.ids.itemsize:
+                raise NotImplementedError('ids dtype changed between snapshots')
+        n = snap['ids'].numel()
+        if snap['coordinates'].numel() != 3 * n or snap['velocities'].numel() != 3 * n:
+            raise ValueError('coordinates/velocities must be (N, 3) with N = len(ids)')
         halos, items, big, scratch, starts, counts, has_prog = self.build_tables(
-            snapshot, centres, bulk_cat, exists, compare, min_buckets)
-        n = ids.numel()
-        nh = len(halos)
-        n_slots = int(has_prog.sum())
-        stream = torch.cuda.current_stream(dev).cuda_stream
-        d_halos = torch.from_numpy(halos.view(np.uint8)).to(dev)
-        d_items = torch.from_numpy(items.view(np.uint8)).to(dev)
-        d_big = torch.from_numpy(big.view(np.uint8)).to(dev)
-        if bulk_cat is None and nh:
-            masses = snapshot['masses']
-            m = to_device(masses, dev) if plan.mass is not None else None
-            hl = torch.arange(nh, dtype=torch.int32, device=dev)
-            N.check(lib.oa_bulk_velocity(v.data_ptr(), int(plan.vel == F64), _ptr(m),
-                                         int(plan.mass == F64), d_halos.data_ptr(),
-                                         hl.data_ptr(), nh, stream), 'oa_bulk_velocity')
-        rec = torch.empty(n * plan.rec_bytes, dtype=torch.uint8, device=dev)
-        a = N.StepArgs()
-        a.ids, a.coords, a.vels, a.n_cur = ids.data_ptr(), x.data_ptr(), v.data_ptr(), n
-        a.rec_out = rec.data_ptr()
-        a.halos, a.n_halos = d_halos.data_ptr(), nh
-        a.items, a.n_items = d_items.data_ptr(), len(items)
-        a.big_items, a.n_big_items = d_big.data_ptr(), len(big)
+            snap, centres, bulk_cat, exists, compare, min_buckets, prev_layout)
+        pr = PreparedStep(plan=plan, n=n, starts=starts, counts=counts, has_prog=has_prog,
+                          items=items, big=big, scratch=scratch, compare=bool(compare),
+                          n_prev=prev_layout[4] if compare else 0)
+        pr.halos = torch.from_numpy(halos.view(np.uint8)).to(dev)
+        pr.d_items = torch.from_numpy(items.view(np.uint8)).to(dev)
+        pr.d_big = torch.from_numpy(big.view(np.uint8)).to(dev)
+        pr.rec = torch.empty(n * plan.rec_bytes, dtype=torch.uint8, device=dev)
+        pr.snap = snap
+        pr.bulk_computed = bulk_cat is None and len(halos) > 0
+        if pr.bulk_computed:
+            pr.halo_list = torch.arange(len(halos), dtype=torch.int32, device=dev)
+        if angles_in is not None and not compare:
+            pr.angles_in = to_device(np.asarray(angles_in, dtype=np.float16).view(np.int16), dev)
+        a = pr.args
+        a.ids, a.coords, a.vels, a.n_cur = (snap['ids'].data_ptr(), snap['coordinates'].data_ptr(),
+                                            snap['velocities'].data_ptr(), n)
+        a.rec_out = pr.rec.data_ptr()
+        a.angles_in = _ptr(pr.angles_in)
+        a.halos, a.n_halos = pr.halos.data_ptr(), len(halos)
+        a.items, a.n_items = pr.d_items.data_ptr(), len(items)
+        a.big_items, a.n_big_items = pr.d_big.data_ptr(), len(big)
         a.H, a.one_plus_z = float(H), float(1 + z)
         a.n_box_dims = len(plan.box)
         for d, L in enumerate(plan.box):
@@ -319,57 +396,52 @@ class OrbitEngine:
         a.compare = int(bool(compare))
         a.lds_entries, a.lds_slots = self.entries, self.slots
         a.big_entries, a.big_slots = self.big_entries, self.big_slots
-        keep = [d_halos, d_items, d_big, rec]
-        ain = None
-        if angles_in is not None and not compare:
-            ain = to_device(np.asarray(angles_in, dtype=np.float16).view(np.int16), dev)
-            a.angles_in = ain.data_ptr()
-        res = StepResult(n_slots=n_slots, has_prog=has_prog, halos=d_halos)
-        res.extra.update(starts=starts, counts=counts, items=items, big=big)
-        if compare:
-            prev = self.prev
-            a.ids_prev, a.rec_prev, a.n_prev = prev.ids.data_ptr(), prev.rec.data_ptr(), prev.ids.numel()
-            n_prev = prev.ids.numel()
-            scr_ids = torch.empty(max(scratch, 1), dtype=ids.dtype, device=dev)
-            scr_ang = torch.empty(max(scratch, 1), dtype=torch.int16, device=dev)
-            dense = torch.empty(max(n_prev, 1) if len(big) else 1, dtype=torch.int16, device=dev)
-            halo_count = torch.zeros(max(n_slots, 1), dtype=torch.int32, device=dev)
-            item_count = torch.zeros(max(len(items), 1), dtype=torch.int32, device=dev)
-            status = torch.zeros(1, dtype=torch.int32, device=dev)
-            a.scratch_ids, a.scratch_ang, a.dense_code = (scr_ids.data_ptr(), scr_ang.data_ptr(),
-                                                         dense.data_ptr())
-            a.halo_count, a.item_count, a.status = (halo_count.data_ptr(), item_count.data_ptr(),
-                                                   status.data_ptr())
-            keep += [scr_ids, scr_ang, dense, halo_count, item_count, status]
-        N.check(lib.oa_step(a, stream), 'oa_step')
-        if not compare:
-            return res, rec, None
-        if len(big):
-            st = int(status.item())
-            if st & N.STATUS_BUCKET_OVERFLOW:
-                mb = np.ones(nh, dtype=np.int64)
-                for h0, nb in zip(big['h0'], big['nbuckets']):
-                    mb[h0] = max(mb[h0], 2 * nb)
-                if min_buckets is not None:
-                    mb = np.maximum(mb, 2 * np.asarray(min_buckets))
-                return res, rec, mb
-        offsets = torch.empty(n_slots + 1, dtype=torch.int64, device=dev)
-        out_ids = torch.empty(max(prev.ids.numel(), 1), dtype=ids.dtype, device=dev)
-        out_ang = torch.empty(max(prev.ids.numel(), 1), dtype=torch.int16, device=dev)
-        total = torch.zeros(1, dtype=torch.int64, device=dev)
-        c = N.CompactArgs()
-        c.halos, c.n_halos = d_halos.data_ptr(), nh
-        c.items, c.n_items = d_items.data_ptr(), len(items)
-        c.big_items, c.n_big_items = d_big.data_ptr(), len(big)
-        c.ids_prev, c.id_bytes = prev.ids.data_ptr(), plan.ids.itemsize
+        return pr
+
+    def launch(self, pr, ws, prev_ids=None, prev_rec=None, stream=None, step_events=None):
+        """Device half of a step: enqueue bulk / step / compact on ``stream``
+        (default: torch's current stream).  Never synchronises."""
+        lib = self.lib
+        st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        a = pr.args
+        if pr.bulk_computed:
+            m = pr.snap.get('masses') if pr.plan.mass is not None else None
+            N.check(lib.oa_bulk_velocity(a.vels, int(pr.plan.vel == F64), _ptr(m),
+                                         int(pr.plan.mass == F64), a.halos,
+                                         pr.halo_list.data_ptr(), a.n_halos, st),
+                    'oa_bulk_velocity')
+        res = StepResult(n_slots=int(pr.has_prog.sum()), has_prog=pr.has_prog, halos=pr.halos)
+        if pr.compare:
+            if prev_ids is None:
+                prev_ids, prev_rec = self.prev.ids, self.prev.rec
+            a.ids_prev, a.rec_prev, a.n_prev = prev_ids.data_ptr(), prev_rec.data_ptr(), pr.n_prev
+            ws.reset(res.n_slots)
+            a.scratch_ids, a.scratch_ang, a.dense_code = (ws.scratch_ids.data_ptr(),
+                                                         ws.scratch_ang.data_ptr(),
+                                                         ws.dense.data_ptr())
+            a.halo_count, a.item_count, a.status = (ws.halo_count.data_ptr(),
+                                                   ws.item_count.data_ptr(), ws.status.data_ptr())
+        if step_events is not None:
+            step_events[0].record()
+        N.check(lib.oa_step(a, st), 'oa_step')
+        if step_events is not None:
+            step_events[1].record()
+        if not pr.compare:
+            return res
+        c = pr.cargs
+        c.halos, c.n_halos = a.halos, a.n_halos
+        c.items, c.n_items = a.items, a.n_items
+        c.big_items, c.n_big_items = a.big_items, a.n_big_items
+        c.ids_prev, c.id_bytes = a.ids_prev, a.id_bytes
         c.scratch_ids, c.scratch_ang, c.dense_code = a.scratch_ids, a.scratch_ang, a.dense_code
-        c.halo_count, c.item_count, c.n_slots = a.halo_count, a.item_count, n_slots
-        c.offsets_out, c.out_ids, c.out_ang = offsets.data_ptr(), out_ids.data_ptr(), out_ang.data_ptr()
-        c.total_out = total.data_ptr()
-        N.check(lib.oa_compact(c, stream), 'oa_compact')
-        res.offsets, res.apsis_ids, res.apsis_ang, res.total = offsets, out_ids, out_ang, total
-        res.extra['keep'] = keep
-        return res, rec, None
+        c.halo_count, c.item_count, c.n_slots = a.halo_count, a.item_count, res.n_slots
+        c.offsets_out, c.out_ids, c.out_ang = (ws.offsets.data_ptr(), ws.out_ids.data_ptr(),
+                                               ws.out_ang.data_ptr())
+        c.total_out = ws.total.data_ptr()
+        N.check(lib.oa_compact(c, st), 'oa_compact')
+        res.offsets = ws.offsets[:res.n_slots + 1]
+        res.apsis_ids, res.apsis_ang, res.total = ws.out_ids, ws.out_ang, ws.total
+        return res
 
     # ------------------------------------------------------------------ host views
     def fetch(self, res, ids_dtype):
