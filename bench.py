@@ -39,10 +39,10 @@ def step_bytes(pr, n_prev, n_apsis):
     current particle reads id + x + v and writes its record; every previous
     particle reads id + record; every apsis writes id + f16 angle."""
     p = pr.plan
-    cur = p.ids.itemsize + 3 * p.coord.itemsize + 3 * p.vel.itemsize + p.rec_bytes
+    cur = p.ids.itemsize + 3 * p.coord.itemsize + 3 * p.vel.itemsize + p.state_bytes
     if p.mass is not None:
         cur += p.mass.itemsize
-    prev = p.ids.itemsize + p.rec_bytes
+    prev = p.ids.itemsize + p.state_bytes
     return pr.n * cur + n_prev * prev + n_apsis * (p.ids.itemsize + 2)
 
 
@@ -111,7 +111,9 @@ def main():
 
     import orbitanalysis_amd  # noqa: F401
     from orbitanalysis_amd import _native
-    from orbitanalysis_amd.engine import OrbitEngine, Workspace
+    from orbitanalysis_amd.engine import OrbitEngine, Workspace, meta_angles
+    from collections import namedtuple
+    State = namedtuple('State', 'ids rhat meta')
     from orbitanalysis_amd.synthetic_device import DevicePlummer
     from orbitanalysis_amd.utils import hubble_parameter
 
@@ -169,7 +171,7 @@ def main():
         if world > 1:
             dist.all_gather_into_tensor(cat_all, cat_local[k])
             pr.halos.view(torch.float64).view(args.halos, 12)[:, 4:10] = cat_all[:args.halos]
-        eng.launch(pr, ws, snaps[ps]['ids'], prev_pr.rec, step_events=events)
+        eng.launch(pr, ws, State(snaps[ps]['ids'], prev_pr.rhat, prev_pr.meta), step_events=events)
 
     for k in range(args.warmup):
         run(k)
@@ -213,9 +215,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         pr_last, s_last = chain[-1]
         prev_pr, s_prev = chain[-2]
-        words = prev_pr.rec.view(torch.int32).view(-1, prev_pr.plan.rec_bytes // 4)
-        ang_prev = (words[:, 3 if prev_pr.plan.rec_bytes == 16 else 6] & 0xFFFF).to(
-            torch.int32).cpu().numpy().astype(np.uint16).view(np.float16)
+        ang_prev = meta_angles(prev_pr.meta)
         offs = ws.offsets[:int(last.has_prog.sum()) + 1].cpu().numpy()
         gids = ws.out_ids[:n_apsis].cpu().numpy()
         nh = min(args.cpu_halos, args.halos)

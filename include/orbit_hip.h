@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OA_ABI_VERSION 1
+#define OA_ABI_VERSION 3
 
 #define OA_OK 0
 #define OA_E_ARG (-1)       /* invalid argument / unsupported dtype plan */
@@ -63,8 +63,9 @@ typedef struct oa_halo {
  *                hashes to `bucket` (blocks larger than one work-group's LDS).   */
 typedef struct oa_item {
     int32_t h0, h1, bucket, nbuckets;
-    int64_t scratch_off;        /* first scratch record of this item (nbuckets == 1) */
-    int64_t reserved;
+    int64_t scratch_off;        /* nbuckets == 1: first scratch slot of this item (a
+                                   multiple of 64; one slot per progenitor particle) */
+    int64_t n_pv;               /* nbuckets == 1: progenitor particles of the item   */
 } oa_item;
 
 /* Arguments of oa_step (one snapshot of the batch driver's inner loop). */
@@ -76,12 +77,12 @@ typedef struct oa_step_args {
     int64_t n_cur;
     /* previous snapshot state (outputs of the previous oa_step) */
     const void *ids_prev;       /* (n_prev,) same dtype as ids                     */
-    const void *rec_prev;       /* (n_prev,) particle records, see rec_out         */
+    const void *rhat_prev;      /* (n_prev,3) r̂ of the previous snapshot (dx dtype)  */
+    const uint32_t *meta_prev;  /* (n_prev,) meta words, see meta_out                */
     int64_t n_prev;
-    /* outputs */
-    void *rec_out;              /* (n_cur,) records: f32 plan {float rhat[3]; u32 meta}
-                                   16 B; f64 plan {double rhat[3]; u32 meta; u32 pad}
-                                   32 B.  meta = f16 angle bits | sign(v_r) << 16
+    /* outputs: the particle state the next snapshot reads */
+    void *rhat_out;             /* (n_cur,3) unit radial vectors, dx dtype           */
+    uint32_t *meta_out;         /* (n_cur,) f16 angle bits | sign(v_r) << 16
                                    (sign: 1 = v_r > 0, 2 = v_r < 0, 0 = neither)    */
     const uint16_t *angles_in;  /* optional (n_cur,) f16 bits used as angles when
                                    compare == 0 (checkpoint resume), NULL -> 0     */
@@ -106,8 +107,10 @@ typedef struct oa_step_args {
     int32_t big_entries;        /* the same for big_items (bucketed halos)        */
     int32_t big_slots;
     /* apsis scratch */
-    void *scratch_ids;          /* nbuckets==1 items: ordered records at scratch_off */
+    void *scratch_ids;          /* nbuckets==1 items: apsis records, one 64-slot segment
+                                   per 64 progenitor positions, packed per segment  */
     uint16_t *scratch_ang;
+    uint8_t *seg_count;         /* records per segment ([scratch slots / 64])        */
     uint16_t *dense_code;       /* nbuckets>1 halos: per previous position, f16 angle
                                    bits of an apsis or 0xFFFF                         */
     int32_t *halo_count;        /* [n_slots] apsis count per halo with a progenitor;
@@ -129,6 +132,7 @@ typedef struct oa_compact_args {
     int32_t id_bytes;
     const void *scratch_ids;
     const uint16_t *scratch_ang;
+    const uint8_t *seg_count;
     const uint16_t *dense_code;
     const int32_t *halo_count;
     const int32_t *item_count;
@@ -145,6 +149,10 @@ int oa_abi_version(void);
 /* sizeof() of the ABI structs (0 oa_halo, 1 oa_item, 2 oa_step_args,
  * 3 oa_compact_args) so a binding can verify its layout; -1 otherwise. */
 int64_t oa_struct_size(int32_t which);
+
+/* Compile-time configuration: 0 work-group size, 1 max halos per item,
+ * 2 phase-1 unroll, 3 phase-2 unroll; -1 otherwise. */
+int32_t oa_build_info(int32_t which);
 
 /* Message of the last failing call on this thread ("" if none). */
 const char *oa_last_error(void);
@@ -167,6 +175,11 @@ int oa_step(const oa_step_args *args, void *stream);
 /* Dynamic LDS bytes oa_step needs per work-group for the given table sizes
  * (bucketed != 0: the big_items layout, which also keeps a local index per entry). */
 int64_t oa_step_lds_bytes(int32_t entries, int32_t slots, int32_t bucketed);
+
+/* Diagnostic builds only (-DOA_STAMPS=1): copy the per-work-group phase timestamps
+ * (s_memrealtime, 100 MHz; 6 per work-group) of the last oa_step to host memory.
+ * Returns the number of values copied, -1 in normal builds. */
+int64_t oa_debug_stamps(uint64_t *host, int64_t n);
 
 /* Largest dynamic LDS allocation a work-group may use on this device (bytes). */
 int64_t oa_max_lds_bytes(void);

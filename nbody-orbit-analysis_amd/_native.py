@@ -11,8 +11,9 @@ import os
 import numpy as np
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, 'liborbit_hip.so')
-ABI_VERSION = 1
+# ORBIT_HIP_LIB selects an alternative build (kernel variants for tuning sweeps)
+LIB_PATH = os.environ.get('ORBIT_HIP_LIB') or os.path.join(PKG, 'liborbit_hip.so')
+ABI_VERSION = 3
 
 c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -21,7 +22,7 @@ HALO_DTYPE = np.dtype([('cur_off', '<i8'), ('cur_cnt', '<i8'), ('prev_off', '<i8
                        ('prev_cnt', '<i8'), ('centre', '<f8', (3,)), ('bulk', '<f8', (3,)),
                        ('out_slot', '<i8'), ('reserved', '<i8')])
 ITEM_DTYPE = np.dtype([('h0', '<i4'), ('h1', '<i4'), ('bucket', '<i4'), ('nbuckets', '<i4'),
-                       ('scratch_off', '<i8'), ('reserved', '<i8')])
+                       ('scratch_off', '<i8'), ('n_pv', '<i8')])
 
 MODE = {'pericentric': 0, 'apocentric': 1}
 STATUS_BUCKET_OVERFLOW = 1
@@ -29,8 +30,8 @@ STATUS_BUCKET_OVERFLOW = 1
 
 class StepArgs(ctypes.Structure):
     _fields_ = [('ids', c_vp), ('coords', c_vp), ('vels', c_vp), ('n_cur', c_i64),
-                ('ids_prev', c_vp), ('rec_prev', c_vp), ('n_prev', c_i64),
-                ('rec_out', c_vp), ('angles_in', c_vp),
+                ('ids_prev', c_vp), ('rhat_prev', c_vp), ('meta_prev', c_vp), ('n_prev', c_i64),
+                ('rhat_out', c_vp), ('meta_out', c_vp), ('angles_in', c_vp),
                 ('halos', c_vp), ('n_halos', c_i32), ('items', c_vp), ('n_items', c_i32),
                 ('big_items', c_vp), ('n_big_items', c_i32),
                 ('H', c_dbl), ('one_plus_z', c_dbl), ('box', c_dbl * 3), ('n_box_dims', c_i32),
@@ -38,7 +39,8 @@ class StepArgs(ctypes.Structure):
                 ('wrap_f64', c_i32), ('id_bytes', c_i32), ('mode', c_i32), ('compare', c_i32),
                 ('lds_entries', c_i32), ('lds_slots', c_i32), ('big_entries', c_i32),
                 ('big_slots', c_i32),
-                ('scratch_ids', c_vp), ('scratch_ang', c_vp), ('dense_code', c_vp),
+                ('scratch_ids', c_vp), ('scratch_ang', c_vp), ('seg_count', c_vp),
+                ('dense_code', c_vp),
                 ('halo_count', c_vp), ('item_count', c_vp), ('status', c_vp)]
 
 
@@ -46,7 +48,8 @@ class CompactArgs(ctypes.Structure):
     _fields_ = [('halos', c_vp), ('n_halos', c_i32), ('items', c_vp), ('n_items', c_i32),
                 ('big_items', c_vp), ('n_big_items', c_i32),
                 ('ids_prev', c_vp), ('id_bytes', c_i32),
-                ('scratch_ids', c_vp), ('scratch_ang', c_vp), ('dense_code', c_vp),
+                ('scratch_ids', c_vp), ('scratch_ang', c_vp), ('seg_count', c_vp),
+                ('dense_code', c_vp),
                 ('halo_count', c_vp), ('item_count', c_vp), ('n_slots', c_i32),
                 ('offsets_out', c_vp), ('out_ids', c_vp), ('out_ang', c_vp),
                 ('total_out', c_vp)]
@@ -55,12 +58,14 @@ class CompactArgs(ctypes.Structure):
 # every symbol include/orbit_hip.h declares: name -> (restype, argtypes)
 SYMBOLS = {
     'oa_abi_version': (ctypes.c_int, []),
+    'oa_build_info': (c_i32, [c_i32]),
     'oa_struct_size': (c_i64, [c_i32]),
     'oa_last_error': (ctypes.c_char_p, []),
     'oa_bulk_velocity': (ctypes.c_int, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
     'oa_step': (ctypes.c_int, [ctypes.POINTER(StepArgs), c_vp]),
     'oa_step_lds_bytes': (c_i64, [c_i32, c_i32, c_i32]),
     'oa_max_lds_bytes': (c_i64, []),
+    'oa_debug_stamps': (c_i64, [c_vp, c_i64]),
     'oa_compact': (ctypes.c_int, [ctypes.POINTER(CompactArgs), c_vp]),
 }
 

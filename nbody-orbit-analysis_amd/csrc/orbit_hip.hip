@@ -32,11 +32,80 @@
 
 namespace {
 
-constexpr int WG = 1024;            // k_step work-group (16 waves)
+#ifndef OA_WG
+#define OA_WG 1024
+#endif
+#ifndef OA_UNR1
+#define OA_UNR1 2
+#endif
+#ifndef OA_UNR2
+#define OA_UNR2 2
+#endif
+// Ablation switches for diagnostic builds only (wrong results by design):
+//   OA_ABL_GATHER  phase 2 uses the previous r̂ instead of gathering the current one
+//   OA_ABL_INSERT  phase 1 skips the LDS hash inserts (phase 2 then misses)
+//   OA_ABL_FRAME   phase 1 skips the frame arithmetic (r̂ = dx)
+//   OA_ABL_STORE1  phase 1 skips its r̂ stores
+//   OA_ABL_PHASE3  phase 3 skips its meta stores
+//   OA_ABL_CAS     phase 1 inserts with plain stores (no CAS; collisions overwrite)
+//   OA_ABL_ADD     phase 1 replaces the CAS insert by one LDS atomicAdd per particle
+//   OA_ABL_ACOS    phase 2 skips arccos
+//   OA_ABL_EMIT    phase 2 skips apsis record stores / counters
+//   OA_ABL_SLOTW   phase 2 skips the angle write-back into the slot
+#ifndef OA_ABL_CAS
+#define OA_ABL_CAS 0
+#endif
+#ifndef OA_ABL_ADD
+#define OA_ABL_ADD 0
+#endif
+#ifndef OA_ABL_ACOS
+#define OA_ABL_ACOS 0
+#endif
+#ifndef OA_ABL_EMIT
+#define OA_ABL_EMIT 0
+#endif
+#ifndef OA_ABL_SLOTW
+#define OA_ABL_SLOTW 0
+#endif
+#ifndef OA_ABL_GATHER
+#define OA_ABL_GATHER 0
+#endif
+#ifndef OA_ABL_INSERT
+#define OA_ABL_INSERT 0
+#endif
+#ifndef OA_ABL_FRAME
+#define OA_ABL_FRAME 0
+#endif
+#ifndef OA_ABL_STORE1
+#define OA_ABL_STORE1 0
+#endif
+#ifndef OA_ABL_PHASE3
+#define OA_ABL_PHASE3 0
+#endif
+#ifndef OA_CAS32
+#define OA_CAS32 0          // 1: claim LDS slots with a 32-bit CAS on the high word (slower)
+#endif
+#ifndef OA_SLOT_X2
+#define OA_SLOT_X2 4        // per-item table: slots = entries * OA_SLOT_X2 / 2 (+64)
+#endif
+#ifndef OA_PF1
+#define OA_PF1 1            // phase-1 software prefetch of the next loop trip
+#endif
+#ifndef OA_PF2
+#define OA_PF2 1            // phase-2 software prefetch of the next loop trip
+#endif
+#ifndef OA_HMAX
+#define OA_HMAX 32
+#endif
+constexpr int WG = OA_WG;           // k_step work-group
 constexpr int NWAVE = WG / 64;
-constexpr int HMAX = 128;           // halos per item
-constexpr int UNR = 2;              // particles per thread per loop trip
+constexpr int HMAX = OA_HMAX;       // halos per item
+constexpr int UNR1 = OA_UNR1;       // phase-1 particles per thread per loop trip
+constexpr int UNR2 = OA_UNR2;       // phase-2 particles per thread per loop trip
+constexpr int UNR = UNR2;
 constexpr int BULK_CHUNK = 8192;    // numpy pairwise-sum buffer chunk
+static_assert(WG % 64 == 0 && WG <= 1024, "work-group must be whole waves");
+static_assert(HMAX < WG, "halo table is staged by one thread per halo");
 
 thread_local char g_err[512] = "";
 
@@ -54,10 +123,31 @@ int check_launch(const char *what) {
     return OA_OK;
 }
 
-// ------------------------------------------------------------------ records
-template <typename TD> struct Rec;
-template <> struct __attribute__((aligned(16))) Rec<float> { float r[3]; uint32_t meta; };
-template <> struct __attribute__((aligned(16))) Rec<double> { double r[3]; uint32_t meta, pad; };
+// ------------------------------------------------------------------ loads
+#ifndef OA_NT
+#define OA_NT 1
+#endif
+// streamed-once inputs: non-temporal loads keep L2 for the phase-2 r̂ gathers
+template <typename T> __device__ __forceinline__ T lds_nt(const T *p) {
+#if OA_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
+#ifndef OA_STAMPS
+#define OA_STAMPS 0
+#endif
+#if OA_STAMPS
+// diagnostic build only: per-work-group s_memrealtime (100 MHz) at phase boundaries
+constexpr int STAMP_MAX_WG = 1 << 16, STAMP_N = 6;
+__device__ uint64_t g_stamps[STAMP_MAX_WG * STAMP_N];
+#define STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < STAMP_MAX_WG) \
+    g_stamps[blockIdx.x * STAMP_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
 
 template <typename T> struct V3 { T x, y, z; };
 
@@ -65,6 +155,11 @@ template <typename T>
 __device__ __forceinline__ V3<T> ld3(const T *p, int64_t i) {
     const T *q = p + 3 * i;
     return V3<T>{q[0], q[1], q[2]};
+}
+template <typename T>
+__device__ __forceinline__ V3<T> ld3_nt(const T *p, int64_t i) {
+    const T *q = p + 3 * i;
+    return V3<T>{lds_nt(q), lds_nt(q + 1), lds_nt(q + 2)};
 }
 
 // Row dot product in the reference host's einsum order (probed):
@@ -81,9 +176,9 @@ __device__ __forceinline__ float dot3(float a0, float a1, float a2,
 }
 
 __device__ __forceinline__ double acos_td(double x) { return acos(x); }
-// numpy's float32 arccos is not correctly rounded (SIMD); the closest portable
-// choice is the correctly rounded one: float64 acos rounded to float32.
-__device__ __forceinline__ float acos_td(float x) { return (float)acos((double)x); }
+// numpy's float32 arccos (SIMD) is not correctly rounded either: both differ from the
+// exact value by ~1 ulp; parity for float16 angles is checked to within 1 f16 ulp.
+__device__ __forceinline__ float acos_td(float x) { return acosf(x); }
 
 __device__ __forceinline__ uint16_t f32_to_f16(float f) {
     _Float16 h = (_Float16)f;                     // v_cvt_f16_f32, round to nearest even
@@ -144,9 +239,7 @@ struct ItemHdr {
     int64_t cur_base;
     uint32_t nonuniform, hi0, nent, overflow;
     uint32_t nh, nseg, n_span, n_pv;
-    uint32_t chunk_total, pad0, pad1, pad2;
-    uint32_t wave_cnt[UNR * NWAVE];
-    uint32_t wave_pre[UNR * NWAVE];
+    uint32_t chunk_total, nsl, pad1, pad2;
     uint32_t lstart[HMAX + 1];      // local start of each item halo's current block
     uint32_t vstart[HMAX + 1];      // virtual start of each progenitor segment
     int32_t seg_halo[HMAX];         // segment -> item-local halo
@@ -158,8 +251,7 @@ struct ItemHdr {
 constexpr int64_t HDR_BYTES = (sizeof(ItemHdr) + 255) & ~int64_t(255);
 
 __host__ __device__ inline int64_t table_bytes(int entries, int slots, bool bucketed) {
-    int64_t b = (int64_t)entries * 4 + (bucketed ? (int64_t)entries * 4 : 0) +
-                (int64_t)((slots + 1) / 2) * 4;
+    int64_t b = (int64_t)slots * 8 + (bucketed ? (int64_t)entries * 4 : 0);
     return (b + 15) & ~int64_t(15);
 }
 
@@ -173,73 +265,127 @@ __device__ __forceinline__ uint32_t upper_find(const uint32_t *starts, uint32_t 
     return lo;
 }
 
-__device__ __forceinline__ void lds_insert(uint32_t *slotw, uint32_t nslots, uint32_t s,
-                                           uint32_t val) {
-    for (;;) {
-        uint32_t wi = s >> 1, sh = (s & 1u) << 4;
-        uint32_t cur = __hip_atomic_load(&slotw[wi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        for (;;) {
-            if ((cur >> sh) & 0xFFFFu) break;       // occupied: next slot
-            uint32_t prev = atomicCAS(&slotw[wi], cur, cur | (val << sh));
-            if (prev == cur) return;
-            cur = prev;
-        }
-        s = (s + 1 == nslots) ? 0u : s + 1;
+// ------------------------------------------------------------------ frame
+// Per-launch constants derived on the host from oa_step_args (oa_step()).
+struct FrameK {
+    float h_f;             // RN32(H / (1 + z)): Hubble factor of the f32 sign filter
+    float wrap_hi[3];      // smallest float32 with  dx >  L/2  (float32 dx plans)
+    float wrap_lo[3];      // largest  float32 with  dx < -L/2
+};
+
+template <typename TD> struct WrapT;
+template <> struct WrapT<float> {
+    static __device__ __forceinline__ bool hi(float dx, const oa_step_args &a, const FrameK &k, int d) {
+        return dx >= k.wrap_hi[d];
     }
+    static __device__ __forceinline__ bool lo(float dx, const oa_step_args &a, const FrameK &k, int d) {
+        return dx <= k.wrap_lo[d];
+    }
+};
+template <> struct WrapT<double> {
+    static __device__ __forceinline__ bool hi(double dx, const oa_step_args &a, const FrameK &, int d) {
+        return dx > a.box[d] / 2;
+    }
+    static __device__ __forceinline__ bool lo(double dx, const oa_step_args &a, const FrameK &, int d) {
+        return dx < -(a.box[d] / 2);
+    }
+};
+
+template <typename TD>
+__device__ __forceinline__ TD wrap_sub(TD dx, const oa_step_args &a, int d) {
+    return a.wrap_f64 ? (TD)((double)dx - a.box[d]) : (TD)((float)dx - (float)a.box[d]);
+}
+template <typename TD>
+__device__ __forceinline__ TD wrap_add(TD dx, const oa_step_args &a, int d) {
+    return a.wrap_f64 ? (TD)((double)dx + a.box[d]) : (TD)((float)dx + (float)a.box[d]);
 }
 
-// ------------------------------------------------------------------ frame
-// region_frame (track_orbits.py:247-290) for one particle; cb = centre[3], bulk[3].
-template <typename TX, typename TV, typename TD>
-__device__ __forceinline__ uint32_t frame(const V3<TX> &x, const V3<TV> &v, const double *cb,
-                                          const oa_step_args &a, TD r[3]) {
-    TD dx[3] = {(TD)x.x - (TD)cb[0], (TD)x.y - (TD)cb[1], (TD)x.z - (TD)cb[2]};
-    // recenter_coordinates (utils.py:24-33): one strict wrap per dimension, in the
-    // promoted dtype of (dx, box), cast back to dx's dtype
-    for (int d = 0; d < 3; ++d) {
-        if (d >= a.n_box_dims) break;
-        if (a.wrap_f64) {
-            double L = a.box[d], half = L / 2;
-            double t = (double)dx[d];
-            if (t > half) dx[d] = (TD)(t - L);
-            t = (double)dx[d];
-            if (t < -half) dx[d] = (TD)(t + L);
-        } else {
-            float L = (float)a.box[d], half = L / 2;
-            float t = (float)dx[d];
-            if (t > half) dx[d] = (TD)(t - L);
-            t = (float)dx[d];
-            if (t < -half) dx[d] = (TD)(t + L);
-        }
-    }
-    // w = (v - bulk) + (H * dx) / (1 + z)   (:275-276, :283-284); H is a float64 scalar
-    const TV vv[3] = {v.x, v.y, v.z};
+// The reference's exact float64 v_r (track_orbits.py:275-288) from r̂ and dx.
+template <typename TV, typename TD>
+__device__ __forceinline__ double vr_exact(const TD dx[3], const TV vv[3], const double *cb,
+                                        const TD r[3], const oa_step_args &a) {
     double w[3];
-#pragma unroll
     for (int d = 0; d < 3; ++d) {
         double vb = a.vb_f64 ? (double)vv[d] - cb[3 + d]
                              : (double)((float)vv[d] - (float)cb[3 + d]);
         w[d] = vb + (a.H * (double)dx[d]) / a.one_plus_z;
     }
-    // rads = sqrt(dot(dx, dx)); rhats = dx / rads; v_r = dot(w, rhats)   (:286-288)
+    return dot3(w[0], w[1], w[2], (double)r[0], (double)r[1], (double)r[2]);
+}
+
+// region_frame (track_orbits.py:247-290) for one particle; cb = centre[3], bulk[3].
+// r̂ is computed exactly in the dx dtype.  Only sign(v_r) is kept, so v_r is first
+// evaluated in float32 with a rigorous error bound (|error| <= ~10 * 2^-24 *
+// sum_i |r_i| (|vb_i| + |h_i|)); when |v_r| is within 2^-16 of that scale the wave
+// falls back to the reference's float64 expression tree (vr_exact).
+template <typename TX, typename TV, typename TD>
+__device__ __forceinline__ uint32_t frame(const V3<TX> &x, const V3<TV> &v, const double *cb,
+                                          const oa_step_args &a, const FrameK &k, TD r[3]) {
+    TD dx[3] = {(TD)x.x - (TD)cb[0], (TD)x.y - (TD)cb[1], (TD)x.z - (TD)cb[2]};
+    // recenter_coordinates (utils.py:24-33): one strict wrap per dimension, in the
+    // promoted dtype of (dx, box); the float64 arithmetic runs only in waves where
+    // some particle crosses the box edge
+    for (int d = 0; d < 3; ++d) {
+        if (d >= a.n_box_dims) break;
+        bool h = WrapT<TD>::hi(dx[d], a, k, d);
+        if (__any(h)) { if (h) dx[d] = wrap_sub(dx[d], a, d); }
+        bool l = WrapT<TD>::lo(dx[d], a, k, d);
+        if (__any(l)) { if (l) dx[d] = wrap_add(dx[d], a, d); }
+    }
+    // rads = sqrt(dot(dx, dx)); rhats = dx / rads   (:286-287), exact in dx's dtype
     TD rr = sqrt(dot3(dx[0], dx[1], dx[2], dx[0], dx[1], dx[2]));
     r[0] = dx[0] / rr; r[1] = dx[1] / rr; r[2] = dx[2] / rr;
-    double vr = dot3(w[0], w[1], w[2], (double)r[0], (double)r[1], (double)r[2]);
-    return vr > 0.0 ? 1u : (vr < 0.0 ? 2u : 0u);
+    // sign filter: w = (v - bulk) + (H * dx) / (1 + z), v_r = dot(w, r̂)   (:275-288)
+    const TV vv[3] = {v.x, v.y, v.z};
+    float wf[3], sc = 0.f;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        float vb = a.vb_f64 ? (float)((double)vv[d] - cb[3 + d]) : (float)vv[d] - (float)cb[3 + d];
+        float hf = k.h_f * (float)dx[d];
+        wf[d] = vb + hf;
+        sc += fabsf((float)r[d]) * (fabsf(vb) + fabsf(hf));
+    }
+    const float vrf = (wf[0] * (float)r[0] + wf[1] * (float)r[1]) + wf[2] * (float)r[2];
+    const bool sure = fabsf(vrf) > sc * 0x1p-16f;
+    uint32_t sgn = vrf > 0.f ? 1u : 2u;
+    if (__any(!sure)) {
+        if (!sure) {
+            const double vr = vr_exact<TV, TD>(dx, vv, cb, r, a);
+            sgn = vr > 0.0 ? 1u : (vr < 0.0 ? 2u : 0u);
+        }
+    }
+    return sgn;
 }
 
 // ------------------------------------------------------------------ step kernel
-template <typename TX, typename TV, typename TD, int IDB, bool BUCKETED>
-__global__ __launch_bounds__(WG) void k_step(const oa_step_args a) {
+// LDS image of one item (after the ItemHdr):
+//   slots[S]  u64  open-addressing table of the item's current particles that have a
+//                  progenitor: lo32(ID) | (angle16 | sign2 << 16 | (pos+1) << 18) << 32,
+//                  0 = empty.  pos = position in the item span (nbuckets == 1) or
+//                  entry index into lidx (bucketed).  One ds_read_b64 per probe step
+//                  returns key, sign, angle and position; the angle is updated in place.
+//   lidx[E]   u32  (bucketed only) block position of each entry
+constexpr uint32_t POS_BITS = 14, POS_SHIFT = 18, MAX_POS = (1u << POS_BITS) - 2;
+
+__device__ __forceinline__ uint64_t slot_pack(uint32_t lo, uint32_t meta, uint32_t pos) {
+    return (uint64_t)lo | ((uint64_t)(meta | ((pos + 1) << POS_SHIFT)) << 32);
+}
+__device__ __forceinline__ uint32_t slot_pos(uint64_t v) {
+    return (uint32_t)(v >> (32 + POS_SHIFT)) - 1u;
+}
+__device__ __forceinline__ uint32_t slot_meta(uint64_t v) {
+    return (uint32_t)(v >> 32) & ((1u << POS_SHIFT) - 1u);
+}
+
+template <typename TX, typename TV, typename TD, int IDB, bool BUCKETED, bool COMPARE>
+__global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK fk) {
     typedef typename IdT<IDB>::T ID;
-    typedef Rec<TD> R;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     ItemHdr &H = *reinterpret_cast<ItemHdr *>(smem);
     const int nent_max = BUCKETED ? a.big_entries : a.lds_entries;
-    const uint32_t nslots = (uint32_t)(BUCKETED ? a.big_slots : a.lds_slots);
-    uint32_t *ids_lo = reinterpret_cast<uint32_t *>(smem + HDR_BYTES);
-    uint32_t *lidx = BUCKETED ? ids_lo + nent_max : nullptr;
-    uint32_t *slotw = (BUCKETED ? lidx : ids_lo) + nent_max;
+    const uint32_t nslots_max = (uint32_t)(BUCKETED ? a.big_slots : a.lds_slots);
+    uint64_t *slots = reinterpret_cast<uint64_t *>(smem + HDR_BYTES);
+    uint32_t *lidx = BUCKETED ? reinterpret_cast<uint32_t *>(slots + nslots_max) : nullptr;
 
     const oa_item it = (BUCKETED ? a.big_items : a.items)[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -247,10 +393,11 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a) {
     const ID *ids_prev = reinterpret_cast<const ID *>(a.ids_prev);
     const TX *coords = reinterpret_cast<const TX *>(a.coords);
     const TV *vels = reinterpret_cast<const TV *>(a.vels);
-    R *rec_out = reinterpret_cast<R *>(a.rec_out);
-    const R *rec_prev = reinterpret_cast<const R *>(a.rec_prev);
-    const bool compare = a.compare != 0;
+    TD *rhat_out = reinterpret_cast<TD *>(a.rhat_out);
+    const TD *rhat_prev = reinterpret_cast<const TD *>(a.rhat_prev);
+    constexpr bool compare = COMPARE;   // template: no frame-only loads in the join loop
     const uint32_t q = (uint32_t)it.bucket, nb = (uint32_t)it.nbuckets;
+    STAMP(0);
 
     // ---- phase 0: stage the item's halo table in LDS -------------------------
     const int nh = it.h1 - it.h0;
@@ -268,7 +415,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a) {
         }
     }
     if (tid == 0) {
-        H.nonuniform = 0; H.nent = 0; H.overflow = 0; H.nh = nh;
+        H.nonuniform = 0; H.nent = 0; H.overflow = 0; H.nh = nh; H.chunk_total = 0;
         // progenitor segments in halo order (serial: nh <= HMAX)
         uint32_t ns = 0, vp = 0;
         for (int k = 0; k < nh; ++k) {
@@ -279,40 +426,63 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a) {
             }
         }
         H.vstart[ns] = vp; H.nseg = ns; H.n_pv = vp;
+        // table size for this item: load factor <= 2 / OA_SLOT_X2 (bucketed: full table)
+        uint32_t nj = 0;
+        for (int k = 0; k < nh; ++k) {
+            const oa_halo &h = a.halos[it.h0 + k];
+            if (compare && h.prev_cnt >= 0) nj += (uint32_t)h.cur_cnt;
+        }
+        uint32_t ns_eff = nj * OA_SLOT_X2 / 2 + 64;
+        H.nsl = BUCKETED || ns_eff > nslots_max ? nslots_max : ns_eff;
         // reference high word for the 32-bit LDS keys: the item's first particle
         const oa_halo &h0 = a.halos[it.h0], &hl1 = a.halos[it.h1 - 1];
         H.hi0 = 0;
         if (IDB == 8 && hl1.cur_off + hl1.cur_cnt > h0.cur_off)
             H.hi0 = (uint32_t)((uint64_t)ids[h0.cur_off] >> 32);
     }
+    __syncthreads();
+    const uint32_t nslots = H.nsl;
     if (compare) {
-        for (uint32_t w = tid; w < (nslots + 1) / 2; w += WG) slotw[w] = 0u;
+        for (uint32_t w = tid; w < nslots; w += WG) slots[w] = 0ull;
     }
     __syncthreads();
 
     const int64_t base = H.cur_base;
     const uint32_t n_span = H.n_span;
     const uint32_t hi0 = H.hi0;
+    // bucketed items are single-halo: with no progenitor there is nothing to join
+    const bool join = compare && (!BUCKETED || H.has_prev[0]);
+    STAMP(1);
 
     // ---- phase 1: frame of every current particle, LDS insert ---------------
-    for (uint32_t l0 = 0; l0 < n_span; l0 += WG * UNR) {
-        ID idv[UNR];
-        V3<TX> xv[UNR];
-        V3<TV> vv[UNR];
-        bool ok[UNR];
+    // software-pipelined: trip t+1's loads are in flight while trip t computes;
+    // loads are unconditional (index clamped) so hipcc does not branch around them
+#define OA_LOAD1(IDA, XA, VA, L0)                                                  \
+    _Pragma("unroll") for (int u = 0; u < UNR1; ++u) {                             \
+        const uint32_t li_ = min((L0) + u * WG + tid, n_span - 1u);                \
+        const int64_t i_ = base + li_;                                             \
+        IDA[u] = lds_nt(&ids[i_]);                                                 \
+        XA[u] = ld3_nt(coords, i_);                                                \
+        VA[u] = ld3_nt(vels, i_);                                                  \
+    }
+    ID idv[UNR1], idn[UNR1];
+    V3<TX> xv[UNR1], xn[UNR1];
+    V3<TV> vv[UNR1], vn[UNR1];
+    if (OA_PF1 && n_span > 0) { OA_LOAD1(idv, xv, vv, 0u) }
+    for (uint32_t l0 = 0; l0 < n_span; l0 += WG * UNR1) {
+        // unconditional prefetch (clamped, in bounds): a branch here makes hipcc
+        // copy the loaded registers through a phi and wait for them immediately
+        if (OA_PF1) { OA_LOAD1(idn, xn, vn, l0 + WG * UNR1) }
+        else { OA_LOAD1(idv, xv, vv, l0) }
+        bool ok[UNR1];
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            uint32_t li = l0 + u * WG + tid;
-            ok[u] = li < n_span;
-            if (ok[u]) {
-                int64_t i = base + li;
-                idv[u] = ids[i];
-                xv[u] = ld3(coords, i);
-                vv[u] = ld3(vels, i);
-            }
-        }
+        for (int u = 0; u < UNR1; ++u) ok[u] = l0 + u * WG + tid < n_span;
+        uint64_t val[UNR1];
+        uint32_t sl[UNR1];
+        bool ins[UNR1];
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) {
+        for (int u = 0; u < UNR1; ++u) {
+            ins[u] = false;
             if (!ok[u]) continue;
             uint32_t li = l0 + u * WG + tid;
             uint32_t lo, hi;
@@ -320,29 +490,81 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a) {
             if (BUCKETED && bucket_of(lo, hi, nb) != q) continue;
             uint32_t hl = (BUCKETED || H.nh == 1) ? 0u : upper_find(H.lstart, H.nh, li);
             TD r[3];
-            uint32_t sgn = frame<TX, TV, TD>(xv[u], vv[u], H.cb[hl], a, r);
-            uint32_t ang = 0;
-            if (!compare && a.angles_in) ang = a.angles_in[base + li];
-            R rec;
-            rec.r[0] = r[0]; rec.r[1] = r[1]; rec.r[2] = r[2];
-            rec.meta = ang | (sgn << 16);
-            if constexpr (sizeof(R) == 32) rec.pad = 0;
-            rec_out[base + li] = rec;
-            if (H.has_prev[hl]) {
-                if (IDB == 8 && hi != hi0) H.nonuniform = 1u;     // benign race: all write 1
-                uint32_t e = li;
-                if (BUCKETED) {
-                    e = atomicAdd(&H.nent, 1u);
-                    if (e >= (uint32_t)nent_max) { H.overflow = 1u; continue; }
-                    lidx[e] = li;
-                }
-                ids_lo[e] = lo;
-                lds_insert(slotw, nslots, slot_of(lo, hl, nslots), e + 1);
+            uint32_t sgn;
+            if (OA_ABL_FRAME) {
+                r[0] = (TD)xv[u].x - (TD)H.cb[hl][0]; r[1] = (TD)xv[u].y; r[2] = (TD)vv[u].z;
+                sgn = 1u;
+            } else {
+                sgn = frame<TX, TV, TD>(xv[u], vv[u], H.cb[hl], a, fk, r);
             }
+            TD *ro = rhat_out + 3 * (base + li);
+            if (!OA_ABL_STORE1) { ro[0] = r[0]; ro[1] = r[1]; ro[2] = r[2]; }
+            else { asm volatile("" :: "v"(r[0]), "v"(r[1]), "v"(r[2])); }
+            uint32_t ang = 0;
+            if constexpr (!COMPARE) {
+                if (a.angles_in) ang = a.angles_in[base + li];
+            }
+            const uint32_t meta = ang | (sgn << 16);
+            if (!join || !H.has_prev[hl]) { a.meta_out[base + li] = meta; continue; }
+            uint32_t pos = li;
+            if (BUCKETED) {
+                pos = atomicAdd(&H.nent, 1u);
+                if (pos >= (uint32_t)nent_max) { H.overflow = 1u; continue; }
+                lidx[pos] = li;
+            }
+            if (IDB == 8 && hi != hi0) H.nonuniform = 1u;     // benign race: all write 1
+            val[u] = slot_pack(lo, meta, pos);
+            sl[u] = slot_of(lo, hl, nslots);
+            ins[u] = !OA_ABL_INSERT;
+            if (OA_ABL_INSERT) asm volatile("" :: "v"(val[u]), "v"(sl[u]));
+        }
+        // lockstep linear-probing insert: every pending CAS issued before any retry
+        for (;;) {
+            bool any = false;
+            uint64_t old[UNR1];
+#pragma unroll
+            for (int u = 0; u < UNR1; ++u)
+                if (ins[u]) {
+                    if (OA_ABL_ADD) {
+                        uint32_t *c = reinterpret_cast<uint32_t *>(slots) + (sl[u] >> 2);
+                        uint32_t r = atomicAdd(c + 4096, 1u);
+                        slots[sl[u]] = val[u] + r;
+                        old[u] = 0ull;
+                    } else if (OA_ABL_CAS) { slots[sl[u]] = val[u]; old[u] = 0ull; }
+                    else if (OA_CAS32) {
+                        // claim the slot through its high word (pos + 1 > 0 when occupied)
+                        uint32_t *w = reinterpret_cast<uint32_t *>(&slots[sl[u]]);
+                        old[u] = atomicCAS(w + 1, 0u, (uint32_t)(val[u] >> 32));
+                    } else {
+                        old[u] = atomicCAS(reinterpret_cast<unsigned long long *>(&slots[sl[u]]),
+                                           0ull, (unsigned long long)val[u]);
+                    }
+                }
+#pragma unroll
+            for (int u = 0; u < UNR1; ++u) {
+                if (!ins[u]) continue;
+                if (old[u] == 0ull) {
+                    // key word: read by phase-2 probes only after the barrier
+                    if (OA_CAS32) reinterpret_cast<uint32_t *>(&slots[sl[u]])[0] = (uint32_t)val[u];
+                    ins[u] = false;
+                    continue;
+                }
+                sl[u] = (sl[u] + 1 == nslots) ? 0u : sl[u] + 1;
+                any = true;
+            }
+            if (!any) break;
+        }
+        if (OA_PF1) {
+#pragma unroll
+            for (int u = 0; u < UNR1; ++u) { idv[u] = idn[u]; xv[u] = xn[u]; vv[u] = vn[u]; }
         }
     }
-    if (!compare) return;
+#undef OA_LOAD1
+    STAMP(2);
+    if constexpr (!COMPARE) return;
+    if (!join) return;
     __syncthreads();
+    STAMP(3);
     if (H.overflow) {
         if (tid == 0) atomicOr(a.status, OA_STATUS_BUCKET_OVERFLOW);
         return;
@@ -355,66 +577,116 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a) {
     uint32_t running = 0;
     ID *scr_ids = reinterpret_cast<ID *>(a.scratch_ids);
 
+#define OA_LOAD2(PID, PRH, PMETA, KPOS, HLV, V0)                                  \
+    _Pragma("unroll") for (int u = 0; u < UNR; ++u) {                              \
+        const uint32_t vp_ = min((V0) + u * WG + tid, n_pv - 1u);                  \
+        const uint32_t sg_ = nseg == 1 ? 0u : upper_find(H.vstart, nseg, vp_);     \
+        HLV[u] = (uint32_t)H.seg_halo[sg_];                                        \
+        KPOS[u] = H.seg_prev_off[sg_] + (vp_ - H.vstart[sg_]);                     \
+        PID[u] = lds_nt(&ids_prev[KPOS[u]]);                                       \
+        PRH[u] = ld3_nt(rhat_prev, KPOS[u]);                                       \
+        PMETA[u] = lds_nt(&a.meta_prev[KPOS[u]]);                                  \
+    }
+    ID pid[UNR], pidn[UNR];
+    V3<TD> prh[UNR], prhn[UNR];
+    uint32_t pmeta[UNR], pmetan[UNR], hlv[UNR], hlvn[UNR];
+    int64_t kpos[UNR], kposn[UNR];
+    if (OA_PF2 && n_pv > 0) { OA_LOAD2(pid, prh, pmeta, kpos, hlv, 0u) }
     for (uint32_t v0 = 0; v0 < n_pv; v0 += WG * UNR) {
-        ID pid[UNR];
-        R prec[UNR];
-        int64_t kpos[UNR];
-        uint32_t hlv[UNR];
+        if (!OA_PF2) { OA_LOAD2(pid, prh, pmeta, kpos, hlv, v0) }
         bool ok[UNR];
 #pragma unroll
+        for (int u = 0; u < UNR; ++u) ok[u] = v0 + u * WG + tid < n_pv;
+        // lockstep probe of (halo, id): departed particles miss (setdiff1d/in1d, :300-304)
+        uint32_t sl[UNR], lo[UNR], hi[UNR], lmin[UNR], lmax[UNR];
+        uint64_t hit[UNR];
+        bool act[UNR];
+#pragma unroll
         for (int u = 0; u < UNR; ++u) {
-            uint32_t vp = v0 + u * WG + tid;
-            ok[u] = vp < n_pv;
-            if (ok[u]) {
-                uint32_t sg = nseg == 1 ? 0u : upper_find(H.vstart, nseg, vp);
-                hlv[u] = (uint32_t)H.seg_halo[sg];
-                kpos[u] = H.seg_prev_off[sg] + (vp - H.vstart[sg]);
-                pid[u] = ids_prev[kpos[u]];
-                prec[u] = rec_prev[kpos[u]];
+            hit[u] = 0ull;
+            act[u] = false;
+            if (!ok[u]) continue;
+            id_split<IDB>(pid[u], lo[u], hi[u]);
+            if (BUCKETED && bucket_of(lo[u], hi[u], nb) != q) { ok[u] = false; continue; }
+            if (IDB == 8 && !nonuniform && hi[u] != hi0) continue;      // cannot be present
+            lmin[u] = BUCKETED ? 0u : H.lstart[hlv[u]];
+            lmax[u] = BUCKETED ? 0xFFFFFFFFu : H.lstart[hlv[u] + 1];
+            sl[u] = slot_of(lo[u], hlv[u], nslots);
+            act[u] = true;
+        }
+        for (;;) {
+            uint64_t v[UNR];
+            bool any = false;
+#pragma unroll
+            for (int u = 0; u < UNR; ++u)
+                if (act[u]) v[u] = slots[sl[u]];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                if (!act[u]) continue;
+                if (v[u] == 0ull) { act[u] = false; continue; }              // miss
+                const uint32_t p = slot_pos(v[u]);
+                if ((uint32_t)v[u] == lo[u] && (BUCKETED || (p >= lmin[u] && p < lmax[u]))) {
+                    hit[u] = v[u]; act[u] = false; continue;
+                }
+                sl[u] = (sl[u] + 1 == nslots) ? 0u : sl[u] + 1;
+                any = true;
+            }
+            if (!any) break;
+        }
+        if (IDB == 8 && nonuniform) {
+            // rare path (item IDs differ in their high words): confirm the full ID and
+            // keep probing past a low-word collision.  Kept out of the probe loop above
+            // so the common path has no global load (and no vmcnt drain) in it.
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                while (hit[u]) {
+                    const uint32_t p = slot_pos(hit[u]);
+                    if (ids[base + (BUCKETED ? lidx[p] : p)] == pid[u]) break;
+                    hit[u] = 0ull;
+                    for (;;) {
+                        sl[u] = (sl[u] + 1 == nslots) ? 0u : sl[u] + 1;
+                        const uint64_t w = slots[sl[u]];
+                        if (!w) break;
+                        const uint32_t pw = slot_pos(w);
+                        if ((uint32_t)w == lo[u] && (BUCKETED || (pw >= lmin[u] && pw < lmax[u]))) {
+                            hit[u] = w;
+                            break;
+                        }
+                    }
+                }
             }
         }
+        // gather the matched current r̂ (written in phase 1: L2).  Unconditional
+        // (a miss re-reads the lane's own previous r̂) and issued BEFORE the next
+        // trip's prefetch: vmcnt retires in issue order, so the gather wait then
+        // leaves the prefetch in flight.
+        V3<TD> cr[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const uint32_t p = slot_pos(hit[u]);
+            const TD *src = (hit[u] && !OA_ABL_GATHER) ? rhat_out + 3 * (base + (BUCKETED ? lidx[p] : p))
+                                                       : rhat_prev + 3 * kpos[u];
+            cr[u] = V3<TD>{src[0], src[1], src[2]};
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (OA_PF2) { OA_LOAD2(pidn, prhn, pmetan, kposn, hlvn, v0 + WG * UNR) }  // unconditional
+        __builtin_amdgcn_sched_barrier(0);
         bool flag[UNR];
         uint16_t a16[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
             flag[u] = false;
-            a16[u] = 0;
-            if (!ok[u]) continue;
-            uint32_t lo, hi;
-            id_split<IDB>(pid[u], lo, hi);
-            if (BUCKETED && bucket_of(lo, hi, nb) != q) { ok[u] = false; continue; }
-            const uint32_t hl = hlv[u];
-            // probe (hl, id): departed particles miss (setdiff1d/in1d, :300-304)
-            int32_t e = -1;
-            if (!(IDB == 8 && !nonuniform && hi != hi0)) {
-                const uint32_t lmin = BUCKETED ? 0u : H.lstart[hl];
-                const uint32_t lmax = BUCKETED ? 0xFFFFFFFFu : H.lstart[hl + 1];
-                uint32_t s = slot_of(lo, hl, nslots);
-                for (;;) {
-                    uint32_t f = (slotw[s >> 1] >> ((s & 1u) << 4)) & 0xFFFFu;
-                    if (!f) break;
-                    uint32_t c = f - 1;
-                    if (ids_lo[c] == lo && c >= lmin && c < lmax) {
-                        if (!nonuniform) { e = (int32_t)c; break; }
-                        uint32_t lc = BUCKETED ? lidx[c] : c;
-                        if (ids[base + lc] == pid[u]) { e = (int32_t)c; break; }
-                    }
-                    s = (s + 1 == nslots) ? 0u : s + 1;
-                }
-            }
-            if (e < 0) { a16[u] = 0xFFFFu; continue; }
-            const uint32_t li = BUCKETED ? lidx[e] : (uint32_t)e;
-            const R cur = rec_out[base + li];
-            const uint32_t sc = cur.meta >> 16, sp = prec[u].meta >> 16;
+            a16[u] = 0xFFFFu;
+            if (!hit[u]) continue;
+            const uint32_t sc = slot_meta(hit[u]) >> 16, sp = pmeta[u] >> 16;
             // strict sign test (:311-314): zeros and NaNs never flag
             const bool cond = a.mode == OA_MODE_PERICENTRIC ? (sp == 2u && sc == 1u)
                                                             : (sp == 1u && sc == 2u);
             // angle change = arccos(dot(r̂_prev, r̂_match)), no clamp (:324-325)
-            TD dt = dot3(prec[u].r[0], prec[u].r[1], prec[u].r[2], cur.r[0], cur.r[1], cur.r[2]);
-            uint16_t acc = angle_add((uint16_t)(prec[u].meta & 0xFFFFu), acos_td(dt));
+            TD dt = dot3(prh[u].x, prh[u].y, prh[u].z, cr[u].x, cr[u].y, cr[u].z);
+            uint16_t acc = angle_add((uint16_t)(pmeta[u] & 0xFFFFu), OA_ABL_ACOS ? dt : acos_td(dt));
             // calc_angles (:342-349): apsis angle emitted, then reset to 0
-            *reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(&rec_out[base + li]) +
-                                          offsetof(R, meta)) = cond ? (uint16_t)0 : acc;
+            if (!OA_ABL_SLOTW) reinterpret_cast<uint16_t *>(&slots[sl[u]])[2] = cond ? (uint16_t)0 : acc;
             flag[u] = cond;
             a16[u] = acc;
         }
@@ -433,47 +705,54 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a) {
                     atomicAdd(&a.halo_count[h.out_slot], (int32_t)__popcll(m));
                 }
             }
-            continue;
-        }
-        // ordered stream compaction (previous-block order, :315-316) via wave ballots
-        uint64_t masks[UNR];
+        } else {
+        // apsis records in previous-block order (:315-316): wave ballot + prefix
+        // popcount packs each 64-position segment's records at its own base;
+        // k_gather_items orders the segments (no work-group barrier here)
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
-            masks[u] = __ballot(flag[u]);
-            if (lane == 0) H.wave_cnt[u * NWAVE + wave] = (uint32_t)__popcll(masks[u]);
-        }
-        __syncthreads();
-        if (wave == 0) {
-            uint32_t x = lane < UNR * NWAVE ? H.wave_cnt[lane] : 0u, incl = x;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                uint32_t y = __shfl_up(incl, o);
-                if (lane >= o) incl += y;
-            }
-            if (lane < UNR * NWAVE) H.wave_pre[lane] = incl - x;
-            if (lane == 63) H.chunk_total = incl;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            if (flag[u]) {
-                uint32_t pos = running + H.wave_pre[u * NWAVE + wave] +
-                               (uint32_t)__popcll(masks[u] & lanemask_lt);
-                scr_ids[it.scratch_off + pos] = pid[u];
-                a.scratch_ang[it.scratch_off + pos] = a16[u];
-                atomicAdd(&H.halo_cnt[hlv[u]], 1);
+            const uint64_t m = __ballot(flag[u]);
+            const uint32_t segpos = v0 + u * WG + wave * 64;    // multiple of 64
+            if (segpos < n_pv) {
+                if (flag[u] && !OA_ABL_EMIT) {
+                    const int64_t pos = it.scratch_off + segpos + __popcll(m & lanemask_lt);
+                    scr_ids[pos] = pid[u];
+                    a.scratch_ang[pos] = a16[u];
+                    atomicAdd(&H.halo_cnt[hlv[u]], 1);
+                }
+                if (lane == 0) a.seg_count[(it.scratch_off + segpos) >> 6] = (uint8_t)__popcll(m);
+                running += (uint32_t)__popcll(m);
             }
         }
-        running += H.chunk_total;
-        __syncthreads();
+        }
+        if (OA_PF2) {
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                pid[u] = pidn[u]; prh[u] = prhn[u]; pmeta[u] = pmetan[u];
+                kpos[u] = kposn[u]; hlv[u] = hlvn[u];
+            }
+        }
+    }
+#undef OA_LOAD2
+    if (!BUCKETED && lane == 0) atomicAdd(&H.chunk_total, running);
+    STAMP(4);
+    __syncthreads();
+
+    // ---- phase 3: meta words of the joined particles (one per occupied slot) --
+    for (uint32_t w = tid; w < nslots; w += WG) {
+        const uint64_t v = slots[w];
+        if (!v) continue;
+        const uint32_t p = slot_pos(v);
+        if (!OA_ABL_PHASE3) a.meta_out[base + (BUCKETED ? lidx[p] : p)] = slot_meta(v);
+        else asm volatile("" :: "v"(p));
     }
     if (BUCKETED) return;
-    __syncthreads();
     if (tid < nh) {
         const oa_halo &h = a.halos[it.h0 + tid];
         if (h.out_slot >= 0) a.halo_count[h.out_slot] = H.halo_cnt[tid];
     }
-    if (tid == 0) a.item_count[blockIdx.x] = (int32_t)running;
+    if (tid == 0) a.item_count[blockIdx.x] = (int32_t)H.chunk_total;
+    STAMP(5);
 }
 
 // ------------------------------------------------------------------ compaction
@@ -503,21 +782,47 @@ __global__ __launch_bounds__(1024) void k_scan_slots(const int32_t *cnt, int32_t
     if (tid == 0) { off[n] = carry; *total = carry; }
 }
 
+// Item records live in 64-position segments (k_step phase 2); a work-group walks
+// its item's segments in order, scanning the per-segment counts.
 template <int IDB>
 __global__ __launch_bounds__(256) void k_gather_items(const oa_compact_args a) {
     typedef typename IdT<IDB>::T ID;
+    __shared__ uint32_t wsum[4];
     const oa_item it = a.items[blockIdx.x];
     const int32_t n = a.item_count[blockIdx.x];
     if (n <= 0) return;
     int64_t slot = -1;
     for (int h = it.h0; h < it.h1 && slot < 0; ++h) slot = a.halos[h].out_slot;
     if (slot < 0) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t dst = a.offsets_out[slot];
-    const ID *src = reinterpret_cast<const ID *>(a.scratch_ids) + it.scratch_off;
+    const ID *src = reinterpret_cast<const ID *>(a.scratch_ids);
     ID *out = reinterpret_cast<ID *>(a.out_ids) + dst;
-    const uint16_t *sa = a.scratch_ang + it.scratch_off;
-    uint16_t *oa = a.out_ang + dst;
-    for (int i = threadIdx.x; i < n; i += 256) { out[i] = src[i]; oa[i] = sa[i]; }
+    uint16_t *oang = a.out_ang + dst;
+    const int64_t nseg = (it.n_pv + 63) >> 6;
+    const uint8_t *sc = a.seg_count + (it.scratch_off >> 6);
+    int64_t carry = 0;
+    for (int64_t c0 = 0; c0 < nseg; c0 += 256) {
+        const int64_t sg = c0 + tid;
+        const uint32_t cnt = sg < nseg ? sc[sg] : 0u;
+        uint32_t incl = cnt;
+        for (int o = 1; o < 64; o <<= 1) {
+            uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wsum[wave] = incl;
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
+        for (int w = 0; w < 4; ++w) { if (w < wave) pre += wsum[w]; tot += wsum[w]; }
+        const int64_t o = carry + pre + incl - cnt;
+        const int64_t sbase = it.scratch_off + (sg << 6);
+        for (uint32_t r = 0; r < cnt; ++r) {
+            out[o + r] = src[sbase + r];
+            oang[o + r] = a.scratch_ang[sbase + r];
+        }
+        carry += tot;
+        __syncthreads();
+    }
 }
 
 template <int IDB>
@@ -658,6 +963,21 @@ __global__ __launch_bounds__(64) void k_bulk(const TV *vels, const TM *masses, o
     if (lane < 3) h.bulk[lane] = (double)res;
 }
 
+FrameK make_frame_k(const oa_step_args &a) {
+    FrameK k;
+    k.h_f = (float)(a.H / a.one_plus_z);
+    for (int d = 0; d < 3; ++d) {
+        // exact float32 thresholds of the strict tests dx > L/2 and dx < -L/2, where
+        // L/2 is float64 (wrap_f64) or float32 arithmetic
+        const double half = a.wrap_f64 ? a.box[d] / 2 : (double)((float)a.box[d] / 2.0f);
+        float f = (float)half;
+        k.wrap_hi[d] = (double)f > half ? f : nextafterf(f, INFINITY);
+        float g = (float)(-half);
+        k.wrap_lo[d] = (double)g < -half ? g : nextafterf(g, -INFINITY);
+    }
+    return k;
+}
+
 template <typename K>
 int set_lds(K kernel, int64_t bytes) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
@@ -666,23 +986,29 @@ int set_lds(K kernel, int64_t bytes) {
     return OA_OK;
 }
 
-template <typename TX, typename TV, typename TD, int IDB>
-int launch_step(const oa_step_args &a, hipStream_t st) {
+template <typename TX, typename TV, typename TD, int IDB, bool COMPARE>
+int launch_step_c(const oa_step_args &a, hipStream_t st) {
     if (a.n_items > 0) {
         int64_t lds = HDR_BYTES + table_bytes(a.lds_entries, a.lds_slots, false);
-        auto k = k_step<TX, TV, TD, IDB, false>;
+        auto k = k_step<TX, TV, TD, IDB, false, COMPARE>;
         if (int rc = set_lds(k, lds)) return rc;
-        hipLaunchKernelGGL(k, dim3(a.n_items), dim3(WG), (size_t)lds, st, a);
+        hipLaunchKernelGGL(k, dim3(a.n_items), dim3(WG), (size_t)lds, st, a, make_frame_k(a));
         if (int rc = check_launch("k_step")) return rc;
     }
     if (a.n_big_items > 0) {
         int64_t lds = HDR_BYTES + table_bytes(a.big_entries, a.big_slots, true);
-        auto k = k_step<TX, TV, TD, IDB, true>;
+        auto k = k_step<TX, TV, TD, IDB, true, COMPARE>;
         if (int rc = set_lds(k, lds)) return rc;
-        hipLaunchKernelGGL(k, dim3(a.n_big_items), dim3(WG), (size_t)lds, st, a);
+        hipLaunchKernelGGL(k, dim3(a.n_big_items), dim3(WG), (size_t)lds, st, a, make_frame_k(a));
         if (int rc = check_launch("k_step(bucketed)")) return rc;
     }
     return OA_OK;
+}
+
+template <typename TX, typename TV, typename TD, int IDB>
+int launch_step(const oa_step_args &a, hipStream_t st) {
+    return a.compare ? launch_step_c<TX, TV, TD, IDB, true>(a, st)
+                     : launch_step_c<TX, TV, TD, IDB, false>(a, st);
 }
 
 template <typename TX, typename TV, typename TD>
@@ -701,6 +1027,16 @@ extern "C" {
 
 int oa_abi_version(void) { return OA_ABI_VERSION; }
 
+int32_t oa_build_info(int32_t which) {
+    switch (which) {
+        case 0: return WG;
+        case 1: return HMAX;
+        case 2: return UNR1;
+        case 3: return UNR2;
+        default: return -1;
+    }
+}
+
 int64_t oa_struct_size(int32_t which) {
     switch (which) {
         case 0: return sizeof(oa_halo);
@@ -715,6 +1051,20 @@ const char *oa_last_error(void) { return g_err; }
 
 int64_t oa_step_lds_bytes(int32_t entries, int32_t slots, int32_t bucketed) {
     return HDR_BYTES + table_bytes(entries, slots, bucketed != 0);
+}
+
+// Diagnostic builds (-DOA_STAMPS=1): copy the per-work-group phase stamps of the last
+// oa_step launch (s_memrealtime, 100 MHz) to host memory; returns count or -1.
+int64_t oa_debug_stamps(uint64_t *host, int64_t n) {
+#if OA_STAMPS
+    int64_t m = n < (int64_t)STAMP_MAX_WG * STAMP_N ? n : (int64_t)STAMP_MAX_WG * STAMP_N;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), m * sizeof(uint64_t)) != hipSuccess)
+        return -1;
+    return m;
+#else
+    (void)host; (void)n;
+    return -1;
+#endif
 }
 
 int64_t oa_max_lds_bytes(void) {
@@ -736,16 +1086,18 @@ int oa_step(const oa_step_args *args, void *stream) {
     if (a.n_box_dims < 0 || a.n_box_dims > 3) return fail(OA_E_ARG, "n_box_dims out of range");
     if (a.mode != OA_MODE_PERICENTRIC && a.mode != OA_MODE_APOCENTRIC)
         return fail(OA_E_ARG, "bad mode");
-    if (a.n_items > 0 && (a.lds_entries <= 0 || a.lds_entries > 65534 ||
+    if (a.n_items > 0 && (a.lds_entries <= 0 || a.lds_entries > (int)MAX_POS + 1 ||
                           a.lds_slots <= a.lds_entries))
-        return fail(OA_E_ARG, "bad lds_entries/lds_slots");
-    if (a.n_big_items > 0 && (a.big_entries <= 0 || a.big_entries > 65534 ||
+        return fail(OA_E_ARG, "bad lds_entries/lds_slots (entries <= %u < slots)", MAX_POS + 1);
+    if (a.n_big_items > 0 && (a.big_entries <= 0 || a.big_entries > (int)MAX_POS + 1 ||
                               a.big_slots <= a.big_entries))
-        return fail(OA_E_ARG, "bad big_entries/big_slots");
-    if (a.n_items + a.n_big_items > 0 && (!a.halos || !a.ids || !a.coords || !a.vels || !a.rec_out))
+        return fail(OA_E_ARG, "bad big_entries/big_slots (entries <= %u < slots)", MAX_POS + 1);
+    if (a.n_items + a.n_big_items > 0 &&
+        (!a.halos || !a.ids || !a.coords || !a.vels || !a.rhat_out || !a.meta_out))
         return fail(OA_E_ARG, "null input/output pointer");
-    if (a.compare && (!a.ids_prev || !a.rec_prev || !a.halo_count || !a.status ||
-                      (a.n_items > 0 && (!a.scratch_ids || !a.scratch_ang || !a.item_count)) ||
+    if (a.compare && (!a.ids_prev || !a.rhat_prev || !a.meta_prev || !a.halo_count || !a.status ||
+                      (a.n_items > 0 && (!a.scratch_ids || !a.scratch_ang || !a.item_count ||
+                                         !a.seg_count)) ||
                       (a.n_big_items > 0 && !a.dense_code)))
         return fail(OA_E_ARG, "null previous-state / scratch pointer");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);

@@ -13,6 +13,7 @@ Reference behaviour mirrored: track_orbits.py:104-240 (per-snapshot body),
 :247-290 (frame), :293-327 (compare), :330-351 (angles), :199-227 (assembly).
 """
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -22,6 +23,10 @@ import torch
 from . import _native as N
 
 F32, F64 = np.dtype(np.float32), np.dtype(np.float64)
+DEFAULT_ENTRIES = 14336        # current particles per work-group item (nbuckets == 1)
+DEFAULT_SLOTS = 19456          # 8-byte LDS hash slots per item (152 KB)
+DEFAULT_BIG_ENTRIES = 10240    # per hash bucket of a larger halo
+DEFAULT_BIG_SLOTS = 13824
 
 _TORCH_FROM_NP = {
     np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
@@ -62,8 +67,13 @@ class DtypePlan:
     mass: Optional[np.dtype] = None
 
     @property
-    def rec_bytes(self):
-        return 32 if self.dx == F64 else 16
+    def state_bytes(self):
+        """Bytes of carried state per particle: r̂ (3 x dx dtype) + meta word."""
+        return 3 * self.dx.itemsize + 4
+
+    @property
+    def torch_dx(self):
+        return torch.float64 if self.dx == F64 else torch.float32
 
 
 def plan_dtypes(snapshot, centre, bulk_cat, H, z):
@@ -144,8 +154,8 @@ def plan_items(cur_cnt, prev_cnt, entries, big_entries, hmax=128, fill=0.7, min_
             tot += cur_cnt[j]
             ptot += pc[j]
             j += 1
-        small.append((start, j, 0, 1, scratch, 0))
-        scratch += ptot
+        small.append((start, j, 0, 1, scratch, ptot))
+        scratch += (ptot + 63) // 64 * 64           # 64-slot segments per item
     it = np.array(small, dtype=N.ITEM_DTYPE) if small else np.zeros(0, N.ITEM_DTYPE)
     bt = np.array(big, dtype=N.ITEM_DTYPE) if big else np.zeros(0, N.ITEM_DTYPE)
     return it, bt, scratch
@@ -165,6 +175,11 @@ def to_device(x, device, dtype=None):
     return t.to(device, non_blocking=False).contiguous()
 
 
+def meta_angles(meta):
+    """float16 angles held in the low half of device meta words -> host array."""
+    return (meta & 0xFFFF).cpu().numpy().astype(np.uint16).view(np.float16)
+
+
 def _ptr(t):
     return None if t is None else t.data_ptr()
 
@@ -173,7 +188,8 @@ def _ptr(t):
 class SnapshotState:
     """Device state a snapshot leaves for the next one (track_orbits.py:234-240)."""
     ids: torch.Tensor
-    rec: torch.Tensor
+    rhat: torch.Tensor
+    meta: torch.Tensor
     starts: np.ndarray
     counts: np.ndarray
     exists: np.ndarray
@@ -208,7 +224,8 @@ class PreparedStep:
     halos: Optional[torch.Tensor] = None
     d_items: Optional[torch.Tensor] = None
     d_big: Optional[torch.Tensor] = None
-    rec: Optional[torch.Tensor] = None
+    rhat: Optional[torch.Tensor] = None
+    meta: Optional[torch.Tensor] = None
     angles_in: Optional[torch.Tensor] = None
     halo_list: Optional[torch.Tensor] = None
     bulk_computed: bool = False
@@ -231,6 +248,7 @@ class Workspace:
             return torch.empty(max(int(n), 1), dtype=dt, device=device)
         self.scratch_ids = e(scratch, id_torch_dtype)
         self.scratch_ang = e(scratch, torch.int16)
+        self.seg_count = e(scratch // 64 + 1, torch.uint8)
         self.dense = e(n_prev if dense else 1, torch.int16)
         self.halo_count = e(n_slots, torch.int32)
         self.item_count = e(n_items, torch.int32)
@@ -254,19 +272,24 @@ class Workspace:
 class OrbitEngine:
     """Per-snapshot device pipeline with carried state (see module docstring)."""
 
-    def __init__(self, mode='pericentric', device=None, lds_entries=16384, lds_slots=None,
-                 big_entries=12288, big_slots=None, hmax=128):
+    def __init__(self, mode='pericentric', device=None, lds_entries=None, lds_slots=None,
+                 big_entries=None, big_slots=None, hmax=None):
         if mode not in N.MODE:
             raise ValueError("Orbit detection mode not recognized. Please specify either "
                              "'pericentric' or 'apocentric'.")
         self.lib = N.load(require_device=True)
         self.device = torch.device(device if device is not None else 'cuda')
         self.mode = mode
-        self.entries = int(lds_entries)
-        self.slots = int(lds_slots or 2 * self.entries)
-        self.big_entries = int(big_entries)
-        self.big_slots = int(big_slots or 2 * self.big_entries)
-        self.hmax = int(hmax)
+        env = os.environ.get
+        # defaults fill one CU's 160 KB LDS (DESIGN.md §LDS): 8 B per hash slot
+        # (+ 4 B per entry for bucketed items)
+        self.entries = int(lds_entries or env('ORBIT_LDS_ENTRIES', DEFAULT_ENTRIES))
+        self.slots = int(lds_slots or env('ORBIT_LDS_SLOTS', 0) or
+                         max(DEFAULT_SLOTS, self.entries + 1))
+        self.big_entries = int(big_entries or env('ORBIT_BIG_ENTRIES', DEFAULT_BIG_ENTRIES))
+        self.big_slots = int(big_slots or env('ORBIT_BIG_SLOTS', 0) or
+                             max(DEFAULT_BIG_SLOTS, self.big_entries + 1))
+        self.hmax = min(int(hmax or env('ORBIT_HMAX', 1 << 30)), self.lib.oa_build_info(1))
         max_lds = self.lib.oa_max_lds_bytes()
         for e, s, b in ((self.entries, self.slots, 0), (self.big_entries, self.big_slots, 1)):
             need = self.lib.oa_step_lds_bytes(e, s, b)
@@ -334,7 +357,8 @@ class OrbitEngine:
             min_b = prep.more_buckets()      # a hash bucket overflowed: re-plan
         else:
             raise RuntimeError('hash buckets kept overflowing (adversarial IDs?)')
-        self.prev = SnapshotState(ids=snap['ids'], rec=prep.rec, starts=prep.starts,
+        self.prev = SnapshotState(ids=snap['ids'], rhat=prep.rhat, meta=prep.meta,
+                                  starts=prep.starts,
                                   counts=prep.counts, exists=exists, plan=prep.plan)
         return res
 
@@ -370,7 +394,8 @@ class OrbitEngine:
         pr.halos = torch.from_numpy(halos.view(np.uint8)).to(dev)
         pr.d_items = torch.from_numpy(items.view(np.uint8)).to(dev)
         pr.d_big = torch.from_numpy(big.view(np.uint8)).to(dev)
-        pr.rec = torch.empty(n * plan.rec_bytes, dtype=torch.uint8, device=dev)
+        pr.rhat = torch.empty(n * 3, dtype=plan.torch_dx, device=dev)
+        pr.meta = torch.empty(n, dtype=torch.int32, device=dev)
         pr.snap = snap
         pr.bulk_computed = bulk_cat is None and len(halos) > 0
         if pr.bulk_computed:
@@ -380,7 +405,7 @@ class OrbitEngine:
         a = pr.args
         a.ids, a.coords, a.vels, a.n_cur = (snap['ids'].data_ptr(), snap['coordinates'].data_ptr(),
                                             snap['velocities'].data_ptr(), n)
-        a.rec_out = pr.rec.data_ptr()
+        a.rhat_out, a.meta_out = pr.rhat.data_ptr(), pr.meta.data_ptr()
         a.angles_in = _ptr(pr.angles_in)
         a.halos, a.n_halos = pr.halos.data_ptr(), len(halos)
         a.items, a.n_items = pr.d_items.data_ptr(), len(items)
@@ -398,7 +423,7 @@ class OrbitEngine:
         a.big_entries, a.big_slots = self.big_entries, self.big_slots
         return pr
 
-    def launch(self, pr, ws, prev_ids=None, prev_rec=None, stream=None, step_events=None):
+    def launch(self, pr, ws, prev=None, stream=None, step_events=None):
         """Device half of a step: enqueue bulk / step / compact on ``stream``
         (default: torch's current stream).  Never synchronises."""
         lib = self.lib
@@ -412,13 +437,15 @@ class OrbitEngine:
                     'oa_bulk_velocity')
         res = StepResult(n_slots=int(pr.has_prog.sum()), has_prog=pr.has_prog, halos=pr.halos)
         if pr.compare:
-            if prev_ids is None:
-                prev_ids, prev_rec = self.prev.ids, self.prev.rec
-            a.ids_prev, a.rec_prev, a.n_prev = prev_ids.data_ptr(), prev_rec.data_ptr(), pr.n_prev
+            p = prev if prev is not None else self.prev
+            a.ids_prev, a.rhat_prev, a.meta_prev = (p.ids.data_ptr(), p.rhat.data_ptr(),
+                                                    p.meta.data_ptr())
+            a.n_prev = pr.n_prev
             ws.reset(res.n_slots)
             a.scratch_ids, a.scratch_ang, a.dense_code = (ws.scratch_ids.data_ptr(),
                                                          ws.scratch_ang.data_ptr(),
                                                          ws.dense.data_ptr())
+            a.seg_count = ws.seg_count.data_ptr()
             a.halo_count, a.item_count, a.status = (ws.halo_count.data_ptr(),
                                                    ws.item_count.data_ptr(), ws.status.data_ptr())
         if step_events is not None:
@@ -434,6 +461,7 @@ class OrbitEngine:
         c.big_items, c.n_big_items = a.big_items, a.n_big_items
         c.ids_prev, c.id_bytes = a.ids_prev, a.id_bytes
         c.scratch_ids, c.scratch_ang, c.dense_code = a.scratch_ids, a.scratch_ang, a.dense_code
+        c.seg_count = a.seg_count
         c.halo_count, c.item_count, c.n_slots = a.halo_count, a.item_count, res.n_slots
         c.offsets_out, c.out_ids, c.out_ang = (ws.offsets.data_ptr(), ws.out_ids.data_ptr(),
                                                ws.out_ang.data_ptr())
@@ -460,7 +488,4 @@ class OrbitEngine:
 
     def angles(self):
         """Current per-particle float16 angles (checkpoint payload, track_orbits.py:390-394)."""
-        p = self.prev
-        words = p.rec.view(torch.int32).view(-1, p.plan.rec_bytes // 4)
-        meta = words[:, 3] if p.plan.rec_bytes == 16 else words[:, 6]
-        return (meta & 0xFFFF).to(torch.int32).cpu().numpy().astype(np.uint16).view(np.float16)
+        return meta_angles(self.prev.meta)

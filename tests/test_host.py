@@ -23,7 +23,10 @@ def test_library_exports_every_declared_symbol():
     assert declared == set(N.SYMBOLS), declared ^ set(N.SYMBOLS)
     assert lib.oa_abi_version() == N.ABI_VERSION
     assert lib.oa_struct_size(0) == 96 and lib.oa_struct_size(1) == 32
-    assert lib.oa_step_lds_bytes(16384, 32768, 0) < 160 * 1024
+    from orbitanalysis_amd import engine as E
+    assert lib.oa_step_lds_bytes(E.DEFAULT_ENTRIES, E.DEFAULT_SLOTS, 0) <= 160 * 1024
+    assert lib.oa_step_lds_bytes(E.DEFAULT_BIG_ENTRIES, E.DEFAULT_BIG_SLOTS, 1) <= 160 * 1024
+    assert lib.oa_build_info(0) % 64 == 0 and lib.oa_build_info(1) >= 1
 
 
 def test_no_silent_cpu_fallback():
@@ -111,7 +114,10 @@ def test_plan_items_invariants():
         assert cur[h] / b['nbuckets'][0] <= 0.7 * 3000
         covered[h] += 1
     assert np.all(covered == 1)
-    assert scratch == sum(np.maximum(prev[it['h0']:it['h1']], 0).sum() for it in items)
+    for it in items:
+        assert it['n_pv'] == np.maximum(prev[it['h0']:it['h1']], 0).sum()
+        assert it['scratch_off'] % 64 == 0
+    assert scratch == sum((int(it['n_pv']) + 63) // 64 * 64 for it in items)
 
 
 def test_synthetic_generator_is_deterministic():

@@ -1,0 +1,51 @@
+"""Diagnostic: per-work-group phase timeline of one oa_step (needs the -DOA_STAMPS=1
+build, e.g. ORBIT_HIP_LIB=nbody-orbit-analysis_amd/variants/lib_stamps.so)."""
+import os
+import sys
+import ctypes
+import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import orbitanalysis_amd  # noqa
+from orbitanalysis_amd import _native as N
+from orbitanalysis_amd.engine import OrbitEngine, Workspace
+from orbitanalysis_amd.synthetic_device import DevicePlummer
+from orbitanalysis_amd.utils import hubble_parameter
+from collections import namedtuple
+
+n = float(os.environ.get('NPART', 1e8)); nh = int(os.environ.get('NHALO', 10000))
+gen = DevicePlummer(n_halos=nh, n_particles=int(n))
+s0, s1 = gen.snapshot(0), gen.snapshot(1)
+c0, c1 = gen.catalogue(0), gen.catalogue(1)
+cos = gen.cosmology
+H = hubble_parameter(cos['redshift'], cos['H0'], cos['Omega_m'], cos['Omega_L'])
+z = cos['redshift']
+ex = np.arange(nh)
+eng = OrbitEngine()
+p0 = eng.prepare(s0, c0[0], c0[2], H, z, ex, False)
+eng.launch(p0, None)
+p1 = eng.prepare(s1, c1[0], c1[2], H, z, ex, True,
+                 prev_layout=(p0.starts, p0.counts, ex, p0.plan, p0.n))
+ws = Workspace.for_step(p1, eng.device)
+St = namedtuple('St', 'ids rhat meta')
+for rep in range(3):
+    eng.launch(p1, ws, St(s0['ids'], p0.rhat, p0.meta))
+torch.cuda.synchronize()
+ni = len(p1.items)
+buf = np.zeros(ni * 6, dtype=np.uint64)
+got = eng.lib.oa_debug_stamps(buf.ctypes.data, buf.size)
+assert got > 0, 'not a stamps build'
+t = buf.reshape(ni, 6).astype(np.float64) * 10.0 / 1000.0   # 100 MHz -> us
+t -= t[:, 0].min()
+start, span = t[:, 0], t[:, 5] - t[:, 0]
+print('items', ni, 'kernel span %.1f us' % (t[:, 5].max()))
+for name, a, b in (('phase0', 0, 1), ('phase1(t0)', 1, 2), ('barrier1', 2, 3),
+                   ('phase2(t0)', 3, 4), ('phase3+', 4, 5), ('total', 0, 5)):
+    d = t[:, b] - t[:, a]
+    print('%-11s mean %7.2f  p10 %7.2f  p50 %7.2f  p90 %7.2f  max %7.2f us'
+          % (name, d.mean(), *np.percentile(d, [10, 50, 90]), d.max()))
+order = np.argsort(start)
+print('start times of first 600 items (us):', np.round(start[order][::40][:15], 1))
+# concurrency: number of items alive at sampled times
+ts = np.linspace(0, t[:, 5].max(), 12)
+print('alive:', [int(((t[:, 0] <= x) & (t[:, 5] > x)).sum()) for x in ts])
