@@ -39,6 +39,8 @@ extern "C" {
 /* Run-time flags reported by the step kernel in `status` (bit mask). */
 #define OA_STATUS_BUCKET_OVERFLOW 1u  /* a hash bucket exceeded its LDS capacity:
                                          re-plan the halo with more buckets */
+#define OA_STATUS_TABLE_OVERFLOW 2u   /* the LDS cuckoo table could not place every
+                                         entry (stash full): re-plan smaller items */
 
 #define OA_MODE_PERICENTRIC 0
 #define OA_MODE_APOCENTRIC 1

@@ -26,6 +26,7 @@ ITEM_DTYPE = np.dtype([('h0', '<i4'), ('h1', '<i4'), ('bucket', '<i4'), ('nbucke
 
 MODE = {'pericentric': 0, 'apocentric': 1}
 STATUS_BUCKET_OVERFLOW = 1
+STATUS_TABLE_OVERFLOW = 2
 
 
 class StepArgs(ctypes.Structure):

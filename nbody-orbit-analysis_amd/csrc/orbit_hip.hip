@@ -47,17 +47,9 @@ namespace {
 //   OA_ABL_FRAME   phase 1 skips the frame arithmetic (r̂ = dx)
 //   OA_ABL_STORE1  phase 1 skips its r̂ stores
 //   OA_ABL_PHASE3  phase 3 skips its meta stores
-//   OA_ABL_CAS     phase 1 inserts with plain stores (no CAS; collisions overwrite)
-//   OA_ABL_ADD     phase 1 replaces the CAS insert by one LDS atomicAdd per particle
 //   OA_ABL_ACOS    phase 2 skips arccos
 //   OA_ABL_EMIT    phase 2 skips apsis record stores / counters
 //   OA_ABL_SLOTW   phase 2 skips the angle write-back into the slot
-#ifndef OA_ABL_CAS
-#define OA_ABL_CAS 0
-#endif
-#ifndef OA_ABL_ADD
-#define OA_ABL_ADD 0
-#endif
 #ifndef OA_ABL_ACOS
 #define OA_ABL_ACOS 0
 #endif
@@ -82,9 +74,6 @@ namespace {
 #ifndef OA_ABL_PHASE3
 #define OA_ABL_PHASE3 0
 #endif
-#ifndef OA_CAS32
-#define OA_CAS32 0          // 1: claim LDS slots with a 32-bit CAS on the high word (slower)
-#endif
 #ifndef OA_SLOT_X2
 #define OA_SLOT_X2 4        // per-item table: slots = entries * OA_SLOT_X2 / 2 (+64)
 #endif
@@ -104,6 +93,8 @@ constexpr int UNR1 = OA_UNR1;       // phase-1 particles per thread per loop tri
 constexpr int UNR2 = OA_UNR2;       // phase-2 particles per thread per loop trip
 constexpr int UNR = UNR2;
 constexpr int BULK_CHUNK = 8192;    // numpy pairwise-sum buffer chunk
+constexpr int STASH = 64;           // cuckoo stash entries per item
+constexpr int MAX_EVICT = 48;       // eviction-chain length before an entry is stashed
 static_assert(WG % 64 == 0 && WG <= 1024, "work-group must be whole waves");
 static_assert(HMAX < WG, "halo table is staged by one thread per halo");
 
@@ -215,10 +206,18 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
     h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
     return h;
 }
-__device__ __forceinline__ uint32_t slot_of(uint32_t lo, uint32_t hl, uint32_t nslots) {
-    uint32_t h = fmix32(lo ^ (hl * 0x9E3779B9u) ^ 0xA511E9B3u);
-    return (uint32_t)(((uint64_t)h * nslots) >> 32);
+// Three cuckoo candidate slots of a key (low 32 bits of the ID) in a table of n slots:
+// one 64-bit mix, three 21-bit fields scaled to [0, n).
+__device__ __forceinline__ void cuckoo_slots(uint32_t lo, uint32_t n, uint32_t s[3]) {
+    uint64_t x = ((uint64_t)lo + 0x632BE59BD9B4E019ull) * 0x9E3779B97F4A7C15ull;
+    x ^= x >> 29;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 32;
+    s[0] = (uint32_t)(((x & 0x1FFFFFull) * n) >> 21);
+    s[1] = (uint32_t)((((x >> 21) & 0x1FFFFFull) * n) >> 21);
+    s[2] = (uint32_t)((((x >> 42) & 0x1FFFFFull) * n) >> 21);
 }
+
 __device__ __forceinline__ uint32_t bucket_of(uint32_t lo, uint32_t hi, uint32_t nb) {
     uint32_t h = fmix32(lo * 0x9E3779B1u + hi * 0x85EBCA77u + 0x27D4EB2Fu);
     return (uint32_t)(((uint64_t)h * nb) >> 32);
@@ -239,7 +238,8 @@ struct ItemHdr {
     int64_t cur_base;
     uint32_t nonuniform, hi0, nent, overflow;
     uint32_t nh, nseg, n_span, n_pv;
-    uint32_t chunk_total, nsl, pad1, pad2;
+    uint32_t chunk_total, nsl, nstash, pad2;
+    uint64_t stash[STASH];          // cuckoo entries whose eviction chain ran out
     uint32_t lstart[HMAX + 1];      // local start of each item halo's current block
     uint32_t vstart[HMAX + 1];      // virtual start of each progenitor segment
     int32_t seg_halo[HMAX];         // segment -> item-local halo
@@ -251,7 +251,7 @@ struct ItemHdr {
 constexpr int64_t HDR_BYTES = (sizeof(ItemHdr) + 255) & ~int64_t(255);
 
 __host__ __device__ inline int64_t table_bytes(int entries, int slots, bool bucketed) {
-    int64_t b = (int64_t)slots * 8 + (bucketed ? (int64_t)entries * 4 : 0);
+    int64_t b = (int64_t)slots * 8 + (int64_t)entries * (bucketed ? 4 : 2);
     return (b + 15) & ~int64_t(15);
 }
 
@@ -386,6 +386,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     const uint32_t nslots_max = (uint32_t)(BUCKETED ? a.big_slots : a.lds_slots);
     uint64_t *slots = reinterpret_cast<uint64_t *>(smem + HDR_BYTES);
     uint32_t *lidx = BUCKETED ? reinterpret_cast<uint32_t *>(slots + nslots_max) : nullptr;
+    // unbucketed: position -> slot (0xFFFF = particle not in the table), for phase 3
+    uint16_t *slotmap = BUCKETED ? nullptr : reinterpret_cast<uint16_t *>(slots + nslots_max);
 
     const oa_item it = (BUCKETED ? a.big_items : a.items)[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -415,7 +417,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         }
     }
     if (tid == 0) {
-        H.nonuniform = 0; H.nent = 0; H.overflow = 0; H.nh = nh; H.chunk_total = 0;
+        H.nonuniform = 0; H.nent = 0; H.overflow = 0; H.nh = nh; H.chunk_total = 0; H.nstash = 0;
         // progenitor segments in halo order (serial: nh <= HMAX)
         uint32_t ns = 0, vp = 0;
         for (int k = 0; k < nh; ++k) {
@@ -444,6 +446,9 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     const uint32_t nslots = H.nsl;
     if (compare) {
         for (uint32_t w = tid; w < nslots; w += WG) slots[w] = 0ull;
+        if (!BUCKETED)
+            for (uint32_t w = tid; w < (H.n_span + 1) / 2; w += WG)
+                reinterpret_cast<uint32_t *>(slotmap)[w] = 0xFFFFFFFFu;
     }
     __syncthreads();
 
@@ -478,7 +483,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
 #pragma unroll
         for (int u = 0; u < UNR1; ++u) ok[u] = l0 + u * WG + tid < n_span;
         uint64_t val[UNR1];
-        uint32_t sl[UNR1];
+        uint32_t sl[UNR1], cs1[UNR1], cs2[UNR1];
         bool ins[UNR1];
 #pragma unroll
         for (int u = 0; u < UNR1; ++u) {
@@ -514,45 +519,65 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
             if (IDB == 8 && hi != hi0) H.nonuniform = 1u;     // benign race: all write 1
             val[u] = slot_pack(lo, meta, pos);
-            sl[u] = slot_of(lo, hl, nslots);
+            uint32_t cs[3];
+            cuckoo_slots(lo, nslots, cs);
+            sl[u] = cs[0];
+            cs1[u] = cs[1];
+            cs2[u] = cs[2];
             ins[u] = !OA_ABL_INSERT;
             if (OA_ABL_INSERT) asm volatile("" :: "v"(val[u]), "v"(sl[u]));
         }
-        // lockstep linear-probing insert: every pending CAS issued before any retry
-        for (;;) {
+        // first try: claim an EMPTY candidate with a CAS (at load <= 1/2 one of the three
+        // almost always is), so eviction chains stay rare
+        {
+            uint64_t c0[UNR1], c1[UNR1], c2[UNR1];
+#pragma unroll
+            for (int u = 0; u < UNR1; ++u)
+                if (ins[u]) { c0[u] = slots[sl[u]]; c1[u] = slots[cs1[u]]; c2[u] = slots[cs2[u]]; }
+#pragma unroll
+            for (int u = 0; u < UNR1; ++u) {
+                if (!ins[u]) continue;
+                const uint32_t t = c0[u] == 0ull ? sl[u] : (c1[u] == 0ull ? cs1[u]
+                                                          : (c2[u] == 0ull ? cs2[u] : 0xFFFFFFFFu));
+                if (t == 0xFFFFFFFFu) continue;
+                const uint64_t o = atomicCAS(reinterpret_cast<unsigned long long *>(&slots[t]),
+                                             0ull, (unsigned long long)val[u]);
+                if (o == 0ull) ins[u] = false;
+            }
+        }
+        // then the cuckoo walk: exchange into a candidate slot; an evicted entry moves
+        // on to its next candidate.  Every pending exchange is issued before any result
+        // is inspected; a chain longer than MAX_EVICT parks its entry in the stash.
+        for (int it_ = 0;; ++it_) {
             bool any = false;
             uint64_t old[UNR1];
 #pragma unroll
             for (int u = 0; u < UNR1; ++u)
-                if (ins[u]) {
-                    if (OA_ABL_ADD) {
-                        uint32_t *c = reinterpret_cast<uint32_t *>(slots) + (sl[u] >> 2);
-                        uint32_t r = atomicAdd(c + 4096, 1u);
-                        slots[sl[u]] = val[u] + r;
-                        old[u] = 0ull;
-                    } else if (OA_ABL_CAS) { slots[sl[u]] = val[u]; old[u] = 0ull; }
-                    else if (OA_CAS32) {
-                        // claim the slot through its high word (pos + 1 > 0 when occupied)
-                        uint32_t *w = reinterpret_cast<uint32_t *>(&slots[sl[u]]);
-                        old[u] = atomicCAS(w + 1, 0u, (uint32_t)(val[u] >> 32));
-                    } else {
-                        old[u] = atomicCAS(reinterpret_cast<unsigned long long *>(&slots[sl[u]]),
-                                           0ull, (unsigned long long)val[u]);
-                    }
-                }
+                if (ins[u]) old[u] = atomicExch(reinterpret_cast<unsigned long long *>(&slots[sl[u]]),
+                                                (unsigned long long)val[u]);
 #pragma unroll
             for (int u = 0; u < UNR1; ++u) {
                 if (!ins[u]) continue;
-                if (old[u] == 0ull) {
-                    // key word: read by phase-2 probes only after the barrier
-                    if (OA_CAS32) reinterpret_cast<uint32_t *>(&slots[sl[u]])[0] = (uint32_t)val[u];
-                    ins[u] = false;
-                    continue;
-                }
-                sl[u] = (sl[u] + 1 == nslots) ? 0u : sl[u] + 1;
+                if (old[u] == 0ull) { ins[u] = false; continue; }
+                uint32_t cs[3];
+                cuckoo_slots((uint32_t)old[u], nslots, cs);
+                const uint32_t j = cs[0] == sl[u] ? 1u : (cs[1] == sl[u] ? 2u : 0u);
+                val[u] = old[u];
+                sl[u] = cs[j];
                 any = true;
             }
             if (!any) break;
+            if (it_ == MAX_EVICT) {
+#pragma unroll
+                for (int u = 0; u < UNR1; ++u) {
+                    if (!ins[u]) continue;
+                    const uint32_t e = atomicAdd(&H.nstash, 1u);
+                    if (e < (uint32_t)STASH) H.stash[e] = val[u];
+                    else H.overflow = 2u;
+                    ins[u] = false;
+                }
+                break;
+            }
         }
         if (OA_PF1) {
 #pragma unroll
@@ -563,16 +588,9 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     STAMP(2);
     if constexpr (!COMPARE) return;
     if (!join) return;
-    __syncthreads();
-    STAMP(3);
-    if (H.overflow) {
-        if (tid == 0) atomicOr(a.status, OA_STATUS_BUCKET_OVERFLOW);
-        return;
-    }
 
     // ---- phase 2: stream progenitor blocks, join, flag, angle, emit ---------
     const uint32_t n_pv = H.n_pv, nseg = H.nseg;
-    const bool nonuniform = IDB == 8 && H.nonuniform != 0;
     const uint64_t lanemask_lt = (1ull << lane) - 1ull;
     uint32_t running = 0;
     ID *scr_ids = reinterpret_cast<ID *>(a.scratch_ids);
@@ -591,69 +609,71 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     V3<TD> prh[UNR], prhn[UNR];
     uint32_t pmeta[UNR], pmetan[UNR], hlv[UNR], hlvn[UNR];
     int64_t kpos[UNR], kposn[UNR];
-    if (OA_PF2 && n_pv > 0) { OA_LOAD2(pid, prh, pmeta, kpos, hlv, 0u) }
+    // The first trip's loads are issued BEFORE the phase-1/2 barrier.  The barrier
+    // then retires only this wave's older VMEM ops (its r̂/meta stores, which other
+    // waves gather in phase 2) with a counted vmcnt that leaves the 3 * UNR prefetch
+    // loads in flight, plus every LDS insert (lgkmcnt), then a raw s_barrier
+    // (a __syncthreads() would drain vmcnt to 0).
+    // An item none of whose halos has a progenitor block has nothing to join (the
+    // work-group-uniform exit keeps the prefetch below unconditional: a predicated
+    // one makes the compiler copy the loaded registers and wait on them here).
+    if (n_pv == 0) {
+        if (!BUCKETED && tid == 0) a.item_count[blockIdx.x] = 0;
+        return;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (OA_PF2) {
+        OA_LOAD2(pid, prh, pmeta, kpos, hlv, 0u)
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(3 * UNR) : "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    STAMP(3);
+    if (H.overflow) {
+        if (tid == 0) atomicOr(a.status, H.overflow == 1u ? OA_STATUS_BUCKET_OVERFLOW
+                                                           : OA_STATUS_TABLE_OVERFLOW);
+        return;
+    }
+    const bool nonuniform = IDB == 8 && H.nonuniform != 0;
     for (uint32_t v0 = 0; v0 < n_pv; v0 += WG * UNR) {
         if (!OA_PF2) { OA_LOAD2(pid, prh, pmeta, kpos, hlv, v0) }
         bool ok[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u) ok[u] = v0 + u * WG + tid < n_pv;
-        // lockstep probe of (halo, id): departed particles miss (setdiff1d/in1d, :300-304)
-        uint32_t sl[UNR], lo[UNR], hi[UNR], lmin[UNR], lmax[UNR];
+        // cuckoo lookup of (halo, id): the three candidate slots are read together (one
+        // LDS round trip); departed particles miss (setdiff1d/in1d, :300-304)
+        uint32_t lo[UNR], hi[UNR], lmin[UNR], lmax[UNR], hs[UNR];
         uint64_t hit[UNR];
-        bool act[UNR];
+        const uint32_t nstash = H.nstash;
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
             hit[u] = 0ull;
-            act[u] = false;
+            hs[u] = 0;
             if (!ok[u]) continue;
             id_split<IDB>(pid[u], lo[u], hi[u]);
             if (BUCKETED && bucket_of(lo[u], hi[u], nb) != q) { ok[u] = false; continue; }
             if (IDB == 8 && !nonuniform && hi[u] != hi0) continue;      // cannot be present
             lmin[u] = BUCKETED ? 0u : H.lstart[hlv[u]];
             lmax[u] = BUCKETED ? 0xFFFFFFFFu : H.lstart[hlv[u] + 1];
-            sl[u] = slot_of(lo[u], hlv[u], nslots);
-            act[u] = true;
-        }
-        for (;;) {
-            uint64_t v[UNR];
-            bool any = false;
-#pragma unroll
-            for (int u = 0; u < UNR; ++u)
-                if (act[u]) v[u] = slots[sl[u]];
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                if (!act[u]) continue;
-                if (v[u] == 0ull) { act[u] = false; continue; }              // miss
-                const uint32_t p = slot_pos(v[u]);
-                if ((uint32_t)v[u] == lo[u] && (BUCKETED || (p >= lmin[u] && p < lmax[u]))) {
-                    hit[u] = v[u]; act[u] = false; continue;
-                }
-                sl[u] = (sl[u] + 1 == nslots) ? 0u : sl[u] + 1;
-                any = true;
-            }
-            if (!any) break;
-        }
-        if (IDB == 8 && nonuniform) {
-            // rare path (item IDs differ in their high words): confirm the full ID and
-            // keep probing past a low-word collision.  Kept out of the probe loop above
-            // so the common path has no global load (and no vmcnt drain) in it.
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                while (hit[u]) {
-                    const uint32_t p = slot_pos(hit[u]);
-                    if (ids[base + (BUCKETED ? lidx[p] : p)] == pid[u]) break;
-                    hit[u] = 0ull;
-                    for (;;) {
-                        sl[u] = (sl[u] + 1 == nslots) ? 0u : sl[u] + 1;
-                        const uint64_t w = slots[sl[u]];
-                        if (!w) break;
-                        const uint32_t pw = slot_pos(w);
-                        if ((uint32_t)w == lo[u] && (BUCKETED || (pw >= lmin[u] && pw < lmax[u]))) {
-                            hit[u] = w;
-                            break;
-                        }
-                    }
-                }
+            uint32_t cs[3];
+            cuckoo_slots(lo[u], nslots, cs);
+            uint64_t c0 = slots[cs[0]], c1 = slots[cs[1]], c2 = slots[cs[2]];
+            auto match = [&](uint64_t v) {
+                const uint32_t p = slot_pos(v);
+                bool m = v != 0ull && (uint32_t)v == lo[u] && (BUCKETED || (p >= lmin[u] && p < lmax[u]));
+                if (IDB == 8 && nonuniform && m)        // rare: confirm the full ID
+                    m = ids[base + (BUCKETED ? lidx[p] : p)] == pid[u];
+                return m;
+            };
+            if (match(c0)) { hit[u] = c0; hs[u] = cs[0]; }
+            else if (match(c1)) { hit[u] = c1; hs[u] = cs[1]; }
+            else if (match(c2)) { hit[u] = c2; hs[u] = cs[2]; }
+            else if (nstash) {
+                for (uint32_t e = 0; e < nstash && e < (uint32_t)STASH; ++e)
+                    if (match(H.stash[e])) { hit[u] = H.stash[e]; hs[u] = nslots + e; break; }
             }
         }
         // gather the matched current r̂ (written in phase 1: L2).  Unconditional
@@ -686,7 +706,10 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             TD dt = dot3(prh[u].x, prh[u].y, prh[u].z, cr[u].x, cr[u].y, cr[u].z);
             uint16_t acc = angle_add((uint16_t)(pmeta[u] & 0xFFFFu), OA_ABL_ACOS ? dt : acos_td(dt));
             // calc_angles (:342-349): apsis angle emitted, then reset to 0
-            if (!OA_ABL_SLOTW) reinterpret_cast<uint16_t *>(&slots[sl[u]])[2] = cond ? (uint16_t)0 : acc;
+            if (!OA_ABL_SLOTW) {
+                uint64_t *sp_ = hs[u] < nslots ? &slots[hs[u]] : &H.stash[hs[u] - nslots];
+                reinterpret_cast<uint16_t *>(sp_)[2] = cond ? (uint16_t)0 : acc;
+            }
             flag[u] = cond;
             a16[u] = acc;
         }
@@ -738,13 +761,28 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     STAMP(4);
     __syncthreads();
 
-    // ---- phase 3: meta words of the joined particles (one per occupied slot) --
-    for (uint32_t w = tid; w < nslots; w += WG) {
-        const uint64_t v = slots[w];
-        if (!v) continue;
-        const uint32_t p = slot_pos(v);
-        if (!OA_ABL_PHASE3) a.meta_out[base + (BUCKETED ? lidx[p] : p)] = slot_meta(v);
-        else asm volatile("" :: "v"(p));
+    // ---- phase 3: meta words of the joined particles -----------------------------
+    const uint32_t nst = min(H.nstash, (uint32_t)STASH);
+    if (BUCKETED) {
+        // bucket members are scattered over the block anyway: one store per slot
+        for (uint32_t w = tid; w < nslots + nst; w += WG) {
+            const uint64_t v = w < nslots ? slots[w] : H.stash[w - nslots];
+            if (!v) continue;
+            if (!OA_ABL_PHASE3) a.meta_out[base + lidx[slot_pos(v)]] = slot_meta(v);
+        }
+    } else {
+        // position -> slot map, then coalesced meta stores in position order
+        for (uint32_t w = tid; w < nslots + nst; w += WG) {
+            const uint64_t v = w < nslots ? slots[w] : H.stash[w - nslots];
+            if (v) slotmap[slot_pos(v)] = (uint16_t)w;
+        }
+        __syncthreads();
+        for (uint32_t li = tid; li < n_span; li += WG) {
+            const uint32_t w = slotmap[li];
+            if (w == 0xFFFFu) continue;
+            const uint64_t v = w < nslots ? slots[w] : H.stash[w - nslots];
+            if (!OA_ABL_PHASE3) a.meta_out[base + li] = slot_meta(v);
+        }
     }
     if (BUCKETED) return;
     if (tid < nh) {

@@ -24,7 +24,7 @@ from . import _native as N
 
 F32, F64 = np.dtype(np.float32), np.dtype(np.float64)
 DEFAULT_ENTRIES = 14336        # current particles per work-group item (nbuckets == 1)
-DEFAULT_SLOTS = 19456          # 8-byte LDS hash slots per item (152 KB)
+DEFAULT_SLOTS = 16128          # 8-byte LDS cuckoo slots per item (126 KB) + 2 B/entry map
 DEFAULT_BIG_ENTRIES = 10240    # per hash bucket of a larger halo
 DEFAULT_BIG_SLOTS = 13824
 
@@ -257,6 +257,7 @@ class Workspace:
         self.out_ids = e(n_prev, id_torch_dtype)
         self.out_ang = e(n_prev, torch.int16)
         self.total = e(1, torch.int64)
+        self.status.zero_()
 
     @classmethod
     def for_step(cls, pr, device):
@@ -265,8 +266,8 @@ class Workspace:
                    len(pr.big) > 0)
 
     def reset(self, n_slots):
+        """Per-launch zeroing (the status word accumulates: callers clear it)."""
         self.halo_count[:max(n_slots, 1)].zero_()
-        self.status.zero_()
 
 
 class OrbitEngine:
@@ -302,7 +303,7 @@ class OrbitEngine:
 
     # ------------------------------------------------------------------ tables
     def build_tables(self, snapshot, centres, bulk_cat, exists, compare, min_buckets=None,
-                     prev_layout=None):
+                     prev_layout=None, entries=None):
         n = int(snapshot['ids'].numel()) if isinstance(snapshot['ids'], torch.Tensor) \
             else len(snapshot['ids'])
         starts = np.asarray(snapshot['region_offsets'], dtype=np.int64).reshape(-1)
@@ -329,8 +330,9 @@ class OrbitEngine:
             halos['prev_off'][has_prog] = p_starts[p[has_prog]]
             halos['prev_cnt'][has_prog] = p_counts[p[has_prog]]
             halos['out_slot'][has_prog] = np.arange(int(has_prog.sum()))
-        items, big, scratch = plan_items(counts, halos['prev_cnt'], self.entries,
-                                         self.big_entries, self.hmax, min_buckets=min_buckets)
+        items, big, scratch = plan_items(counts, halos['prev_cnt'], entries or self.entries,
+                                         min(self.big_entries, entries or self.big_entries),
+                                         self.hmax, min_buckets=min_buckets)
         return halos, items, big, scratch, starts, counts, has_prog
 
     # ------------------------------------------------------------------ step
@@ -345,25 +347,30 @@ class OrbitEngine:
             snap[k] = to_device(snapshot[k], dev)
         if is_array(snapshot['masses']):
             snap['masses'] = to_device(snapshot['masses'], dev)
-        min_b = None
+        min_b, entries = None, None
         for _ in range(8):
             prep = self.prepare(snap, centres, bulk_cat, H, z, exists, compare,
-                                angles_in=angles_in, min_buckets=min_b, plan_src=snapshot)
+                                angles_in=angles_in, min_buckets=min_b, plan_src=snapshot,
+                                entries=entries)
             ws = Workspace.for_step(prep, dev)
+            ws.status.zero_()
             res = self.launch(prep, ws)
-            if not compare or not len(prep.big) or not (int(ws.status.item()) &
-                                                        N.STATUS_BUCKET_OVERFLOW):
+            st = int(ws.status.item()) if compare else 0
+            if not st:
                 break
-            min_b = prep.more_buckets()      # a hash bucket overflowed: re-plan
+            if st & N.STATUS_BUCKET_OVERFLOW:
+                min_b = prep.more_buckets()          # a hash bucket overflowed: re-plan
+            if st & N.STATUS_TABLE_OVERFLOW:         # cuckoo stash full: smaller items
+                entries = max(256, (entries or self.entries) // 2)
         else:
-            raise RuntimeError('hash buckets kept overflowing (adversarial IDs?)')
+            raise RuntimeError('LDS hash tables kept overflowing (adversarial IDs?)')
         self.prev = SnapshotState(ids=snap['ids'], rhat=prep.rhat, meta=prep.meta,
                                   starts=prep.starts,
                                   counts=prep.counts, exists=exists, plan=prep.plan)
         return res
 
     def prepare(self, snap, centres, bulk_cat, H, z, exists, compare, angles_in=None,
-                min_buckets=None, plan_src=None, prev_layout=None):
+                min_buckets=None, plan_src=None, prev_layout=None, entries=None):
         """Host half of a step: dtype plan, halo/item tables, device uploads.
 
         ``snap`` holds device tensors for ids/coordinates/velocities(/masses);
@@ -387,7 +394,7 @@ class OrbitEngine:
         if snap['coordinates'].numel() != 3 * n or snap['velocities'].numel() != 3 * n:
             raise ValueError('coordinates/velocities must be (N, 3) with N = len(ids)')
         halos, items, big, scratch, starts, counts, has_prog = self.build_tables(
-            snap, centres, bulk_cat, exists, compare, min_buckets, prev_layout)
+            snap, centres, bulk_cat, exists, compare, min_buckets, prev_layout, entries)
         pr = PreparedStep(plan=plan, n=n, starts=starts, counts=counts, has_prog=has_prog,
                           items=items, big=big, scratch=scratch, compare=bool(compare),
                           n_prev=prev_layout[4] if compare else 0)

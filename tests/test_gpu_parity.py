@@ -89,8 +89,11 @@ def test_bucketed_and_packed_paths_match(name):
     from orbitanalysis_amd.engine import OrbitEngine
     fix = load(name)
     u, meta = universe(fix)
-    for entries, big in ((256, 200), (700, 128)):
-        eng = OrbitEngine(mode=meta['run']['mode'], lds_entries=entries, big_entries=big, hmax=7)
+    # (entries, big entries, slots): the last config packs the cuckoo tables to ~90 %
+    # load so insert chains hit the stash and the table-overflow re-plan path
+    for entries, big, slots in ((256, 200, None), (700, 128, None), (700, 128, 760)):
+        eng = OrbitEngine(mode=meta['run']['mode'], lds_entries=entries, big_entries=big, hmax=7,
+                          lds_slots=slots)
         out = run_driver(u, meta['run'], engine=eng)
         compare_groups(out.groups, groups(fix), {})
 
