@@ -50,6 +50,18 @@ namespace {
 //   OA_ABL_ACOS    phase 2 skips arccos
 //   OA_ABL_EMIT    phase 2 skips apsis record stores / counters
 //   OA_ABL_SLOTW   phase 2 skips the angle write-back into the slot
+#ifndef OA_ABL_CAS
+#define OA_ABL_CAS 0
+#endif
+#ifndef OA_ABL_WALK
+#define OA_ABL_WALK 0
+#endif
+#ifndef OA_IMMEDIATE_WALK
+#define OA_IMMEDIATE_WALK 0
+#endif
+#ifndef OA_HASH
+#define OA_HASH 1
+#endif
 #ifndef OA_ABL_ACOS
 #define OA_ABL_ACOS 0
 #endif
@@ -209,6 +221,17 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
 // Three cuckoo candidate slots of a key (low 32 bits of the ID) in a table of n slots:
 // one 64-bit mix, three 21-bit fields scaled to [0, n).
 __device__ __forceinline__ void cuckoo_slots(uint32_t lo, uint32_t n, uint32_t s[3]) {
+#if OA_HASH == 1
+    // two 32-bit multiplicative mixes; 16-bit fields scaled by 24-bit (full-rate) products
+    const uint32_t a = lo ^ (lo >> 16);
+    uint32_t h1 = a * 0x9E3779B1u, h2 = (a ^ 0x5BD1E995u) * 0x85EBCA6Bu;
+    h1 ^= h1 >> 15;
+    h2 ^= h2 >> 13;
+    s[0] = __umul24(h1 >> 16, n) >> 16;
+    s[1] = __umul24(h1 & 0xFFFFu, n) >> 16;
+    s[2] = __umul24(h2 >> 16, n) >> 16;
+    return;
+#endif
     uint64_t x = ((uint64_t)lo + 0x632BE59BD9B4E019ull) * 0x9E3779B97F4A7C15ull;
     x ^= x >> 29;
     x *= 0xBF58476D1CE4E5B9ull;
@@ -238,7 +261,7 @@ struct ItemHdr {
     int64_t cur_base;
     uint32_t nonuniform, hi0, nent, overflow;
     uint32_t nh, nseg, n_span, n_pv;
-    uint32_t chunk_total, nsl, nstash, pad2;
+    uint32_t chunk_total, nsl, nstash, npend;
     uint64_t stash[STASH];          // cuckoo entries whose eviction chain ran out
     uint32_t lstart[HMAX + 1];      // local start of each item halo's current block
     uint32_t vstart[HMAX + 1];      // virtual start of each progenitor segment
@@ -386,8 +409,11 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     const uint32_t nslots_max = (uint32_t)(BUCKETED ? a.big_slots : a.lds_slots);
     uint64_t *slots = reinterpret_cast<uint64_t *>(smem + HDR_BYTES);
     uint32_t *lidx = BUCKETED ? reinterpret_cast<uint32_t *>(slots + nslots_max) : nullptr;
-    // unbucketed: position -> slot (0xFFFF = particle not in the table), for phase 3
+    // unbucketed: position -> slot (0xFFFF = particle not in the table), for phase 3;
+    // during phase 1 the same bytes hold the list of deferred cuckoo inserts
     uint16_t *slotmap = BUCKETED ? nullptr : reinterpret_cast<uint16_t *>(slots + nslots_max);
+    uint64_t *pend = reinterpret_cast<uint64_t *>(slotmap);
+    const uint32_t pend_cap = BUCKETED ? 0u : (uint32_t)a.lds_entries / 4u;
 
     const oa_item it = (BUCKETED ? a.big_items : a.items)[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -418,6 +444,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     }
     if (tid == 0) {
         H.nonuniform = 0; H.nent = 0; H.overflow = 0; H.nh = nh; H.chunk_total = 0; H.nstash = 0;
+        H.npend = 0;
         // progenitor segments in halo order (serial: nh <= HMAX)
         uint32_t ns = 0, vp = 0;
         for (int k = 0; k < nh; ++k) {
@@ -446,9 +473,6 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     const uint32_t nslots = H.nsl;
     if (compare) {
         for (uint32_t w = tid; w < nslots; w += WG) slots[w] = 0ull;
-        if (!BUCKETED)
-            for (uint32_t w = tid; w < (H.n_span + 1) / 2; w += WG)
-                reinterpret_cast<uint32_t *>(slotmap)[w] = 0xFFFFFFFFu;
     }
     __syncthreads();
 
@@ -540,15 +564,26 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                 const uint32_t t = c0[u] == 0ull ? sl[u] : (c1[u] == 0ull ? cs1[u]
                                                           : (c2[u] == 0ull ? cs2[u] : 0xFFFFFFFFu));
                 if (t == 0xFFFFFFFFu) continue;
+                if (OA_ABL_CAS) { slots[t] = val[u]; ins[u] = false; continue; }
                 const uint64_t o = atomicCAS(reinterpret_cast<unsigned long long *>(&slots[t]),
                                              0ull, (unsigned long long)val[u]);
                 if (o == 0ull) ins[u] = false;
             }
         }
+        // an entry whose three candidates are taken is deferred: the walks run after the
+        // loop, spread over the whole work-group, instead of stalling this wave per trip
+        if (!BUCKETED && !OA_IMMEDIATE_WALK) {
+#pragma unroll
+            for (int u = 0; u < UNR1; ++u) {
+                if (!ins[u]) continue;
+                const uint32_t e = atomicAdd(&H.npend, 1u);
+                if (e < pend_cap) { pend[e] = val[u]; ins[u] = false; }
+            }
+        }
         // then the cuckoo walk: exchange into a candidate slot; an evicted entry moves
         // on to its next candidate.  Every pending exchange is issued before any result
         // is inspected; a chain longer than MAX_EVICT parks its entry in the stash.
-        for (int it_ = 0;; ++it_) {
+        for (int it_ = 0; !OA_ABL_WALK; ++it_) {
             bool any = false;
             uint64_t old[UNR1];
 #pragma unroll
@@ -620,6 +655,30 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     if (n_pv == 0) {
         if (!BUCKETED && tid == 0) a.item_count[blockIdx.x] = 0;
         return;
+    }
+    if (!BUCKETED && !OA_IMMEDIATE_WALK) {
+        __syncthreads();
+        const uint32_t np = min(H.npend, pend_cap);
+        for (uint32_t e = tid; e < np; e += WG) {
+            uint64_t v = pend[e];
+            uint32_t cs[3];
+            cuckoo_slots((uint32_t)v, nslots, cs);
+            uint32_t t = cs[0];
+            for (int it_ = 0;; ++it_) {
+                const uint64_t old = atomicExch(reinterpret_cast<unsigned long long *>(&slots[t]),
+                                                (unsigned long long)v);
+                if (old == 0ull) break;
+                if (it_ == MAX_EVICT) {
+                    const uint32_t k = atomicAdd(&H.nstash, 1u);
+                    if (k < (uint32_t)STASH) H.stash[k] = old;
+                    else H.overflow = 2u;
+                    break;
+                }
+                cuckoo_slots((uint32_t)old, nslots, cs);
+                t = cs[cs[0] == t ? 1 : (cs[1] == t ? 2 : 0)];
+                v = old;
+            }
+        }
     }
     __builtin_amdgcn_sched_barrier(0);
     if (OA_PF2) {
@@ -771,11 +830,16 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             if (!OA_ABL_PHASE3) a.meta_out[base + lidx[slot_pos(v)]] = slot_meta(v);
         }
     } else {
-        // position -> slot map, then coalesced meta stores in position order
+        // position -> slot map (halos without a progenitor block: not in the table,
+        // their meta was stored in phase 1), then coalesced stores in position order
         for (uint32_t w = tid; w < nslots + nst; w += WG) {
             const uint64_t v = w < nslots ? slots[w] : H.stash[w - nslots];
             if (v) slotmap[slot_pos(v)] = (uint16_t)w;
         }
+        for (uint32_t k = 0; k < (uint32_t)nh; ++k)
+            if (!H.has_prev[k])
+                for (uint32_t li = H.lstart[k] + tid; li < H.lstart[k + 1]; li += WG)
+                    slotmap[li] = 0xFFFFu;
         __syncthreads();
         for (uint32_t li = tid; li < n_span; li += WG) {
             const uint32_t w = slotmap[li];

@@ -489,6 +489,43 @@ class OrbitEngine:
             np.zeros(0, dtype=np.float16)
         return offsets, ids, ang
 
+    def block_bulk(self, snapshot, halo_idx):
+        """Bulk velocities (track_orbits.py:269-280) of the listed region blocks of a
+        snapshot, computed on the device (oa_bulk_velocity) from those blocks only.
+        Returns an (len(halo_idx), 3) array in the reference's result dtype."""
+        halo_idx = np.asarray(halo_idx, dtype=np.int64)
+        vel = snapshot['velocities']
+        n = len(snapshot['ids'])
+        starts = np.asarray(snapshot['region_offsets'], dtype=np.int64).reshape(-1)
+        counts = np.append(starts[1:], n) - starts
+        plan = plan_dtypes(snapshot, np.zeros(3), None, 0.0, 0.0)
+        c = counts[halo_idx]
+        rows = np.concatenate([np.arange(s, s + k) for s, k in zip(starts[halo_idx], c)]) \
+            if len(halo_idx) else np.zeros(0, dtype=np.int64)
+        dev = self.device
+        if isinstance(vel, torch.Tensor):
+            v = vel.reshape(-1, 3)[torch.from_numpy(rows).to(vel.device)].to(dev).contiguous()
+        else:
+            v = to_device(np.asarray(vel).reshape(-1, 3)[rows], dev)
+        m = None
+        if plan.mass is not None:
+            ms = snapshot['masses']
+            m = ms[torch.from_numpy(rows).to(ms.device)].to(dev).contiguous() \
+                if isinstance(ms, torch.Tensor) else to_device(np.asarray(ms)[rows], dev)
+        halos = np.zeros(len(halo_idx), dtype=N.HALO_DTYPE)
+        halos['cur_off'] = np.concatenate([[0], np.cumsum(c)[:-1]]) if len(c) else c
+        halos['cur_cnt'] = c
+        d_h = torch.from_numpy(halos.view(np.uint8)).to(dev)
+        lst = torch.arange(len(halo_idx), dtype=torch.int32, device=dev)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        if len(halo_idx):
+            N.check(self.lib.oa_bulk_velocity(v.data_ptr(), int(plan.vel == F64), _ptr(m),
+                                              int(plan.mass == F64), d_h.data_ptr(),
+                                              lst.data_ptr(), len(halo_idx), st),
+                    'oa_bulk_velocity')
+        out = d_h.cpu().numpy().view(N.HALO_DTYPE)['bulk']
+        return out.astype(plan.bulk)
+
     def bulk_velocities(self, res, plan):
         h = res.halos.cpu().numpy().view(N.HALO_DTYPE)
         return h['bulk'].astype(plan.bulk)

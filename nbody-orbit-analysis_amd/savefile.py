@@ -77,6 +77,29 @@ class HDF5Savefile:
             return hf['angles'][:]
 
 
+class RankSink:
+    """Savefile stand-in for ranks other than 0 in a sharded run: writes are dropped
+    (rank 0 writes the file); resume reads go to the real savefile."""
+
+    def __init__(self, source=None):
+        self.source = source
+
+    def initialize(self, mode, box_size):
+        pass
+
+    def write_group(self, name, datasets):
+        pass
+
+    def write_checkpoint(self, angles):
+        pass
+
+    def last_snapshot_number(self):
+        return self.source.last_snapshot_number()
+
+    def read_checkpoint(self):
+        return self.source.read_checkpoint()
+
+
 def open_savefile(savefile):
     if isinstance(savefile, (str, bytes)) or hasattr(savefile, '__fspath__'):
         return HDF5Savefile(str(savefile))

@@ -12,7 +12,7 @@ import time
 import numpy as np
 
 from .engine import OrbitEngine
-from .savefile import open_savefile, group_datasets
+from .savefile import RankSink, open_savefile, group_datasets
 from .utils import hubble_parameter
 
 
@@ -58,6 +58,10 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
     eng = engine if engine is not None else OrbitEngine(mode=mode)
     if eng.mode != mode:
         raise ValueError('engine mode %r != mode %r' % (eng.mode, mode))
+    if getattr(eng, 'rank', 0) != 0:
+        # sharded run (sharding.ShardedEngine): every rank computes, rank 0 writes
+        out = RankSink(out)
+        verbose = False
     eng.reset()
 
     istart, started = 0, False

@@ -122,3 +122,16 @@ def test_random_cases_match_oracle(kw, mode):
     compare_groups(run_driver(u, dict(mode=mode)).groups, _oracle_run(u, mode), rep)
     assert rep['angles'] > 0
     assert rep['angle_mismatch'] / rep['angles'] < ANGLE_MISMATCH_MAX, rep
+
+
+@pytest.mark.parametrize('name,owner', [('g2_overlap_birth_massarray', 'hash'),
+                                        ('g3_apo_periodic', 'range')])
+def test_sharded_hip_engine_matches_reference(name, owner):
+    """Two ranks on this GPU (gloo for the small collectives), each running the HIP
+    engine on its ID shard; rank 0's savefile must equal the reference's."""
+    from test_sharding import run_sharded, _groups
+    fix = load(name)
+    got = run_sharded(name, 2, owner, local='hip')
+    rep = {}
+    compare_groups(_groups(got), groups(fix), rep)
+    assert rep.get('angle_mismatch', 0) <= ANGLE_MISMATCH_MAX * max(rep.get('angles', 1), 1)
