@@ -103,7 +103,6 @@ constexpr int NWAVE = WG / 64;
 constexpr int HMAX = OA_HMAX;       // halos per item
 constexpr int UNR1 = OA_UNR1;       // phase-1 particles per thread per loop trip
 constexpr int UNR2 = OA_UNR2;       // phase-2 particles per thread per loop trip
-constexpr int UNR = UNR2;
 constexpr int BULK_CHUNK = 8192;    // numpy pairwise-sum buffer chunk
 constexpr int STASH = 64;           // cuckoo stash entries per item
 constexpr int MAX_EVICT = 48;       // eviction-chain length before an entry is stashed
@@ -357,7 +356,31 @@ __device__ __forceinline__ uint32_t frame(const V3<TX> &x, const V3<TV> &v, cons
     }
     // rads = sqrt(dot(dx, dx)); rhats = dx / rads   (:286-287), exact in dx's dtype
     TD rr = sqrt(dot3(dx[0], dx[1], dx[2], dx[0], dx[1], dx[2]));
-    r[0] = dx[0] / rr; r[1] = dx[1] / rr; r[2] = dx[2] / rr;
+    if constexpr (std::is_same<TD, float>::value) {
+        // Correctly rounded float32 quotients from ONE float64 reciprocal: with
+        // y = 1/rr to 2^-52 (v_rcp_f64 + two Newton steps), q = dx * y is within
+        // 2^-51 (relative) of dx / rr, while a quotient of two floats is never closer
+        // than 2^-50 to a float32 rounding midpoint -- so rounding q to
+        // float32 gives RN(dx / rr) exactly.  Valid for normal quotients and a normal
+        // rr; any other wave takes the IEEE division.
+        bool fast = rr >= 0x1p-100f && rr <= 0x1p100f;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) fast = fast && (dx[d] == 0.f || fabsf(dx[d]) >= rr * 0x1p-100f);
+        if (__all(fast)) {
+            const double b = (double)rr;
+            double y = __builtin_amdgcn_rcp(b);
+            double e = __builtin_fma(-b, y, 1.0);
+            y = __builtin_fma(y, e, y);
+            e = __builtin_fma(-b, y, 1.0);
+            y = __builtin_fma(y, e, y);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) r[d] = (TD)((double)dx[d] * y);
+        } else {
+            r[0] = dx[0] / rr; r[1] = dx[1] / rr; r[2] = dx[2] / rr;
+        }
+    } else {
+        r[0] = dx[0] / rr; r[1] = dx[1] / rr; r[2] = dx[2] / rr;
+    }
     // sign filter: w = (v - bulk) + (H * dx) / (1 + z), v_r = dot(w, r̂)   (:275-288)
     const TV vv[3] = {v.x, v.y, v.z};
     float wf[3], sc = 0.f;
@@ -423,6 +446,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     const TV *vels = reinterpret_cast<const TV *>(a.vels);
     TD *rhat_out = reinterpret_cast<TD *>(a.rhat_out);
     const TD *rhat_prev = reinterpret_cast<const TD *>(a.rhat_prev);
+    // phase-2 unroll: float64 r̂ trips hold twice the registers (keep 4 waves/SIMD, no spills)
+    constexpr int UNR = sizeof(TD) == 8 ? 1 : UNR2;
     constexpr bool compare = COMPARE;   // template: no frame-only loads in the join loop
     const uint32_t q = (uint32_t)it.bucket, nb = (uint32_t)it.nbuckets;
     STAMP(0);

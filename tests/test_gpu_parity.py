@@ -135,3 +135,43 @@ def test_sharded_hip_engine_matches_reference(name, owner):
     rep = {}
     compare_groups(_groups(got), groups(fix), rep)
     assert rep.get('angle_mismatch', 0) <= ANGLE_MISMATCH_MAX * max(rep.get('angles', 1), 1)
+
+
+@pytest.mark.parametrize('dtype,centre_dtype', [(np.float32, np.float32), (np.float32, np.float64),
+                                                (np.float64, np.float64)])
+def test_frame_state_bits_match_oracle(dtype, centre_dtype):
+    """The carried state itself: r̂ bit-for-bit and sign(v_r) against the oracle's
+    region_frame (track_orbits.py:247-290), on scales from 1e-30 to 1e30 (exercising
+    the float32 reciprocal-division fast path, its IEEE fallback and the float64
+    v_r fallback), plus a particle exactly at the centre (NaN r̂, no sign)."""
+    import torch
+    from orbitanalysis_amd.engine import OrbitEngine, meta_angles  # noqa: F401
+    from oracle import orbit_oracle as O
+    rng = np.random.default_rng(7)
+    nh, per = 6, 40000
+    n = nh * per
+    centres = rng.uniform(-50, 50, (nh, 3)).astype(centre_dtype)
+    scale = 10.0 ** rng.uniform(-30, 30, n)
+    scale[: n // 2] = 10.0 ** rng.uniform(-3, 3, n // 2)
+    dxs = rng.normal(size=(n, 3)) * scale[:, None]
+    x = (np.repeat(centres.astype(np.float64), per, axis=0) + dxs).astype(dtype)
+    x[5] = centres[0]                                        # exactly at the centre
+    v = rng.normal(size=(n, 3)).astype(dtype)
+    bulk = rng.normal(size=(nh, 3)).astype(centre_dtype)
+    snap = {'ids': rng.permutation(n).astype(np.int64), 'coordinates': x, 'velocities': v,
+            'masses': 1.0, 'region_offsets': np.arange(nh) * per, 'redshift': 0.3}
+    H = np.float64(0.07)                   # hubble_parameter returns np.float64
+    eng = OrbitEngine(mode='pericentric')
+    eng.step(snap, centres, bulk, H, snap['redshift'], np.arange(nh), False)
+    rh = eng.prev.rhat.cpu().numpy().reshape(-1, 3)
+    meta = eng.prev.meta.cpu().numpy().view(np.uint32)
+    sgn = (meta >> 16) & 3
+    for j in range(nh):
+        sl = (j * per, (j + 1) * per)
+        r_o, vr_o, _ = O.region_frame(snap, sl, centres[j], bulk[j], H)
+        got = rh[sl[0]:sl[1]]
+        assert got.dtype == r_o.dtype
+        same = (got == r_o) | (np.isnan(got) & np.isnan(r_o))
+        assert same.all(), (j, int((~same).sum()), got[~same.all(1)][:3], r_o[~same.all(1)][:3])
+        want = np.where(vr_o > 0, 1, np.where(vr_o < 0, 2, 0))
+        assert np.array_equal(sgn[sl[0]:sl[1]], want), j
