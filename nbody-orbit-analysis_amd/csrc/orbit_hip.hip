@@ -92,9 +92,6 @@ namespace {
 #ifndef OA_PF1
 #define OA_PF1 1            // phase-1 software prefetch of the next loop trip
 #endif
-#ifndef OA_PF2
-#define OA_PF2 1            // phase-2 software prefetch of the next loop trip
-#endif
 #ifndef OA_HMAX
 #define OA_HMAX 32
 #endif
@@ -706,13 +703,9 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         }
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (OA_PF2) {
-        OA_LOAD2(pid, prh, pmeta, kpos, hlv, 0u)
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(3 * UNR) : "memory");
-    } else {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    }
+    OA_LOAD2(pid, prh, pmeta, kpos, hlv, 0u)
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(3 * UNR) : "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     STAMP(3);
@@ -722,8 +715,12 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         return;
     }
     const bool nonuniform = IDB == 8 && H.nonuniform != 0;
-    for (uint32_t v0 = 0; v0 < n_pv; v0 += WG * UNR) {
-        if (!OA_PF2) { OA_LOAD2(pid, prh, pmeta, kpos, hlv, v0) }
+    // one loop trip; the caller alternates two register sets (ping-pong), so the
+    // prefetched trip never has to be copied into the current one
+    auto trip = [&](ID (&pid)[UNR], V3<TD> (&prh)[UNR], uint32_t (&pmeta)[UNR],
+                    int64_t (&kpos)[UNR], uint32_t (&hlv)[UNR], ID (&pidn)[UNR],
+                    V3<TD> (&prhn)[UNR], uint32_t (&pmetan)[UNR], int64_t (&kposn)[UNR],
+                    uint32_t (&hlvn)[UNR], uint32_t v0) __attribute__((always_inline)) {
         bool ok[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u) ok[u] = v0 + u * WG + tid < n_pv;
@@ -741,13 +738,14 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             if (BUCKETED && bucket_of(lo[u], hi[u], nb) != q) { ok[u] = false; continue; }
             if (IDB == 8 && !nonuniform && hi[u] != hi0) continue;      // cannot be present
             lmin[u] = BUCKETED ? 0u : H.lstart[hlv[u]];
-            lmax[u] = BUCKETED ? 0xFFFFFFFFu : H.lstart[hlv[u] + 1];
+            lmax[u] = BUCKETED ? 0xFFFFFFFFu : H.lstart[hlv[u] + 1] - lmin[u];   // span length
             uint32_t cs[3];
             cuckoo_slots(lo[u], nslots, cs);
             uint64_t c0 = slots[cs[0]], c1 = slots[cs[1]], c2 = slots[cs[2]];
             auto match = [&](uint64_t v) {
                 const uint32_t p = slot_pos(v);
-                bool m = v != 0ull && (uint32_t)v == lo[u] && (BUCKETED || (p >= lmin[u] && p < lmax[u]));
+                // the halo's position range also rejects empty slots (slot_pos(0) = ~0u)
+                bool m = (uint32_t)v == lo[u] && (BUCKETED ? v != 0ull : p - lmin[u] < lmax[u]);
                 if (IDB == 8 && nonuniform && m)        // rare: confirm the full ID
                     m = ids[base + (BUCKETED ? lidx[p] : p)] == pid[u];
                 return m;
@@ -773,7 +771,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             cr[u] = V3<TD>{src[0], src[1], src[2]};
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (OA_PF2) { OA_LOAD2(pidn, prhn, pmetan, kposn, hlvn, v0 + WG * UNR) }  // unconditional
+        OA_LOAD2(pidn, prhn, pmetan, kposn, hlvn, v0 + WG * UNR)   // unconditional
         __builtin_amdgcn_sched_barrier(0);
         bool flag[UNR];
         uint16_t a16[UNR];
@@ -832,13 +830,11 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
         }
         }
-        if (OA_PF2) {
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                pid[u] = pidn[u]; prh[u] = prhn[u]; pmeta[u] = pmetan[u];
-                kpos[u] = kposn[u]; hlv[u] = hlvn[u];
-            }
-        }
+    };
+    for (uint32_t v0 = 0; v0 < n_pv; v0 += 2 * WG * UNR) {
+        trip(pid, prh, pmeta, kpos, hlv, pidn, prhn, pmetan, kposn, hlvn, v0);
+        if (v0 + WG * UNR >= n_pv) break;
+        trip(pidn, prhn, pmetan, kposn, hlvn, pid, prh, pmeta, kpos, hlv, v0 + WG * UNR);
     }
 #undef OA_LOAD2
     if (!BUCKETED && lane == 0) atomicAdd(&H.chunk_total, running);
