@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OA_ABI_VERSION 3
+#define OA_ABI_VERSION 4
 
 #define OA_OK 0
 #define OA_E_ARG (-1)       /* invalid argument / unsupported dtype plan */
@@ -119,6 +119,17 @@ typedef struct oa_step_args {
                                    must be zero on entry                             */
     int32_t *item_count;        /* [n_items] */
     uint32_t *status;           /* device word, OA_STATUS_* bits; zero on entry       */
+    /* on-the-fly driver (track_orbits_onthefly.py:71-205); onthefly = 0: unused.
+     * Frame semantics of that driver: dx stored in the coordinate dtype (r̂ too),
+     * w = v - bulk stored in the velocity dtype, no Hubble term, v_r in
+     * promote(velocity, coordinate) dtype (vr_f64). */
+    int32_t onthefly;
+    int32_t vr_f64;
+    void *angle_out;            /* (n_prev,) coordinate dtype: arccos(r̂_prev . r̂_match)
+                                   of every matched previous particle (:173-174)      */
+    uint8_t *matched_prev;      /* (n_prev,) 1 = matched, 0 = departed (:145-148)     */
+    uint8_t *matched_cur;       /* (n_cur,) set to 1 when matched; zero on entry
+                                   (0 = entered, :168)                                */
 } oa_step_args;
 
 /* Arguments of oa_compact: gather the per-item apsis records into the reference's

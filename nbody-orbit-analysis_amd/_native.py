@@ -13,7 +13,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.abspath(__file__))
 # ORBIT_HIP_LIB selects an alternative build (kernel variants for tuning sweeps)
 LIB_PATH = os.environ.get('ORBIT_HIP_LIB') or os.path.join(PKG, 'liborbit_hip.so')
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -42,7 +42,9 @@ class StepArgs(ctypes.Structure):
                 ('big_slots', c_i32),
                 ('scratch_ids', c_vp), ('scratch_ang', c_vp), ('seg_count', c_vp),
                 ('dense_code', c_vp),
-                ('halo_count', c_vp), ('item_count', c_vp), ('status', c_vp)]
+                ('halo_count', c_vp), ('item_count', c_vp), ('status', c_vp),
+                ('onthefly', c_i32), ('vr_f64', c_i32), ('angle_out', c_vp),
+                ('matched_prev', c_vp), ('matched_cur', c_vp)]
 
 
 class CompactArgs(ctypes.Structure):

@@ -319,6 +319,37 @@ __device__ __forceinline__ TD wrap_add(TD dx, const oa_step_args &a, int d) {
     return a.wrap_f64 ? (TD)((double)dx + a.box[d]) : (TD)((float)dx + (float)a.box[d]);
 }
 
+// rads = sqrt(dot(dx, dx)); r̂ = dx / rads, correctly rounded in TD.
+template <typename TD>
+__device__ __forceinline__ void unit_vector(const TD dx[3], TD r[3]) {
+    TD rr = sqrt(dot3(dx[0], dx[1], dx[2], dx[0], dx[1], dx[2]));
+    if constexpr (std::is_same<TD, float>::value) {
+        // Correctly rounded float32 quotients from ONE float64 reciprocal: with
+        // y = 1/rr to 2^-52 (v_rcp_f64 + two Newton steps), q = dx * y is within
+        // 2^-51 (relative) of dx / rr, while a quotient of two floats is never closer
+        // than 2^-50 to a float32 rounding midpoint (DESIGN.md §5) -- so rounding q to
+        // float32 gives RN(dx / rr) exactly.  Valid for normal quotients and a normal
+        // rr; any other wave takes the IEEE division.
+        bool fast = rr >= 0x1p-100f && rr <= 0x1p100f;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) fast = fast && (dx[d] == 0.f || fabsf(dx[d]) >= rr * 0x1p-100f);
+        if (__all(fast)) {
+            const double b = (double)rr;
+            double y = __builtin_amdgcn_rcp(b);
+            double e = __builtin_fma(-b, y, 1.0);
+            y = __builtin_fma(y, e, y);
+            e = __builtin_fma(-b, y, 1.0);
+            y = __builtin_fma(y, e, y);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) r[d] = (TD)((double)dx[d] * y);
+        } else {
+            r[0] = dx[0] / rr; r[1] = dx[1] / rr; r[2] = dx[2] / rr;
+        }
+    } else {
+        r[0] = dx[0] / rr; r[1] = dx[1] / rr; r[2] = dx[2] / rr;
+    }
+}
+
 // The reference's exact float64 v_r (track_orbits.py:275-288) from r̂ and dx.
 template <typename TV, typename TD>
 __device__ __forceinline__ double vr_exact(const TD dx[3], const TV vv[3], const double *cb,
@@ -352,32 +383,7 @@ __device__ __forceinline__ uint32_t frame(const V3<TX> &x, const V3<TV> &v, cons
         if (__any(l)) { if (l) dx[d] = wrap_add(dx[d], a, d); }
     }
     // rads = sqrt(dot(dx, dx)); rhats = dx / rads   (:286-287), exact in dx's dtype
-    TD rr = sqrt(dot3(dx[0], dx[1], dx[2], dx[0], dx[1], dx[2]));
-    if constexpr (std::is_same<TD, float>::value) {
-        // Correctly rounded float32 quotients from ONE float64 reciprocal: with
-        // y = 1/rr to 2^-52 (v_rcp_f64 + two Newton steps), q = dx * y is within
-        // 2^-51 (relative) of dx / rr, while a quotient of two floats is never closer
-        // than 2^-50 to a float32 rounding midpoint (DESIGN.md §5) -- so rounding q to
-        // float32 gives RN(dx / rr) exactly.  Valid for normal quotients and a normal
-        // rr; any other wave takes the IEEE division.
-        bool fast = rr >= 0x1p-100f && rr <= 0x1p100f;
-#pragma unroll
-        for (int d = 0; d < 3; ++d) fast = fast && (dx[d] == 0.f || fabsf(dx[d]) >= rr * 0x1p-100f);
-        if (__all(fast)) {
-            const double b = (double)rr;
-            double y = __builtin_amdgcn_rcp(b);
-            double e = __builtin_fma(-b, y, 1.0);
-            y = __builtin_fma(y, e, y);
-            e = __builtin_fma(-b, y, 1.0);
-            y = __builtin_fma(y, e, y);
-#pragma unroll
-            for (int d = 0; d < 3; ++d) r[d] = (TD)((double)dx[d] * y);
-        } else {
-            r[0] = dx[0] / rr; r[1] = dx[1] / rr; r[2] = dx[2] / rr;
-        }
-    } else {
-        r[0] = dx[0] / rr; r[1] = dx[1] / rr; r[2] = dx[2] / rr;
-    }
+    unit_vector(dx, r);
     // sign filter: w = (v - bulk) + (H * dx) / (1 + z), v_r = dot(w, r̂)   (:275-288)
     const TV vv[3] = {v.x, v.y, v.z};
     float wf[3], sc = 0.f;
@@ -400,6 +406,48 @@ __device__ __forceinline__ uint32_t frame(const V3<TX> &x, const V3<TV> &v, cons
     return sgn;
 }
 
+// region_frame of the on-the-fly driver (track_orbits_onthefly.py:71-120) for one
+// particle: dx = recenter(x - c) in the promoted dtype of (x, c, box), stored in the
+// coordinate dtype TD (:82-91); w = v - bulk stored in the velocity dtype (:93-110);
+// no Hubble term; v_r = dot(w, r̂) in promote(TV, TD) (:112-114), evaluated exactly.
+template <typename TX, typename TV, typename TD>
+__device__ __forceinline__ uint32_t frame_otf(const V3<TX> &x, const V3<TV> &v, const double *cb,
+                                              const oa_step_args &a, const FrameK &k, TD r[3]) {
+    const TX xs[3] = {x.x, x.y, x.z};
+    TD dx[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        if (a.dx_f64) {
+            double t = (double)xs[d] - cb[d];
+            if (d < a.n_box_dims) {
+                if (t > a.box[d] / 2) t = t - a.box[d];
+                if (t < -(a.box[d] / 2)) t = t + a.box[d];
+            }
+            dx[d] = (TD)t;
+        } else {
+            float t = (float)xs[d] - (float)cb[d];
+            if (d < a.n_box_dims) {
+                if (t >= k.wrap_hi[d]) t = wrap_sub(t, a, d);
+                if (t <= k.wrap_lo[d]) t = wrap_add(t, a, d);
+            }
+            dx[d] = (TD)t;
+        }
+    }
+    unit_vector(dx, r);
+    const TV vs[3] = {v.x, v.y, v.z};
+    TV w[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+        w[d] = a.vb_f64 ? (TV)((double)vs[d] - cb[3 + d]) : (TV)((float)vs[d] - (float)cb[3 + d]);
+    if (a.vr_f64) {
+        const double vr = dot3((double)w[0], (double)w[1], (double)w[2],
+                               (double)r[0], (double)r[1], (double)r[2]);
+        return vr > 0.0 ? 1u : (vr < 0.0 ? 2u : 0u);
+    }
+    const float vr = dot3((float)w[0], (float)w[1], (float)w[2], (float)r[0], (float)r[1], (float)r[2]);
+    return vr > 0.f ? 1u : (vr < 0.f ? 2u : 0u);
+}
+
 // ------------------------------------------------------------------ step kernel
 // LDS image of one item (after the ItemHdr):
 //   slots[S]  u64  open-addressing table of the item's current particles that have a
@@ -420,7 +468,7 @@ __device__ __forceinline__ uint32_t slot_meta(uint64_t v) {
     return (uint32_t)(v >> 32) & ((1u << POS_SHIFT) - 1u);
 }
 
-template <typename TX, typename TV, typename TD, int IDB, bool BUCKETED, bool COMPARE>
+template <typename TX, typename TV, typename TD, int IDB, bool BUCKETED, bool COMPARE, bool OTF>
 __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK fk) {
     typedef typename IdT<IDB>::T ID;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -546,7 +594,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                 r[0] = (TD)xv[u].x - (TD)H.cb[hl][0]; r[1] = (TD)xv[u].y; r[2] = (TD)vv[u].z;
                 sgn = 1u;
             } else {
-                sgn = frame<TX, TV, TD>(xv[u], vv[u], H.cb[hl], a, fk, r);
+                sgn = OTF ? frame_otf<TX, TV, TD>(xv[u], vv[u], H.cb[hl], a, fk, r)
+                          : frame<TX, TV, TD>(xv[u], vv[u], H.cb[hl], a, fk, r);
             }
             TD *ro = rhat_out + 3 * (base + li);
             if (!OA_ABL_STORE1) { ro[0] = r[0]; ro[1] = r[1]; ro[2] = r[2]; }
@@ -786,7 +835,15 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                                                             : (sp == 1u && sc == 2u);
             // angle change = arccos(dot(r̂_prev, r̂_match)), no clamp (:324-325)
             TD dt = dot3(prh[u].x, prh[u].y, prh[u].z, cr[u].x, cr[u].y, cr[u].z);
-            uint16_t acc = angle_add((uint16_t)(pmeta[u] & 0xFFFFu), OA_ABL_ACOS ? dt : acos_td(dt));
+            const TD change = OA_ABL_ACOS ? dt : acos_td(dt);
+            uint16_t acc = angle_add((uint16_t)(pmeta[u] & 0xFFFFu), change);
+            if (OTF) {
+                // on-the-fly outputs (track_orbits_onthefly.py:145-174): the angle
+                // change of every matched particle, and which current ones matched
+                static_cast<TD *>(a.angle_out)[kpos[u]] = change;
+                const uint32_t p = slot_pos(hit[u]);
+                a.matched_cur[base + (BUCKETED ? lidx[p] : p)] = 1;
+            }
             // calc_angles (:342-349): apsis angle emitted, then reset to 0
             if (!OA_ABL_SLOTW) {
                 uint64_t *sp_ = hs[u] < nslots ? &slots[hs[u]] : &H.stash[hs[u] - nslots];
@@ -794,6 +851,11 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
             flag[u] = cond;
             a16[u] = acc;
+        }
+        if (OTF) {
+#pragma unroll
+            for (int u = 0; u < UNR; ++u)
+                if (ok[u]) a.matched_prev[kpos[u]] = hit[u] ? 1 : 0;
         }
         if (BUCKETED) {
             // dense per-previous-position code; order restored by k_gather_dense
@@ -1109,18 +1171,18 @@ int set_lds(K kernel, int64_t bytes) {
     return OA_OK;
 }
 
-template <typename TX, typename TV, typename TD, int IDB, bool COMPARE>
+template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
 int launch_step_c(const oa_step_args &a, hipStream_t st) {
     if (a.n_items > 0) {
         int64_t lds = HDR_BYTES + table_bytes(a.lds_entries, a.lds_slots, false);
-        auto k = k_step<TX, TV, TD, IDB, false, COMPARE>;
+        auto k = k_step<TX, TV, TD, IDB, false, COMPARE, OTF>;
         if (int rc = set_lds(k, lds)) return rc;
         hipLaunchKernelGGL(k, dim3(a.n_items), dim3(WG), (size_t)lds, st, a, make_frame_k(a));
         if (int rc = check_launch("k_step")) return rc;
     }
     if (a.n_big_items > 0) {
         int64_t lds = HDR_BYTES + table_bytes(a.big_entries, a.big_slots, true);
-        auto k = k_step<TX, TV, TD, IDB, true, COMPARE>;
+        auto k = k_step<TX, TV, TD, IDB, true, COMPARE, OTF>;
         if (int rc = set_lds(k, lds)) return rc;
         hipLaunchKernelGGL(k, dim3(a.n_big_items), dim3(WG), (size_t)lds, st, a, make_frame_k(a));
         if (int rc = check_launch("k_step(bucketed)")) return rc;
@@ -1130,8 +1192,13 @@ int launch_step_c(const oa_step_args &a, hipStream_t st) {
 
 template <typename TX, typename TV, typename TD, int IDB>
 int launch_step(const oa_step_args &a, hipStream_t st) {
-    return a.compare ? launch_step_c<TX, TV, TD, IDB, true>(a, st)
-                     : launch_step_c<TX, TV, TD, IDB, false>(a, st);
+    if constexpr (std::is_same<TX, TD>::value) {    // on-the-fly: r̂ in the coordinate dtype
+        if (a.onthefly)
+            return a.compare ? launch_step_c<TX, TV, TD, IDB, true, true>(a, st)
+                             : launch_step_c<TX, TV, TD, IDB, false, true>(a, st);
+    }
+    return a.compare ? launch_step_c<TX, TV, TD, IDB, true, false>(a, st)
+                     : launch_step_c<TX, TV, TD, IDB, false, false>(a, st);
 }
 
 template <typename TX, typename TV, typename TD>
@@ -1223,7 +1290,11 @@ int oa_step(const oa_step_args *args, void *stream) {
                                          !a.seg_count)) ||
                       (a.n_big_items > 0 && !a.dense_code)))
         return fail(OA_E_ARG, "null previous-state / scratch pointer");
+    if (a.onthefly && a.compare && (!a.angle_out || !a.matched_prev || !a.matched_cur))
+        return fail(OA_E_ARG, "null on-the-fly output pointer");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (a.onthefly)
+        return a.coord_f64 ? launch_step_v<double, double>(a, st) : launch_step_v<float, float>(a, st);
     if (a.dx_f64) {
         return a.coord_f64 ? launch_step_v<double, double>(a, st)
                            : launch_step_v<float, double>(a, st);

@@ -41,6 +41,12 @@ class MemorySavefile:
     def read_checkpoint(self):
         return self.checkpoint
 
+    def write_file(self, snapshot_number, datasets, attrs):
+        """On-the-fly driver: one 'file' per snapshot (track_orbits_onthefly.py:229)."""
+        self.files = getattr(self, 'files', {})
+        self.files[int(snapshot_number)] = ({k: np.asarray(v) for k, v in datasets.items()},
+                                            dict(attrs))
+
 
 class HDF5Savefile:
     def __init__(self, path):

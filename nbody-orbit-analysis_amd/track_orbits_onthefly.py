@@ -1,0 +1,242 @@
+"""Drop-in on-the-fly driver: ``track_orbits`` of orbitanalysis/track_orbits_onthefly.py.
+
+One call compares snapshot ``s`` with ``s - 1`` through ``progenitor_links`` (2, n)
+(row 0: halos at s, row 1: their progenitors at s - 1, -1 = absent) and writes one
+file per snapshot (``savefile.format('%0.3d' % s)``) with the reference's datasets
+(track_orbits_onthefly.py:208-252):
+
+    {peri|apo}center_offsets / _IDs  (key ``mode[:8] + 'er'``: apocentric ->
+                                      'apocentrer', the reference's spelling)
+    angles                           arccos(r̂_prev . r̂) of every matched particle
+    entered_offsets / entered_IDs    setdiff1d(current, previous) per halo
+    departed_offsets / departed_IDs  setdiff1d(previous, current) per halo
+    progenitor_links, region_radii, region_positions, bulk_velocities, attr box_size
+
+Both frames and the join run on the device (``OrbitEngine`` in on-the-fly mode:
+r̂ in the coordinate dtype, no Hubble term, v_r in promote(velocity, coordinate);
+track_orbits_onthefly.py:71-120).  The per-halo entered / departed lists are
+compacted and sorted on the device from the kernel's match flags.
+"""
+import time
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .engine import OrbitEngine, SnapshotState, Workspace, to_device, F64
+
+_TORCH = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64}
+
+
+def repack(arr, length, inds):
+    """track_orbits_onthefly.py:61-68: rows of absent halos filled with -1."""
+    arr = np.asarray(arr)
+    shape = list(np.shape(arr))
+    shape[0] = length
+    out = -np.ones(tuple(shape), dtype=arr.dtype)
+    out[inds] = arr
+    return out
+
+
+def _block_starts(slices, n):
+    """Repacked (start, end) rows (-1, -1 = absent) -> non-decreasing block starts that
+    tile [0, n) (an absent halo gets an empty block)."""
+    starts = np.empty(len(slices), dtype=np.int64)
+    pos = 0
+    for j, (a, b) in enumerate(np.asarray(slices, dtype=np.int64)):
+        if a >= 0:
+            if a < pos:
+                raise ValueError('region blocks must follow halo order')
+            starts[j], pos = a, b
+        else:
+            starts[j] = pos
+    return starts
+
+
+def _sort_key(ids_t, unsigned):
+    k = ids_t.to(torch.int64)
+    if unsigned:
+        k = (k & 0xFFFFFFFF) if ids_t.dtype == torch.int32 else k ^ (-(1 << 63))
+    return k
+
+
+def _grouped(values, halo, key, n):
+    """Stable (halo, key) ordering of the rows; returns (values, offsets)."""
+    if values.numel() == 0:
+        return values, np.zeros(n + 1, dtype=np.int64)
+    o1 = torch.argsort(key, stable=True)
+    o2 = torch.argsort(halo[o1], stable=True)
+    order = o1[o2]
+    counts = torch.bincount(halo, minlength=n).cpu().numpy()
+    return values[order], np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+
+
+class OnTheFly:
+    """Pairwise (s, s-1) device pipeline on top of an ``OrbitEngine``."""
+
+    def __init__(self, engine=None, mode='pericentric'):
+        self.eng = engine if engine is not None else OrbitEngine(mode=mode)
+        self.mode = self.eng.mode
+
+    def _prepare(self, snap, slices, centres, compare, prev=None, entries=None):
+        eng = self.eng
+        n = len(snap['ids'])
+        s = dict(snap)
+        s['region_offsets'] = _block_starts(slices, n)
+        dev = {k: to_device(snap[k], eng.device) for k in ('ids', 'coordinates', 'velocities')}
+        dsnap = dict(s)
+        dsnap.update(dev)
+        if isinstance(snap['masses'], np.ndarray):
+            dsnap['masses'] = to_device(snap['masses'], eng.device)
+        nh = len(slices)
+        layout = None
+        if compare:
+            layout = (prev.starts, prev.counts, prev.exists, prev.plan, prev.ids.numel())
+        pr = eng.prepare(dsnap, centres, None, np.float64(0.0), 0.0, np.arange(nh), compare,
+                         plan_src=s, prev_layout=layout, entries=entries)
+        plan = pr.plan
+        coord = np.dtype(plan.coord)
+        # on-the-fly frame: r̂ stored in the coordinate dtype (:82-83, 112-113)
+        pr.rhat = torch.empty(3 * n, dtype=_TORCH[coord], device=eng.device)
+        a = pr.args
+        a.rhat_out = pr.rhat.data_ptr()
+        a.onthefly = 1
+        a.vr_f64 = int(np.result_type(plan.vel, coord) == F64)
+        return pr
+
+    def run(self, snaps, slices, centres):
+        """snaps / slices / centres: [current, previous].  Returns host outputs."""
+        eng = self.eng
+        cur, prv = snaps
+        if np.dtype(cur['coordinates'].dtype) != np.dtype(prv['coordinates'].dtype):
+            raise NotImplementedError('coordinate dtype differs between the two snapshots')
+        # previous snapshot: frame only
+        pp = self._prepare(prv, slices[1], centres[1], False)
+        eng.launch(pp, None)
+        prev = SnapshotState(ids=pp.snap['ids'], rhat=pp.rhat, meta=pp.meta, starts=pp.starts,
+                             counts=pp.counts, exists=np.arange(len(slices[1])), plan=pp.plan)
+        n_prev = prev.ids.numel()
+        entries = None
+        for _ in range(8):
+            pc = self._prepare(cur, slices[0], centres[0], True, prev=prev, entries=entries)
+            coord = _TORCH[np.dtype(pc.plan.coord)]
+            angle_out = torch.empty(max(n_prev, 1), dtype=coord, device=eng.device)
+            matched_prev = torch.zeros(max(n_prev, 1), dtype=torch.uint8, device=eng.device)
+            matched_cur = torch.zeros(max(pc.n, 1), dtype=torch.uint8, device=eng.device)
+            a = pc.args
+            a.angle_out, a.matched_prev, a.matched_cur = (angle_out.data_ptr(),
+                                                          matched_prev.data_ptr(),
+                                                          matched_cur.data_ptr())
+            ws = Workspace.for_step(pc, eng.device)
+            ws.status.zero_()
+            res = eng.launch(pc, ws, prev=prev)
+            st = int(ws.status.item())
+            if not st:
+                break
+            if st & N.STATUS_TABLE_OVERFLOW or st & N.STATUS_BUCKET_OVERFLOW:
+                entries = max(256, (entries or eng.entries) // 2)
+        else:
+            raise RuntimeError('LDS hash tables kept overflowing (adversarial IDs?)')
+        nh = len(slices[0])
+        ids_dtype = np.dtype(cur['ids'].dtype)
+        unsigned = ids_dtype.kind == 'u'
+        # apsis records per halo, previous-block order (:154-166)
+        offsets, apsis_ids, _ = eng.fetch(res, ids_dtype)
+        # angle changes of every matched particle, previous-block order (:173-174)
+        mp = matched_prev[:n_prev].bool()
+        angles = angle_out[:n_prev][mp].cpu().numpy()
+        p_has = pc.halos.cpu().numpy().view(N.HALO_DTYPE)['prev_cnt'] > 0
+        # departed: previous particles without a match, sorted per halo (:145)
+        pcnt = torch.from_numpy(prev.counts).to(eng.device)
+        ph = torch.repeat_interleave(torch.arange(nh, device=eng.device), pcnt)
+        dsel = torch.nonzero(~mp).squeeze(1)
+        d_ids = prev.ids[dsel]
+        departed, d_off = _grouped(d_ids, ph[dsel], _sort_key(d_ids, unsigned), nh)
+        # entered: current particles without a match, sorted per halo (:168); all of
+        # a halo's particles, in loader order, when its progenitor block is empty (:178)
+        ccnt = torch.from_numpy(pc.counts).to(eng.device)
+        ch = torch.repeat_interleave(torch.arange(nh, device=eng.device), ccnt)
+        esel = torch.nonzero(matched_cur[:pc.n] == 0).squeeze(1)
+        e_ids = pc.snap['ids'][esel]
+        sorted_h = torch.from_numpy(p_has).to(eng.device)[ch[esel]]
+        key = torch.where(sorted_h, _sort_key(e_ids, unsigned), esel.to(torch.int64))
+        entered, e_off = _grouped(e_ids, ch[esel], key, nh)
+        # concatenation dtype of the reference's per-halo lists (:183, :203): an empty
+        # halo contributes np.array([], dtype=ids.dtype)
+        parts = [np.zeros(0, np.dtype(pc.plan.coord))] * int(p_has.sum()) + \
+                [np.zeros(0, ids_dtype)] * int((~p_has).sum())
+        adt = np.concatenate(parts).dtype if parts else np.dtype(np.float64)
+
+        def host_ids(t):
+            return t.cpu().numpy().view(ids_dtype) if t.numel() else np.zeros(0, ids_dtype)
+
+        bulk_c = pc.halos.cpu().numpy().view(N.HALO_DTYPE)['bulk'].astype(pc.plan.bulk)
+        bulk_p = pp.halos.cpu().numpy().view(N.HALO_DTYPE)['bulk'].astype(pp.plan.bulk)
+        return {'apsis_offsets': offsets, 'apsis_ids': apsis_ids,
+                'angles': angles.astype(adt),
+                'entered_offsets': e_off, 'entered_ids': host_ids(entered),
+                'departed_offsets': d_off, 'departed_ids': host_ids(departed),
+                'bulk_velocities': [bulk_c, bulk_p]}
+
+
+def track_orbits(snapshot_number, progenitor_links, regions, load_snapshot_data,
+                 savefile, mode='pericentric', verbose=True, engine=None):
+    """track_orbits_onthefly.py:8-58 (signature, callbacks and errors of the reference;
+    ``engine`` optionally supplies a configured ``OrbitEngine``)."""
+    if (mode != 'pericentric') and (mode != 'apocentric'):
+        raise ValueError(
+            "Orbit detection mode not recognized. Please specify either "
+            "'pericentric' or 'apocentric'.")
+    progenitor_links = np.asarray(progenitor_links)
+    snaps, slices, positions, radii = [], [], [], []
+    box_size = None
+    for s, halo_ids_ in zip([snapshot_number, snapshot_number - 1], progenitor_links):
+        halo_exists = np.argwhere(halo_ids_ != -1).flatten()
+        halo_ids = halo_ids_[halo_exists]
+        region_pos, region_rad = regions(s, halo_ids)
+        positions.append(repack(region_pos, len(halo_ids_), halo_exists))
+        radii.append(repack(region_rad, len(halo_ids_), halo_exists))
+        snapshot = load_snapshot_data(s, region_pos, region_rad)
+        snaps.append(snapshot)
+        offsets = list(snapshot['region_offsets']) + [len(snapshot['ids'])]
+        sl = np.array(list(zip(offsets[:-1], offsets[1:])))
+        slices.append(repack(sl, len(halo_ids_), halo_exists))
+        box_size = snapshot['box_size'] if 'box_size' in snapshot else None
+    if verbose:
+        print('Identifying {}ers...'.format(mode[:8]))
+        t0 = time.time()
+    otf = OnTheFly(engine, mode)
+    if otf.mode != mode:
+        raise ValueError('engine mode %r != mode %r' % (otf.mode, mode))
+    out = otf.run(snaps, slices, positions)
+    if verbose:
+        print('Identified {}ers in {} s\n'.format(mode[:8], time.time() - t0))
+    tag = mode[:8] + 'er'
+    data = {tag + '_offsets': out['apsis_offsets'], tag + '_IDs': out['apsis_ids'],
+            'angles': out['angles'],
+            'entered_offsets': out['entered_offsets'], 'entered_IDs': out['entered_ids'],
+            'departed_offsets': out['departed_offsets'], 'departed_IDs': out['departed_ids'],
+            'progenitor_links': progenitor_links, 'region_radii': np.array(radii),
+            'region_positions': np.array(positions),
+            'bulk_velocities': np.array(out['bulk_velocities'])}
+    attrs = {} if box_size is None else {'box_size': box_size}
+    save_to_file(savefile, snapshot_number, data, attrs, verbose)
+    return data
+
+
+def save_to_file(savefile, snapshot_number, data, attrs, verbose):
+    """track_orbits_onthefly.py:208-252: one file per snapshot."""
+    if verbose:
+        print('Saving to file...')
+        t0 = time.time()
+    if isinstance(savefile, str):
+        import h5py
+        with h5py.File(savefile.format('%0.3d' % snapshot_number), 'w') as hf:
+            for k, v in data.items():
+                hf.create_dataset(k, data=v)
+            for k, v in attrs.items():
+                hf.attrs[k] = v
+    else:
+        savefile.write_file(snapshot_number, data, attrs)
+    if verbose:
+        print('Saved to file in {} s\n'.format(time.time() - t0))

@@ -175,3 +175,38 @@ def test_frame_state_bits_match_oracle(dtype, centre_dtype):
         assert same.all(), (j, int((~same).sum()), got[~same.all(1)][:3], r_o[~same.all(1)][:3])
         want = np.where(vr_o > 0, 1, np.where(vr_o < 0, 2, 0))
         assert np.array_equal(sgn[sl[0]:sl[1]], want), j
+
+
+@pytest.mark.parametrize('name', ['g6_onthefly', 'g6b_onthefly_f32', 'g6c_onthefly_f32_c64'])
+@pytest.mark.parametrize('mode', ['pericentric', 'apocentric'])
+def test_onthefly_matches_reference_golden(name, mode):
+    """On-the-fly driver (track_orbits_onthefly.py) on the device vs the reference's
+    files: IDs, offsets, radii, positions, bulk velocities bit-exact; the float
+    angle changes within 2 ulp of their dtype (numpy's arccos is not correctly
+    rounded), NaN where the reference has NaN."""
+    from orbitanalysis_amd.track_orbits_onthefly import track_orbits as otf
+    from orbitanalysis_amd.savefile import MemorySavefile
+    fix = load(name)
+    u, meta = universe(fix)
+    s = meta.get('snapshot', 5)
+    out = MemorySavefile()
+    otf(s, fix['links'], u.regions, u.load_snapshot_data, out, mode=mode, verbose=False)
+    data, attrs = out.files[s]
+    keys = [k for k in fix.files if k.startswith(mode + '/')]
+    want = {k.split('/', 1)[1]: fix[k] for k in keys}
+    if 'attr_box_size' in want:
+        assert np.array_equal(np.asarray(attrs['box_size']), want.pop('attr_box_size'))
+    assert sorted(data) == sorted(want), (sorted(data), sorted(want))
+    for k, w in want.items():
+        v = np.asarray(data[k])
+        assert v.dtype == w.dtype and v.shape == w.shape, (k, v.dtype, w.dtype, v.shape, w.shape)
+        if k == 'angles':
+            nan = np.isnan(w)
+            assert np.array_equal(np.isnan(v), nan), k
+            cd = np.dtype(meta['gen'].get('dtype', 'float64'))    # arccos computed in
+            ulp = np.spacing(np.abs(w[~nan]).astype(cd)).astype(np.float64)   # r̂'s dtype
+            assert np.all(np.abs(v[~nan].astype(np.float64) - w[~nan]) <= 2 * ulp), k
+        elif w.dtype.kind == 'f':
+            assert np.array_equal(v, w, equal_nan=True), k
+        else:
+            assert np.array_equal(v, w), k

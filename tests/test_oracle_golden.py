@@ -38,14 +38,19 @@ def test_resume_matches_reference(name):
     assert_groups_equal(rec.groups, groups(fix, 'resume/'))
 
 
-def test_onthefly_matches_reference():
-    fix = load('g6_onthefly')
+ONTHEFLY = ['g6_onthefly', 'g6b_onthefly_f32', 'g6c_onthefly_f32_c64']
+
+
+@pytest.mark.parametrize('name', ONTHEFLY)
+def test_onthefly_matches_reference(name):
+    fix = load(name)
     u, meta = universe(fix)
     for mode in ('pericentric', 'apocentric'):
-        got = O.onthefly_track_orbits(5, fix['links'], u.regions, u.load_snapshot_data, mode)
-        for k in fix.files:
-            if not k.startswith(mode + '/'):
-                continue
+        got = O.onthefly_track_orbits(meta.get('snapshot', 5), fix['links'], u.regions,
+                                      u.load_snapshot_data, mode)
+        keys = [k for k in fix.files if k.startswith(mode + '/')]
+        assert sorted(k.split('/', 1)[1] for k in keys) == sorted(got), (mode, sorted(got))
+        for k in keys:
             d = k.split('/', 1)[1]
             assert_same(np.asarray(got[d]), fix[k], mode + '/' + d)
 

@@ -182,23 +182,53 @@ def run_batch(name, case, syn, T):
     return out
 
 
-def run_onthefly(syn, O):
+ONTHEFLY_CASES = {
+    # float64, periodic box, a halo whose progenitor is absent
+    'g6_onthefly': dict(
+        gen=dict(n_halos=3, n_per_halo=[900, 700, 500], n_snapshots=7, seed=7, dt=0.5,
+                 box_size=40.0, centres=[[5.0, 5.0, 5.0], [20.0, 20.0, 20.0], [39.0, 1.0, 20.0]],
+                 region_returns=2),
+        links=[[0, 1, 2], [0, -1, 2]], snapshot=5),
+    # float32 data and centres, float32 mass array, int32 IDs, no box, an absent
+    # current halo and an overlapping pair of regions
+    'g6b_onthefly_f32': dict(
+        gen=dict(n_halos=4, n_per_halo=[1200, 800, 600, 400], n_snapshots=4, seed=17, dt=0.5,
+                 dtype='float32', centre_dtype='float32', masses='array', id_dtype='int32',
+                 centres=[[0.0, 0.0, 0.0], [2.0, 1.0, 0.0], [30.0, 30.0, 30.0], [-30.0, 5.0, 5.0]],
+                 region_returns=2),
+        links=[[0, 1, 2, -1], [0, 1, -1, 3]], snapshot=2),
+    # float32 data with float64 centres (dx promoted, stored float32), list box,
+    # uint64 IDs past 2^63
+    'g6c_onthefly_f32_c64': dict(
+        gen=dict(n_halos=3, n_per_halo=[1000, 700, 900], n_snapshots=4, seed=27, dt=0.5,
+                 dtype='float32', centre_dtype='float64', box_size=[60.0, 70.0, 80.0],
+                 id_dtype='uint64', id_offset=2 ** 63 + 11,
+                 centres=[[1.0, 1.0, 1.0], [30.0, 69.0, 40.0], [59.5, 35.0, 79.0]],
+                 region_returns=2),
+        links=[[0, 1, 2], [0, 1, 2]], snapshot=3),
+}
+
+
+def run_onthefly(syn, O, case):
     out = {}
-    gen = dict(n_halos=3, n_per_halo=[900, 700, 500], n_snapshots=7, seed=7, dt=0.5,
-               box_size=40.0, centres=[[5.0, 5.0, 5.0], [20.0, 20.0, 20.0], [39.0, 1.0, 20.0]],
-               region_returns=2)
-    u = syn.PlummerSnapshots(**gen)
-    out['meta_json'] = np.array(json.dumps({'gen': gen}))
+    g = dict(case['gen'])
+    for k in ('dtype', 'centre_dtype', 'id_dtype'):
+        if k in g:
+            g[k] = np.dtype(g[k])
+    u = syn.PlummerSnapshots(**g)
+    out['meta_json'] = np.array(json.dumps({'gen': case['gen'], 'snapshot': case['snapshot']}))
     out['input_sha256'] = np.array(u.input_digest())
-    links = np.array([[0, 1, 2], [0, -1, 2]])
+    links = np.array(case['links'])
+    s = case['snapshot']
     for mode in ('pericentric', 'apocentric'):
-        path = '/mem/otf_%s_{}.hdf5' % mode
-        O.track_orbits(5, links, u.regions, u.load_snapshot_data, path, mode=mode,
+        path = '/mem/otf_%s_%d_{}.hdf5' % (mode, id(case))
+        O.track_orbits(s, links, u.regions, u.load_snapshot_data, path, mode=mode,
                        verbose=False)
-        f = FILES[path.format('%0.3d' % 5)]
+        f = FILES[path.format('%0.3d' % s)]
         for dname, arr in f.items():
             out['%s/%s' % (mode, dname)] = arr
-        out['%s/attr_box_size' % mode] = np.array(f.attrs['box_size'])
+        if 'box_size' in f.attrs:
+            out['%s/attr_box_size' % mode] = np.array(f.attrs['box_size'])
     out['links'] = links
     return out
 
@@ -287,14 +317,21 @@ def main():
     import orbitanalysis.utils as U
     syn = load_synthetic()
     os.makedirs(OUT, exist_ok=True)
+    only = set(sys.argv[1:])          # optional: regenerate just the named fixtures
     for name, case in BATCH_CASES.items():
+        if only and name not in only:
+            continue
         out = run_batch(name, case, syn, T)
         np.savez_compressed(os.path.join(OUT, name + '.npz'), **out)
         print('wrote', name, len(out), 'arrays')
-    np.savez_compressed(os.path.join(OUT, 'g6_onthefly.npz'), **run_onthefly(syn, O))
-    print('wrote g6_onthefly')
-    np.savez_compressed(os.path.join(OUT, 'g7_functions.npz'), **run_functions(T, U))
-    print('wrote g7_functions')
+    for name, case in ONTHEFLY_CASES.items():
+        if only and name not in only:
+            continue
+        np.savez_compressed(os.path.join(OUT, name + '.npz'), **run_onthefly(syn, O, case))
+        print('wrote', name)
+    if not only or 'g7_functions' in only:
+        np.savez_compressed(os.path.join(OUT, 'g7_functions.npz'), **run_functions(T, U))
+        print('wrote g7_functions')
 
 
 if __name__ == '__main__':
