@@ -96,18 +96,33 @@ def main():
     ap.add_argument('--max-snapshots', type=int, default=16)
     ap.add_argument('--cpu-halos', type=int, default=1500)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--backend', default='nccl',
+                    help="collective backend for N > 1 ('gloo': rehearsal with several "
+                         "ranks on one GPU; collectives go through host memory)")
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     import torch
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     dist = None
+    gloo = args.backend == 'gloo'
+    cdev = torch.device('cpu') if gloo else dev           # where collective tensors live
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group('nccl', device_id=dev)
+        if gloo:
+            dist.init_process_group('gloo')
+        else:
+            dist.init_process_group('nccl', device_id=dev)
+
+    def barrier():
+        if gloo:
+            dist.barrier()
+        else:
+            dist.barrier(device_ids=[local])
 
     import orbitanalysis_amd  # noqa: F401
     from orbitanalysis_amd import _native
@@ -151,14 +166,14 @@ def main():
     nl = -(-args.halos // world)
     cat_local, cat_all = [], None
     if world > 1:
-        cat_all = torch.empty(nl * world, 6, dtype=torch.float64, device=dev)
+        cat_all = torch.empty(nl * world, 6, dtype=torch.float64, device=cdev)
         for pr in preps:
             hv = pr.halos.view(torch.float64).view(args.halos, 12)
             rows = torch.zeros(nl, 6, dtype=torch.float64, device=dev)
             lo, hi = rank * nl, min((rank + 1) * nl, args.halos)
             if hi > lo:
                 rows[:hi - lo] = hv[lo:hi, 4:10]
-            cat_local.append(rows)
+            cat_local.append(rows.to(cdev))
     log('setup %.1f s; items/step %d, big %d' % (time.perf_counter() - t_setup,
                                                   len(preps[0].items), len(preps[0].big)))
 
@@ -170,29 +185,30 @@ def main():
         prev_pr, ps = chain[k]
         if world > 1:
             dist.all_gather_into_tensor(cat_all, cat_local[k])
-            pr.halos.view(torch.float64).view(args.halos, 12)[:, 4:10] = cat_all[:args.halos]
+            pr.halos.view(torch.float64).view(args.halos, 12)[:, 4:10] = \
+                cat_all[:args.halos].to(dev, non_blocking=True)
         eng.launch(pr, ws, State(snaps[ps]['ids'], prev_pr.rhat, prev_pr.meta), step_events=events)
 
     for k in range(args.warmup):
         run(k)
     torch.cuda.synchronize()
     if dist:
-        dist.barrier(device_ids=[local])
+        barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         run(args.warmup + i, evs[i])
     torch.cuda.synchronize()
     if dist:
-        dist.barrier(device_ids=[local])
+        barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     units = sum(chain[args.warmup + i + 1][0].n for i in range(args.steps))
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        u = torch.tensor([units], dtype=torch.float64, device=dev)
+        u = torch.tensor([units], dtype=torch.float64, device=cdev)
         dist.all_reduce(u, op=dist.ReduceOp.SUM)
         units = float(u.item())
     status = int(ws.status.item())
@@ -212,7 +228,11 @@ def main():
     pmc = os.path.join(ROOT, 'profiles', 'pmc_k_step.json')
     if os.path.exists(pmc):
         with open(pmc) as f:
-            traffic = json.load(f).get('hbm_bytes_per_launch')
+            pj = json.load(f)
+        # only for the workload the counters were collected on
+        if (pj.get('particles'), pj.get('halos'), pj.get('n_gpus', 1)) == \
+                (int(args.particles), args.halos, world):
+            traffic = pj.get('hbm_bytes_per_launch')
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

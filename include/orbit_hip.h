@@ -130,6 +130,9 @@ typedef struct oa_step_args {
     uint8_t *matched_prev;      /* (n_prev,) 1 = matched, 0 = departed (:145-148)     */
     uint8_t *matched_cur;       /* (n_cur,) set to 1 when matched; zero on entry
                                    (0 = entered, :168)                                */
+    double *vr_out;             /* optional (n_cur,) float64 radial velocities of a
+                                   frame-only batch launch (the module-level
+                                   region_frame, track_orbits.py:247-290); NULL = off */
 } oa_step_args;
 
 /* Arguments of oa_compact: gather the per-item apsis records into the reference's
@@ -199,6 +202,29 @@ int64_t oa_max_lds_bytes(void);
 
 /* Scan the per-halo / per-item apsis counts and gather the records in output order. */
 int oa_compact(const oa_compact_args *args, void *stream);
+
+/* ---- block helpers: the module-level functions on arbitrary arrays ---------------- */
+
+/* Device workspace bytes oa_match_ids needs for n_cur current IDs. */
+int64_t oa_match_workspace_bytes(int64_t n_cur);
+
+/* For every previous ID, the index of the equal current ID or -1: the in1d / myin1d /
+ * setdiff1d join of compare_radial_velocities (track_orbits.py:300-306, utils.py:4-11).
+ * Current IDs must be unique (myin1d's precondition).  Open addressing in `workspace`. */
+int oa_match_ids(const void *ids_cur, int64_t n_cur, const void *ids_prev, int64_t n_prev,
+                 int32_t id_bytes, void *workspace, int64_t *match_out, void *stream);
+
+/* Per previous particle with match[i] >= 0: strict sign-flip flag (:311-314) and the
+ * angle change arccos(dot(r̂_prev[i], r̂[match[i]])) in the r̂ dtype (:324-325).
+ * vr / vr_prev are float64 (exact copies of the caller's values). */
+int oa_compare_pairs(const int64_t *match, int64_t n_prev, const double *vr, const double *vr_prev,
+                     const void *rhat, const void *rhat_prev, int32_t td_f64, int32_t mode,
+                     uint8_t *flag_out, void *change_out, void *stream);
+
+/* out[i] = float16(angles_prev[i] + change[i]) with NumPy's promotion (f16 + f32 in
+ * float32, f16 + f64 in float64, rounded directly to f16): calc_angles :342-351. */
+int oa_angle_add(const uint16_t *angles_prev, const void *change, int64_t n, int32_t td_f64,
+                 uint16_t *out, void *stream);
 
 #ifdef __cplusplus
 }

@@ -44,7 +44,7 @@ class StepArgs(ctypes.Structure):
                 ('dense_code', c_vp),
                 ('halo_count', c_vp), ('item_count', c_vp), ('status', c_vp),
                 ('onthefly', c_i32), ('vr_f64', c_i32), ('angle_out', c_vp),
-                ('matched_prev', c_vp), ('matched_cur', c_vp)]
+                ('matched_prev', c_vp), ('matched_cur', c_vp), ('vr_out', c_vp)]
 
 
 class CompactArgs(ctypes.Structure):
@@ -70,6 +70,11 @@ SYMBOLS = {
     'oa_max_lds_bytes': (c_i64, []),
     'oa_debug_stamps': (c_i64, [c_vp, c_i64]),
     'oa_compact': (ctypes.c_int, [ctypes.POINTER(CompactArgs), c_vp]),
+    'oa_match_workspace_bytes': (c_i64, [c_i64]),
+    'oa_match_ids': (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp]),
+    'oa_compare_pairs': (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,
+                                        c_vp, c_vp, c_vp]),
+    'oa_angle_add': (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
 }
 
 

@@ -370,7 +370,8 @@ __device__ __forceinline__ double vr_exact(const TD dx[3], const TV vv[3], const
 // falls back to the reference's float64 expression tree (vr_exact).
 template <typename TX, typename TV, typename TD>
 __device__ __forceinline__ uint32_t frame(const V3<TX> &x, const V3<TV> &v, const double *cb,
-                                          const oa_step_args &a, const FrameK &k, TD r[3]) {
+                                          const oa_step_args &a, const FrameK &k, TD r[3],
+                                          double *vr_full = nullptr) {
     TD dx[3] = {(TD)x.x - (TD)cb[0], (TD)x.y - (TD)cb[1], (TD)x.z - (TD)cb[2]};
     // recenter_coordinates (utils.py:24-33): one strict wrap per dimension, in the
     // promoted dtype of (dx, box); the float64 arithmetic runs only in waves where
@@ -397,6 +398,11 @@ __device__ __forceinline__ uint32_t frame(const V3<TX> &x, const V3<TV> &v, cons
     const float vrf = (wf[0] * (float)r[0] + wf[1] * (float)r[1]) + wf[2] * (float)r[2];
     const bool sure = fabsf(vrf) > sc * 0x1p-16f;
     uint32_t sgn = vrf > 0.f ? 1u : 2u;
+    if (vr_full) {                         // module-level region_frame: the value itself
+        const double vr = vr_exact<TV, TD>(dx, vv, cb, r, a);
+        *vr_full = vr;
+        return vr > 0.0 ? 1u : (vr < 0.0 ? 2u : 0u);
+    }
     if (__any(!sure)) {
         if (!sure) {
             const double vr = vr_exact<TV, TD>(dx, vv, cb, r, a);
@@ -594,8 +600,14 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                 r[0] = (TD)xv[u].x - (TD)H.cb[hl][0]; r[1] = (TD)xv[u].y; r[2] = (TD)vv[u].z;
                 sgn = 1u;
             } else {
-                sgn = OTF ? frame_otf<TX, TV, TD>(xv[u], vv[u], H.cb[hl], a, fk, r)
-                          : frame<TX, TV, TD>(xv[u], vv[u], H.cb[hl], a, fk, r);
+                if (!COMPARE && !OTF && a.vr_out) {
+                    double vr;
+                    sgn = frame<TX, TV, TD>(xv[u], vv[u], H.cb[hl], a, fk, r, &vr);
+                    a.vr_out[base + li] = vr;
+                } else {
+                    sgn = OTF ? frame_otf<TX, TV, TD>(xv[u], vv[u], H.cb[hl], a, fk, r)
+                              : frame<TX, TV, TD>(xv[u], vv[u], H.cb[hl], a, fk, r);
+                }
             }
             TD *ro = rhat_out + 3 * (base + li);
             if (!OA_ABL_STORE1) { ro[0] = r[0]; ro[1] = r[1]; ro[2] = r[2]; }
@@ -1211,6 +1223,74 @@ int launch_step_v(const oa_step_args &a, hipStream_t st) {
     return a.vel_f64 ? launch_step_id<TX, double, TD>(a, st) : launch_step_id<TX, float, TD>(a, st);
 }
 
+// ------------------------------------------------------------------ block helpers
+// Module-level compare_radial_velocities / calc_angles (track_orbits.py:293-351) on
+// arbitrary arrays: a global-memory open-addressing table of the current IDs (unique
+// within a block, the myin1d precondition, utils.py:4-11), probed by the previous IDs.
+__device__ __forceinline__ uint64_t id_hash64(uint64_t x) {
+    x ^= x >> 33; x *= 0xFF51AFD7ED558CCDull; x ^= x >> 33; x *= 0xC4CEB9FE1A85EC53ull;
+    return x ^ (x >> 33);
+}
+template <int IDB>
+__device__ __forceinline__ uint64_t load_id(const void *p, int64_t i) {
+    return IDB == 8 ? static_cast<const uint64_t *>(p)[i]
+                    : (uint64_t)static_cast<const uint32_t *>(p)[i];
+}
+template <int IDB>
+__global__ __launch_bounds__(256) void k_match_insert(const void *ids, int64_t n, uint64_t *keys,
+                                                      uint32_t *vals, uint64_t cap) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t id = load_id<IDB>(ids, i);
+    uint64_t s = id_hash64(id) & (cap - 1);
+    for (uint64_t t = 0; t < cap; ++t) {
+        if (atomicCAS(&vals[s], 0u, (uint32_t)(i + 1)) == 0u) { keys[s] = id; return; }
+        s = (s + 1) & (cap - 1);
+    }
+}
+template <int IDB>
+__global__ __launch_bounds__(256) void k_match_probe(const void *ids_prev, int64_t n_prev,
+                                                     const uint64_t *keys, const uint32_t *vals,
+                                                     uint64_t cap, int64_t *match) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n_prev) return;
+    const uint64_t id = load_id<IDB>(ids_prev, i);
+    uint64_t s = id_hash64(id) & (cap - 1);
+    int64_t m = -1;
+    for (uint64_t t = 0; t < cap; ++t) {
+        const uint32_t v = vals[s];
+        if (v == 0u) break;
+        if (keys[s] == id) { m = (int64_t)v - 1; break; }
+        s = (s + 1) & (cap - 1);
+    }
+    match[i] = m;
+}
+// per previous particle: matched flag, strict sign-flip flag (:311-314) and
+// arccos(dot(r̂_prev, r̂_match)) in TD (:324-325)
+template <typename TD>
+__global__ __launch_bounds__(256) void k_compare_pairs(const int64_t *match, int64_t n_prev,
+                                                       const double *vr, const double *vr_prev,
+                                                       const TD *rhat, const TD *rhat_prev,
+                                                       int32_t mode, uint8_t *flag, TD *change) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n_prev) return;
+    const int64_t j = match[i];
+    if (j < 0) { flag[i] = 0; return; }
+    const double a = vr_prev[i], b = vr[j];
+    const bool c = mode == OA_MODE_PERICENTRIC ? (a < 0.0 && b > 0.0) : (a > 0.0 && b < 0.0);
+    flag[i] = c ? 1 : 0;
+    const TD d = dot3(rhat_prev[3 * i], rhat_prev[3 * i + 1], rhat_prev[3 * i + 2],
+                      rhat[3 * j], rhat[3 * j + 1], rhat[3 * j + 2]);
+    change[i] = acos_td(d);
+}
+// f16 angles + TD changes, rounded straight to f16 (calc_angles :342-351)
+template <typename TD>
+__global__ __launch_bounds__(256) void k_angle_add(const uint16_t *prev, const TD *change,
+                                                   int64_t n, uint16_t *out) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i < n) out[i] = angle_add(prev[i], change[i]);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1352,6 +1432,77 @@ int oa_bulk_velocity(const void *vels, int32_t vel_f64, const void *masses, int3
                            (const float *)vels, (const float *)masses, halos, halo_list);
     }
     return check_launch("k_bulk");
+}
+
+int64_t oa_match_workspace_bytes(int64_t n_cur) {
+    uint64_t cap = 64;
+    while (cap < 2 * (uint64_t)(n_cur > 0 ? n_cur : 1)) cap <<= 1;
+    return (int64_t)(cap * (8 + 4));
+}
+
+int oa_match_ids(const void *ids_cur, int64_t n_cur, const void *ids_prev, int64_t n_prev,
+                 int32_t id_bytes, void *workspace, int64_t *match_out, void *stream) {
+    g_err[0] = 0;
+    if (id_bytes != 4 && id_bytes != 8) return fail(OA_E_ARG, "id_bytes must be 4 or 8");
+    if (n_cur < 0 || n_prev < 0 || n_cur >= (int64_t)0xFFFFFFFF)
+        return fail(OA_E_ARG, "oa_match_ids: bad sizes");
+    if (n_prev > 0 && (!ids_prev || !match_out || !workspace || (n_cur > 0 && !ids_cur)))
+        return fail(OA_E_ARG, "oa_match_ids: null pointer");
+    if (n_prev == 0) return OA_OK;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    uint64_t cap = 64;
+    while (cap < 2 * (uint64_t)(n_cur > 0 ? n_cur : 1)) cap <<= 1;
+    uint64_t *keys = static_cast<uint64_t *>(workspace);
+    uint32_t *vals = reinterpret_cast<uint32_t *>(keys + cap);
+    if (hipMemsetAsync(vals, 0, cap * 4, st) != hipSuccess)
+        return fail(OA_E_LAUNCH, "oa_match_ids: memset");
+    if (n_cur > 0) {
+        dim3 g((unsigned)((n_cur + 255) / 256));
+        if (id_bytes == 8) hipLaunchKernelGGL(k_match_insert<8>, g, dim3(256), 0, st, ids_cur, n_cur, keys, vals, cap);
+        else hipLaunchKernelGGL(k_match_insert<4>, g, dim3(256), 0, st, ids_cur, n_cur, keys, vals, cap);
+        if (int rc = check_launch("k_match_insert")) return rc;
+    }
+    dim3 g((unsigned)((n_prev + 255) / 256));
+    if (id_bytes == 8) hipLaunchKernelGGL(k_match_probe<8>, g, dim3(256), 0, st, ids_prev, n_prev, keys, vals, cap, match_out);
+    else hipLaunchKernelGGL(k_match_probe<4>, g, dim3(256), 0, st, ids_prev, n_prev, keys, vals, cap, match_out);
+    return check_launch("k_match_probe");
+}
+
+int oa_compare_pairs(const int64_t *match, int64_t n_prev, const double *vr, const double *vr_prev,
+                     const void *rhat, const void *rhat_prev, int32_t td_f64, int32_t mode,
+                     uint8_t *flag_out, void *change_out, void *stream) {
+    g_err[0] = 0;
+    if (mode != OA_MODE_PERICENTRIC && mode != OA_MODE_APOCENTRIC) return fail(OA_E_ARG, "bad mode");
+    if (n_prev <= 0) return OA_OK;
+    if (!match || !vr_prev || !rhat_prev || !flag_out || !change_out)
+        return fail(OA_E_ARG, "oa_compare_pairs: null pointer");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    dim3 g((unsigned)((n_prev + 255) / 256));
+    if (td_f64)
+        hipLaunchKernelGGL(k_compare_pairs<double>, g, dim3(256), 0, st, match, n_prev, vr, vr_prev,
+                           static_cast<const double *>(rhat), static_cast<const double *>(rhat_prev),
+                           mode, flag_out, static_cast<double *>(change_out));
+    else
+        hipLaunchKernelGGL(k_compare_pairs<float>, g, dim3(256), 0, st, match, n_prev, vr, vr_prev,
+                           static_cast<const float *>(rhat), static_cast<const float *>(rhat_prev),
+                           mode, flag_out, static_cast<float *>(change_out));
+    return check_launch("k_compare_pairs");
+}
+
+int oa_angle_add(const uint16_t *angles_prev, const void *change, int64_t n, int32_t td_f64,
+                 uint16_t *out, void *stream) {
+    g_err[0] = 0;
+    if (n <= 0) return OA_OK;
+    if (!angles_prev || !change || !out) return fail(OA_E_ARG, "oa_angle_add: null pointer");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    dim3 g((unsigned)((n + 255) / 256));
+    if (td_f64)
+        hipLaunchKernelGGL(k_angle_add<double>, g, dim3(256), 0, st, angles_prev,
+                           static_cast<const double *>(change), n, out);
+    else
+        hipLaunchKernelGGL(k_angle_add<float>, g, dim3(256), 0, st, angles_prev,
+                           static_cast<const float *>(change), n, out);
+    return check_launch("k_angle_add");
 }
 
 }  // extern "C"

@@ -12,6 +12,7 @@ import time
 import numpy as np
 
 from .engine import OrbitEngine
+from .functions import region_frame, compare_radial_velocities, calc_angles  # noqa: F401
 from .savefile import RankSink, open_savefile, group_datasets
 from .utils import hubble_parameter
 

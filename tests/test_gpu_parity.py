@@ -210,3 +210,51 @@ def test_onthefly_matches_reference_golden(name, mode):
             assert np.array_equal(v, w, equal_nan=True), k
         else:
             assert np.array_equal(v, w), k
+
+
+def test_module_functions_match_reference_golden():
+    """region_frame / compare_radial_velocities / calc_angles as importable device
+    functions (track_orbits.py:247-351) vs the reference's own outputs (g7)."""
+    from orbitanalysis_amd.track_orbits import (region_frame, compare_radial_velocities,
+                                                calc_angles)
+    from orbitanalysis_amd.utils import hubble_parameter
+    fix = load('g7_functions')
+    for dt in ('float64', 'float32'):
+        base = 'frame_%s' % dt
+        x, v, c, m = (fix[base + s] for s in ('/x', '/v', '/c', '/m'))
+        for tag, masses, bulk, H0, z in (('mean', 1.0, None, 0.0, 0.0), ('marr', m, None, 72.0, 0.3),
+                                         ('cat', 1.0, np.array([0.1, -0.2, 0.3], dtype=dt), 70.0, 1.0)):
+            snap = {'coordinates': x, 'velocities': v, 'masses': masses, 'box_size': 10.0,
+                    'redshift': z}
+            rh, vr, b = region_frame(snap, np.array([0, len(x)]), c, bulk,
+                                     hubble_parameter(z, H0, 0.3, 0.7))
+            key = 'frame_%s_%s' % (dt, tag)
+            for got, name in ((rh, 'rhat'), (vr, 'vr'), (np.asarray(b), 'bulk')):
+                w = fix[key + '/' + name]
+                assert got.dtype == w.dtype and got.shape == w.shape, (key, name)
+                assert np.array_equal(got, w, equal_nan=True), (key, name)
+    for dt in ('float64', 'float32'):
+        base = 'cmp_%s' % dt
+        ins = {s: fix[base + '/' + s] for s in
+               ('ids', 'ids_prev', 'vr', 'vr_prev', 'rhat', 'rhat_prev', 'angles_prev')}
+        for mode in ('pericentric', 'apocentric'):
+            key = 'cmp_%s_%s' % (dt, mode)
+            d = compare_radial_velocities(ins['ids'], ins['ids_prev'], ins['vr'], ins['vr_prev'],
+                                          ins['rhat'], ins['rhat_prev'], mode)
+            for k, val in d.items():
+                w = fix[key + '/out_' + k]
+                val = np.asarray(val)
+                if k == 'angle_changes':
+                    assert val.dtype == w.dtype and val.shape == w.shape
+                    nan = np.isnan(w)
+                    assert np.array_equal(np.isnan(val), nan)
+                    ulp = np.spacing(np.abs(w[~nan])).astype(np.float64)
+                    assert np.all(np.abs(val[~nan].astype(np.float64) - w[~nan]) <= 2 * ulp), key
+                else:
+                    assert np.array_equal(val.astype(w.dtype), w), (key, k)
+            # calc_angles on the reference's own compare output: exact (pure f16 rounding)
+            dref = {k: fix[key + '/out_' + k] for k in
+                    ('apsis_inds', 'inds_match', 'inds_departed', 'angle_changes')}
+            a, aa = calc_angles(len(ins['ids']), ins['angles_prev'], dref)
+            assert np.array_equal(a, fix[key + '/angles'], equal_nan=True), key
+            assert np.array_equal(aa, fix[key + '/apsis_angles'], equal_nan=True), key

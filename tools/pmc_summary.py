@@ -57,6 +57,7 @@ def main():
     res = {
         'kernel': 'k_step<float,float,float,8,unbucketed,compare>',
         'workload': 'bench.py defaults (1e8 particles, 1e4 halos, f32)',
+        'particles': 100000000, 'halos': 10000, 'n_gpus': 1,
         'dispatches': {'frame_only': 1, 'compared': len(cmp_)},
         'calibration': {'frame_only_particles': n0, 'frame_only_read_bytes': n0 * 32,
                         'frame_only_fetch_size_bytes': fetch0, 'k': k,
