@@ -93,6 +93,8 @@ def main():
     ap.add_argument('--particles', type=float, default=1e8, help='per GPU')
     ap.add_argument('--halos', type=int, default=10000)
     ap.add_argument('--mode', default='pericentric')
+    ap.add_argument('--dtype', default='float32', choices=['float32', 'float64'],
+                    help='coordinates / velocities / catalogue dtype (configs[1] is float64)')
     ap.add_argument('--max-snapshots', type=int, default=16)
     ap.add_argument('--cpu-halos', type=int, default=1500)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -134,7 +136,7 @@ def main():
 
     t_setup = time.perf_counter()
     gen = DevicePlummer(n_halos=args.halos, n_particles=int(args.particles), seed=0,
-                        rank=rank, world=world, device=dev)
+                        rank=rank, world=world, device=dev, dtype=args.dtype)
     S = min(args.steps + args.warmup + 1, args.max_snapshots)
     snaps, cats = [], []
     for s in range(S):
@@ -161,7 +163,7 @@ def main():
     ws = Workspace(dev, torch.int64 if preps[0].plan.ids.itemsize == 8 else torch.int32,
                    max(p.scratch for p in preps), max(p.n_prev for p in preps),
                    max(int(p.has_prog.sum()) for p in preps), max(len(p.items) for p in preps),
-                   any(len(p.big) for p in preps))
+                   False)
     # catalogue exchange (N > 1): rank r holds catalogue rows [r*nl, (r+1)*nl)
     nl = -(-args.halos // world)
     cat_local, cat_all = [], None
@@ -174,8 +176,8 @@ def main():
             if hi > lo:
                 rows[:hi - lo] = hv[lo:hi, 4:10]
             cat_local.append(rows.to(cdev))
-    log('setup %.1f s; items/step %d, big %d' % (time.perf_counter() - t_setup,
-                                                  len(preps[0].items), len(preps[0].big)))
+    log('setup %.1f s; items/step %d (large halos %d)'
+        % (time.perf_counter() - t_setup, preps[0].n_small, preps[0].n_global))
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
@@ -260,11 +262,15 @@ def main():
             'data': 'synthetic: %d Plummer spheres (device-generated, AHW sampling, leapfrog '
                     'orbits), region cut r<4a, per-snapshot shuffled blocks, int64 randperm IDs'
                     % args.halos,
-            'config': {'workload': 'BASELINE configs[2]: %.0e particles/GPU, %d halos, f32 '
+            'config': {'workload': 'BASELINE configs[%d]: %.0e particles/GPU, %d halos, %s '
                                    'coords/vels/centres, catalogue bulk velocities, periodic '
-                                   'box, Hubble term, %s' % (args.particles, args.halos, args.mode),
+                                   'box, Hubble term, %s'
+                                   % (2 if args.dtype == 'float32' else 1, args.particles,
+                                      args.halos, last.plan.coord.name.replace('float', 'f'),
+                                      args.mode),
                        'particles_per_step_per_gpu': int(last.n),
-                       'halos': args.halos, 'work_items': int(len(last.items)),
+                       'halos': args.halos, 'work_items': int(last.n_small),
+                       'large_halos': int(last.n_global),
                        'parallelism': 'id-range shards x%d' % world},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,

@@ -133,6 +133,18 @@ typedef struct oa_step_args {
     double *vr_out;             /* optional (n_cur,) float64 radial velocities of a
                                    frame-only batch launch (the module-level
                                    region_frame, track_orbits.py:247-290); NULL = off */
+    /* large halos (blocks beyond one work-group's LDS table): items[n_items ..
+     * n_items + n_global_items) are single-halo items joined through per-halo
+     * open-addressing tables in global memory (any number of work-groups per halo) */
+    int32_t n_global_items;
+    int32_t n_gchunk1, n_gchunk2;
+    const int64_t *gchunk1;     /* (item, start, count) chunks of current blocks      */
+    const int64_t *gchunk2;     /* (item, start, count) chunks of previous blocks,
+                                   start a multiple of 64                             */
+    const int64_t *gtab;        /* per global item: (slot offset, capacity = 2^k)     */
+    uint64_t *gkeys;            /* table keys (IDs)                                   */
+    uint32_t *gvals;            /* table values (position + 1, 0 = empty); zeroed here */
+    int64_t gtab_total;         /* slots over all global items                        */
 } oa_step_args;
 
 /* Arguments of oa_compact: gather the per-item apsis records into the reference's

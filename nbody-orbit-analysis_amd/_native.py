@@ -44,7 +44,10 @@ class StepArgs(ctypes.Structure):
                 ('dense_code', c_vp),
                 ('halo_count', c_vp), ('item_count', c_vp), ('status', c_vp),
                 ('onthefly', c_i32), ('vr_f64', c_i32), ('angle_out', c_vp),
-                ('matched_prev', c_vp), ('matched_cur', c_vp), ('vr_out', c_vp)]
+                ('matched_prev', c_vp), ('matched_cur', c_vp), ('vr_out', c_vp),
+                ('n_global_items', c_i32), ('n_gchunk1', c_i32), ('n_gchunk2', c_i32),
+                ('gchunk1', c_vp), ('gchunk2', c_vp), ('gtab', c_vp), ('gkeys', c_vp),
+                ('gvals', c_vp), ('gtab_total', c_i64)]
 
 
 class CompactArgs(ctypes.Structure):

@@ -1184,6 +1184,9 @@ int set_lds(K kernel, int64_t bytes) {
 }
 
 template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
+int launch_big(const oa_step_args &a, hipStream_t st);
+
+template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
 int launch_step_c(const oa_step_args &a, hipStream_t st) {
     if (a.n_items > 0) {
         int64_t lds = HDR_BYTES + table_bytes(a.lds_entries, a.lds_slots, false);
@@ -1199,7 +1202,7 @@ int launch_step_c(const oa_step_args &a, hipStream_t st) {
         hipLaunchKernelGGL(k, dim3(a.n_big_items), dim3(WG), (size_t)lds, st, a, make_frame_k(a));
         if (int rc = check_launch("k_step(bucketed)")) return rc;
     }
-    return OA_OK;
+    return launch_big<TX, TV, TD, IDB, COMPARE, OTF>(a, st);
 }
 
 template <typename TX, typename TV, typename TD, int IDB>
@@ -1291,6 +1294,159 @@ __global__ __launch_bounds__(256) void k_angle_add(const uint16_t *prev, const T
     if (i < n) out[i] = angle_add(prev[i], change[i]);
 }
 
+// ------------------------------------------------------------------ large halos
+// A halo whose block exceeds one work-group's LDS table is joined through a
+// per-halo open-addressing table in global memory (L2 / Infinity Cache resident),
+// so any number of work-groups can share it and every particle is streamed once:
+//   k_big_frame  chunks of the halo's current block: frame, r̂ / meta stores, and
+//                (compare) insert id -> position (device-scope CAS on the slot)
+//   k_big_join   chunks of its previous block, 64-position segments per wave:
+//                probe, gather the current r̂ + meta, flag, angle, state update,
+//                apsis records packed per segment exactly as k_step does
+// Chunks are (item, start, count) triples built by the host (engine.plan_items).
+constexpr int BIG_WG = 256;
+
+template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
+__global__ __launch_bounds__(BIG_WG) void k_big_frame(const oa_step_args a, const FrameK fk) {
+    typedef typename IdT<IDB>::T ID;
+    const int64_t *ch = a.gchunk1 + 3 * blockIdx.x;
+    const int64_t gi = ch[0], start = ch[1], cnt = ch[2];
+    const oa_item it = a.items[gi];
+    const oa_halo &h = a.halos[it.h0];
+    double cb[6];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) { cb[d] = h.centre[d]; cb[3 + d] = h.bulk[d]; }
+    const int64_t base = h.cur_off;
+    const bool ins = COMPARE && h.prev_cnt >= 0;
+    const ID *ids = static_cast<const ID *>(a.ids);
+    const TX *xs = static_cast<const TX *>(a.coords);
+    const TV *vs = static_cast<const TV *>(a.vels);
+    TD *rhat_out = static_cast<TD *>(a.rhat_out);
+    const int64_t gk = gi - a.n_items;             // global items follow the packed ones
+    uint64_t *keys = a.gkeys + a.gtab[2 * gk];
+    uint32_t *vals = a.gvals + a.gtab[2 * gk];
+    const uint64_t cap = (uint64_t)a.gtab[2 * gk + 1];
+    for (int64_t p = start + threadIdx.x; p < start + cnt; p += BIG_WG) {
+        const int64_t i = base + p;
+        const ID id = lds_nt(&ids[i]);
+        const V3<TX> x = ld3_nt(xs, i);
+        const V3<TV> v = ld3_nt(vs, i);
+        TD r[3];
+        const uint32_t sgn = OTF ? frame_otf<TX, TV, TD>(x, v, cb, a, fk, r)
+                                 : frame<TX, TV, TD>(x, v, cb, a, fk, r);
+        TD *ro = rhat_out + 3 * i;
+        ro[0] = r[0]; ro[1] = r[1]; ro[2] = r[2];
+        uint32_t ang = 0;
+        if (!COMPARE && a.angles_in) ang = a.angles_in[i];
+        a.meta_out[i] = ang | (sgn << 16);
+        if (ins) {
+            uint64_t sl = id_hash64((uint64_t)id) & (cap - 1);
+            for (uint64_t t = 0; t < cap; ++t) {
+                if (atomicCAS(&vals[sl], 0u, (uint32_t)(p + 1)) == 0u) {
+                    keys[sl] = (uint64_t)id;
+                    break;
+                }
+                sl = (sl + 1) & (cap - 1);
+            }
+        }
+    }
+}
+
+template <typename TD, int IDB, bool OTF>
+__global__ __launch_bounds__(BIG_WG) void k_big_join(const oa_step_args a) {
+    typedef typename IdT<IDB>::T ID;
+    const int64_t *ch = a.gchunk2 + 3 * blockIdx.x;
+    const int64_t gi = ch[0], start = ch[1], cnt = ch[2];
+    const oa_item it = a.items[gi];
+    const oa_halo &h = a.halos[it.h0];
+    const int64_t cbase = h.cur_off, pbase = h.prev_off;
+    const ID *ids_prev = static_cast<const ID *>(a.ids_prev);
+    const TD *rhat_prev = static_cast<const TD *>(a.rhat_prev);
+    const TD *rhat_out = static_cast<const TD *>(a.rhat_out);
+    const int64_t gk = gi - a.n_items;
+    const uint64_t *keys = a.gkeys + a.gtab[2 * gk];
+    const uint32_t *vals = a.gvals + a.gtab[2 * gk];
+    const uint64_t cap = (uint64_t)a.gtab[2 * gk + 1];
+    ID *scr_ids = static_cast<ID *>(a.scratch_ids);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lanemask_lt = (1ull << lane) - 1ull;
+    for (int64_t v0 = start; v0 < start + cnt; v0 += BIG_WG) {
+        const int64_t p = v0 + threadIdx.x;
+        const bool ok = p < start + cnt;
+        bool flag = false, hit = false;
+        uint16_t a16 = 0;
+        ID pid = 0;
+        if (ok) {
+            const int64_t k = pbase + p;
+            pid = lds_nt(&ids_prev[k]);
+            const V3<TD> prh = ld3_nt(rhat_prev, k);
+            const uint32_t pmeta = lds_nt(&a.meta_prev[k]);
+            uint64_t sl = id_hash64((uint64_t)pid) & (cap - 1);
+            int64_t j = -1;
+            for (uint64_t t = 0; t < cap; ++t) {
+                const uint32_t vv = vals[sl];
+                if (vv == 0u) break;
+                if (keys[sl] == (uint64_t)pid) { j = (int64_t)vv - 1; break; }
+                sl = (sl + 1) & (cap - 1);
+            }
+            if (j >= 0) {
+                hit = true;
+                const int64_t c = cbase + j;
+                const TD *cr = rhat_out + 3 * c;
+                const uint32_t cmeta = a.meta_out[c];
+                const uint32_t sc = cmeta >> 16, sp = pmeta >> 16;
+                // strict sign test (:311-314)
+                flag = a.mode == OA_MODE_PERICENTRIC ? (sp == 2u && sc == 1u) : (sp == 1u && sc == 2u);
+                // arccos(dot(r̂_prev, r̂_match)) (:324-325), f16 + change (:342-351)
+                const TD dt = dot3(prh.x, prh.y, prh.z, cr[0], cr[1], cr[2]);
+                const TD change = acos_td(dt);
+                const uint16_t acc = angle_add((uint16_t)(pmeta & 0xFFFFu), change);
+                a16 = acc;
+                a.meta_out[c] = (uint32_t)(flag ? 0u : acc) | (sc << 16);
+                if (OTF) {
+                    static_cast<TD *>(a.angle_out)[k] = change;
+                    a.matched_cur[c] = 1;
+                }
+            }
+            if (OTF) a.matched_prev[k] = hit ? 1 : 0;
+        }
+        // apsis records in previous-block order (:315-316), one 64-position segment
+        // per wave, packed at the segment's scratch base as in k_step
+        const uint64_t m = __ballot(flag);
+        const int64_t segpos = v0 + wave * 64;
+        if (segpos < start + cnt) {
+            if (flag) {
+                const int64_t pos = it.scratch_off + segpos + __popcll(m & lanemask_lt);
+                scr_ids[pos] = pid;
+                a.scratch_ang[pos] = a16;
+            }
+            if (lane == 0) {
+                const uint32_t c = (uint32_t)__popcll(m);
+                a.seg_count[(it.scratch_off + segpos) >> 6] = (uint8_t)c;
+                if (c) {
+                    atomicAdd(&a.halo_count[h.out_slot], (int32_t)c);
+                    atomicAdd(&a.item_count[gi], (int32_t)c);
+                }
+            }
+        }
+    }
+}
+
+template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
+int launch_big(const oa_step_args &a, hipStream_t st) {
+    if (a.n_gchunk1 > 0) {
+        hipLaunchKernelGGL((k_big_frame<TX, TV, TD, IDB, COMPARE, OTF>), dim3((unsigned)a.n_gchunk1),
+                           dim3(BIG_WG), 0, st, a, make_frame_k(a));
+        if (int rc = check_launch("k_big_frame")) return rc;
+    }
+    if (COMPARE && a.n_gchunk2 > 0) {
+        hipLaunchKernelGGL((k_big_join<TD, IDB, OTF>), dim3((unsigned)a.n_gchunk2), dim3(BIG_WG), 0,
+                           st, a);
+        if (int rc = check_launch("k_big_join")) return rc;
+    }
+    return OA_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1372,7 +1528,16 @@ int oa_step(const oa_step_args *args, void *stream) {
         return fail(OA_E_ARG, "null previous-state / scratch pointer");
     if (a.onthefly && a.compare && (!a.angle_out || !a.matched_prev || !a.matched_cur))
         return fail(OA_E_ARG, "null on-the-fly output pointer");
+    if (a.n_gchunk1 > 0 && (!a.gchunk1 || !a.gtab || (a.compare && (!a.gkeys || !a.gvals))))
+        return fail(OA_E_ARG, "null large-halo table pointer");
+    if (a.compare && a.n_gchunk2 > 0 && !a.gchunk2)
+        return fail(OA_E_ARG, "null large-halo chunk pointer");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (a.compare && a.n_global_items > 0) {
+        if (hipMemsetAsync(a.gvals, 0, (size_t)a.gtab_total * 4, st) != hipSuccess ||
+            hipMemsetAsync(a.item_count + a.n_items, 0, (size_t)a.n_global_items * 4, st) != hipSuccess)
+            return fail(OA_E_LAUNCH, "oa_step: large-halo table reset");
+    }
     if (a.onthefly)
         return a.coord_f64 ? launch_step_v<double, double>(a, st) : launch_step_v<float, float>(a, st);
     if (a.dx_f64) {

@@ -127,38 +127,64 @@ def plan_dtypes(snapshot, centre, bulk_cat, H, z):
 
 
 # ---------------------------------------------------------------- items
-def plan_items(cur_cnt, prev_cnt, entries, big_entries, hmax=128, fill=0.7, min_buckets=None):
-    """Greedy packing of consecutive halos into work-group items.
+GCHUNK = 4096                  # particles per work-group chunk of a large halo
 
-    Returns (items, big_items) as ITEM_DTYPE arrays.  ``min_buckets`` (per halo)
-    forces more buckets after an overflow."""
+
+def plan_items(cur_cnt, prev_cnt, entries, hmax=128):
+    """Work-group items of one snapshot.
+
+    Consecutive halos whose current blocks fit one LDS table (<= ``entries``
+    particles, <= ``hmax`` halos) are packed greedily into *items* (k_step).  A halo
+    larger than that becomes a *global* item: joined through its own table in global
+    memory by as many work-groups as it has chunks (k_big_frame / k_big_join).
+
+    Returns (items, global_items, scratch): ITEM_DTYPE arrays and the apsis-scratch
+    size (64-slot segments per item, global items after the packed ones)."""
     nh = len(cur_cnt)
-    small, big = [], []
+    small, glob = [], []
     scratch = 0
     j = 0
     pc = np.maximum(prev_cnt, 0)
     while j < nh:
-        need_b = 1
         if cur_cnt[j] > entries:
-            need_b = max(2, int(math.ceil(cur_cnt[j] / (fill * big_entries))))
-        if min_buckets is not None and min_buckets[j] > need_b:
-            need_b = int(min_buckets[j])
-        if need_b > 1:
-            for q in range(need_b):
-                big.append((j, j + 1, q, need_b, 0, 0))
+            glob.append((j, j + 1, 0, 1, 0, pc[j]))
             j += 1
             continue
         start, tot, ptot = j, 0, 0
-        while (j < nh and j - start < hmax and tot + cur_cnt[j] <= entries
-               and (min_buckets is None or min_buckets[j] <= 1)):
+        while j < nh and j - start < hmax and tot + cur_cnt[j] <= entries:
             tot += cur_cnt[j]
             ptot += pc[j]
             j += 1
         small.append((start, j, 0, 1, scratch, ptot))
         scratch += (ptot + 63) // 64 * 64           # 64-slot segments per item
+    for k, g in enumerate(glob):
+        glob[k] = g[:4] + (scratch, g[5])
+        scratch += (g[5] + 63) // 64 * 64
     it = np.array(small, dtype=N.ITEM_DTYPE) if small else np.zeros(0, N.ITEM_DTYPE)
-    bt = np.array(big, dtype=N.ITEM_DTYPE) if big else np.zeros(0, N.ITEM_DTYPE)
-    return it, bt, scratch
+    gt = np.array(glob, dtype=N.ITEM_DTYPE) if glob else np.zeros(0, N.ITEM_DTYPE)
+    return it, gt, scratch
+
+
+def plan_global(glob, cur_cnt, prev_cnt, first_index, compare):
+    """Chunk lists and table layout of the global items (k_big_frame / k_big_join)."""
+    ch1, ch2, tab = [], [], []
+    off = 0
+    for k, g in enumerate(glob):
+        gi = first_index + k
+        h = int(g['h0'])
+        n = int(cur_cnt[h])
+        for st in range(0, n, GCHUNK):
+            ch1.append((gi, st, min(GCHUNK, n - st)))
+        cap = 64
+        while cap < 2 * n:
+            cap <<= 1
+        tab.append((off, cap))
+        off += cap
+        m = int(max(prev_cnt[h], 0)) if compare else 0
+        for st in range(0, m, GCHUNK):
+            ch2.append((gi, st, min(GCHUNK, m - st)))
+    as3 = lambda x: np.array(x, dtype=np.int64).reshape(-1, 3)          # noqa: E731
+    return as3(ch1), as3(ch2), np.array(tab, dtype=np.int64).reshape(-1, 2), off
 
 
 def to_device(x, device, dtype=None):
@@ -216,14 +242,14 @@ class PreparedStep:
     starts: np.ndarray
     counts: np.ndarray
     has_prog: np.ndarray
-    items: np.ndarray
-    big: np.ndarray
+    items: np.ndarray              # packed items, then global (large-halo) items
+    n_small: int
     scratch: int
     compare: bool
     n_prev: int = 0
     halos: Optional[torch.Tensor] = None
     d_items: Optional[torch.Tensor] = None
-    d_big: Optional[torch.Tensor] = None
+    glob: dict = field(default_factory=dict)       # device chunk lists / tables
     rhat: Optional[torch.Tensor] = None
     meta: Optional[torch.Tensor] = None
     angles_in: Optional[torch.Tensor] = None
@@ -233,11 +259,9 @@ class PreparedStep:
     args: N.StepArgs = field(default_factory=N.StepArgs)
     cargs: N.CompactArgs = field(default_factory=N.CompactArgs)
 
-    def more_buckets(self):
-        mb = np.ones(len(self.counts), dtype=np.int64)
-        for h0, nb in zip(self.big['h0'], self.big['nbuckets']):
-            mb[h0] = max(mb[h0], 2 * nb)
-        return mb
+    @property
+    def n_global(self):
+        return len(self.items) - self.n_small
 
 
 class Workspace:
@@ -263,7 +287,7 @@ class Workspace:
     def for_step(cls, pr, device):
         dt = torch.int64 if pr.plan.ids.itemsize == 8 else torch.int32
         return cls(device, dt, pr.scratch, pr.n_prev, int(pr.has_prog.sum()), len(pr.items),
-                   len(pr.big) > 0)
+                   False)
 
     def reset(self, n_slots):
         """Per-launch zeroing (the status word accumulates: callers clear it)."""
@@ -330,10 +354,9 @@ class OrbitEngine:
             halos['prev_off'][has_prog] = p_starts[p[has_prog]]
             halos['prev_cnt'][has_prog] = p_counts[p[has_prog]]
             halos['out_slot'][has_prog] = np.arange(int(has_prog.sum()))
-        items, big, scratch = plan_items(counts, halos['prev_cnt'], entries or self.entries,
-                                         min(self.big_entries, entries or self.big_entries),
-                                         self.hmax, min_buckets=min_buckets)
-        return halos, items, big, scratch, starts, counts, has_prog
+        items, glob, scratch = plan_items(counts, halos['prev_cnt'], entries or self.entries,
+                                          self.hmax)
+        return halos, items, glob, scratch, starts, counts, has_prog
 
     # ------------------------------------------------------------------ step
     def step(self, snapshot, centres, bulk_cat, H, z, exists, compare, angles_in=None):
@@ -358,9 +381,8 @@ class OrbitEngine:
             st = int(ws.status.item()) if compare else 0
             if not st:
                 break
-            if st & N.STATUS_BUCKET_OVERFLOW:
-                min_b = prep.more_buckets()          # a hash bucket overflowed: re-plan
-            if st & N.STATUS_TABLE_OVERFLOW:         # cuckoo stash full: smaller items
+            if st & (N.STATUS_TABLE_OVERFLOW | N.STATUS_BUCKET_OVERFLOW):
+                # cuckoo stash full: smaller items (larger halos move to the global path)
                 entries = max(256, (entries or self.entries) // 2)
         else:
             raise RuntimeError('LDS hash tables kept overflowing (adversarial IDs?)')
@@ -393,14 +415,26 @@ class OrbitEngine:
         n = snap['ids'].numel()
         if snap['coordinates'].numel() != 3 * n or snap['velocities'].numel() != 3 * n:
             raise ValueError('coordinates/velocities must be (N, 3) with N = len(ids)')
-        halos, items, big, scratch, starts, counts, has_prog = self.build_tables(
+        halos, items, glob, scratch, starts, counts, has_prog = self.build_tables(
             snap, centres, bulk_cat, exists, compare, min_buckets, prev_layout, entries)
+        all_items = np.concatenate([items, glob])
         pr = PreparedStep(plan=plan, n=n, starts=starts, counts=counts, has_prog=has_prog,
-                          items=items, big=big, scratch=scratch, compare=bool(compare),
-                          n_prev=prev_layout[4] if compare else 0)
+                          items=all_items, n_small=len(items), scratch=scratch,
+                          compare=bool(compare), n_prev=prev_layout[4] if compare else 0)
         pr.halos = torch.from_numpy(halos.view(np.uint8)).to(dev)
-        pr.d_items = torch.from_numpy(items.view(np.uint8)).to(dev)
-        pr.d_big = torch.from_numpy(big.view(np.uint8)).to(dev)
+        pr.d_items = torch.from_numpy(all_items.view(np.uint8)).to(dev)
+        if len(glob):
+            ch1, ch2, tab, total = plan_global(glob, counts, halos['prev_cnt'], len(items),
+                                               compare)
+            g = pr.glob
+            g['ch1'] = torch.from_numpy(ch1).to(dev)
+            g['ch2'] = torch.from_numpy(ch2).to(dev) if len(ch2) else None
+            g['tab'] = torch.from_numpy(tab).to(dev)
+            g['total'] = total
+            if compare:
+                g['keys'] = torch.empty(total, dtype=torch.int64, device=dev)
+                g['vals'] = torch.empty(total, dtype=torch.int32, device=dev)
+            g['n1'], g['n2'] = len(ch1), len(ch2)
         pr.rhat = torch.empty(n * 3, dtype=plan.torch_dx, device=dev)
         pr.meta = torch.empty(n, dtype=torch.int32, device=dev)
         pr.snap = snap
@@ -416,7 +450,14 @@ class OrbitEngine:
         a.angles_in = _ptr(pr.angles_in)
         a.halos, a.n_halos = pr.halos.data_ptr(), len(halos)
         a.items, a.n_items = pr.d_items.data_ptr(), len(items)
-        a.big_items, a.n_big_items = pr.d_big.data_ptr(), len(big)
+        a.big_items, a.n_big_items = None, 0
+        g = pr.glob
+        a.n_global_items = len(glob)
+        if len(glob):
+            a.n_gchunk1, a.n_gchunk2 = g['n1'], g['n2']
+            a.gchunk1, a.gchunk2 = g['ch1'].data_ptr(), _ptr(g['ch2'])
+            a.gtab, a.gtab_total = g['tab'].data_ptr(), g['total']
+            a.gkeys, a.gvals = _ptr(g.get('keys')), _ptr(g.get('vals'))
         a.H, a.one_plus_z = float(H), float(1 + z)
         a.n_box_dims = len(plan.box)
         for d, L in enumerate(plan.box):
@@ -464,8 +505,8 @@ class OrbitEngine:
             return res
         c = pr.cargs
         c.halos, c.n_halos = a.halos, a.n_halos
-        c.items, c.n_items = a.items, a.n_items
-        c.big_items, c.n_big_items = a.big_items, a.n_big_items
+        c.items, c.n_items = a.items, a.n_items + a.n_global_items
+        c.big_items, c.n_big_items = None, 0
         c.ids_prev, c.id_bytes = a.ids_prev, a.id_bytes
         c.scratch_ids, c.scratch_ang, c.dense_code = a.scratch_ids, a.scratch_ang, a.dense_code
         c.seg_count = a.seg_count

@@ -47,8 +47,10 @@ class DevicePlummer:
 
     def __init__(self, n_halos=10000, n_particles=100_000_000, seed=0, rank=0, world=1,
                  r_cut=4.0, dt=0.5, substeps=5, box_size=None, halo_velocity=0.3,
-                 device='cuda', cosmology=None):
+                 device='cuda', cosmology=None, dtype='float32'):
         self.device = torch.device(device)
+        self.np_dtype = np.dtype(dtype)             # loader dtype of coordinates / velocities
+        self.t_dtype = torch.float64 if self.np_dtype == np.float64 else torch.float32
         self.n_halos = int(n_halos)
         # population per halo so that ≈ n_particles sit inside the region cuts:
         # Plummer M(<r) = r^3 / (r^2 + 1)^1.5
@@ -87,8 +89,8 @@ class DevicePlummer:
     def catalogue(self, s):
         t = s * self.dt
         c = np.mod(self.centres0 + self.halo_vel * t, self.box)
-        return c.astype(np.float32), np.full(self.n_halos, self.r_cut, np.float32), \
-            self.halo_vel.astype(np.float32)
+        dt = self.np_dtype
+        return c.astype(dt), np.full(self.n_halos, self.r_cut, dt), self.halo_vel.astype(dt)
 
     def snapshot(self, s):
         """Snapshot s (s must not decrease between calls)."""
@@ -102,8 +104,8 @@ class DevicePlummer:
         h = self.halo_of[sel]
         t = s * self.dt
         c = torch.remainder(self.d_c0 + self.d_hv * t, self.box)
-        coords = torch.remainder(self.x[sel].double() + c[h], self.box).float().contiguous()
-        vels = (self.v[sel].double() + self.d_hv[h]).float().contiguous()
+        coords = torch.remainder(self.x[sel].double() + c[h], self.box).to(self.t_dtype).contiguous()
+        vels = (self.v[sel].double() + self.d_hv[h]).to(self.t_dtype).contiguous()
         counts = torch.bincount(h, minlength=self.n_halos).cpu().numpy()
         offsets = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
         snap = {'ids': self.ids[sel].contiguous(), 'coordinates': coords, 'velocities': vels,

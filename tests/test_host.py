@@ -96,28 +96,36 @@ def test_wrap_dtype_python_list_box_is_weak():
 
 
 def test_plan_items_invariants():
-    from orbitanalysis_amd.engine import plan_items
+    from orbitanalysis_amd.engine import plan_items, plan_global, GCHUNK
     rng = np.random.default_rng(0)
     cur = rng.integers(0, 3000, 500)
     cur[::37] = 50000
     prev = cur + rng.integers(-10, 10, 500)
     prev[::11] = -1
-    items, big, scratch = plan_items(cur, prev, 4096, 3000, hmax=16)
+    items, glob, scratch = plan_items(cur, prev, 4096, hmax=16)
     covered = np.zeros(500, int)
     for it in items:
         assert it['nbuckets'] == 1 and it['h1'] - it['h0'] <= 16
         assert cur[it['h0']:it['h1']].sum() <= 4096
         covered[it['h0']:it['h1']] += 1
-    for h in np.unique(big['h0']):
-        b = big[big['h0'] == h]
-        assert sorted(b['bucket']) == list(range(b['nbuckets'][0]))
-        assert cur[h] / b['nbuckets'][0] <= 0.7 * 3000
-        covered[h] += 1
+    for g in glob:                                  # large halos: single-halo global items
+        assert g['h1'] == g['h0'] + 1 and cur[g['h0']] > 4096
+        covered[g['h0']] += 1
     assert np.all(covered == 1)
-    for it in items:
+    segs = 0
+    for it in np.concatenate([items, glob]):
         assert it['n_pv'] == np.maximum(prev[it['h0']:it['h1']], 0).sum()
-        assert it['scratch_off'] % 64 == 0
-    assert scratch == sum((int(it['n_pv']) + 63) // 64 * 64 for it in items)
+        assert it['scratch_off'] % 64 == 0 and it['scratch_off'] == segs
+        segs += (int(it['n_pv']) + 63) // 64 * 64
+    assert scratch == segs
+    ch1, ch2, tab, total = plan_global(glob, cur, prev, len(items), True)
+    assert total == tab[:, 1].sum() and np.all(tab[:, 1] >= 2 * cur[glob['h0']])
+    assert np.all((tab[:, 1] & (tab[:, 1] - 1)) == 0)          # power-of-two capacities
+    for k, g in enumerate(glob):
+        c1 = ch1[ch1[:, 0] == len(items) + k]
+        assert c1[:, 2].sum() == cur[g['h0']] and np.all(c1[:, 1] % GCHUNK == 0)
+        c2 = ch2[ch2[:, 0] == len(items) + k]
+        assert c2[:, 2].sum() == max(prev[g['h0']], 0) and np.all(c2[:, 1] % 64 == 0)
 
 
 def test_synthetic_generator_is_deterministic():
