@@ -142,8 +142,9 @@ typedef struct oa_step_args {
     const int64_t *gchunk2;     /* (item, start, count) chunks of previous blocks,
                                    start a multiple of 64                             */
     const int64_t *gtab;        /* per global item: (slot offset, capacity = 2^k)     */
-    uint64_t *gkeys;            /* table keys (IDs)                                   */
-    uint32_t *gvals;            /* table values (position + 1, 0 = empty); zeroed here */
+    uint64_t *gkeys;            /* table entries, 16 B each: {u64 id, u32 position + 1
+                                   (0 = empty), u32 pad}; zeroed by oa_step          */
+    uint32_t *gvals;            /* unused (NULL)                                      */
     int64_t gtab_total;         /* slots over all global items                        */
 } oa_step_args;
 

@@ -1323,8 +1323,9 @@ __global__ __launch_bounds__(BIG_WG) void k_big_frame(const oa_step_args a, cons
     const TV *vs = static_cast<const TV *>(a.vels);
     TD *rhat_out = static_cast<TD *>(a.rhat_out);
     const int64_t gk = gi - a.n_items;             // global items follow the packed ones
-    uint64_t *keys = a.gkeys + a.gtab[2 * gk];
-    uint32_t *vals = a.gvals + a.gtab[2 * gk];
+    // table entries: 16 bytes {u64 id, u32 position + 1 (0 = empty), pad}: a probe
+    // touches one cache line
+    uint64_t *tab = a.gkeys + 2 * a.gtab[2 * gk];
     const uint64_t cap = (uint64_t)a.gtab[2 * gk + 1];
     for (int64_t p = start + threadIdx.x; p < start + cnt; p += BIG_WG) {
         const int64_t i = base + p;
@@ -1342,8 +1343,9 @@ __global__ __launch_bounds__(BIG_WG) void k_big_frame(const oa_step_args a, cons
         if (ins) {
             uint64_t sl = id_hash64((uint64_t)id) & (cap - 1);
             for (uint64_t t = 0; t < cap; ++t) {
-                if (atomicCAS(&vals[sl], 0u, (uint32_t)(p + 1)) == 0u) {
-                    keys[sl] = (uint64_t)id;
+                uint32_t *val = reinterpret_cast<uint32_t *>(tab + 2 * sl + 1);
+                if (atomicCAS(val, 0u, (uint32_t)(p + 1)) == 0u) {
+                    tab[2 * sl] = (uint64_t)id;
                     break;
                 }
                 sl = (sl + 1) & (cap - 1);
@@ -1364,8 +1366,7 @@ __global__ __launch_bounds__(BIG_WG) void k_big_join(const oa_step_args a) {
     const TD *rhat_prev = static_cast<const TD *>(a.rhat_prev);
     const TD *rhat_out = static_cast<const TD *>(a.rhat_out);
     const int64_t gk = gi - a.n_items;
-    const uint64_t *keys = a.gkeys + a.gtab[2 * gk];
-    const uint32_t *vals = a.gvals + a.gtab[2 * gk];
+    const uint64_t *tab = a.gkeys + 2 * a.gtab[2 * gk];
     const uint64_t cap = (uint64_t)a.gtab[2 * gk + 1];
     ID *scr_ids = static_cast<ID *>(a.scratch_ids);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1384,9 +1385,9 @@ __global__ __launch_bounds__(BIG_WG) void k_big_join(const oa_step_args a) {
             uint64_t sl = id_hash64((uint64_t)pid) & (cap - 1);
             int64_t j = -1;
             for (uint64_t t = 0; t < cap; ++t) {
-                const uint32_t vv = vals[sl];
-                if (vv == 0u) break;
-                if (keys[sl] == (uint64_t)pid) { j = (int64_t)vv - 1; break; }
+                const uint4 e = *reinterpret_cast<const uint4 *>(tab + 2 * sl);
+                if (e.z == 0u) break;
+                if ((((uint64_t)e.y << 32) | e.x) == (uint64_t)pid) { j = (int64_t)e.z - 1; break; }
                 sl = (sl + 1) & (cap - 1);
             }
             if (j >= 0) {
@@ -1528,13 +1529,13 @@ int oa_step(const oa_step_args *args, void *stream) {
         return fail(OA_E_ARG, "null previous-state / scratch pointer");
     if (a.onthefly && a.compare && (!a.angle_out || !a.matched_prev || !a.matched_cur))
         return fail(OA_E_ARG, "null on-the-fly output pointer");
-    if (a.n_gchunk1 > 0 && (!a.gchunk1 || !a.gtab || (a.compare && (!a.gkeys || !a.gvals))))
+    if (a.n_gchunk1 > 0 && (!a.gchunk1 || !a.gtab || (a.compare && !a.gkeys)))
         return fail(OA_E_ARG, "null large-halo table pointer");
     if (a.compare && a.n_gchunk2 > 0 && !a.gchunk2)
         return fail(OA_E_ARG, "null large-halo chunk pointer");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (a.compare && a.n_global_items > 0) {
-        if (hipMemsetAsync(a.gvals, 0, (size_t)a.gtab_total * 4, st) != hipSuccess ||
+        if (hipMemsetAsync(a.gkeys, 0, (size_t)a.gtab_total * 16, st) != hipSuccess ||
             hipMemsetAsync(a.item_count + a.n_items, 0, (size_t)a.n_global_items * 4, st) != hipSuccess)
             return fail(OA_E_LAUNCH, "oa_step: large-halo table reset");
     }

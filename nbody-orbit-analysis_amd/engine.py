@@ -432,8 +432,7 @@ class OrbitEngine:
             g['tab'] = torch.from_numpy(tab).to(dev)
             g['total'] = total
             if compare:
-                g['keys'] = torch.empty(total, dtype=torch.int64, device=dev)
-                g['vals'] = torch.empty(total, dtype=torch.int32, device=dev)
+                g['keys'] = torch.empty(2 * total, dtype=torch.int64, device=dev)
             g['n1'], g['n2'] = len(ch1), len(ch2)
         pr.rhat = torch.empty(n * 3, dtype=plan.torch_dx, device=dev)
         pr.meta = torch.empty(n, dtype=torch.int32, device=dev)
