@@ -37,8 +37,6 @@ extern "C" {
 #define OA_E_DEVICE (-3)    /* no HIP device */
 
 /* Run-time flags reported by the step kernel in `status` (bit mask). */
-#define OA_STATUS_BUCKET_OVERFLOW 1u  /* a hash bucket exceeded its LDS capacity:
-                                         re-plan the halo with more buckets */
 #define OA_STATUS_TABLE_OVERFLOW 2u   /* the LDS cuckoo table could not place every
                                          entry (stash full): re-plan smaller items */
 
@@ -60,14 +58,14 @@ typedef struct oa_halo {
 } oa_halo;
 
 /* One work-group's share of a snapshot.  32 bytes, device array.
- * nbuckets == 1: halos [h0,h1) whose current blocks total <= lds_entries.
- * nbuckets  > 1: the single halo h0 (= h1-1), restricted to the particles whose ID
- *                hashes to `bucket` (blocks larger than one work-group's LDS).   */
+ * Packed items (k_step): halos [h0,h1) whose current blocks total <= lds_entries.
+ * Global items (large halos, items[n_items ..]): the single halo h0 = h1 - 1.   */
 typedef struct oa_item {
-    int32_t h0, h1, bucket, nbuckets;
-    int64_t scratch_off;        /* nbuckets == 1: first scratch slot of this item (a
-                                   multiple of 64; one slot per progenitor particle) */
-    int64_t n_pv;               /* nbuckets == 1: progenitor particles of the item   */
+    int32_t h0, h1;
+    int32_t reserved0, reserved1; /* 0, 1 */
+    int64_t scratch_off;        /* first apsis-scratch slot of this item (a multiple
+                                   of 64; one slot per progenitor particle)           */
+    int64_t n_pv;               /* progenitor particles of the item                  */
 } oa_item;
 
 /* Arguments of oa_step (one snapshot of the batch driver's inner loop). */
@@ -88,13 +86,11 @@ typedef struct oa_step_args {
                                    (sign: 1 = v_r > 0, 2 = v_r < 0, 0 = neither)    */
     const uint16_t *angles_in;  /* optional (n_cur,) f16 bits used as angles when
                                    compare == 0 (checkpoint resume), NULL -> 0     */
-    /* tables: items (nbuckets == 1) and big_items (nbuckets > 1), any order */
+    /* tables: packed items [0, n_items), then n_global_items global items */
     const oa_halo *halos;
     int32_t n_halos;
     const oa_item *items;
     int32_t n_items;
-    const oa_item *big_items;
-    int32_t n_big_items;
     /* per-snapshot scalars (hubble_parameter, utils.py:36-39) */
     double H, one_plus_z;
     double box[3];
@@ -106,18 +102,14 @@ typedef struct oa_step_args {
     int32_t compare;            /* 0: frame only (first processed snapshot)       */
     int32_t lds_entries;        /* hash-table entries per work-group (items)      */
     int32_t lds_slots;          /* open-addressing slots per work-group (> entries) */
-    int32_t big_entries;        /* the same for big_items (bucketed halos)        */
-    int32_t big_slots;
     /* apsis scratch */
-    void *scratch_ids;          /* nbuckets==1 items: apsis records, one 64-slot segment
-                                   per 64 progenitor positions, packed per segment  */
+    void *scratch_ids;          /* apsis records, one 64-slot segment per 64
+                                   progenitor positions, packed per segment          */
     uint16_t *scratch_ang;
     uint8_t *seg_count;         /* records per segment ([scratch slots / 64])        */
-    uint16_t *dense_code;       /* nbuckets>1 halos: per previous position, f16 angle
-                                   bits of an apsis or 0xFFFF                         */
     int32_t *halo_count;        /* [n_slots] apsis count per halo with a progenitor;
                                    must be zero on entry                             */
-    int32_t *item_count;        /* [n_items] */
+    int32_t *item_count;        /* [n_items + n_global_items] */
     uint32_t *status;           /* device word, OA_STATUS_* bits; zero on entry       */
     /* on-the-fly driver (track_orbits_onthefly.py:71-205); onthefly = 0: unused.
      * Frame semantics of that driver: dx stored in the coordinate dtype (r̂ too),
@@ -155,14 +147,11 @@ typedef struct oa_compact_args {
     int32_t n_halos;
     const oa_item *items;
     int32_t n_items;
-    const oa_item *big_items;
-    int32_t n_big_items;
     const void *ids_prev;
     int32_t id_bytes;
     const void *scratch_ids;
     const uint16_t *scratch_ang;
     const uint8_t *seg_count;
-    const uint16_t *dense_code;
     const int32_t *halo_count;
     const int32_t *item_count;
     int32_t n_slots;
@@ -201,9 +190,8 @@ int oa_bulk_velocity(const void *vels, int32_t vel_f64, const void *masses, int3
  * (:293-351), emitting apsis records in previous-block order. */
 int oa_step(const oa_step_args *args, void *stream);
 
-/* Dynamic LDS bytes oa_step needs per work-group for the given table sizes
- * (bucketed != 0: the big_items layout, which also keeps a local index per entry). */
-int64_t oa_step_lds_bytes(int32_t entries, int32_t slots, int32_t bucketed);
+/* Dynamic LDS bytes k_step needs per work-group for the given table sizes. */
+int64_t oa_step_lds_bytes(int32_t entries, int32_t slots);
 
 /* Diagnostic builds only (-DOA_STAMPS=1): copy the per-work-group phase timestamps
  * (s_memrealtime, 100 MHz; 6 per work-group) of the last oa_step to host memory.

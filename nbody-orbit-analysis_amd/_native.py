@@ -21,11 +21,10 @@ c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, cty
 HALO_DTYPE = np.dtype([('cur_off', '<i8'), ('cur_cnt', '<i8'), ('prev_off', '<i8'),
                        ('prev_cnt', '<i8'), ('centre', '<f8', (3,)), ('bulk', '<f8', (3,)),
                        ('out_slot', '<i8'), ('reserved', '<i8')])
-ITEM_DTYPE = np.dtype([('h0', '<i4'), ('h1', '<i4'), ('bucket', '<i4'), ('nbuckets', '<i4'),
+ITEM_DTYPE = np.dtype([('h0', '<i4'), ('h1', '<i4'), ('reserved0', '<i4'), ('reserved1', '<i4'),
                        ('scratch_off', '<i8'), ('n_pv', '<i8')])
 
 MODE = {'pericentric': 0, 'apocentric': 1}
-STATUS_BUCKET_OVERFLOW = 1
 STATUS_TABLE_OVERFLOW = 2
 
 
@@ -34,14 +33,11 @@ class StepArgs(ctypes.Structure):
                 ('ids_prev', c_vp), ('rhat_prev', c_vp), ('meta_prev', c_vp), ('n_prev', c_i64),
                 ('rhat_out', c_vp), ('meta_out', c_vp), ('angles_in', c_vp),
                 ('halos', c_vp), ('n_halos', c_i32), ('items', c_vp), ('n_items', c_i32),
-                ('big_items', c_vp), ('n_big_items', c_i32),
                 ('H', c_dbl), ('one_plus_z', c_dbl), ('box', c_dbl * 3), ('n_box_dims', c_i32),
                 ('coord_f64', c_i32), ('vel_f64', c_i32), ('dx_f64', c_i32), ('vb_f64', c_i32),
                 ('wrap_f64', c_i32), ('id_bytes', c_i32), ('mode', c_i32), ('compare', c_i32),
-                ('lds_entries', c_i32), ('lds_slots', c_i32), ('big_entries', c_i32),
-                ('big_slots', c_i32),
+                ('lds_entries', c_i32), ('lds_slots', c_i32),
                 ('scratch_ids', c_vp), ('scratch_ang', c_vp), ('seg_count', c_vp),
-                ('dense_code', c_vp),
                 ('halo_count', c_vp), ('item_count', c_vp), ('status', c_vp),
                 ('onthefly', c_i32), ('vr_f64', c_i32), ('angle_out', c_vp),
                 ('matched_prev', c_vp), ('matched_cur', c_vp), ('vr_out', c_vp),
@@ -52,10 +48,8 @@ class StepArgs(ctypes.Structure):
 
 class CompactArgs(ctypes.Structure):
     _fields_ = [('halos', c_vp), ('n_halos', c_i32), ('items', c_vp), ('n_items', c_i32),
-                ('big_items', c_vp), ('n_big_items', c_i32),
                 ('ids_prev', c_vp), ('id_bytes', c_i32),
                 ('scratch_ids', c_vp), ('scratch_ang', c_vp), ('seg_count', c_vp),
-                ('dense_code', c_vp),
                 ('halo_count', c_vp), ('item_count', c_vp), ('n_slots', c_i32),
                 ('offsets_out', c_vp), ('out_ids', c_vp), ('out_ang', c_vp),
                 ('total_out', c_vp)]
@@ -69,7 +63,7 @@ SYMBOLS = {
     'oa_last_error': (ctypes.c_char_p, []),
     'oa_bulk_velocity': (ctypes.c_int, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
     'oa_step': (ctypes.c_int, [ctypes.POINTER(StepArgs), c_vp]),
-    'oa_step_lds_bytes': (c_i64, [c_i32, c_i32, c_i32]),
+    'oa_step_lds_bytes': (c_i64, [c_i32, c_i32]),
     'oa_max_lds_bytes': (c_i64, []),
     'oa_debug_stamps': (c_i64, [c_vp, c_i64]),
     'oa_compact': (ctypes.c_int, [ctypes.POINTER(CompactArgs), c_vp]),

@@ -5,18 +5,22 @@
 //   region_frame               track_orbits.py:247-290    -> k_step phase 1
 //   compare_radial_velocities  track_orbits.py:293-327    -> k_step phase 2
 //   calc_angles                track_orbits.py:330-351    -> k_step phase 2
-//   result assembly            track_orbits.py:199-227    -> k_scan_slots, k_gather_*
+//   result assembly            track_orbits.py:199-227    -> k_scan_slots, k_gather_items
 //   bulk velocity (sum/mean)   track_orbits.py:262-284    -> k_bulk
+//   large halos                (same functions)           -> k_big_frame, k_big_join
+//   on-the-fly driver          track_orbits_onthefly.py   -> k_step<..., OTF>, k_big_*
+//   module-level helpers       track_orbits.py:293-351    -> k_match_*, k_compare_pairs,
+//                                                            k_angle_add
 //
 // Design: one work-group per *item* (a run of consecutive halos whose
-// current blocks fit the LDS hash table, or one hash bucket of a halo too large for
-// it).  Phase 1 streams the item's current blocks (ids, AoS x, AoS v) once,
+// current blocks fit the LDS hash table; larger halos go through per-halo tables in
+// global memory, k_big_*).  Phase 1 streams the item's current blocks (ids, AoS x, AoS v) once,
 // computes the frame in registers, writes the particle record {r̂, meta} and inserts
 // (halo, id) -> local index into an LDS open-addressing table.  Phase 2 streams the
 // progenitor blocks (ids, records), probes the table, gathers the just-written
 // current record from L2, applies the strict sign test and the arccos angle update
 // and compacts apsis records in previous-block order with wave ballots.  Every
-// input byte is read from HBM once; no sort, no global hash table.
+// input byte is read from HBM once; no sort.
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (no FMA contraction:
 // the reference's NumPy arithmetic rounds every product and sum).
@@ -237,11 +241,6 @@ __device__ __forceinline__ void cuckoo_slots(uint32_t lo, uint32_t n, uint32_t s
     s[2] = (uint32_t)((((x >> 42) & 0x1FFFFFull) * n) >> 21);
 }
 
-__device__ __forceinline__ uint32_t bucket_of(uint32_t lo, uint32_t hi, uint32_t nb) {
-    uint32_t h = fmix32(lo * 0x9E3779B1u + hi * 0x85EBCA77u + 0x27D4EB2Fu);
-    return (uint32_t)(((uint64_t)h * nb) >> 32);
-}
-
 template <int IDB> struct IdT;
 template <> struct IdT<4> { typedef uint32_t T; };
 template <> struct IdT<8> { typedef uint64_t T; };
@@ -255,7 +254,7 @@ __device__ __forceinline__ void id_split(typename IdT<IDB>::T id, uint32_t &lo, 
 // ------------------------------------------------------------------ LDS layout
 struct ItemHdr {
     int64_t cur_base;
-    uint32_t nonuniform, hi0, nent, overflow;
+    uint32_t nonuniform, hi0, pad0, overflow;
     uint32_t nh, nseg, n_span, n_pv;
     uint32_t chunk_total, nsl, nstash, npend;
     uint64_t stash[STASH];          // cuckoo entries whose eviction chain ran out
@@ -269,8 +268,8 @@ struct ItemHdr {
 };
 constexpr int64_t HDR_BYTES = (sizeof(ItemHdr) + 255) & ~int64_t(255);
 
-__host__ __device__ inline int64_t table_bytes(int entries, int slots, bool bucketed) {
-    int64_t b = (int64_t)slots * 8 + (int64_t)entries * (bucketed ? 4 : 2);
+__host__ __device__ inline int64_t table_bytes(int entries, int slots) {
+    int64_t b = (int64_t)slots * 8 + (int64_t)entries * 2;
     return (b + 15) & ~int64_t(15);
 }
 
@@ -458,10 +457,10 @@ __device__ __forceinline__ uint32_t frame_otf(const V3<TX> &x, const V3<TV> &v, 
 // LDS image of one item (after the ItemHdr):
 //   slots[S]  u64  open-addressing table of the item's current particles that have a
 //                  progenitor: lo32(ID) | (angle16 | sign2 << 16 | (pos+1) << 18) << 32,
-//                  0 = empty.  pos = position in the item span (nbuckets == 1) or
-//                  entry index into lidx (bucketed).  One ds_read_b64 per probe step
-//                  returns key, sign, angle and position; the angle is updated in place.
-//   lidx[E]   u32  (bucketed only) block position of each entry
+//                  0 = empty.  pos = position in the item span.  One ds_read_b64 per
+//                  probe returns key, sign, angle and position; the angle is updated in
+//                  place.
+//   slotmap[E] u16 position -> slot for phase 3 (phase 1: the deferred-insert list)
 constexpr uint32_t POS_BITS = 14, POS_SHIFT = 18, MAX_POS = (1u << POS_BITS) - 2;
 
 __device__ __forceinline__ uint64_t slot_pack(uint32_t lo, uint32_t meta, uint32_t pos) {
@@ -474,22 +473,20 @@ __device__ __forceinline__ uint32_t slot_meta(uint64_t v) {
     return (uint32_t)(v >> 32) & ((1u << POS_SHIFT) - 1u);
 }
 
-template <typename TX, typename TV, typename TD, int IDB, bool BUCKETED, bool COMPARE, bool OTF>
+template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
 __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK fk) {
     typedef typename IdT<IDB>::T ID;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     ItemHdr &H = *reinterpret_cast<ItemHdr *>(smem);
-    const int nent_max = BUCKETED ? a.big_entries : a.lds_entries;
-    const uint32_t nslots_max = (uint32_t)(BUCKETED ? a.big_slots : a.lds_slots);
+    const uint32_t nslots_max = (uint32_t)a.lds_slots;
     uint64_t *slots = reinterpret_cast<uint64_t *>(smem + HDR_BYTES);
-    uint32_t *lidx = BUCKETED ? reinterpret_cast<uint32_t *>(slots + nslots_max) : nullptr;
-    // unbucketed: position -> slot (0xFFFF = particle not in the table), for phase 3;
-    // during phase 1 the same bytes hold the list of deferred cuckoo inserts
-    uint16_t *slotmap = BUCKETED ? nullptr : reinterpret_cast<uint16_t *>(slots + nslots_max);
+    // position -> slot (0xFFFF = particle not in the table), for phase 3; during
+    // phase 1 the same bytes hold the list of deferred cuckoo inserts
+    uint16_t *slotmap = reinterpret_cast<uint16_t *>(slots + nslots_max);
     uint64_t *pend = reinterpret_cast<uint64_t *>(slotmap);
-    const uint32_t pend_cap = BUCKETED ? 0u : (uint32_t)a.lds_entries / 4u;
+    const uint32_t pend_cap = (uint32_t)a.lds_entries / 4u;
 
-    const oa_item it = (BUCKETED ? a.big_items : a.items)[blockIdx.x];
+    const oa_item it = a.items[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const ID *ids = reinterpret_cast<const ID *>(a.ids);
     const ID *ids_prev = reinterpret_cast<const ID *>(a.ids_prev);
@@ -500,7 +497,6 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // phase-2 unroll: float64 r̂ trips hold twice the registers (keep 4 waves/SIMD, no spills)
     constexpr int UNR = sizeof(TD) == 8 ? 1 : UNR2;
     constexpr bool compare = COMPARE;   // template: no frame-only loads in the join loop
-    const uint32_t q = (uint32_t)it.bucket, nb = (uint32_t)it.nbuckets;
     STAMP(0);
 
     // ---- phase 0: stage the item's halo table in LDS -------------------------
@@ -519,7 +515,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         }
     }
     if (tid == 0) {
-        H.nonuniform = 0; H.nent = 0; H.overflow = 0; H.nh = nh; H.chunk_total = 0; H.nstash = 0;
+        H.nonuniform = 0; H.overflow = 0; H.nh = nh; H.chunk_total = 0; H.nstash = 0;
         H.npend = 0;
         // progenitor segments in halo order (serial: nh <= HMAX)
         uint32_t ns = 0, vp = 0;
@@ -531,14 +527,14 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
         }
         H.vstart[ns] = vp; H.nseg = ns; H.n_pv = vp;
-        // table size for this item: load factor <= 2 / OA_SLOT_X2 (bucketed: full table)
+        // table size for this item: load factor <= 2 / OA_SLOT_X2
         uint32_t nj = 0;
         for (int k = 0; k < nh; ++k) {
             const oa_halo &h = a.halos[it.h0 + k];
             if (compare && h.prev_cnt >= 0) nj += (uint32_t)h.cur_cnt;
         }
         uint32_t ns_eff = nj * OA_SLOT_X2 / 2 + 64;
-        H.nsl = BUCKETED || ns_eff > nslots_max ? nslots_max : ns_eff;
+        H.nsl = ns_eff > nslots_max ? nslots_max : ns_eff;
         // reference high word for the 32-bit LDS keys: the item's first particle
         const oa_halo &h0 = a.halos[it.h0], &hl1 = a.halos[it.h1 - 1];
         H.hi0 = 0;
@@ -555,8 +551,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     const int64_t base = H.cur_base;
     const uint32_t n_span = H.n_span;
     const uint32_t hi0 = H.hi0;
-    // bucketed items are single-halo: with no progenitor there is nothing to join
-    const bool join = compare && (!BUCKETED || H.has_prev[0]);
+    const bool join = compare;
     STAMP(1);
 
     // ---- phase 1: frame of every current particle, LDS insert ---------------
@@ -592,8 +587,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             uint32_t li = l0 + u * WG + tid;
             uint32_t lo, hi;
             id_split<IDB>(idv[u], lo, hi);
-            if (BUCKETED && bucket_of(lo, hi, nb) != q) continue;
-            uint32_t hl = (BUCKETED || H.nh == 1) ? 0u : upper_find(H.lstart, H.nh, li);
+            uint32_t hl = H.nh == 1 ? 0u : upper_find(H.lstart, H.nh, li);
             TD r[3];
             uint32_t sgn;
             if (OA_ABL_FRAME) {
@@ -618,12 +612,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
             const uint32_t meta = ang | (sgn << 16);
             if (!join || !H.has_prev[hl]) { a.meta_out[base + li] = meta; continue; }
-            uint32_t pos = li;
-            if (BUCKETED) {
-                pos = atomicAdd(&H.nent, 1u);
-                if (pos >= (uint32_t)nent_max) { H.overflow = 1u; continue; }
-                lidx[pos] = li;
-            }
+            const uint32_t pos = li;
             if (IDB == 8 && hi != hi0) H.nonuniform = 1u;     // benign race: all write 1
             val[u] = slot_pack(lo, meta, pos);
             uint32_t cs[3];
@@ -655,7 +644,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         }
         // an entry whose three candidates are taken is deferred: the walks run after the
         // loop, spread over the whole work-group, instead of stalling this wave per trip
-        if (!BUCKETED && !OA_IMMEDIATE_WALK) {
+        if (!OA_IMMEDIATE_WALK) {
 #pragma unroll
             for (int u = 0; u < UNR1; ++u) {
                 if (!ins[u]) continue;
@@ -736,10 +725,10 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // work-group-uniform exit keeps the prefetch below unconditional: a predicated
     // one makes the compiler copy the loaded registers and wait on them here).
     if (n_pv == 0) {
-        if (!BUCKETED && tid == 0) a.item_count[blockIdx.x] = 0;
+        if (tid == 0) a.item_count[blockIdx.x] = 0;
         return;
     }
-    if (!BUCKETED && !OA_IMMEDIATE_WALK) {
+    if (!OA_IMMEDIATE_WALK) {
         __syncthreads();
         const uint32_t np = min(H.npend, pend_cap);
         for (uint32_t e = tid; e < np; e += WG) {
@@ -771,8 +760,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     __builtin_amdgcn_sched_barrier(0);
     STAMP(3);
     if (H.overflow) {
-        if (tid == 0) atomicOr(a.status, H.overflow == 1u ? OA_STATUS_BUCKET_OVERFLOW
-                                                           : OA_STATUS_TABLE_OVERFLOW);
+        if (tid == 0) atomicOr(a.status, OA_STATUS_TABLE_OVERFLOW);
         return;
     }
     const bool nonuniform = IDB == 8 && H.nonuniform != 0;
@@ -796,19 +784,18 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             hs[u] = 0;
             if (!ok[u]) continue;
             id_split<IDB>(pid[u], lo[u], hi[u]);
-            if (BUCKETED && bucket_of(lo[u], hi[u], nb) != q) { ok[u] = false; continue; }
             if (IDB == 8 && !nonuniform && hi[u] != hi0) continue;      // cannot be present
-            lmin[u] = BUCKETED ? 0u : H.lstart[hlv[u]];
-            lmax[u] = BUCKETED ? 0xFFFFFFFFu : H.lstart[hlv[u] + 1] - lmin[u];   // span length
+            lmin[u] = H.lstart[hlv[u]];
+            lmax[u] = H.lstart[hlv[u] + 1] - lmin[u];                  // span length
             uint32_t cs[3];
             cuckoo_slots(lo[u], nslots, cs);
             uint64_t c0 = slots[cs[0]], c1 = slots[cs[1]], c2 = slots[cs[2]];
             auto match = [&](uint64_t v) {
                 const uint32_t p = slot_pos(v);
                 // the halo's position range also rejects empty slots (slot_pos(0) = ~0u)
-                bool m = (uint32_t)v == lo[u] && (BUCKETED ? v != 0ull : p - lmin[u] < lmax[u]);
+                bool m = (uint32_t)v == lo[u] && p - lmin[u] < lmax[u];
                 if (IDB == 8 && nonuniform && m)        // rare: confirm the full ID
-                    m = ids[base + (BUCKETED ? lidx[p] : p)] == pid[u];
+                    m = ids[base + p] == pid[u];
                 return m;
             };
             if (match(c0)) { hit[u] = c0; hs[u] = cs[0]; }
@@ -827,7 +814,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
             const uint32_t p = slot_pos(hit[u]);
-            const TD *src = (hit[u] && !OA_ABL_GATHER) ? rhat_out + 3 * (base + (BUCKETED ? lidx[p] : p))
+            const TD *src = (hit[u] && !OA_ABL_GATHER) ? rhat_out + 3 * (base + p)
                                                        : rhat_prev + 3 * kpos[u];
             cr[u] = V3<TD>{src[0], src[1], src[2]};
         }
@@ -854,7 +841,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                 // change of every matched particle, and which current ones matched
                 static_cast<TD *>(a.angle_out)[kpos[u]] = change;
                 const uint32_t p = slot_pos(hit[u]);
-                a.matched_cur[base + (BUCKETED ? lidx[p] : p)] = 1;
+                a.matched_cur[base + p] = 1;
             }
             // calc_angles (:342-349): apsis angle emitted, then reset to 0
             if (!OA_ABL_SLOTW) {
@@ -869,22 +856,6 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             for (int u = 0; u < UNR; ++u)
                 if (ok[u]) a.matched_prev[kpos[u]] = hit[u] ? 1 : 0;
         }
-        if (BUCKETED) {
-            // dense per-previous-position code; order restored by k_gather_dense
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                if (ok[u]) {
-                    uint16_t code = flag[u] ? a16[u] : (uint16_t)0xFFFFu;
-                    if (flag[u] && code == 0xFFFFu) code = 0x7E00u;   // keep the sentinel free
-                    a.dense_code[kpos[u]] = code;
-                }
-                uint64_t m = __ballot(flag[u]);
-                if (lane == 0 && m) {
-                    const oa_halo &h = a.halos[it.h0];
-                    atomicAdd(&a.halo_count[h.out_slot], (int32_t)__popcll(m));
-                }
-            }
-        } else {
         // apsis records in previous-block order (:315-316): wave ballot + prefix
         // popcount packs each 64-position segment's records at its own base;
         // k_gather_items orders the segments (no work-group barrier here)
@@ -903,7 +874,6 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                 running += (uint32_t)__popcll(m);
             }
         }
-        }
     };
     for (uint32_t v0 = 0; v0 < n_pv; v0 += 2 * WG * UNR) {
         trip(pid, prh, pmeta, kpos, hlv, pidn, prhn, pmetan, kposn, hlvn, v0);
@@ -911,39 +881,29 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         trip(pidn, prhn, pmetan, kposn, hlvn, pid, prh, pmeta, kpos, hlv, v0 + WG * UNR);
     }
 #undef OA_LOAD2
-    if (!BUCKETED && lane == 0) atomicAdd(&H.chunk_total, running);
+    if (lane == 0) atomicAdd(&H.chunk_total, running);
     STAMP(4);
     __syncthreads();
 
     // ---- phase 3: meta words of the joined particles -----------------------------
     const uint32_t nst = min(H.nstash, (uint32_t)STASH);
-    if (BUCKETED) {
-        // bucket members are scattered over the block anyway: one store per slot
-        for (uint32_t w = tid; w < nslots + nst; w += WG) {
-            const uint64_t v = w < nslots ? slots[w] : H.stash[w - nslots];
-            if (!v) continue;
-            if (!OA_ABL_PHASE3) a.meta_out[base + lidx[slot_pos(v)]] = slot_meta(v);
-        }
-    } else {
-        // position -> slot map (halos without a progenitor block: not in the table,
-        // their meta was stored in phase 1), then coalesced stores in position order
-        for (uint32_t w = tid; w < nslots + nst; w += WG) {
-            const uint64_t v = w < nslots ? slots[w] : H.stash[w - nslots];
-            if (v) slotmap[slot_pos(v)] = (uint16_t)w;
-        }
-        for (uint32_t k = 0; k < (uint32_t)nh; ++k)
-            if (!H.has_prev[k])
-                for (uint32_t li = H.lstart[k] + tid; li < H.lstart[k + 1]; li += WG)
-                    slotmap[li] = 0xFFFFu;
-        __syncthreads();
-        for (uint32_t li = tid; li < n_span; li += WG) {
-            const uint32_t w = slotmap[li];
-            if (w == 0xFFFFu) continue;
-            const uint64_t v = w < nslots ? slots[w] : H.stash[w - nslots];
-            if (!OA_ABL_PHASE3) a.meta_out[base + li] = slot_meta(v);
-        }
+    // position -> slot map (halos without a progenitor block: not in the table, their
+    // meta was stored in phase 1), then coalesced stores in position order
+    for (uint32_t w = tid; w < nslots + nst; w += WG) {
+        const uint64_t v = w < nslots ? slots[w] : H.stash[w - nslots];
+        if (v) slotmap[slot_pos(v)] = (uint16_t)w;
     }
-    if (BUCKETED) return;
+    for (uint32_t k = 0; k < (uint32_t)nh; ++k)
+        if (!H.has_prev[k])
+            for (uint32_t li = H.lstart[k] + tid; li < H.lstart[k + 1]; li += WG)
+                slotmap[li] = 0xFFFFu;
+    __syncthreads();
+    for (uint32_t li = tid; li < n_span; li += WG) {
+        const uint32_t w = slotmap[li];
+        if (w == 0xFFFFu) continue;
+        const uint64_t v = w < nslots ? slots[w] : H.stash[w - nslots];
+        if (!OA_ABL_PHASE3) a.meta_out[base + li] = slot_meta(v);
+    }
     if (tid < nh) {
         const oa_halo &h = a.halos[it.h0 + tid];
         if (h.out_slot >= 0) a.halo_count[h.out_slot] = H.halo_cnt[tid];
@@ -1018,39 +978,6 @@ __global__ __launch_bounds__(256) void k_gather_items(const oa_compact_args a) {
             oang[o + r] = a.scratch_ang[sbase + r];
         }
         carry += tot;
-        __syncthreads();
-    }
-}
-
-template <int IDB>
-__global__ __launch_bounds__(1024) void k_gather_dense(const oa_compact_args a) {
-    typedef typename IdT<IDB>::T ID;
-    __shared__ uint32_t wcnt[16];
-    const oa_item it = a.big_items[blockIdx.x];
-    if (it.bucket != 0) return;
-    const oa_halo h = a.halos[it.h0];
-    if (h.out_slot < 0 || h.prev_cnt <= 0) return;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t lanemask_lt = (1ull << lane) - 1ull;
-    const ID *ids_prev = reinterpret_cast<const ID *>(a.ids_prev);
-    ID *out = reinterpret_cast<ID *>(a.out_ids) + a.offsets_out[h.out_slot];
-    uint16_t *oa = a.out_ang + a.offsets_out[h.out_slot];
-    int64_t running = 0;
-    for (int64_t b = 0; b < h.prev_cnt; b += 1024) {
-        int64_t k = b + tid;
-        uint16_t code = k < h.prev_cnt ? a.dense_code[h.prev_off + k] : (uint16_t)0xFFFFu;
-        bool f = code != 0xFFFFu;
-        uint64_t m = __ballot(f);
-        if (lane == 0) wcnt[wave] = (uint32_t)__popcll(m);
-        __syncthreads();
-        uint32_t pre = 0, tot = 0;
-        for (int w = 0; w < 16; ++w) { uint32_t c = wcnt[w]; if (w < wave) pre += c; tot += c; }
-        if (f) {
-            int64_t pos = running + pre + __popcll(m & lanemask_lt);
-            out[pos] = ids_prev[h.prev_off + k];
-            oa[pos] = code;
-        }
-        running += tot;
         __syncthreads();
     }
 }
@@ -1189,18 +1116,11 @@ int launch_big(const oa_step_args &a, hipStream_t st);
 template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
 int launch_step_c(const oa_step_args &a, hipStream_t st) {
     if (a.n_items > 0) {
-        int64_t lds = HDR_BYTES + table_bytes(a.lds_entries, a.lds_slots, false);
-        auto k = k_step<TX, TV, TD, IDB, false, COMPARE, OTF>;
+        int64_t lds = HDR_BYTES + table_bytes(a.lds_entries, a.lds_slots);
+        auto k = k_step<TX, TV, TD, IDB, COMPARE, OTF>;
         if (int rc = set_lds(k, lds)) return rc;
         hipLaunchKernelGGL(k, dim3(a.n_items), dim3(WG), (size_t)lds, st, a, make_frame_k(a));
         if (int rc = check_launch("k_step")) return rc;
-    }
-    if (a.n_big_items > 0) {
-        int64_t lds = HDR_BYTES + table_bytes(a.big_entries, a.big_slots, true);
-        auto k = k_step<TX, TV, TD, IDB, true, COMPARE, OTF>;
-        if (int rc = set_lds(k, lds)) return rc;
-        hipLaunchKernelGGL(k, dim3(a.n_big_items), dim3(WG), (size_t)lds, st, a, make_frame_k(a));
-        if (int rc = check_launch("k_step(bucketed)")) return rc;
     }
     return launch_big<TX, TV, TD, IDB, COMPARE, OTF>(a, st);
 }
@@ -1476,8 +1396,8 @@ int64_t oa_struct_size(int32_t which) {
 
 const char *oa_last_error(void) { return g_err; }
 
-int64_t oa_step_lds_bytes(int32_t entries, int32_t slots, int32_t bucketed) {
-    return HDR_BYTES + table_bytes(entries, slots, bucketed != 0);
+int64_t oa_step_lds_bytes(int32_t entries, int32_t slots) {
+    return HDR_BYTES + table_bytes(entries, slots);
 }
 
 // Diagnostic builds (-DOA_STAMPS=1): copy the per-work-group phase stamps of the last
@@ -1516,16 +1436,12 @@ int oa_step(const oa_step_args *args, void *stream) {
     if (a.n_items > 0 && (a.lds_entries <= 0 || a.lds_entries > (int)MAX_POS + 1 ||
                           a.lds_slots <= a.lds_entries))
         return fail(OA_E_ARG, "bad lds_entries/lds_slots (entries <= %u < slots)", MAX_POS + 1);
-    if (a.n_big_items > 0 && (a.big_entries <= 0 || a.big_entries > (int)MAX_POS + 1 ||
-                              a.big_slots <= a.big_entries))
-        return fail(OA_E_ARG, "bad big_entries/big_slots (entries <= %u < slots)", MAX_POS + 1);
-    if (a.n_items + a.n_big_items > 0 &&
+    if (a.n_items + a.n_global_items > 0 &&
         (!a.halos || !a.ids || !a.coords || !a.vels || !a.rhat_out || !a.meta_out))
         return fail(OA_E_ARG, "null input/output pointer");
     if (a.compare && (!a.ids_prev || !a.rhat_prev || !a.meta_prev || !a.halo_count || !a.status ||
                       (a.n_items > 0 && (!a.scratch_ids || !a.scratch_ang || !a.item_count ||
-                                         !a.seg_count)) ||
-                      (a.n_big_items > 0 && !a.dense_code)))
+                                         !a.seg_count))))
         return fail(OA_E_ARG, "null previous-state / scratch pointer");
     if (a.onthefly && a.compare && (!a.angle_out || !a.matched_prev || !a.matched_cur))
         return fail(OA_E_ARG, "null on-the-fly output pointer");
@@ -1563,11 +1479,6 @@ int oa_compact(const oa_compact_args *args, void *stream) {
         if (a.id_bytes == 8) hipLaunchKernelGGL(k_gather_items<8>, dim3(a.n_items), dim3(256), 0, st, a);
         else hipLaunchKernelGGL(k_gather_items<4>, dim3(a.n_items), dim3(256), 0, st, a);
         if (int rc = check_launch("k_gather_items")) return rc;
-    }
-    if (a.n_big_items > 0) {
-        if (a.id_bytes == 8) hipLaunchKernelGGL(k_gather_dense<8>, dim3(a.n_big_items), dim3(1024), 0, st, a);
-        else hipLaunchKernelGGL(k_gather_dense<4>, dim3(a.n_big_items), dim3(1024), 0, st, a);
-        if (int rc = check_launch("k_gather_dense")) return rc;
     }
     return OA_OK;
 }

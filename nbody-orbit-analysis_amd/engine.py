@@ -23,10 +23,8 @@ import torch
 from . import _native as N
 
 F32, F64 = np.dtype(np.float32), np.dtype(np.float64)
-DEFAULT_ENTRIES = 14336        # current particles per work-group item (nbuckets == 1)
+DEFAULT_ENTRIES = 14336        # current particles per work-group item
 DEFAULT_SLOTS = 16128          # 8-byte LDS cuckoo slots per item (126 KB) + 2 B/entry map
-DEFAULT_BIG_ENTRIES = 10240    # per hash bucket of a larger halo
-DEFAULT_BIG_SLOTS = 13824
 
 _TORCH_FROM_NP = {
     np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
@@ -267,13 +265,12 @@ class PreparedStep:
 class Workspace:
     """Reusable scratch for compare steps (sized for the largest step it serves)."""
 
-    def __init__(self, device, id_torch_dtype, scratch, n_prev, n_slots, n_items, dense):
+    def __init__(self, device, id_torch_dtype, scratch, n_prev, n_slots, n_items):
         def e(n, dt):
             return torch.empty(max(int(n), 1), dtype=dt, device=device)
         self.scratch_ids = e(scratch, id_torch_dtype)
         self.scratch_ang = e(scratch, torch.int16)
         self.seg_count = e(scratch // 64 + 1, torch.uint8)
-        self.dense = e(n_prev if dense else 1, torch.int16)
         self.halo_count = e(n_slots, torch.int32)
         self.item_count = e(n_items, torch.int32)
         self.status = e(1, torch.int32)
@@ -286,8 +283,7 @@ class Workspace:
     @classmethod
     def for_step(cls, pr, device):
         dt = torch.int64 if pr.plan.ids.itemsize == 8 else torch.int32
-        return cls(device, dt, pr.scratch, pr.n_prev, int(pr.has_prog.sum()), len(pr.items),
-                   False)
+        return cls(device, dt, pr.scratch, pr.n_prev, int(pr.has_prog.sum()), len(pr.items))
 
     def reset(self, n_slots):
         """Per-launch zeroing (the status word accumulates: callers clear it)."""
@@ -298,7 +294,7 @@ class OrbitEngine:
     """Per-snapshot device pipeline with carried state (see module docstring)."""
 
     def __init__(self, mode='pericentric', device=None, lds_entries=None, lds_slots=None,
-                 big_entries=None, big_slots=None, hmax=None):
+                 hmax=None):
         if mode not in N.MODE:
             raise ValueError("Orbit detection mode not recognized. Please specify either "
                              "'pericentric' or 'apocentric'.")
@@ -306,28 +302,24 @@ class OrbitEngine:
         self.device = torch.device(device if device is not None else 'cuda')
         self.mode = mode
         env = os.environ.get
-        # defaults fill one CU's 160 KB LDS: 8 B per hash slot
-        # (+ 4 B per entry for bucketed items)
+        # defaults fill one CU's 160 KB LDS: 8 B per cuckoo slot + 2 B
+        # per entry; halos larger than `entries` take the global-table path
         self.entries = int(lds_entries or env('ORBIT_LDS_ENTRIES', DEFAULT_ENTRIES))
         self.slots = int(lds_slots or env('ORBIT_LDS_SLOTS', 0) or
                          max(DEFAULT_SLOTS, self.entries + 1))
-        self.big_entries = int(big_entries or env('ORBIT_BIG_ENTRIES', DEFAULT_BIG_ENTRIES))
-        self.big_slots = int(big_slots or env('ORBIT_BIG_SLOTS', 0) or
-                             max(DEFAULT_BIG_SLOTS, self.big_entries + 1))
         self.hmax = min(int(hmax or env('ORBIT_HMAX', 1 << 30)), self.lib.oa_build_info(1))
         max_lds = self.lib.oa_max_lds_bytes()
-        for e, s, b in ((self.entries, self.slots, 0), (self.big_entries, self.big_slots, 1)):
-            need = self.lib.oa_step_lds_bytes(e, s, b)
-            if need > max_lds:
-                raise ValueError('LDS table needs %d bytes > device limit %d' % (need, max_lds))
+        need = self.lib.oa_step_lds_bytes(self.entries, self.slots)
+        if need > max_lds:
+            raise ValueError('LDS table needs %d bytes > device limit %d' % (need, max_lds))
         self.prev: Optional[SnapshotState] = None
 
     def reset(self):
         self.prev = None
 
     # ------------------------------------------------------------------ tables
-    def build_tables(self, snapshot, centres, bulk_cat, exists, compare, min_buckets=None,
-                     prev_layout=None, entries=None):
+    def build_tables(self, snapshot, centres, bulk_cat, exists, compare, prev_layout=None,
+                     entries=None):
         n = int(snapshot['ids'].numel()) if isinstance(snapshot['ids'], torch.Tensor) \
             else len(snapshot['ids'])
         starts = np.asarray(snapshot['region_offsets'], dtype=np.int64).reshape(-1)
@@ -370,10 +362,10 @@ class OrbitEngine:
             snap[k] = to_device(snapshot[k], dev)
         if is_array(snapshot['masses']):
             snap['masses'] = to_device(snapshot['masses'], dev)
-        min_b, entries = None, None
+        entries = None
         for _ in range(8):
             prep = self.prepare(snap, centres, bulk_cat, H, z, exists, compare,
-                                angles_in=angles_in, min_buckets=min_b, plan_src=snapshot,
+                                angles_in=angles_in, plan_src=snapshot,
                                 entries=entries)
             ws = Workspace.for_step(prep, dev)
             ws.status.zero_()
@@ -381,7 +373,7 @@ class OrbitEngine:
             st = int(ws.status.item()) if compare else 0
             if not st:
                 break
-            if st & (N.STATUS_TABLE_OVERFLOW | N.STATUS_BUCKET_OVERFLOW):
+            if st & N.STATUS_TABLE_OVERFLOW:
                 # cuckoo stash full: smaller items (larger halos move to the global path)
                 entries = max(256, (entries or self.entries) // 2)
         else:
@@ -392,7 +384,7 @@ class OrbitEngine:
         return res
 
     def prepare(self, snap, centres, bulk_cat, H, z, exists, compare, angles_in=None,
-                min_buckets=None, plan_src=None, prev_layout=None, entries=None):
+                plan_src=None, prev_layout=None, entries=None):
         """Host half of a step: dtype plan, halo/item tables, device uploads.
 
         ``snap`` holds device tensors for ids/coordinates/velocities(/masses);
@@ -416,7 +408,7 @@ class OrbitEngine:
         if snap['coordinates'].numel() != 3 * n or snap['velocities'].numel() != 3 * n:
             raise ValueError('coordinates/velocities must be (N, 3) with N = len(ids)')
         halos, items, glob, scratch, starts, counts, has_prog = self.build_tables(
-            snap, centres, bulk_cat, exists, compare, min_buckets, prev_layout, entries)
+            snap, centres, bulk_cat, exists, compare, prev_layout, entries)
         all_items = np.concatenate([items, glob])
         pr = PreparedStep(plan=plan, n=n, starts=starts, counts=counts, has_prog=has_prog,
                           items=all_items, n_small=len(items), scratch=scratch,
@@ -449,7 +441,6 @@ class OrbitEngine:
         a.angles_in = _ptr(pr.angles_in)
         a.halos, a.n_halos = pr.halos.data_ptr(), len(halos)
         a.items, a.n_items = pr.d_items.data_ptr(), len(items)
-        a.big_items, a.n_big_items = None, 0
         g = pr.glob
         a.n_global_items = len(glob)
         if len(glob):
@@ -467,7 +458,6 @@ class OrbitEngine:
         a.mode = N.MODE[self.mode]
         a.compare = int(bool(compare))
         a.lds_entries, a.lds_slots = self.entries, self.slots
-        a.big_entries, a.big_slots = self.big_entries, self.big_slots
         return pr
 
     def launch(self, pr, ws, prev=None, stream=None, step_events=None):
@@ -489,9 +479,7 @@ class OrbitEngine:
                                                     p.meta.data_ptr())
             a.n_prev = pr.n_prev
             ws.reset(res.n_slots)
-            a.scratch_ids, a.scratch_ang, a.dense_code = (ws.scratch_ids.data_ptr(),
-                                                         ws.scratch_ang.data_ptr(),
-                                                         ws.dense.data_ptr())
+            a.scratch_ids, a.scratch_ang = ws.scratch_ids.data_ptr(), ws.scratch_ang.data_ptr()
             a.seg_count = ws.seg_count.data_ptr()
             a.halo_count, a.item_count, a.status = (ws.halo_count.data_ptr(),
                                                    ws.item_count.data_ptr(), ws.status.data_ptr())
@@ -505,9 +493,8 @@ class OrbitEngine:
         c = pr.cargs
         c.halos, c.n_halos = a.halos, a.n_halos
         c.items, c.n_items = a.items, a.n_items + a.n_global_items
-        c.big_items, c.n_big_items = None, 0
         c.ids_prev, c.id_bytes = a.ids_prev, a.id_bytes
-        c.scratch_ids, c.scratch_ang, c.dense_code = a.scratch_ids, a.scratch_ang, a.dense_code
+        c.scratch_ids, c.scratch_ang = a.scratch_ids, a.scratch_ang
         c.seg_count = a.seg_count
         c.halo_count, c.item_count, c.n_slots = a.halo_count, a.item_count, res.n_slots
         c.offsets_out, c.out_ids, c.out_ang = (ws.offsets.data_ptr(), ws.out_ids.data_ptr(),

@@ -133,7 +133,7 @@ class OnTheFly:
             st = int(ws.status.item())
             if not st:
                 break
-            if st & N.STATUS_TABLE_OVERFLOW or st & N.STATUS_BUCKET_OVERFLOW:
+            if st & N.STATUS_TABLE_OVERFLOW:
                 entries = max(256, (entries or eng.entries) // 2)
         else:
             raise RuntimeError('LDS hash tables kept overflowing (adversarial IDs?)')

@@ -83,17 +83,16 @@ def test_resume_matches_reference_golden(name):
 
 @pytest.mark.parametrize('name', ['g1_config1', 'g2_overlap_birth_massarray', 'g3_apo_periodic',
                                   'g5_fp32_centre32', 'g8_many_small_halos'])
-def test_bucketed_and_packed_paths_match(name):
-    """Tiny LDS tables force every halo through the hash-bucketed multi-work-group
-    path (and many halos per item through the packed path): same outputs."""
+def test_global_and_packed_paths_match(name):
+    """Tiny LDS tables push every larger halo through the global-table path
+    (k_big_frame / k_big_join) and pack many small halos per item: same outputs."""
     from orbitanalysis_amd.engine import OrbitEngine
     fix = load(name)
     u, meta = universe(fix)
-    # (entries, big entries, slots): the last config packs the cuckoo tables to ~90 %
-    # load so insert chains hit the stash and the table-overflow re-plan path
-    for entries, big, slots in ((256, 200, None), (700, 128, None), (700, 128, 760)):
-        eng = OrbitEngine(mode=meta['run']['mode'], lds_entries=entries, big_entries=big, hmax=7,
-                          lds_slots=slots)
+    # (entries, slots): the last config packs the cuckoo tables to ~90 % load so insert
+    # chains hit the stash and the table-overflow re-plan path
+    for entries, slots in ((256, None), (700, None), (700, 760)):
+        eng = OrbitEngine(mode=meta['run']['mode'], lds_entries=entries, hmax=7, lds_slots=slots)
         out = run_driver(u, meta['run'], engine=eng)
         compare_groups(out.groups, groups(fix), {})
 

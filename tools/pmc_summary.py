@@ -55,7 +55,7 @@ def main():
     fetch = mean['FETCH_SIZE'] * 1024.0
     write = mean['WRITE_SIZE'] * 1024.0
     res = {
-        'kernel': 'k_step<float,float,float,8,unbucketed,compare>',
+        'kernel': 'k_step<float,float,float,8,compare>',
         'workload': 'bench.py defaults (1e8 particles, 1e4 halos, f32)',
         'particles': 100000000, 'halos': 10000, 'n_gpus': 1,
         'dispatches': {'frame_only': 1, 'compared': len(cmp_)},

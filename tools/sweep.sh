@@ -1,14 +1,13 @@
 #!/bin/bash
-# Kernel-variant sweep on the MI355X box: name lib entries slots [big_entries big_slots]
+# Kernel-variant sweep on the MI355X box: name lib entries slots
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; O=$R/gpurun_out; mkdir -p "$O"
 TAG=${TAG:-sweep}
 STEPS=${STEPS:-4}
 : > "$O/$TAG.jsonl"
-while read -r name lib entries slots be bs; do
+while read -r name lib entries slots; do
   [ -z "$name" ] && continue
   ORBIT_HIP_LIB=$R/nbody-orbit-analysis_amd/variants/$lib ORBIT_LDS_ENTRIES=$entries ORBIT_LDS_SLOTS=$slots \
-  ORBIT_BIG_ENTRIES=${be:-10240} ORBIT_BIG_SLOTS=${bs:-13824} \
     timeout -k 10 300 python bench.py --steps $STEPS --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} \
     > "$O/${TAG}_$name.json" 2> "$O/${TAG}_$name.err"
   rc=$?
