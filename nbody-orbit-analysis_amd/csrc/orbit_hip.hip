@@ -93,8 +93,11 @@ namespace {
 #ifndef OA_SLOT_X2
 #define OA_SLOT_X2 4        // per-item table: slots = entries * OA_SLOT_X2 / 2 (+64)
 #endif
-#ifndef OA_PF1
-#define OA_PF1 1            // phase-1 software prefetch of the next loop trip
+#ifndef OA_PF1D
+#define OA_PF1D 1           // phase-1 loop trips of loads in flight ahead (1 or 2)
+#endif
+#ifndef OA_DYN
+#define OA_DYN 1            // waves take loop trips from an LDS counter (else static)
 #endif
 #ifndef OA_HMAX
 #define OA_HMAX 32
@@ -257,6 +260,7 @@ struct ItemHdr {
     uint32_t nonuniform, hi0, pad0, overflow;
     uint32_t nh, nseg, n_span, n_pv;
     uint32_t chunk_total, nsl, nstash, npend;
+    uint32_t ctr1, ctr2, pad1, pad2;    // trip counters of phases 1 and 2
     uint64_t stash[STASH];          // cuckoo entries whose eviction chain ran out
     uint32_t lstart[HMAX + 1];      // local start of each item halo's current block
     uint32_t vstart[HMAX + 1];      // virtual start of each progenitor segment
@@ -473,6 +477,17 @@ __device__ __forceinline__ uint32_t slot_meta(uint64_t v) {
     return (uint32_t)(v >> 32) & ((1u << POS_SHIFT) - 1u);
 }
 
+// Next loop trip of a wave.  Trips are runs of 64 * UNR consecutive positions; with
+// OA_DYN the waves of a work-group take them from an LDS counter (a wave that gets
+// ahead takes more), so all waves finish a phase within about one trip of each
+// other instead of waiting at the barrier for the slowest static share.
+__device__ __forceinline__ uint32_t next_trip(uint32_t *ctr, uint32_t t, int lane) {
+    if (!OA_DYN) return t + NWAVE;
+    uint32_t v = 0;
+    if (lane == 0) v = atomicAdd(ctr, 1u);
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
 template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
 __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK fk) {
     typedef typename IdT<IDB>::T ID;
@@ -517,6 +532,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     if (tid == 0) {
         H.nonuniform = 0; H.overflow = 0; H.nh = nh; H.chunk_total = 0; H.nstash = 0;
         H.npend = 0;
+        H.ctr1 = NWAVE; H.ctr2 = NWAVE;     // every wave starts on trip `wave`
         // progenitor segments in halo order (serial: nh <= HMAX)
         uint32_t ns = 0, vp = 0;
         for (int k = 0; k < nh; ++k) {
@@ -559,24 +575,40 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // loads are unconditional (index clamped) so hipcc does not branch around them
 #define OA_LOAD1(IDA, XA, VA, L0)                                                  \
     _Pragma("unroll") for (int u = 0; u < UNR1; ++u) {                             \
-        const uint32_t li_ = min((L0) + u * WG + tid, n_span - 1u);                \
+        const uint32_t li_ = min((L0) * T1 + u * 64 + lane, n_span - 1u);         \
         const int64_t i_ = base + li_;                                             \
         IDA[u] = lds_nt(&ids[i_]);                                                 \
         XA[u] = ld3_nt(coords, i_);                                                \
         VA[u] = ld3_nt(vels, i_);                                                  \
     }
-    ID idv[UNR1], idn[UNR1];
-    V3<TX> xv[UNR1], xn[UNR1];
-    V3<TV> vv[UNR1], vn[UNR1];
-    if (OA_PF1 && n_span > 0) { OA_LOAD1(idv, xv, vv, 0u) }
-    for (uint32_t l0 = 0; l0 < n_span; l0 += WG * UNR1) {
+    // float64 inputs: one trip ahead only (two would exceed 128 VGPRs and spill)
+    constexpr int PF1D = (sizeof(TX) == 8 || sizeof(TV) == 8) ? 1 : OA_PF1D;
+    ID idv[UNR1], idn[UNR1], idm[UNR1];
+    V3<TX> xv[UNR1], xn[UNR1], xm[UNR1];
+    V3<TV> vv[UNR1], vn[UNR1], vm[UNR1];
+    constexpr uint32_t T1 = 64 * UNR1;               // positions per wave trip
+    const uint32_t ntr1 = (n_span + T1 - 1) / T1;
+    uint32_t t1 = wave, t1n = 0;
+    if (n_span > 0) { OA_LOAD1(idv, xv, vv, t1) }
+    if (PF1D == 2) {
+        t1n = next_trip(&H.ctr1, t1, lane);
+        if (n_span > 0) { OA_LOAD1(idn, xn, vn, t1n) }
+    }
+    while (t1 < ntr1) {
         // unconditional prefetch (clamped, in bounds): a branch here makes hipcc
-        // copy the loaded registers through a phi and wait for them immediately
-        if (OA_PF1) { OA_LOAD1(idn, xn, vn, l0 + WG * UNR1) }
-        else { OA_LOAD1(idv, xv, vv, l0) }
+        // copy the loaded registers through a phi and wait for them immediately;
+        // OA_PF1D trips of loads are in flight while this one computes
+        uint32_t t1m = 0;
+        if (PF1D == 2) {
+            t1m = next_trip(&H.ctr1, t1n, lane);
+            OA_LOAD1(idm, xm, vm, t1m)
+        } else {
+            t1n = next_trip(&H.ctr1, t1, lane);
+            OA_LOAD1(idn, xn, vn, t1n)
+        }
         bool ok[UNR1];
 #pragma unroll
-        for (int u = 0; u < UNR1; ++u) ok[u] = l0 + u * WG + tid < n_span;
+        for (int u = 0; u < UNR1; ++u) ok[u] = t1 * T1 + u * 64 + lane < n_span;
         uint64_t val[UNR1];
         uint32_t sl[UNR1], cs1[UNR1], cs2[UNR1];
         bool ins[UNR1];
@@ -584,7 +616,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         for (int u = 0; u < UNR1; ++u) {
             ins[u] = false;
             if (!ok[u]) continue;
-            uint32_t li = l0 + u * WG + tid;
+            const uint32_t li = t1 * T1 + u * 64 + lane;
             uint32_t lo, hi;
             id_split<IDB>(idv[u], lo, hi);
             uint32_t hl = H.nh == 1 ? 0u : upper_find(H.lstart, H.nh, li);
@@ -686,10 +718,13 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                 break;
             }
         }
-        if (OA_PF1) {
 #pragma unroll
-            for (int u = 0; u < UNR1; ++u) { idv[u] = idn[u]; xv[u] = xn[u]; vv[u] = vn[u]; }
+        for (int u = 0; u < UNR1; ++u) {
+            idv[u] = idn[u]; xv[u] = xn[u]; vv[u] = vn[u];
+            if (PF1D == 2) { idn[u] = idm[u]; xn[u] = xm[u]; vn[u] = vm[u]; }
         }
+        t1 = t1n;
+        if (PF1D == 2) t1n = t1m;
     }
 #undef OA_LOAD1
     STAMP(2);
@@ -698,13 +733,15 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
 
     // ---- phase 2: stream progenitor blocks, join, flag, angle, emit ---------
     const uint32_t n_pv = H.n_pv, nseg = H.nseg;
+    constexpr uint32_t T2 = 64 * UNR;                 // positions per wave trip
+    const uint32_t ntr2 = (n_pv + T2 - 1) / T2;
     const uint64_t lanemask_lt = (1ull << lane) - 1ull;
     uint32_t running = 0;
     ID *scr_ids = reinterpret_cast<ID *>(a.scratch_ids);
 
 #define OA_LOAD2(PID, PRH, PMETA, KPOS, HLV, V0)                                  \
     _Pragma("unroll") for (int u = 0; u < UNR; ++u) {                              \
-        const uint32_t vp_ = min((V0) + u * WG + tid, n_pv - 1u);                  \
+        const uint32_t vp_ = min((V0) * T2 + u * 64 + lane, n_pv - 1u);           \
         const uint32_t sg_ = nseg == 1 ? 0u : upper_find(H.vstart, nseg, vp_);     \
         HLV[u] = (uint32_t)H.seg_halo[sg_];                                        \
         KPOS[u] = H.seg_prev_off[sg_] + (vp_ - H.vstart[sg_]);                     \
@@ -753,7 +790,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         }
     }
     __builtin_amdgcn_sched_barrier(0);
-    OA_LOAD2(pid, prh, pmeta, kpos, hlv, 0u)
+    OA_LOAD2(pid, prh, pmeta, kpos, hlv, (uint32_t)wave)
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(3 * UNR) : "memory");
     __builtin_amdgcn_s_barrier();
@@ -769,10 +806,11 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     auto trip = [&](ID (&pid)[UNR], V3<TD> (&prh)[UNR], uint32_t (&pmeta)[UNR],
                     int64_t (&kpos)[UNR], uint32_t (&hlv)[UNR], ID (&pidn)[UNR],
                     V3<TD> (&prhn)[UNR], uint32_t (&pmetan)[UNR], int64_t (&kposn)[UNR],
-                    uint32_t (&hlvn)[UNR], uint32_t v0) __attribute__((always_inline)) {
+                    uint32_t (&hlvn)[UNR], uint32_t t, uint32_t tn) __attribute__((always_inline)) {
+        const uint32_t v0 = t * T2;
         bool ok[UNR];
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) ok[u] = v0 + u * WG + tid < n_pv;
+        for (int u = 0; u < UNR; ++u) ok[u] = v0 + u * 64 + lane < n_pv;
         // cuckoo lookup of (halo, id): the three candidate slots are read together (one
         // LDS round trip); departed particles miss (setdiff1d/in1d, :300-304)
         uint32_t lo[UNR], hi[UNR], lmin[UNR], lmax[UNR], hs[UNR];
@@ -819,7 +857,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             cr[u] = V3<TD>{src[0], src[1], src[2]};
         }
         __builtin_amdgcn_sched_barrier(0);
-        OA_LOAD2(pidn, prhn, pmetan, kposn, hlvn, v0 + WG * UNR)   // unconditional
+        OA_LOAD2(pidn, prhn, pmetan, kposn, hlvn, tn)   // unconditional (clamped)
         __builtin_amdgcn_sched_barrier(0);
         bool flag[UNR];
         uint16_t a16[UNR];
@@ -862,7 +900,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
             const uint64_t m = __ballot(flag[u]);
-            const uint32_t segpos = v0 + u * WG + wave * 64;    // multiple of 64
+            const uint32_t segpos = v0 + u * 64;                // multiple of 64
             if (segpos < n_pv) {
                 if (flag[u] && !OA_ABL_EMIT) {
                     const int64_t pos = it.scratch_off + segpos + __popcll(m & lanemask_lt);
@@ -875,10 +913,15 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
         }
     };
-    for (uint32_t v0 = 0; v0 < n_pv; v0 += 2 * WG * UNR) {
-        trip(pid, prh, pmeta, kpos, hlv, pidn, prhn, pmetan, kposn, hlvn, v0);
-        if (v0 + WG * UNR >= n_pv) break;
-        trip(pidn, prhn, pmetan, kposn, hlvn, pid, prh, pmeta, kpos, hlv, v0 + WG * UNR);
+    uint32_t t2 = wave;
+    while (t2 < ntr2) {
+        uint32_t tn = next_trip(&H.ctr2, t2, lane);
+        trip(pid, prh, pmeta, kpos, hlv, pidn, prhn, pmetan, kposn, hlvn, t2, tn);
+        if (tn >= ntr2) break;
+        t2 = tn;
+        tn = next_trip(&H.ctr2, t2, lane);
+        trip(pidn, prhn, pmetan, kposn, hlvn, pid, prh, pmeta, kpos, hlv, t2, tn);
+        t2 = tn;
     }
 #undef OA_LOAD2
     if (lane == 0) atomicAdd(&H.chunk_total, running);
