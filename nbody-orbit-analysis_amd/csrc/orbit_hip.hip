@@ -110,6 +110,8 @@ constexpr int UNR2 = OA_UNR2;       // phase-2 particles per thread per loop tri
 constexpr int BULK_CHUNK = 8192;    // numpy pairwise-sum buffer chunk
 constexpr int STASH = 64;           // cuckoo stash entries per item
 constexpr int MAX_EVICT = 48;       // eviction-chain length before an entry is stashed
+constexpr int P3R = 7;              // phase 3: overlaid slots held per thread, so an
+                                    // item spans <= 2 * P3R * WG positions
 static_assert(WG % 64 == 0 && WG <= 1024, "work-group must be whole waves");
 static_assert(HMAX < WG, "halo table is staged by one thread per halo");
 
@@ -267,8 +269,10 @@ struct ItemHdr {
     int32_t seg_halo[HMAX];         // segment -> item-local halo
     int32_t halo_cnt[HMAX];         // apsis records per item halo
     int32_t has_prev[HMAX];
+    uint32_t seg_cnt[HMAX];         // progenitor particles of each segment
     int64_t seg_prev_off[HMAX];
     double cb[HMAX][6];             // centre[3], bulk[3]
+    float cf[HMAX][6];              // the same, rounded to float32
 };
 constexpr int64_t HDR_BYTES = (sizeof(ItemHdr) + 255) & ~int64_t(255);
 
@@ -366,25 +370,33 @@ __device__ __forceinline__ double vr_exact(const TD dx[3], const TV vv[3], const
     return dot3(w[0], w[1], w[2], (double)r[0], (double)r[1], (double)r[2]);
 }
 
-// region_frame (track_orbits.py:247-290) for one particle; cb = centre[3], bulk[3].
+// region_frame (track_orbits.py:247-290) for one particle; cb = centre[3], bulk[3];
+// cf = the same six values rounded to float32 (exact for a float32 dx plan).
 // r̂ is computed exactly in the dx dtype.  Only sign(v_r) is kept, so v_r is first
 // evaluated in float32 with a rigorous error bound (|error| <= ~10 * 2^-24 *
 // sum_i |r_i| (|vb_i| + |h_i|)); when |v_r| is within 2^-16 of that scale the wave
 // falls back to the reference's float64 expression tree (vr_exact).
 template <typename TX, typename TV, typename TD>
 __device__ __forceinline__ uint32_t frame(const V3<TX> &x, const V3<TV> &v, const double *cb,
-                                          const oa_step_args &a, const FrameK &k, TD r[3],
-                                          double *vr_full = nullptr) {
-    TD dx[3] = {(TD)x.x - (TD)cb[0], (TD)x.y - (TD)cb[1], (TD)x.z - (TD)cb[2]};
+                                          const float *cf, const oa_step_args &a,
+                                          const FrameK &k, TD r[3], double *vr_full = nullptr) {
+    TD dx[3];
+    if constexpr (sizeof(TD) == 4) {
+        dx[0] = (float)x.x - cf[0]; dx[1] = (float)x.y - cf[1]; dx[2] = (float)x.z - cf[2];
+    } else {
+        dx[0] = (TD)x.x - cb[0]; dx[1] = (TD)x.y - cb[1]; dx[2] = (TD)x.z - cb[2];
+    }
     // recenter_coordinates (utils.py:24-33): one strict wrap per dimension, in the
     // promoted dtype of (dx, box); the float64 arithmetic runs only in waves where
     // some particle crosses the box edge
+#pragma unroll
     for (int d = 0; d < 3; ++d) {
-        if (d >= a.n_box_dims) break;
-        bool h = WrapT<TD>::hi(dx[d], a, k, d);
-        if (__any(h)) { if (h) dx[d] = wrap_sub(dx[d], a, d); }
-        bool l = WrapT<TD>::lo(dx[d], a, k, d);
-        if (__any(l)) { if (l) dx[d] = wrap_add(dx[d], a, d); }
+        if (d < a.n_box_dims) {
+            bool h = WrapT<TD>::hi(dx[d], a, k, d);
+            if (__any(h)) { if (h) dx[d] = wrap_sub(dx[d], a, d); }
+            bool l = WrapT<TD>::lo(dx[d], a, k, d);
+            if (__any(l)) { if (l) dx[d] = wrap_add(dx[d], a, d); }
+        }
     }
     // rads = sqrt(dot(dx, dx)); rhats = dx / rads   (:286-287), exact in dx's dtype
     unit_vector(dx, r);
@@ -393,7 +405,7 @@ __device__ __forceinline__ uint32_t frame(const V3<TX> &x, const V3<TV> &v, cons
     float wf[3], sc = 0.f;
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
-        float vb = a.vb_f64 ? (float)((double)vv[d] - cb[3 + d]) : (float)vv[d] - (float)cb[3 + d];
+        float vb = a.vb_f64 ? (float)((double)vv[d] - cb[3 + d]) : (float)vv[d] - cf[3 + d];
         float hf = k.h_f * (float)dx[d];
         wf[d] = vb + hf;
         sc += fabsf((float)r[d]) * (fabsf(vb) + fabsf(hf));
@@ -464,7 +476,8 @@ __device__ __forceinline__ uint32_t frame_otf(const V3<TX> &x, const V3<TV> &v, 
 //                  0 = empty.  pos = position in the item span.  One ds_read_b64 per
 //                  probe returns key, sign, angle and position; the angle is updated in
 //                  place.
-//   slotmap[E] u16 position -> slot for phase 3 (phase 1: the deferred-insert list)
+//   pend[E/4] u64 phase 1: the deferred-insert list
+//   phase 3 overlays slots[0 .. E/2) with a position-indexed u32 array of state words
 constexpr uint32_t POS_BITS = 14, POS_SHIFT = 18, MAX_POS = (1u << POS_BITS) - 2;
 
 __device__ __forceinline__ uint64_t slot_pack(uint32_t lo, uint32_t meta, uint32_t pos) {
@@ -477,15 +490,86 @@ __device__ __forceinline__ uint32_t slot_meta(uint64_t v) {
     return (uint32_t)(v >> 32) & ((1u << POS_SHIFT) - 1u);
 }
 
-// Next loop trip of a wave.  Trips are runs of 64 * UNR consecutive positions; with
-// OA_DYN the waves of a work-group take them from an LDS counter (a wave that gets
-// ahead takes more), so all waves finish a phase within about one trip of each
-// other instead of waiting at the barrier for the slowest static share.
-__device__ __forceinline__ uint32_t next_trip(uint32_t *ctr, uint32_t t, int lane) {
-    if (!OA_DYN) return t + NWAVE;
+// ---- buffer resources --------------------------------------------------------------
+// Row loops address memory through buffer resources built from uniform (SGPR) bases
+// with 32-bit per-lane offsets: no 64-bit address arithmetic per access, and lanes past
+// a resource's end read 0 / drop their stores, so partial rows need no clamping.
+// The LLVM buffer intrinsics are bound directly (v4i32 resource form): this hipcc's
+// __builtin_amdgcn_raw_buffer_load_b96 lowers to a 4-byte load, and b128 loads read
+// through vector swizzles lose their upper half.
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x3 __attribute__((ext_vector_type(3)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef i32x4 Rsrc;
+__device__ int32_t rbl_i32(i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.load.i32");
+__device__ int64_t rbl_i64(i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.load.i64");
+__device__ f32x3 rbl_v3f32(i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.load.v3f32");
+__device__ f64x2 rbl_v2f64(i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.load.v2f64");
+__device__ double rbl_f64(i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.load.f64");
+__device__ void rbs_i32(int32_t, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.i32");
+__device__ void rbs_v3f32(f32x3, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.v3f32");
+__device__ void rbs_v2f64(f64x2, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.v2f64");
+__device__ void rbs_f64(double, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.f64");
+constexpr int AUX_NT = 2;      // nt: streamed-once inputs (keeps L2 for the r̂ gathers)
+
+// raw buffer resource (stride 0): 48-bit base, num_records in bytes, 32-bit data format
+__device__ __forceinline__ Rsrc make_rsrc(const void *p, uint32_t bytes) {
+    const uint64_t a = (uint64_t)p;
+    Rsrc r;
+    r.x = __builtin_amdgcn_readfirstlane((int32_t)(uint32_t)a);
+    r.y = __builtin_amdgcn_readfirstlane((int32_t)((uint32_t)(a >> 32) & 0xFFFFu));
+    r.z = __builtin_amdgcn_readfirstlane((int32_t)bytes);
+    r.w = 0x00020000;
+    return r;
+}
+template <typename T, int AUX> __device__ __forceinline__ T bld(Rsrc r, uint32_t o) {
+    if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, rbl_i32(r, (int32_t)o, 0, AUX));
+    else return __builtin_bit_cast(T, rbl_i64(r, (int32_t)o, 0, AUX));
+}
+template <typename T, int AUX> __device__ __forceinline__ V3<T> bld3(Rsrc r, uint32_t o) {
+    if constexpr (sizeof(T) == 4) {
+        const f32x3 v = rbl_v3f32(r, (int32_t)o, 0, AUX);
+        return V3<T>{v.x, v.y, v.z};
+    } else {
+        const f64x2 v = rbl_v2f64(r, (int32_t)o, 0, AUX);
+        const double w = rbl_f64(r, (int32_t)(o + 16u), 0, AUX);
+        return V3<T>{v.x, v.y, w};
+    }
+}
+__device__ __forceinline__ void bst32(Rsrc r, uint32_t o, uint32_t v) {
+    rbs_i32((int32_t)v, r, (int32_t)o, 0, 0);
+}
+template <typename T> __device__ __forceinline__ void bst3(Rsrc r, uint32_t o, const T v[3]) {
+    if constexpr (sizeof(T) == 4) {
+        const f32x3 w = {v[0], v[1], v[2]};
+        rbs_v3f32(w, r, (int32_t)o, 0, 0);
+    } else {
+        const f64x2 w = {v[0], v[1]};
+        rbs_v2f64(w, r, (int32_t)o, 0, 0);
+        rbs_f64(v[2], r, (int32_t)(o + 16u), 0, 0);
+    }
+}
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ int64_t uni64(int64_t x) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Trip counters: trips are runs of 64 * UNR consecutive (virtual) positions.  Every
+// wave starts on trips `wave` and `wave + NWAVE`; later trips come from an LDS counter
+// (a wave that gets ahead takes more, so all waves end a phase within about one trip
+// of each other).  The counter is read one trip ahead, so its LDS round trip overlaps
+// a trip's work.
+__device__ __forceinline__ uint32_t trip_fetch(uint32_t *ctr, int lane) {
     uint32_t v = 0;
-    if (lane == 0) v = atomicAdd(ctr, 1u);
-    return __builtin_amdgcn_readfirstlane(v);
+    if (OA_DYN) {
+        if (lane == 0) v = atomicAdd(ctr, 1u);
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t trip_take(uint32_t fetched, uint32_t t_prev) {
+    return OA_DYN ? __builtin_amdgcn_readfirstlane(fetched) : t_prev + NWAVE;
 }
 
 template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
@@ -495,23 +579,19 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     ItemHdr &H = *reinterpret_cast<ItemHdr *>(smem);
     const uint32_t nslots_max = (uint32_t)a.lds_slots;
     uint64_t *slots = reinterpret_cast<uint64_t *>(smem + HDR_BYTES);
-    // position -> slot (0xFFFF = particle not in the table), for phase 3; during
-    // phase 1 the same bytes hold the list of deferred cuckoo inserts
-    uint16_t *slotmap = reinterpret_cast<uint16_t *>(slots + nslots_max);
-    uint64_t *pend = reinterpret_cast<uint64_t *>(slotmap);
+    // phase 1: the list of deferred cuckoo inserts
+    uint64_t *pend = slots + nslots_max;
     const uint32_t pend_cap = (uint32_t)a.lds_entries / 4u;
 
     const oa_item it = a.items[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const ID *ids = reinterpret_cast<const ID *>(a.ids);
     const ID *ids_prev = reinterpret_cast<const ID *>(a.ids_prev);
-    const TX *coords = reinterpret_cast<const TX *>(a.coords);
-    const TV *vels = reinterpret_cast<const TV *>(a.vels);
     TD *rhat_out = reinterpret_cast<TD *>(a.rhat_out);
     const TD *rhat_prev = reinterpret_cast<const TD *>(a.rhat_prev);
-    // phase-2 unroll: float64 r̂ trips hold twice the registers (keep 4 waves/SIMD, no spills)
+    constexpr uint32_t SX = 3 * sizeof(TX), SV = 3 * sizeof(TV), SD = 3 * sizeof(TD);
+    // phase-2 unroll: float64 r̂ trips hold twice the registers (no spills)
     constexpr int UNR = sizeof(TD) == 8 ? 1 : UNR2;
-    constexpr bool compare = COMPARE;   // template: no frame-only loads in the join loop
     STAMP(0);
 
     // ---- phase 0: stage the item's halo table in LDS -------------------------
@@ -520,9 +600,10 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         const oa_halo &h = a.halos[it.h0 + tid];
         const oa_halo &h0 = a.halos[it.h0];
         H.lstart[tid] = (uint32_t)(h.cur_off - h0.cur_off);
-        H.has_prev[tid] = compare && h.prev_cnt >= 0;
+        H.has_prev[tid] = COMPARE && h.prev_cnt >= 0;
         H.halo_cnt[tid] = 0;
         for (int d = 0; d < 3; ++d) { H.cb[tid][d] = h.centre[d]; H.cb[tid][3 + d] = h.bulk[d]; }
+        for (int d = 0; d < 3; ++d) { H.cf[tid][d] = (float)h.centre[d]; H.cf[tid][3 + d] = (float)h.bulk[d]; }
         if (tid == nh - 1) {
             H.lstart[nh] = (uint32_t)(h.cur_off + h.cur_cnt - h0.cur_off);
             H.n_span = H.lstart[nh];
@@ -532,14 +613,16 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     if (tid == 0) {
         H.nonuniform = 0; H.overflow = 0; H.nh = nh; H.chunk_total = 0; H.nstash = 0;
         H.npend = 0;
-        H.ctr1 = NWAVE; H.ctr2 = NWAVE;     // every wave starts on trip `wave`
-        // progenitor segments in halo order (serial: nh <= HMAX)
+        H.ctr1 = 2 * NWAVE; H.ctr2 = 2 * NWAVE;   // trips wave, wave + NWAVE are static
+        // progenitor segments in halo order (serial: nh <= HMAX); each starts on a
+        // 64-position row of the virtual (padded) progenitor space
         uint32_t ns = 0, vp = 0;
         for (int k = 0; k < nh; ++k) {
             const oa_halo &h = a.halos[it.h0 + k];
-            if (compare && h.prev_cnt > 0) {
+            if (COMPARE && h.prev_cnt > 0) {
                 H.seg_halo[ns] = k; H.seg_prev_off[ns] = h.prev_off; H.vstart[ns] = vp;
-                vp += (uint32_t)h.prev_cnt; ++ns;
+                H.seg_cnt[ns] = (uint32_t)h.prev_cnt;
+                vp += ((uint32_t)h.prev_cnt + 63u) & ~63u; ++ns;
             }
         }
         H.vstart[ns] = vp; H.nseg = ns; H.n_pv = vp;
@@ -547,7 +630,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         uint32_t nj = 0;
         for (int k = 0; k < nh; ++k) {
             const oa_halo &h = a.halos[it.h0 + k];
-            if (compare && h.prev_cnt >= 0) nj += (uint32_t)h.cur_cnt;
+            if (COMPARE && h.prev_cnt >= 0) nj += (uint32_t)h.cur_cnt;
         }
         uint32_t ns_eff = nj * OA_SLOT_X2 / 2 + 64;
         H.nsl = ns_eff > nslots_max ? nslots_max : ns_eff;
@@ -558,95 +641,86 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             H.hi0 = (uint32_t)((uint64_t)ids[h0.cur_off] >> 32);
     }
     __syncthreads();
-    const uint32_t nslots = H.nsl;
-    if (compare) {
+    const uint32_t nslots = uni(H.nsl);
+    if (COMPARE) {
         for (uint32_t w = tid; w < nslots; w += WG) slots[w] = 0ull;
     }
     __syncthreads();
 
-    const int64_t base = H.cur_base;
-    const uint32_t n_span = H.n_span;
-    const uint32_t hi0 = H.hi0;
-    const bool join = compare;
+    const int64_t base = uni64(H.cur_base);
+    const uint32_t n_span = uni(H.n_span);
+    const uint32_t hi0 = uni(H.hi0);
+    const uint32_t nhu = uni(H.nh);
+    const Rsrc r_id = make_rsrc(ids + base, n_span * IDB);
+    const Rsrc r_x = make_rsrc(reinterpret_cast<const TX *>(a.coords) + 3 * base, n_span * SX);
+    const Rsrc r_v = make_rsrc(reinterpret_cast<const TV *>(a.vels) + 3 * base, n_span * SV);
+    const Rsrc r_rh = make_rsrc(rhat_out + 3 * base, n_span * SD);   // phase 1 stores, phase 2 gathers
+    const Rsrc r_mt = make_rsrc(a.meta_out + base, n_span * 4u);
     STAMP(1);
 
     // ---- phase 1: frame of every current particle, LDS insert ---------------
-    // software-pipelined: trip t+1's loads are in flight while trip t computes;
-    // loads are unconditional (index clamped) so hipcc does not branch around them
-#define OA_LOAD1(IDA, XA, VA, L0)                                                  \
+    // software-pipelined: trip t+1's loads are in flight while trip t computes
+#define OA_LOAD1(IDA, XA, VA, T)                                                   \
     _Pragma("unroll") for (int u = 0; u < UNR1; ++u) {                             \
-        const uint32_t li_ = min((L0) * T1 + u * 64 + lane, n_span - 1u);         \
-        const int64_t i_ = base + li_;                                             \
-        IDA[u] = lds_nt(&ids[i_]);                                                 \
-        XA[u] = ld3_nt(coords, i_);                                                \
-        VA[u] = ld3_nt(vels, i_);                                                  \
+        const uint32_t li_ = (T) * T1 + u * 64 + lane;                             \
+        IDA[u] = bld<ID, AUX_NT>(r_id, li_ * IDB);                                 \
+        XA[u] = bld3<TX, AUX_NT>(r_x, li_ * SX);                                   \
+        VA[u] = bld3<TV, AUX_NT>(r_v, li_ * SV);                                   \
     }
-    // float64 inputs: one trip ahead only (two would exceed 128 VGPRs and spill)
-    constexpr int PF1D = (sizeof(TX) == 8 || sizeof(TV) == 8) ? 1 : OA_PF1D;
-    ID idv[UNR1], idn[UNR1], idm[UNR1];
-    V3<TX> xv[UNR1], xn[UNR1], xm[UNR1];
-    V3<TV> vv[UNR1], vn[UNR1], vm[UNR1];
+    ID idv[UNR1], idn[UNR1];
+    V3<TX> xv[UNR1], xn[UNR1];
+    V3<TV> vv[UNR1], vn[UNR1];
     constexpr uint32_t T1 = 64 * UNR1;               // positions per wave trip
     const uint32_t ntr1 = (n_span + T1 - 1) / T1;
-    uint32_t t1 = wave, t1n = 0;
-    if (n_span > 0) { OA_LOAD1(idv, xv, vv, t1) }
-    if (PF1D == 2) {
-        t1n = next_trip(&H.ctr1, t1, lane);
-        if (n_span > 0) { OA_LOAD1(idn, xn, vn, t1n) }
-    }
+    uint32_t t1 = wave, t1n = wave + NWAVE;
+    OA_LOAD1(idv, xv, vv, t1)
     while (t1 < ntr1) {
-        // unconditional prefetch (clamped, in bounds): a branch here makes hipcc
-        // copy the loaded registers through a phi and wait for them immediately;
-        // OA_PF1D trips of loads are in flight while this one computes
-        uint32_t t1m = 0;
-        if (PF1D == 2) {
-            t1m = next_trip(&H.ctr1, t1n, lane);
-            OA_LOAD1(idm, xm, vm, t1m)
-        } else {
-            t1n = next_trip(&H.ctr1, t1, lane);
-            OA_LOAD1(idn, xn, vn, t1n)
-        }
-        bool ok[UNR1];
-#pragma unroll
-        for (int u = 0; u < UNR1; ++u) ok[u] = t1 * T1 + u * 64 + lane < n_span;
+        const uint32_t f1 = trip_fetch(&H.ctr1, lane);   // the trip after next
+        OA_LOAD1(idn, xn, vn, t1n)                       // the next trip (out of range: zeros)
         uint64_t val[UNR1];
         uint32_t sl[UNR1], cs1[UNR1], cs2[UNR1];
         bool ins[UNR1];
 #pragma unroll
         for (int u = 0; u < UNR1; ++u) {
             ins[u] = false;
-            if (!ok[u]) continue;
-            const uint32_t li = t1 * T1 + u * 64 + lane;
+            const uint32_t r0 = t1 * T1 + u * 64;       // the row's first position (uniform)
+            if (r0 >= n_span) continue;
+            const uint32_t li = r0 + lane;
+            const bool ok = li < n_span;
+            // the row's halo (uniform search); rows that cross into later halos of a
+            // packed item step each lane forward
+            uint32_t hl = 0;
+            if (nhu > 1) {
+                hl = uni(upper_find(H.lstart, nhu, r0));
+                if (r0 + 63u >= H.lstart[hl + 1])
+                    while (hl + 1 < nhu && li >= H.lstart[hl + 1]) ++hl;
+            }
             uint32_t lo, hi;
             id_split<IDB>(idv[u], lo, hi);
-            uint32_t hl = H.nh == 1 ? 0u : upper_find(H.lstart, H.nh, li);
             TD r[3];
             uint32_t sgn;
             if (OA_ABL_FRAME) {
                 r[0] = (TD)xv[u].x - (TD)H.cb[hl][0]; r[1] = (TD)xv[u].y; r[2] = (TD)vv[u].z;
                 sgn = 1u;
+            } else if (!COMPARE && !OTF && a.vr_out) {
+                double vr;
+                sgn = frame<TX, TV, TD>(xv[u], vv[u], H.cb[hl], H.cf[hl], a, fk, r, &vr);
+                if (ok) a.vr_out[base + li] = vr;
             } else {
-                if (!COMPARE && !OTF && a.vr_out) {
-                    double vr;
-                    sgn = frame<TX, TV, TD>(xv[u], vv[u], H.cb[hl], a, fk, r, &vr);
-                    a.vr_out[base + li] = vr;
-                } else {
-                    sgn = OTF ? frame_otf<TX, TV, TD>(xv[u], vv[u], H.cb[hl], a, fk, r)
-                              : frame<TX, TV, TD>(xv[u], vv[u], H.cb[hl], a, fk, r);
-                }
+                sgn = OTF ? frame_otf<TX, TV, TD>(xv[u], vv[u], H.cb[hl], a, fk, r)
+                          : frame<TX, TV, TD>(xv[u], vv[u], H.cb[hl], H.cf[hl], a, fk, r);
             }
-            TD *ro = rhat_out + 3 * (base + li);
-            if (!OA_ABL_STORE1) { ro[0] = r[0]; ro[1] = r[1]; ro[2] = r[2]; }
-            else { asm volatile("" :: "v"(r[0]), "v"(r[1]), "v"(r[2])); }
+            if (!OA_ABL_STORE1) bst3<TD>(r_rh, li * SD, r);
+            else asm volatile("" :: "v"(r[0]), "v"(r[1]), "v"(r[2]));
             uint32_t ang = 0;
             if constexpr (!COMPARE) {
-                if (a.angles_in) ang = a.angles_in[base + li];
+                if (a.angles_in && ok) ang = a.angles_in[base + li];
             }
             const uint32_t meta = ang | (sgn << 16);
-            if (!join || !H.has_prev[hl]) { a.meta_out[base + li] = meta; continue; }
-            const uint32_t pos = li;
+            if (!COMPARE || !H.has_prev[hl]) { bst32(r_mt, li * 4u, meta); continue; }
+            if (!ok) continue;
             if (IDB == 8 && hi != hi0) H.nonuniform = 1u;     // benign race: all write 1
-            val[u] = slot_pack(lo, meta, pos);
+            val[u] = slot_pack(lo, meta, li);
             uint32_t cs[3];
             cuckoo_slots(lo, nslots, cs);
             sl[u] = cs[0];
@@ -655,9 +729,9 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             ins[u] = !OA_ABL_INSERT;
             if (OA_ABL_INSERT) asm volatile("" :: "v"(val[u]), "v"(sl[u]));
         }
-        // first try: claim an EMPTY candidate with a CAS (at load <= 1/2 one of the three
-        // almost always is), so eviction chains stay rare
-        {
+        if (COMPARE) {
+            // first try: claim an EMPTY candidate with a CAS (at load <= 1/2 one of the
+            // three almost always is), so eviction chains stay rare
             uint64_t c0[UNR1], c1[UNR1], c2[UNR1];
 #pragma unroll
             for (int u = 0; u < UNR1; ++u)
@@ -668,96 +742,57 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                 const uint32_t t = c0[u] == 0ull ? sl[u] : (c1[u] == 0ull ? cs1[u]
                                                           : (c2[u] == 0ull ? cs2[u] : 0xFFFFFFFFu));
                 if (t == 0xFFFFFFFFu) continue;
-                if (OA_ABL_CAS) { slots[t] = val[u]; ins[u] = false; continue; }
                 const uint64_t o = atomicCAS(reinterpret_cast<unsigned long long *>(&slots[t]),
                                              0ull, (unsigned long long)val[u]);
                 if (o == 0ull) ins[u] = false;
             }
-        }
-        // an entry whose three candidates are taken is deferred: the walks run after the
-        // loop, spread over the whole work-group, instead of stalling this wave per trip
-        if (!OA_IMMEDIATE_WALK) {
+            // an entry whose three candidates are taken is deferred: the walks run after
+            // the loop, spread over the whole work-group
 #pragma unroll
             for (int u = 0; u < UNR1; ++u) {
                 if (!ins[u]) continue;
                 const uint32_t e = atomicAdd(&H.npend, 1u);
-                if (e < pend_cap) { pend[e] = val[u]; ins[u] = false; }
-            }
-        }
-        // then the cuckoo walk: exchange into a candidate slot; an evicted entry moves
-        // on to its next candidate.  Every pending exchange is issued before any result
-        // is inspected; a chain longer than MAX_EVICT parks its entry in the stash.
-        for (int it_ = 0; !OA_ABL_WALK; ++it_) {
-            bool any = false;
-            uint64_t old[UNR1];
-#pragma unroll
-            for (int u = 0; u < UNR1; ++u)
-                if (ins[u]) old[u] = atomicExch(reinterpret_cast<unsigned long long *>(&slots[sl[u]]),
-                                                (unsigned long long)val[u]);
-#pragma unroll
-            for (int u = 0; u < UNR1; ++u) {
-                if (!ins[u]) continue;
-                if (old[u] == 0ull) { ins[u] = false; continue; }
-                uint32_t cs[3];
-                cuckoo_slots((uint32_t)old[u], nslots, cs);
-                const uint32_t j = cs[0] == sl[u] ? 1u : (cs[1] == sl[u] ? 2u : 0u);
-                val[u] = old[u];
-                sl[u] = cs[j];
-                any = true;
-            }
-            if (!any) break;
-            if (it_ == MAX_EVICT) {
-#pragma unroll
-                for (int u = 0; u < UNR1; ++u) {
-                    if (!ins[u]) continue;
-                    const uint32_t e = atomicAdd(&H.nstash, 1u);
-                    if (e < (uint32_t)STASH) H.stash[e] = val[u];
-                    else H.overflow = 2u;
-                    ins[u] = false;
-                }
-                break;
+                if (e < pend_cap) pend[e] = val[u];
+                else H.overflow = 2u;
             }
         }
 #pragma unroll
-        for (int u = 0; u < UNR1; ++u) {
-            idv[u] = idn[u]; xv[u] = xn[u]; vv[u] = vn[u];
-            if (PF1D == 2) { idn[u] = idm[u]; xn[u] = xm[u]; vn[u] = vm[u]; }
-        }
+        for (int u = 0; u < UNR1; ++u) { idv[u] = idn[u]; xv[u] = xn[u]; vv[u] = vn[u]; }
         t1 = t1n;
-        if (PF1D == 2) t1n = t1m;
+        t1n = trip_take(f1, t1n);
     }
 #undef OA_LOAD1
     STAMP(2);
     if constexpr (!COMPARE) return;
-    if (!join) return;
 
     // ---- phase 2: stream progenitor blocks, join, flag, angle, emit ---------
-    const uint32_t n_pv = H.n_pv, nseg = H.nseg;
+    // Rows are 64 virtual positions; progenitor segment s occupies
+    // [vstart[s], vstart[s] + seg_cnt[s]) and starts on a row, so a row lies in one
+    // segment: its halo, block offset and resources are uniform.
+    const uint32_t n_pv = uni(H.n_pv), nseg = uni(H.nseg);
     constexpr uint32_t T2 = 64 * UNR;                 // positions per wave trip
     const uint32_t ntr2 = (n_pv + T2 - 1) / T2;
     const uint64_t lanemask_lt = (1ull << lane) - 1ull;
     uint32_t running = 0;
     ID *scr_ids = reinterpret_cast<ID *>(a.scratch_ids);
 
-#define OA_LOAD2(PID, PRH, PMETA, KPOS, HLV, V0)                                  \
+#define OA_LOAD2(PID, PRH, PMETA, KB, HLV, NV, T)                                  \
     _Pragma("unroll") for (int u = 0; u < UNR; ++u) {                              \
-        const uint32_t vp_ = min((V0) * T2 + u * 64 + lane, n_pv - 1u);           \
-        const uint32_t sg_ = nseg == 1 ? 0u : upper_find(H.vstart, nseg, vp_);     \
-        HLV[u] = (uint32_t)H.seg_halo[sg_];                                        \
-        KPOS[u] = H.seg_prev_off[sg_] + (vp_ - H.vstart[sg_]);                     \
-        PID[u] = lds_nt(&ids_prev[KPOS[u]]);                                       \
-        PRH[u] = ld3_nt(rhat_prev, KPOS[u]);                                       \
-        PMETA[u] = lds_nt(&a.meta_prev[KPOS[u]]);                                  \
+        const uint32_t r0_ = (T) * T2 + u * 64;                                    \
+        uint32_t s_ = 0;                                                           \
+        if (nseg > 1) s_ = uni(upper_find(H.vstart, nseg, min(r0_, n_pv - 1u)));  \
+        const uint32_t ro_ = r0_ - uni(H.vstart[s_]), cnt_ = uni(H.seg_cnt[s_]);   \
+        NV[u] = (r0_ < n_pv && ro_ < cnt_) ? min(cnt_ - ro_, 64u) : 0u;            \
+        HLV[u] = uni((uint32_t)H.seg_halo[s_]);                                    \
+        KB[u] = uni64(H.seg_prev_off[s_]) + ro_;                                   \
+        PID[u] = bld<ID, AUX_NT>(make_rsrc(ids_prev + KB[u], NV[u] * IDB), lane * IDB);  \
+        PRH[u] = bld3<TD, AUX_NT>(make_rsrc(rhat_prev + 3 * KB[u], NV[u] * SD), lane * SD); \
+        PMETA[u] = bld<uint32_t, AUX_NT>(make_rsrc(a.meta_prev + KB[u], NV[u] * 4u), lane * 4u); \
     }
     ID pid[UNR], pidn[UNR];
     V3<TD> prh[UNR], prhn[UNR];
-    uint32_t pmeta[UNR], pmetan[UNR], hlv[UNR], hlvn[UNR];
-    int64_t kpos[UNR], kposn[UNR];
-    // The first trip's loads are issued BEFORE the phase-1/2 barrier.  The barrier
-    // then retires only this wave's older VMEM ops (its r̂/meta stores, which other
-    // waves gather in phase 2) with a counted vmcnt that leaves the 3 * UNR prefetch
-    // loads in flight, plus every LDS insert (lgkmcnt), then a raw s_barrier
-    // (a __syncthreads() would drain vmcnt to 0).
+    uint32_t pmeta[UNR], pmetan[UNR], hlv[UNR], hlvn[UNR], nv[UNR], nvn[UNR];
+    int64_t kb[UNR], kbn[UNR];
     // An item none of whose halos has a progenitor block has nothing to join (the
     // work-group-uniform exit keeps the prefetch below unconditional: a predicated
     // one makes the compiler copy the loaded registers and wait on them here).
@@ -789,8 +824,12 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
         }
     }
+    // The first trip's loads are issued BEFORE the phase-1/2 barrier.  The barrier
+    // then retires only this wave's older VMEM ops with a counted vmcnt that leaves
+    // the prefetch loads in flight, plus every LDS insert (lgkmcnt), then a raw
+    // s_barrier (a __syncthreads() would drain vmcnt to 0).
     __builtin_amdgcn_sched_barrier(0);
-    OA_LOAD2(pid, prh, pmeta, kpos, hlv, (uint32_t)wave)
+    OA_LOAD2(pid, prh, pmeta, kb, hlv, nv, (uint32_t)wave)
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(3 * UNR) : "memory");
     __builtin_amdgcn_s_barrier();
@@ -800,64 +839,68 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         if (tid == 0) atomicOr(a.status, OA_STATUS_TABLE_OVERFLOW);
         return;
     }
-    const bool nonuniform = IDB == 8 && H.nonuniform != 0;
+    const bool nonuniform = IDB == 8 && uni(H.nonuniform) != 0;
+    const uint32_t nstash = min(uni(H.nstash), (uint32_t)STASH);
     // one loop trip; the caller alternates two register sets (ping-pong), so the
     // prefetched trip never has to be copied into the current one
     auto trip = [&](ID (&pid)[UNR], V3<TD> (&prh)[UNR], uint32_t (&pmeta)[UNR],
-                    int64_t (&kpos)[UNR], uint32_t (&hlv)[UNR], ID (&pidn)[UNR],
-                    V3<TD> (&prhn)[UNR], uint32_t (&pmetan)[UNR], int64_t (&kposn)[UNR],
-                    uint32_t (&hlvn)[UNR], uint32_t t, uint32_t tn) __attribute__((always_inline)) {
-        const uint32_t v0 = t * T2;
-        bool ok[UNR];
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) ok[u] = v0 + u * 64 + lane < n_pv;
+                    int64_t (&kb)[UNR], uint32_t (&hlv)[UNR], uint32_t (&nv)[UNR],
+                    ID (&pidn)[UNR], V3<TD> (&prhn)[UNR], uint32_t (&pmetan)[UNR],
+                    int64_t (&kbn)[UNR], uint32_t (&hlvn)[UNR], uint32_t (&nvn)[UNR],
+                    uint32_t t, uint32_t tn) __attribute__((always_inline)) {
         // cuckoo lookup of (halo, id): the three candidate slots are read together (one
-        // LDS round trip); departed particles miss (setdiff1d/in1d, :300-304)
-        uint32_t lo[UNR], hi[UNR], lmin[UNR], lmax[UNR], hs[UNR];
+        // LDS round trip) and the match is selected without branches; departed
+        // particles miss (setdiff1d/in1d, :300-304).  The halo's position range tells
+        // copies of one ID in overlapping regions apart and rejects empty slots.
+        uint32_t lo[UNR];
+        bool can[UNR];
         uint64_t hit[UNR];
-        const uint32_t nstash = H.nstash;
+        uint32_t hs[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
-            hit[u] = 0ull;
-            hs[u] = 0;
-            if (!ok[u]) continue;
-            id_split<IDB>(pid[u], lo[u], hi[u]);
-            if (IDB == 8 && !nonuniform && hi[u] != hi0) continue;      // cannot be present
-            lmin[u] = H.lstart[hlv[u]];
-            lmax[u] = H.lstart[hlv[u] + 1] - lmin[u];                  // span length
+            uint32_t hi;
+            id_split<IDB>(pid[u], lo[u], hi);
+            can[u] = (uint32_t)lane < nv[u] && (IDB != 8 || nonuniform || hi == hi0);
+            const uint32_t lmin = uni(H.lstart[hlv[u]]);
+            const uint32_t lmax = uni(H.lstart[hlv[u] + 1]) - lmin;   // span length
             uint32_t cs[3];
             cuckoo_slots(lo[u], nslots, cs);
-            uint64_t c0 = slots[cs[0]], c1 = slots[cs[1]], c2 = slots[cs[2]];
-            auto match = [&](uint64_t v) {
-                const uint32_t p = slot_pos(v);
-                // the halo's position range also rejects empty slots (slot_pos(0) = ~0u)
-                bool m = (uint32_t)v == lo[u] && p - lmin[u] < lmax[u];
-                if (IDB == 8 && nonuniform && m)        // rare: confirm the full ID
-                    m = ids[base + p] == pid[u];
-                return m;
-            };
-            if (match(c0)) { hit[u] = c0; hs[u] = cs[0]; }
-            else if (match(c1)) { hit[u] = c1; hs[u] = cs[1]; }
-            else if (match(c2)) { hit[u] = c2; hs[u] = cs[2]; }
-            else if (nstash) {
-                for (uint32_t e = 0; e < nstash && e < (uint32_t)STASH; ++e)
-                    if (match(H.stash[e])) { hit[u] = H.stash[e]; hs[u] = nslots + e; break; }
+            const uint64_t c0 = slots[cs[0]], c1 = slots[cs[1]], c2 = slots[cs[2]];
+            auto m = [&](uint64_t v) { return (uint32_t)v == lo[u] && slot_pos(v) - lmin < lmax; };
+            const bool m0 = can[u] && m(c0), m1 = can[u] && m(c1), m2 = can[u] && m(c2);
+            if (IDB == 8 && nonuniform) {
+                // rare: candidates whose low word matches are confirmed on the full ID
+                hit[u] = 0ull; hs[u] = 0u;
+                if (m0 && ids[base + slot_pos(c0)] == pid[u]) { hit[u] = c0; hs[u] = cs[0]; }
+                else if (m1 && ids[base + slot_pos(c1)] == pid[u]) { hit[u] = c1; hs[u] = cs[1]; }
+                else if (m2 && ids[base + slot_pos(c2)] == pid[u]) { hit[u] = c2; hs[u] = cs[2]; }
+            } else {
+                hit[u] = m0 ? c0 : (m1 ? c1 : (m2 ? c2 : 0ull));
+                hs[u] = m0 ? cs[0] : (m1 ? cs[1] : cs[2]);
+            }
+            if (nstash) {
+                if (can[u] && !hit[u]) {
+                    for (uint32_t e = 0; e < nstash; ++e) {
+                        const uint64_t v = H.stash[e];
+                        if (m(v) && (!(IDB == 8 && nonuniform) || ids[base + slot_pos(v)] == pid[u])) {
+                            hit[u] = v; hs[u] = nslots + e;
+                            break;
+                        }
+                    }
+                }
             }
         }
-        // gather the matched current r̂ (written in phase 1: L2).  Unconditional
-        // (a miss re-reads the lane's own previous r̂) and issued BEFORE the next
-        // trip's prefetch: vmcnt retires in issue order, so the gather wait then
-        // leaves the prefetch in flight.
+        // gather the matched current r̂ (written in phase 1: L2).  Unconditional (a
+        // miss re-reads row 0) and issued BEFORE the next trip's prefetch: vmcnt
+        // retires in issue order, so the gather wait then leaves the prefetch in flight.
         V3<TD> cr[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
-            const uint32_t p = slot_pos(hit[u]);
-            const TD *src = (hit[u] && !OA_ABL_GATHER) ? rhat_out + 3 * (base + p)
-                                                       : rhat_prev + 3 * kpos[u];
-            cr[u] = V3<TD>{src[0], src[1], src[2]};
+            const uint32_t p = (hit[u] && !OA_ABL_GATHER) ? slot_pos(hit[u]) : 0u;
+            cr[u] = bld3<TD, 0>(r_rh, p * SD);
         }
         __builtin_amdgcn_sched_barrier(0);
-        OA_LOAD2(pidn, prhn, pmetan, kposn, hlvn, tn)   // unconditional (clamped)
+        OA_LOAD2(pidn, prhn, pmetan, kbn, hlvn, nvn, tn)   // unconditional (out of range: zeros)
         __builtin_amdgcn_sched_barrier(0);
         bool flag[UNR];
         uint16_t a16[UNR];
@@ -871,15 +914,15 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             const bool cond = a.mode == OA_MODE_PERICENTRIC ? (sp == 2u && sc == 1u)
                                                             : (sp == 1u && sc == 2u);
             // angle change = arccos(dot(r̂_prev, r̂_match)), no clamp (:324-325)
+            if (OA_ABL_GATHER) cr[u] = prh[u];
             TD dt = dot3(prh[u].x, prh[u].y, prh[u].z, cr[u].x, cr[u].y, cr[u].z);
             const TD change = OA_ABL_ACOS ? dt : acos_td(dt);
             uint16_t acc = angle_add((uint16_t)(pmeta[u] & 0xFFFFu), change);
             if (OTF) {
                 // on-the-fly outputs (track_orbits_onthefly.py:145-174): the angle
                 // change of every matched particle, and which current ones matched
-                static_cast<TD *>(a.angle_out)[kpos[u]] = change;
-                const uint32_t p = slot_pos(hit[u]);
-                a.matched_cur[base + p] = 1;
+                static_cast<TD *>(a.angle_out)[kb[u] + lane] = change;
+                a.matched_cur[base + slot_pos(hit[u])] = 1;
             }
             // calc_angles (:342-349): apsis angle emitted, then reset to 0
             if (!OA_ABL_SLOTW) {
@@ -892,60 +935,80 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         if (OTF) {
 #pragma unroll
             for (int u = 0; u < UNR; ++u)
-                if (ok[u]) a.matched_prev[kpos[u]] = hit[u] ? 1 : 0;
+                if ((uint32_t)lane < nv[u]) a.matched_prev[kb[u] + lane] = hit[u] ? 1 : 0;
         }
         // apsis records in previous-block order (:315-316): wave ballot + prefix
-        // popcount packs each 64-position segment's records at its own base;
-        // k_gather_items orders the segments (no work-group barrier here)
+        // popcount packs each 64-position row's records at its own scratch base;
+        // k_gather_items orders the rows (no work-group barrier here)
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
-            const uint64_t m = __ballot(flag[u]);
-            const uint32_t segpos = v0 + u * 64;                // multiple of 64
-            if (segpos < n_pv) {
+            const uint32_t r0 = t * T2 + u * 64;                // multiple of 64
+            if (r0 < n_pv) {
+                const uint64_t m = __ballot(flag[u]);
+                const uint32_t c = (uint32_t)__popcll(m);
+                const int64_t sb = it.scratch_off + r0;
                 if (flag[u] && !OA_ABL_EMIT) {
-                    const int64_t pos = it.scratch_off + segpos + __popcll(m & lanemask_lt);
-                    scr_ids[pos] = pid[u];
-                    a.scratch_ang[pos] = a16[u];
-                    atomicAdd(&H.halo_cnt[hlv[u]], 1);
+                    const uint32_t q = (uint32_t)__popcll(m & lanemask_lt);
+                    scr_ids[sb + q] = pid[u];
+                    a.scratch_ang[sb + q] = a16[u];
                 }
-                if (lane == 0) a.seg_count[(it.scratch_off + segpos) >> 6] = (uint8_t)__popcll(m);
-                running += (uint32_t)__popcll(m);
+                if (lane == 0) {
+                    a.seg_count[sb >> 6] = (uint8_t)c;
+                    if (c && !OA_ABL_EMIT) atomicAdd(&H.halo_cnt[hlv[u]], (int)c);
+                }
+                running += c;
             }
         }
     };
-    uint32_t t2 = wave;
+    uint32_t t2 = wave, tn = wave + NWAVE;
     while (t2 < ntr2) {
-        uint32_t tn = next_trip(&H.ctr2, t2, lane);
-        trip(pid, prh, pmeta, kpos, hlv, pidn, prhn, pmetan, kposn, hlvn, t2, tn);
+        uint32_t f2 = trip_fetch(&H.ctr2, lane);
+        trip(pid, prh, pmeta, kb, hlv, nv, pidn, prhn, pmetan, kbn, hlvn, nvn, t2, tn);
         if (tn >= ntr2) break;
         t2 = tn;
-        tn = next_trip(&H.ctr2, t2, lane);
-        trip(pidn, prhn, pmetan, kposn, hlvn, pid, prh, pmeta, kpos, hlv, t2, tn);
+        tn = trip_take(f2, tn);
+        f2 = trip_fetch(&H.ctr2, lane);
+        trip(pidn, prhn, pmetan, kbn, hlvn, nvn, pid, prh, pmeta, kb, hlv, nv, t2, tn);
         t2 = tn;
+        tn = trip_take(f2, tn);
     }
 #undef OA_LOAD2
     if (lane == 0) atomicAdd(&H.chunk_total, running);
     STAMP(4);
     __syncthreads();
 
-    // ---- phase 3: meta words of the joined particles -----------------------------
-    const uint32_t nst = min(H.nstash, (uint32_t)STASH);
-    // position -> slot map (halos without a progenitor block: not in the table, their
-    // meta was stored in phase 1), then coalesced stores in position order
-    for (uint32_t w = tid; w < nslots + nst; w += WG) {
-        const uint64_t v = w < nslots ? slots[w] : H.stash[w - nslots];
-        if (v) slotmap[slot_pos(v)] = (uint16_t)w;
-    }
-    for (uint32_t k = 0; k < (uint32_t)nh; ++k)
-        if (!H.has_prev[k])
-            for (uint32_t li = H.lstart[k] + tid; li < H.lstart[k + 1]; li += WG)
-                slotmap[li] = 0xFFFFu;
-    __syncthreads();
-    for (uint32_t li = tid; li < n_span; li += WG) {
-        const uint32_t w = slotmap[li];
-        if (w == 0xFFFFu) continue;
-        const uint64_t v = w < nslots ? slots[w] : H.stash[w - nslots];
-        if (!OA_ABL_PHASE3) a.meta_out[base + li] = slot_meta(v);
+    // ---- phase 3: state words of the joined particles, in position order ----------
+    // Every table entry's word goes to pm[pos], a position-indexed array that overlays
+    // the first ceil(n_span / 2) slots (4 B per position): those slots are read into
+    // registers first (<= P3R per thread), the others and the stash are read after
+    // the barrier (pm never reaches them), then pm is stored out coalesced.
+    {
+        uint32_t *pm = reinterpret_cast<uint32_t *>(slots);
+        const uint32_t nst = min(H.nstash, (uint32_t)STASH);
+        const uint32_t nlow = min((n_span + 1) / 2, nslots);
+        uint64_t keep[P3R];
+#pragma unroll
+        for (int r = 0; r < P3R; ++r) {
+            const uint32_t w = tid + r * WG;
+            keep[r] = w < nlow ? slots[w] : 0ull;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < P3R; ++r)
+            if (keep[r]) pm[slot_pos(keep[r])] = slot_meta(keep[r]);
+        for (uint32_t w = nlow + tid; w < nslots + nst; w += WG) {
+            const uint64_t v = w < nslots ? slots[w] : H.stash[w - nslots];
+            if (v) pm[slot_pos(v)] = slot_meta(v);
+        }
+        __syncthreads();
+        // halos without a progenitor block are not in the table: their words were
+        // stored in phase 1
+        for (uint32_t k = 0; k < (uint32_t)nh; ++k) {
+            if (!H.has_prev[k]) continue;
+            const uint32_t e = H.lstart[k + 1];
+            for (uint32_t li = H.lstart[k] + tid; li < e; li += WG)
+                if (!OA_ABL_PHASE3) a.meta_out[base + li] = pm[li];
+        }
     }
     if (tid < nh) {
         const oa_halo &h = a.halos[it.h0 + tid];
@@ -1277,8 +1340,11 @@ __global__ __launch_bounds__(BIG_WG) void k_big_frame(const oa_step_args a, cons
     const oa_item it = a.items[gi];
     const oa_halo &h = a.halos[it.h0];
     double cb[6];
+    float cf[6];
 #pragma unroll
     for (int d = 0; d < 3; ++d) { cb[d] = h.centre[d]; cb[3 + d] = h.bulk[d]; }
+#pragma unroll
+    for (int d = 0; d < 6; ++d) cf[d] = (float)cb[d];
     const int64_t base = h.cur_off;
     const bool ins = COMPARE && h.prev_cnt >= 0;
     const ID *ids = static_cast<const ID *>(a.ids);
@@ -1297,7 +1363,7 @@ __global__ __launch_bounds__(BIG_WG) void k_big_frame(const oa_step_args a, cons
         const V3<TV> v = ld3_nt(vs, i);
         TD r[3];
         const uint32_t sgn = OTF ? frame_otf<TX, TV, TD>(x, v, cb, a, fk, r)
-                                 : frame<TX, TV, TD>(x, v, cb, a, fk, r);
+                                 : frame<TX, TV, TD>(x, v, cb, cf, a, fk, r);
         TD *ro = rhat_out + 3 * i;
         ro[0] = r[0]; ro[1] = r[1]; ro[2] = r[2];
         uint32_t ang = 0;
@@ -1477,6 +1543,7 @@ int oa_step(const oa_step_args *args, void *stream) {
     if (a.mode != OA_MODE_PERICENTRIC && a.mode != OA_MODE_APOCENTRIC)
         return fail(OA_E_ARG, "bad mode");
     if (a.n_items > 0 && (a.lds_entries <= 0 || a.lds_entries > (int)MAX_POS + 1 ||
+                          a.lds_entries > 2 * P3R * WG ||
                           a.lds_slots <= a.lds_entries))
         return fail(OA_E_ARG, "bad lds_entries/lds_slots (entries <= %u < slots)", MAX_POS + 1);
     if (a.n_items + a.n_global_items > 0 &&

@@ -137,7 +137,9 @@ def plan_items(cur_cnt, prev_cnt, entries, hmax=128):
     memory by as many work-groups as it has chunks (k_big_frame / k_big_join).
 
     Returns (items, global_items, scratch): ITEM_DTYPE arrays and the apsis-scratch
-    size (64-slot segments per item, global items after the packed ones)."""
+    size (64-slot segments per item, global items after the packed ones).  An item's
+    ``n_pv`` counts its progenitor rows of 64 virtual positions: every progenitor block
+    is padded to whole rows, so a row of k_step's phase 2 lies in one block."""
     nh = len(cur_cnt)
     small, glob = [], []
     scratch = 0
@@ -145,19 +147,19 @@ def plan_items(cur_cnt, prev_cnt, entries, hmax=128):
     pc = np.maximum(prev_cnt, 0)
     while j < nh:
         if cur_cnt[j] > entries:
-            glob.append((j, j + 1, 0, 1, 0, pc[j]))
+            glob.append((j, j + 1, 0, 1, 0, (pc[j] + 63) // 64 * 64))
             j += 1
             continue
         start, tot, ptot = j, 0, 0
         while j < nh and j - start < hmax and tot + cur_cnt[j] <= entries:
             tot += cur_cnt[j]
-            ptot += pc[j]
+            ptot += (pc[j] + 63) // 64 * 64      # each progenitor block starts a 64-row
             j += 1
         small.append((start, j, 0, 1, scratch, ptot))
-        scratch += (ptot + 63) // 64 * 64           # 64-slot segments per item
+        scratch += ptot                          # one 64-slot scratch segment per row
     for k, g in enumerate(glob):
         glob[k] = g[:4] + (scratch, g[5])
-        scratch += (g[5] + 63) // 64 * 64
+        scratch += g[5]
     it = np.array(small, dtype=N.ITEM_DTYPE) if small else np.zeros(0, N.ITEM_DTYPE)
     gt = np.array(glob, dtype=N.ITEM_DTYPE) if glob else np.zeros(0, N.ITEM_DTYPE)
     return it, gt, scratch

@@ -113,7 +113,7 @@ def test_plan_items_invariants():
     assert np.all(covered == 1)
     segs = 0
     for it in np.concatenate([items, glob]):
-        assert it['n_pv'] == np.maximum(prev[it['h0']:it['h1']], 0).sum()
+        assert it['n_pv'] == ((np.maximum(prev[it['h0']:it['h1']], 0) + 63) // 64 * 64).sum()
         assert it['scratch_off'] % 64 == 0 and it['scratch_off'] == segs
         segs += (int(it['n_pv']) + 63) // 64 * 64
     assert scratch == segs
