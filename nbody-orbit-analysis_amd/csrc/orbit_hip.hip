@@ -149,12 +149,17 @@ template <typename T> __device__ __forceinline__ T lds_nt(const T *p) {
 #endif
 #if OA_STAMPS
 // diagnostic build only: per-work-group s_memrealtime (100 MHz) at phase boundaries
-constexpr int STAMP_MAX_WG = 1 << 16, STAMP_N = 6;
+// plus, per wave, the ends of its phase-1 and phase-2 loops (WSTAMP 0/1)
+constexpr int STAMP_MAX_WG = 1 << 16, STAMP_N = 6 + 2 * (OA_WG / 64);
 __device__ uint64_t g_stamps[STAMP_MAX_WG * STAMP_N];
 #define STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < STAMP_MAX_WG) \
     g_stamps[blockIdx.x * STAMP_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define WSTAMP(k) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < STAMP_MAX_WG) \
+    g_stamps[blockIdx.x * STAMP_N + 6 + 2 * (threadIdx.x >> 6) + (k)] = \
+        __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define STAMP(k) do { } while (0)
+#define WSTAMP(k) do { } while (0)
 #endif
 
 template <typename T> struct V3 { T x, y, z; };
@@ -337,9 +342,10 @@ __device__ __forceinline__ void unit_vector(const TD dx[3], TD r[3]) {
         // than 2^-50 to a float32 rounding midpoint -- so rounding q to
         // float32 gives RN(dx / rr) exactly.  Valid for normal quotients and a normal
         // rr; any other wave takes the IEEE division.
-        bool fast = rr >= 0x1p-100f && rr <= 0x1p100f;
+        const float qmin = rr * 0x1p-100f;
+        bool fast = (rr >= 0x1p-100f) & (rr <= 0x1p100f);
 #pragma unroll
-        for (int d = 0; d < 3; ++d) fast = fast && (dx[d] == 0.f || fabsf(dx[d]) >= rr * 0x1p-100f);
+        for (int d = 0; d < 3; ++d) fast = fast & ((dx[d] == 0.f) | (fabsf(dx[d]) >= qmin));
         if (__all(fast)) {
             const double b = (double)rr;
             double y = __builtin_amdgcn_rcp(b);
@@ -389,13 +395,21 @@ __device__ __forceinline__ uint32_t frame(const V3<TX> &x, const V3<TV> &v, cons
     // recenter_coordinates (utils.py:24-33): one strict wrap per dimension, in the
     // promoted dtype of (dx, box); the float64 arithmetic runs only in waves where
     // some particle crosses the box edge
+    if (a.n_box_dims > 0) {
+        // one wave-level test for the common case (no particle beyond half a box)
+        bool w = false;
 #pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        if (d < a.n_box_dims) {
-            bool h = WrapT<TD>::hi(dx[d], a, k, d);
-            if (__any(h)) { if (h) dx[d] = wrap_sub(dx[d], a, d); }
-            bool l = WrapT<TD>::lo(dx[d], a, k, d);
-            if (__any(l)) { if (l) dx[d] = wrap_add(dx[d], a, d); }
+        for (int d = 0; d < 3; ++d)
+            if (d < a.n_box_dims)
+                w = w | WrapT<TD>::hi(dx[d], a, k, d) | WrapT<TD>::lo(dx[d], a, k, d);
+        if (__any(w)) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                if (d < a.n_box_dims) {
+                    if (WrapT<TD>::hi(dx[d], a, k, d)) dx[d] = wrap_sub(dx[d], a, d);
+                    if (WrapT<TD>::lo(dx[d], a, k, d)) dx[d] = wrap_add(dx[d], a, d);
+                }
+            }
         }
     }
     // rads = sqrt(dot(dx, dx)); rhats = dx / rads   (:286-287), exact in dx's dtype
@@ -584,7 +598,10 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     const uint32_t pend_cap = (uint32_t)a.lds_entries / 4u;
 
     const oa_item it = a.items[blockIdx.x];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // the wave index is uniform: readfirstlane lets every trip / row quantity derived
+    // from it live in SGPRs (scalar arithmetic, scalar branches)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const ID *ids = reinterpret_cast<const ID *>(a.ids);
     const ID *ids_prev = reinterpret_cast<const ID *>(a.ids_prev);
     TD *rhat_out = reinterpret_cast<TD *>(a.rhat_out);
@@ -762,6 +779,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         t1n = trip_take(f1, t1n);
     }
 #undef OA_LOAD1
+    WSTAMP(0);
     STAMP(2);
     if constexpr (!COMPARE) return;
 
@@ -973,6 +991,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         tn = trip_take(f2, tn);
     }
 #undef OA_LOAD2
+    WSTAMP(1);
     if (lane == 0) atomicAdd(&H.chunk_total, running);
     STAMP(4);
     __syncthreads();

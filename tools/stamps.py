@@ -32,11 +32,20 @@ for rep in range(3):
     eng.launch(p1, ws, St(s0['ids'], p0.rhat, p0.meta))
 torch.cuda.synchronize()
 ni = len(p1.items)
-buf = np.zeros(ni * 6, dtype=np.uint64)
+nw = eng.lib.oa_build_info(0) // 64
+sn = 6 + 2 * nw
+buf = np.zeros(ni * sn, dtype=np.uint64)
 got = eng.lib.oa_debug_stamps(buf.ctypes.data, buf.size)
 assert got > 0, 'not a stamps build'
-t = buf.reshape(ni, 6).astype(np.float64) * 10.0 / 1000.0   # 100 MHz -> us
-t -= t[:, 0].min()
+tw = buf.reshape(ni, sn).astype(np.float64) * 10.0 / 1000.0   # 100 MHz -> us
+tw -= tw[:, 0].min()
+t = tw[:, :6]
+w1, w2 = tw[:, 6::2], tw[:, 7::2]                  # per-wave ends of the phase-1 / 2 loops
+for name, w in (('wave skew phase1 end', w1), ('wave skew phase2 end', w2)):
+    d = w.max(1) - w.min(1)
+    m = w.max(1) - w.mean(1)
+    print('%-22s max-min mean %6.2f p90 %6.2f | max-mean mean %6.2f us'
+          % (name, d.mean(), np.percentile(d, 90), m.mean()))
 start, span = t[:, 0], t[:, 5] - t[:, 0]
 print('items', ni, 'kernel span %.1f us' % (t[:, 5].max()))
 for name, a, b in (('phase0', 0, 1), ('phase1(t0)', 1, 2), ('barrier1', 2, 3),
