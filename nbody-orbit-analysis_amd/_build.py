@@ -11,6 +11,9 @@ HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-shared',
          # the reference's NumPy arithmetic rounds every product and sum: no FMA
          '-ffp-contract=off', '-fno-fast-math',
+         # the work-counter atomics are issued a loop trip before their results are
+         # used: the atomic optimizer's wave-reduction rewrite would wait on them at once
+         '-mllvm', '-amdgpu-atomic-optimizer-strategy=None',
          '-I' + os.path.join(ROOT, 'include')]
 
 

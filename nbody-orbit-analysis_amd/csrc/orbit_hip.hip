@@ -302,6 +302,7 @@ struct FrameK {
     float h_f;             // RN32(H / (1 + z)): Hubble factor of the f32 sign filter
     float wrap_hi[3];      // smallest float32 with  dx >  L/2  (float32 dx plans)
     float wrap_lo[3];      // largest  float32 with  dx < -L/2
+    float wrap_abs[3];     // min(wrap_hi, -wrap_lo): |dx| below it never wraps
 };
 
 template <typename TD> struct WrapT;
@@ -334,19 +335,27 @@ __device__ __forceinline__ TD wrap_add(TD dx, const oa_step_args &a, int d) {
 // rads = sqrt(dot(dx, dx)); r̂ = dx / rads, correctly rounded in TD.
 template <typename TD>
 __device__ __forceinline__ void unit_vector(const TD dx[3], TD r[3]) {
-    TD rr = sqrt(dot3(dx[0], dx[1], dx[2], dx[0], dx[1], dx[2]));
     if constexpr (std::is_same<TD, float>::value) {
-        // Correctly rounded float32 quotients from ONE float64 reciprocal: with
-        // y = 1/rr to 2^-52 (v_rcp_f64 + two Newton steps), q = dx * y is within
-        // 2^-51 (relative) of dx / rr, while a quotient of two floats is never closer
-        // than 2^-50 to a float32 rounding midpoint -- so rounding q to
-        // float32 gives RN(dx / rr) exactly.  Valid for normal quotients and a normal
-        // rr; any other wave takes the IEEE division.
-        const float qmin = rr * 0x1p-100f;
-        bool fast = (rr >= 0x1p-100f) & (rr <= 0x1p100f);
+        const float s = dot3(dx[0], dx[1], dx[2], dx[0], dx[1], dx[2]);
+        // Fast path for waves whose s lies in [2^-96, 2^100] and whose nonzero
+        // components are >= 2^-75 (so rr is normal and every quotient >= 2^-125 is a
+        // normal float); any other wave takes sqrtf and the IEEE division.
+        //  * rr = RN(sqrt(s)): v_sqrt_f32 (<= 1 ulp) and a residual test on each
+        //    neighbour -- the compiler's IEEE expansion without the denormal scaling
+        //    and special-value handling, which such an s never needs.
+        //  * r̂ = RN(dx / rr) from ONE float64 reciprocal: with y = 1/rr to 2^-52
+        //    (v_rcp_f64 + two Newton steps), q = dx * y is within 2^-51 (relative) of
+        //    dx / rr, while a quotient of two floats is never closer than 2^-50 to a
+        //    float32 rounding midpoint, so rounding q gives RN(dx / rr).
+        bool fast = (s >= 0x1p-96f) & (s <= 0x1p100f);
 #pragma unroll
-        for (int d = 0; d < 3; ++d) fast = fast & ((dx[d] == 0.f) | (fabsf(dx[d]) >= qmin));
+        for (int d = 0; d < 3; ++d) fast = fast & ((dx[d] == 0.f) | (fabsf(dx[d]) >= 0x1p-75f));
         if (__all(fast)) {
+            const float r0 = __builtin_amdgcn_sqrtf(s);
+            const float rm = __uint_as_float(__float_as_uint(r0) - 1u);
+            const float rp = __uint_as_float(__float_as_uint(r0) + 1u);
+            float rr = __builtin_fmaf(-rm, r0, s) <= 0.f ? rm : r0;
+            rr = __builtin_fmaf(-rp, r0, s) > 0.f ? rp : rr;
             const double b = (double)rr;
             double y = __builtin_amdgcn_rcp(b);
             double e = __builtin_fma(-b, y, 1.0);
@@ -356,9 +365,11 @@ __device__ __forceinline__ void unit_vector(const TD dx[3], TD r[3]) {
 #pragma unroll
             for (int d = 0; d < 3; ++d) r[d] = (TD)((double)dx[d] * y);
         } else {
+            const float rr = sqrtf(s);
             r[0] = dx[0] / rr; r[1] = dx[1] / rr; r[2] = dx[2] / rr;
         }
     } else {
+        const TD rr = sqrt(dot3(dx[0], dx[1], dx[2], dx[0], dx[1], dx[2]));
         r[0] = dx[0] / rr; r[1] = dx[1] / rr; r[2] = dx[2] / rr;
     }
 }
@@ -399,9 +410,12 @@ __device__ __forceinline__ uint32_t frame(const V3<TX> &x, const V3<TV> &v, cons
         // one wave-level test for the common case (no particle beyond half a box)
         bool w = false;
 #pragma unroll
-        for (int d = 0; d < 3; ++d)
-            if (d < a.n_box_dims)
-                w = w | WrapT<TD>::hi(dx[d], a, k, d) | WrapT<TD>::lo(dx[d], a, k, d);
+        for (int d = 0; d < 3; ++d) {
+            if (d < a.n_box_dims) {
+                if constexpr (sizeof(TD) == 4) w = w | (fabsf(dx[d]) >= k.wrap_abs[d]);
+                else w = w | WrapT<TD>::hi(dx[d], a, k, d) | WrapT<TD>::lo(dx[d], a, k, d);
+            }
+        }
         if (__any(w)) {
 #pragma unroll
             for (int d = 0; d < 3; ++d) {
@@ -416,13 +430,16 @@ __device__ __forceinline__ uint32_t frame(const V3<TX> &x, const V3<TV> &v, cons
     unit_vector(dx, r);
     // sign filter: w = (v - bulk) + (H * dx) / (1 + z), v_r = dot(w, r̂)   (:275-288)
     const TV vv[3] = {v.x, v.y, v.z};
+    // error scale: sum_i |vb_i| + |h_i| bounds sum_i |r_i| (|vb_i| + |h_i|) since
+    // |r_i| <= 1 + 2^-23, and the 2^-16 threshold leaves a margin of 2^4 over the
+    // float32 evaluation error
     float wf[3], sc = 0.f;
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
         float vb = a.vb_f64 ? (float)((double)vv[d] - cb[3 + d]) : (float)vv[d] - cf[3 + d];
         float hf = k.h_f * (float)dx[d];
         wf[d] = vb + hf;
-        sc += fabsf((float)r[d]) * (fabsf(vb) + fabsf(hf));
+        sc += fabsf(vb) + fabsf(hf);
     }
     const float vrf = (wf[0] * (float)r[0] + wf[1] * (float)r[1]) + wf[2] * (float)r[2];
     const bool sure = fabsf(vrf) > sc * 0x1p-16f;
@@ -617,7 +634,9 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         const oa_halo &h = a.halos[it.h0 + tid];
         const oa_halo &h0 = a.halos[it.h0];
         H.lstart[tid] = (uint32_t)(h.cur_off - h0.cur_off);
-        H.has_prev[tid] = COMPARE && h.prev_cnt >= 0;
+        // joined halos: those with a non-empty progenitor block (an empty one matches
+        // nothing: its particles keep angle 0, written in phase 1)
+        H.has_prev[tid] = COMPARE && h.prev_cnt > 0;
         H.halo_cnt[tid] = 0;
         for (int d = 0; d < 3; ++d) { H.cb[tid][d] = h.centre[d]; H.cb[tid][3 + d] = h.bulk[d]; }
         for (int d = 0; d < 3; ++d) { H.cf[tid][d] = (float)h.centre[d]; H.cf[tid][3 + d] = (float)h.bulk[d]; }
@@ -630,7 +649,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     if (tid == 0) {
         H.nonuniform = 0; H.overflow = 0; H.nh = nh; H.chunk_total = 0; H.nstash = 0;
         H.npend = 0;
-        H.ctr1 = 2 * NWAVE; H.ctr2 = 2 * NWAVE;   // trips wave, wave + NWAVE are static
+        // static first trips: phase 1 wave, wave + NWAVE; phase 2 also wave + 2 NWAVE
+        H.ctr1 = 2 * NWAVE; H.ctr2 = 3 * NWAVE;
         // progenitor segments in halo order (serial: nh <= HMAX); each starts on a
         // 64-position row of the virtual (padded) progenitor space
         uint32_t ns = 0, vp = 0;
@@ -647,7 +667,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         uint32_t nj = 0;
         for (int k = 0; k < nh; ++k) {
             const oa_halo &h = a.halos[it.h0 + k];
-            if (COMPARE && h.prev_cnt >= 0) nj += (uint32_t)h.cur_cnt;
+            if (COMPARE && h.prev_cnt > 0) nj += (uint32_t)h.cur_cnt;
         }
         uint32_t ns_eff = nj * OA_SLOT_X2 / 2 + 64;
         H.nsl = ns_eff > nslots_max ? nslots_max : ns_eff;
@@ -794,23 +814,45 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     uint32_t running = 0;
     ID *scr_ids = reinterpret_cast<ID *>(a.scratch_ids);
 
-#define OA_LOAD2(PID, PRH, PMETA, KB, HLV, NV, T)                                  \
-    _Pragma("unroll") for (int u = 0; u < UNR; ++u) {                              \
-        const uint32_t r0_ = (T) * T2 + u * 64;                                    \
-        uint32_t s_ = 0;                                                           \
-        if (nseg > 1) s_ = uni(upper_find(H.vstart, nseg, min(r0_, n_pv - 1u)));  \
-        const uint32_t ro_ = r0_ - uni(H.vstart[s_]), cnt_ = uni(H.seg_cnt[s_]);   \
-        NV[u] = (r0_ < n_pv && ro_ < cnt_) ? min(cnt_ - ro_, 64u) : 0u;            \
-        HLV[u] = uni((uint32_t)H.seg_halo[s_]);                                    \
-        KB[u] = uni64(H.seg_prev_off[s_]) + ro_;                                   \
-        PID[u] = bld<ID, AUX_NT>(make_rsrc(ids_prev + KB[u], NV[u] * IDB), lane * IDB);  \
-        PRH[u] = bld3<TD, AUX_NT>(make_rsrc(rhat_prev + 3 * KB[u], NV[u] * SD), lane * SD); \
-        PMETA[u] = bld<uint32_t, AUX_NT>(make_rsrc(a.meta_prev + KB[u], NV[u] * 4u), lane * 4u); \
-    }
-    ID pid[UNR], pidn[UNR];
-    V3<TD> prh[UNR], prhn[UNR];
-    uint32_t pmeta[UNR], pmetan[UNR], hlv[UNR], hlvn[UNR], nv[UNR], nvn[UNR];
-    int64_t kb[UNR], kbn[UNR];
+    // three register sets of streamed rows (ids, r̂, meta and the row's uniform
+    // segment data) and two of lookup results rotate through a 3-stage pipeline:
+    // trip t+2 loads, trip t+1 looks up and gathers, trip t computes and emits
+    struct Rows {
+        ID pid[UNR];
+        V3<TD> prh[UNR];
+        uint32_t pmeta[UNR], hlv[UNR], nv[UNR];
+        int64_t kb[UNR];
+    };
+    struct Look {
+        uint64_t hit[UNR];
+        uint32_t hs[UNR];
+        V3<TD> cr[UNR];
+    };
+    // segment 0 in SGPRs: single-segment items (one joined halo) never touch LDS for
+    // their row set-up
+    const uint32_t cnt0 = uni(H.seg_cnt[0]), hal0 = uni((uint32_t)H.seg_halo[0]);
+    const int64_t off0 = uni64(H.seg_prev_off[0]);
+    auto load_rows = [&](Rows &S, uint32_t T) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const uint32_t r0 = T * T2 + u * 64;
+            uint32_t ro = r0, cnt = cnt0, hs = hal0;
+            int64_t off = off0;
+            if (nseg > 1) {
+                const uint32_t s = uni(upper_find(H.vstart, nseg, min(r0, n_pv - 1u)));
+                ro = r0 - uni(H.vstart[s]);
+                cnt = uni(H.seg_cnt[s]);
+                hs = uni((uint32_t)H.seg_halo[s]);
+                off = uni64(H.seg_prev_off[s]);
+            }
+            S.nv[u] = (r0 < n_pv && ro < cnt) ? min(cnt - ro, 64u) : 0u;
+            S.hlv[u] = hs;
+            S.kb[u] = off + ro;
+            S.pid[u] = bld<ID, AUX_NT>(make_rsrc(ids_prev + S.kb[u], S.nv[u] * IDB), lane * IDB);
+            S.prh[u] = bld3<TD, AUX_NT>(make_rsrc(rhat_prev + 3 * S.kb[u], S.nv[u] * SD), lane * SD);
+            S.pmeta[u] = bld<uint32_t, AUX_NT>(make_rsrc(a.meta_prev + S.kb[u], S.nv[u] * 4u), lane * 4u);
+        }
+    };
     // An item none of whose halos has a progenitor block has nothing to join (the
     // work-group-uniform exit keeps the prefetch below unconditional: a predicated
     // one makes the compiler copy the loaded registers and wait on them here).
@@ -842,12 +884,14 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
         }
     }
+    Rows SA, SB, SC;
+    Look LA, LB;
     // The first trip's loads are issued BEFORE the phase-1/2 barrier.  The barrier
     // then retires only this wave's older VMEM ops with a counted vmcnt that leaves
     // the prefetch loads in flight, plus every LDS insert (lgkmcnt), then a raw
     // s_barrier (a __syncthreads() would drain vmcnt to 0).
     __builtin_amdgcn_sched_barrier(0);
-    OA_LOAD2(pid, prh, pmeta, kb, hlv, nv, (uint32_t)wave)
+    load_rows(SA, (uint32_t)wave);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(3 * UNR) : "memory");
     __builtin_amdgcn_s_barrier();
@@ -859,92 +903,83 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     }
     const bool nonuniform = IDB == 8 && uni(H.nonuniform) != 0;
     const uint32_t nstash = min(uni(H.nstash), (uint32_t)STASH);
-    // one loop trip; the caller alternates two register sets (ping-pong), so the
-    // prefetched trip never has to be copied into the current one
-    auto trip = [&](ID (&pid)[UNR], V3<TD> (&prh)[UNR], uint32_t (&pmeta)[UNR],
-                    int64_t (&kb)[UNR], uint32_t (&hlv)[UNR], uint32_t (&nv)[UNR],
-                    ID (&pidn)[UNR], V3<TD> (&prhn)[UNR], uint32_t (&pmetan)[UNR],
-                    int64_t (&kbn)[UNR], uint32_t (&hlvn)[UNR], uint32_t (&nvn)[UNR],
-                    uint32_t t, uint32_t tn) __attribute__((always_inline)) {
-        // cuckoo lookup of (halo, id): the three candidate slots are read together (one
-        // LDS round trip) and the match is selected without branches; departed
-        // particles miss (setdiff1d/in1d, :300-304).  The halo's position range tells
-        // copies of one ID in overlapping regions apart and rejects empty slots.
-        uint32_t lo[UNR];
-        bool can[UNR];
-        uint64_t hit[UNR];
-        uint32_t hs[UNR];
+    // cuckoo lookup of (halo, id) for one trip of rows, then the gather of the matched
+    // current r̂ rows (written in phase 1: L2).  The three candidate slots are read
+    // together (one LDS round trip) and the match is selected without branches;
+    // departed particles miss (setdiff1d/in1d, :300-304).  The halo's position range
+    // tells copies of one ID in overlapping regions apart and rejects empty slots.
+    // The gather is unconditional (a miss re-reads row 0).
+    auto lookup = [&](const Rows &S, Look &L) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
-            uint32_t hi;
-            id_split<IDB>(pid[u], lo[u], hi);
-            can[u] = (uint32_t)lane < nv[u] && (IDB != 8 || nonuniform || hi == hi0);
-            const uint32_t lmin = uni(H.lstart[hlv[u]]);
-            const uint32_t lmax = uni(H.lstart[hlv[u] + 1]) - lmin;   // span length
+            uint32_t lo, hi;
+            id_split<IDB>(S.pid[u], lo, hi);
+            const bool can = ((uint32_t)lane < S.nv[u]) & (IDB != 8 || nonuniform || hi == hi0);
+            uint32_t lmin = 0, lmax = n_span;                 // the halo's position span
+            if (nhu > 1) {
+                lmin = uni(H.lstart[S.hlv[u]]);
+                lmax = uni(H.lstart[S.hlv[u] + 1]) - lmin;
+            }
             uint32_t cs[3];
-            cuckoo_slots(lo[u], nslots, cs);
+            cuckoo_slots(lo, nslots, cs);
             const uint64_t c0 = slots[cs[0]], c1 = slots[cs[1]], c2 = slots[cs[2]];
-            auto m = [&](uint64_t v) { return (uint32_t)v == lo[u] && slot_pos(v) - lmin < lmax; };
-            const bool m0 = can[u] && m(c0), m1 = can[u] && m(c1), m2 = can[u] && m(c2);
+            auto m = [&](uint64_t v) { return ((uint32_t)v == lo) & (slot_pos(v) - lmin < lmax); };
+            const bool m0 = can & m(c0), m1 = can & m(c1), m2 = can & m(c2);
             if (IDB == 8 && nonuniform) {
                 // rare: candidates whose low word matches are confirmed on the full ID
-                hit[u] = 0ull; hs[u] = 0u;
-                if (m0 && ids[base + slot_pos(c0)] == pid[u]) { hit[u] = c0; hs[u] = cs[0]; }
-                else if (m1 && ids[base + slot_pos(c1)] == pid[u]) { hit[u] = c1; hs[u] = cs[1]; }
-                else if (m2 && ids[base + slot_pos(c2)] == pid[u]) { hit[u] = c2; hs[u] = cs[2]; }
+                L.hit[u] = 0ull; L.hs[u] = 0u;
+                if (m0 && ids[base + slot_pos(c0)] == S.pid[u]) { L.hit[u] = c0; L.hs[u] = cs[0]; }
+                else if (m1 && ids[base + slot_pos(c1)] == S.pid[u]) { L.hit[u] = c1; L.hs[u] = cs[1]; }
+                else if (m2 && ids[base + slot_pos(c2)] == S.pid[u]) { L.hit[u] = c2; L.hs[u] = cs[2]; }
             } else {
-                hit[u] = m0 ? c0 : (m1 ? c1 : (m2 ? c2 : 0ull));
-                hs[u] = m0 ? cs[0] : (m1 ? cs[1] : cs[2]);
+                L.hit[u] = m0 ? c0 : (m1 ? c1 : (m2 ? c2 : 0ull));
+                L.hs[u] = m0 ? cs[0] : (m1 ? cs[1] : cs[2]);
             }
             if (nstash) {
-                if (can[u] && !hit[u]) {
+                if (can && !L.hit[u]) {
                     for (uint32_t e = 0; e < nstash; ++e) {
                         const uint64_t v = H.stash[e];
-                        if (m(v) && (!(IDB == 8 && nonuniform) || ids[base + slot_pos(v)] == pid[u])) {
-                            hit[u] = v; hs[u] = nslots + e;
+                        if (m(v) && (!(IDB == 8 && nonuniform) || ids[base + slot_pos(v)] == S.pid[u])) {
+                            L.hit[u] = v; L.hs[u] = nslots + e;
                             break;
                         }
                     }
                 }
             }
         }
-        // gather the matched current r̂ (written in phase 1: L2).  Unconditional (a
-        // miss re-reads row 0) and issued BEFORE the next trip's prefetch: vmcnt
-        // retires in issue order, so the gather wait then leaves the prefetch in flight.
-        V3<TD> cr[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
-            const uint32_t p = (hit[u] && !OA_ABL_GATHER) ? slot_pos(hit[u]) : 0u;
-            cr[u] = bld3<TD, 0>(r_rh, p * SD);
+            const uint32_t p = (L.hit[u] && !OA_ABL_GATHER) ? slot_pos(L.hit[u]) : 0u;
+            L.cr[u] = bld3<TD, 0>(r_rh, p * SD);
         }
-        __builtin_amdgcn_sched_barrier(0);
-        OA_LOAD2(pidn, prhn, pmetan, kbn, hlvn, nvn, tn)   // unconditional (out of range: zeros)
-        __builtin_amdgcn_sched_barrier(0);
+    };
+    // flag, angle and apsis records of one trip
+    auto compute = [&](const Rows &S, const Look &L, uint32_t t) __attribute__((always_inline)) {
         bool flag[UNR];
         uint16_t a16[UNR];
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
             flag[u] = false;
             a16[u] = 0xFFFFu;
-            if (!hit[u]) continue;
-            const uint32_t sc = slot_meta(hit[u]) >> 16, sp = pmeta[u] >> 16;
+            if (!L.hit[u]) continue;
+            const uint32_t sc = slot_meta(L.hit[u]) >> 16, sp = S.pmeta[u] >> 16;
             // strict sign test (:311-314): zeros and NaNs never flag
             const bool cond = a.mode == OA_MODE_PERICENTRIC ? (sp == 2u && sc == 1u)
                                                             : (sp == 1u && sc == 2u);
             // angle change = arccos(dot(r̂_prev, r̂_match)), no clamp (:324-325)
-            if (OA_ABL_GATHER) cr[u] = prh[u];
-            TD dt = dot3(prh[u].x, prh[u].y, prh[u].z, cr[u].x, cr[u].y, cr[u].z);
+            const V3<TD> cr = OA_ABL_GATHER ? S.prh[u] : L.cr[u];
+            TD dt = dot3(S.prh[u].x, S.prh[u].y, S.prh[u].z, cr.x, cr.y, cr.z);
             const TD change = OA_ABL_ACOS ? dt : acos_td(dt);
-            uint16_t acc = angle_add((uint16_t)(pmeta[u] & 0xFFFFu), change);
+            uint16_t acc = angle_add((uint16_t)(S.pmeta[u] & 0xFFFFu), change);
             if (OTF) {
                 // on-the-fly outputs (track_orbits_onthefly.py:145-174): the angle
                 // change of every matched particle, and which current ones matched
-                static_cast<TD *>(a.angle_out)[kb[u] + lane] = change;
-                a.matched_cur[base + slot_pos(hit[u])] = 1;
+                static_cast<TD *>(a.angle_out)[S.kb[u] + lane] = change;
+                a.matched_cur[base + slot_pos(L.hit[u])] = 1;
             }
             // calc_angles (:342-349): apsis angle emitted, then reset to 0
             if (!OA_ABL_SLOTW) {
-                uint64_t *sp_ = hs[u] < nslots ? &slots[hs[u]] : &H.stash[hs[u] - nslots];
+                uint64_t *sp_ = L.hs[u] < nslots ? &slots[L.hs[u]] : &H.stash[L.hs[u] - nslots];
                 reinterpret_cast<uint16_t *>(sp_)[2] = cond ? (uint16_t)0 : acc;
             }
             flag[u] = cond;
@@ -953,7 +988,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         if (OTF) {
 #pragma unroll
             for (int u = 0; u < UNR; ++u)
-                if ((uint32_t)lane < nv[u]) a.matched_prev[kb[u] + lane] = hit[u] ? 1 : 0;
+                if ((uint32_t)lane < S.nv[u]) a.matched_prev[S.kb[u] + lane] = L.hit[u] ? 1 : 0;
         }
         // apsis records in previous-block order (:315-316): wave ballot + prefix
         // popcount packs each 64-position row's records at its own scratch base;
@@ -967,30 +1002,44 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                 const int64_t sb = it.scratch_off + r0;
                 if (flag[u] && !OA_ABL_EMIT) {
                     const uint32_t q = (uint32_t)__popcll(m & lanemask_lt);
-                    scr_ids[sb + q] = pid[u];
+                    scr_ids[sb + q] = S.pid[u];
                     a.scratch_ang[sb + q] = a16[u];
                 }
                 if (lane == 0) {
                     a.seg_count[sb >> 6] = (uint8_t)c;
-                    if (c && !OA_ABL_EMIT) atomicAdd(&H.halo_cnt[hlv[u]], (int)c);
+                    if (c && !OA_ABL_EMIT) atomicAdd(&H.halo_cnt[S.hlv[u]], (int)c);
                 }
                 running += c;
             }
         }
     };
-    uint32_t t2 = wave, tn = wave + NWAVE;
-    while (t2 < ntr2) {
-        uint32_t f2 = trip_fetch(&H.ctr2, lane);
-        trip(pid, prh, pmeta, kb, hlv, nv, pidn, prhn, pmetan, kbn, hlvn, nvn, t2, tn);
-        if (tn >= ntr2) break;
-        t2 = tn;
-        tn = trip_take(f2, tn);
-        f2 = trip_fetch(&H.ctr2, lane);
-        trip(pidn, prhn, pmetan, kbn, hlvn, nvn, pid, prh, pmeta, kb, hlv, nv, t2, tn);
-        t2 = tn;
-        tn = trip_take(f2, tn);
+    // pipeline: trips t (compute), t1 (lookup), t2 (loads); every wave starts with
+    // trips wave, wave + NWAVE, wave + 2 NWAVE, later ones come from the counter
+    uint32_t tc = wave, tl = wave + NWAVE, tp = wave + 2 * NWAVE;
+    load_rows(SB, tl);
+    lookup(SA, LA);
+    auto stage = [&](Rows &S0, Look &L0, Rows &S1, Look &L1, Rows &S2) __attribute__((always_inline)) {
+        const uint32_t f = trip_fetch(&H.ctr2, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        load_rows(S2, tp);            // out of range: zeros
+        __builtin_amdgcn_sched_barrier(0);
+        lookup(S1, L1);               // its rows were loaded a stage ago
+        compute(S0, L0, tc);           // its gathers were issued a stage ago
+        tc = tl; tl = tp; tp = trip_take(f, tp);
+    };
+    while (tc < ntr2) {
+        stage(SA, LA, SB, LB, SC);
+        if (tc >= ntr2) break;
+        stage(SB, LB, SC, LA, SA);
+        if (tc >= ntr2) break;
+        stage(SC, LA, SA, LB, SB);
+        if (tc >= ntr2) break;
+        stage(SA, LB, SB, LA, SC);
+        if (tc >= ntr2) break;
+        stage(SB, LA, SC, LB, SA);
+        if (tc >= ntr2) break;
+        stage(SC, LB, SA, LA, SB);
     }
-#undef OA_LOAD2
     WSTAMP(1);
     if (lane == 0) atomicAdd(&H.chunk_total, running);
     STAMP(4);
@@ -1223,6 +1272,7 @@ FrameK make_frame_k(const oa_step_args &a) {
         k.wrap_hi[d] = (double)f > half ? f : nextafterf(f, INFINITY);
         float g = (float)(-half);
         k.wrap_lo[d] = (double)g < -half ? g : nextafterf(g, -INFINITY);
+        k.wrap_abs[d] = fminf(k.wrap_hi[d], -k.wrap_lo[d]);
     }
     return k;
 }

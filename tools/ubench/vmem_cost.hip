@@ -81,5 +81,9 @@ int main() {
     time([&] { k_gather<3><<<nwg, 1024>>>(reg, out, 10240, iters); }, "gather_x3", iters);
     time([&] { k_gather<4><<<nwg, 1024>>>(reg, out, 10240, iters); }, "gather_x4", iters);
     time([&] { k_gather<2><<<nwg, 1024>>>(reg, out, 10240 * 2, iters); }, "gather_x2", iters);
+    time([&] { k_gather<3><<<nwg, 1024>>>(reg, out, 1365, iters); }, "gather_x3_16K", iters);
+    time([&] { k_gather<3><<<nwg, 1024>>>(reg, out, 2730, iters); }, "gather_x3_32K", iters);
+    time([&] { k_gather<3><<<nwg, 1024>>>(reg, out, 5460, iters); }, "gather_x3_64K", iters);
+    time([&] { k_gather<3><<<nwg, 1024>>>(reg, out, 40960, iters); }, "gather_x3_480K", iters);
     return 0;
 }

@@ -9,7 +9,7 @@ pids=()
 while read -r name flags; do
   [ -z "$name" ] && continue
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off \
-    -fno-fast-math -I"$R/include" $flags -o "$D/lib_$name.so" "$SRC" &
+    -fno-fast-math -mllvm -amdgpu-atomic-optimizer-strategy=None -I"$R/include" $flags -o "$D/lib_$name.so" "$SRC" &
   pids+=($!)
   if [ ${#pids[@]} -ge 6 ]; then wait "${pids[0]}"; pids=("${pids[@]:1}"); fi
 done < "${VARIANT_FILE:-$R/tools/variants.txt}"
