@@ -1113,12 +1113,16 @@ __global__ __launch_bounds__(1024) void k_scan_slots(const int32_t *cnt, int32_t
     if (tid == 0) { off[n] = carry; *total = carry; }
 }
 
-// Item records live in 64-position segments (k_step phase 2); a work-group walks
-// its item's segments in order, scanning the per-segment counts.
+// Item records live in 64-position rows (k_step phase 2), packed at each row's base.
+// One work-group per item, rows in chunks of 256: a block-wide exclusive scan of the
+// chunk's row counts (LDS), then the chunk's records are copied flat -- thread t moves
+// records t, t + 256, ... (consecutive records of consecutive rows: coalesced), each
+// finding its row by a binary search over the scanned offsets.
 template <int IDB>
 __global__ __launch_bounds__(256) void k_gather_items(const oa_compact_args a) {
     typedef typename IdT<IDB>::T ID;
     __shared__ uint32_t wsum[4];
+    __shared__ uint32_t roff[257];
     const oa_item it = a.items[blockIdx.x];
     const int32_t n = a.item_count[blockIdx.x];
     if (n <= 0) return;
@@ -1145,11 +1149,15 @@ __global__ __launch_bounds__(256) void k_gather_items(const oa_compact_args a) {
         __syncthreads();
         uint32_t pre = 0, tot = 0;
         for (int w = 0; w < 4; ++w) { if (w < wave) pre += wsum[w]; tot += wsum[w]; }
-        const int64_t o = carry + pre + incl - cnt;
-        const int64_t sbase = it.scratch_off + (sg << 6);
-        for (uint32_t r = 0; r < cnt; ++r) {
-            out[o + r] = src[sbase + r];
-            oang[o + r] = a.scratch_ang[sbase + r];
+        roff[tid] = pre + incl - cnt;
+        if (tid == 255) roff[256] = tot;
+        __syncthreads();
+        const uint32_t rows = (uint32_t)(nseg - c0 < 256 ? nseg - c0 : 256);
+        for (uint32_t j = tid; j < tot; j += 256) {
+            const uint32_t r = upper_find(roff, rows, j);      // roff[r] <= j < roff[r + 1]
+            const int64_t from = it.scratch_off + ((c0 + r) << 6) + (j - roff[r]);
+            out[carry + j] = src[from];
+            oang[carry + j] = a.scratch_ang[from];
         }
         carry += tot;
         __syncthreads();
