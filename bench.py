@@ -162,7 +162,8 @@ def main():
     preps = [c[0] for c in chain[1:]]
     ws = Workspace(dev, torch.int64 if preps[0].plan.ids.itemsize == 8 else torch.int32,
                    max(p.scratch for p in preps), max(p.n_prev for p in preps),
-                   max(int(p.has_prog.sum()) for p in preps), max(len(p.items) for p in preps))
+                   max(int(p.has_prog.sum()) for p in preps), max(len(p.items) for p in preps),
+                   eng.entries, eng.n_wg)
     # catalogue exchange (N > 1): rank r holds catalogue rows [r*nl, (r+1)*nl)
     nl = -(-args.halos // world)
     cat_local, cat_all = [], None

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OA_ABI_VERSION 4
+#define OA_ABI_VERSION 5
 
 #define OA_OK 0
 #define OA_E_ARG (-1)       /* invalid argument / unsupported dtype plan */
@@ -138,6 +138,15 @@ typedef struct oa_step_args {
                                    (0 = empty), u32 pad}; zeroed by oa_step          */
     uint32_t *gvals;            /* unused (NULL)                                      */
     int64_t gtab_total;         /* slots over all global items                        */
+    /* persistent join (compare != 0, ABI >= 5): n_wg work-groups each process packed
+     * items in turn, taking them from *work, the frame of the next item interleaved
+     * with the join of the current one.  stage: n_wg * 2 * lds_entries * 8 bytes of
+     * device scratch; work: device counter, zero on entry.  stage == NULL: one
+     * work-group per packed item (no interleaving). */
+    uint32_t *work;
+    void *stage;
+    int32_t n_wg;               /* 0: one per compute unit                            */
+    int32_t reserved_p;
 } oa_step_args;
 
 /* Arguments of oa_compact: gather the per-item apsis records into the reference's
@@ -190,8 +199,11 @@ int oa_bulk_velocity(const void *vels, int32_t vel_f64, const void *masses, int3
  * (:293-351), emitting apsis records in previous-block order. */
 int oa_step(const oa_step_args *args, void *stream);
 
-/* Dynamic LDS bytes k_step needs per work-group for the given table sizes. */
+/* Dynamic LDS bytes a join work-group needs for the given table sizes. */
 int64_t oa_step_lds_bytes(int32_t entries, int32_t slots);
+
+/* Compute units of the current device (the persistent join's default n_wg). */
+int32_t oa_device_units(void);
 
 /* Diagnostic builds only (-DOA_STAMPS=1): copy the per-work-group phase timestamps
  * (s_memrealtime, 100 MHz; 6 per work-group) of the last oa_step to host memory.

@@ -13,7 +13,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.abspath(__file__))
 # ORBIT_HIP_LIB selects an alternative build (kernel variants for tuning sweeps)
 LIB_PATH = os.environ.get('ORBIT_HIP_LIB') or os.path.join(PKG, 'liborbit_hip.so')
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -43,7 +43,8 @@ class StepArgs(ctypes.Structure):
                 ('matched_prev', c_vp), ('matched_cur', c_vp), ('vr_out', c_vp),
                 ('n_global_items', c_i32), ('n_gchunk1', c_i32), ('n_gchunk2', c_i32),
                 ('gchunk1', c_vp), ('gchunk2', c_vp), ('gtab', c_vp), ('gkeys', c_vp),
-                ('gvals', c_vp), ('gtab_total', c_i64)]
+                ('gvals', c_vp), ('gtab_total', c_i64),
+                ('work', c_vp), ('stage', c_vp), ('n_wg', c_i32), ('reserved_p', c_i32)]
 
 
 class CompactArgs(ctypes.Structure):
@@ -64,6 +65,7 @@ SYMBOLS = {
     'oa_bulk_velocity': (ctypes.c_int, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
     'oa_step': (ctypes.c_int, [ctypes.POINTER(StepArgs), c_vp]),
     'oa_step_lds_bytes': (c_i64, [c_i32, c_i32]),
+    'oa_device_units': (c_i32, []),
     'oa_max_lds_bytes': (c_i64, []),
     'oa_debug_stamps': (c_i64, [c_vp, c_i64]),
     'oa_compact': (ctypes.c_int, [ctypes.POINTER(CompactArgs), c_vp]),

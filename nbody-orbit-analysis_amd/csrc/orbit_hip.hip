@@ -99,6 +99,9 @@ namespace {
 #ifndef OA_DYN
 #define OA_DYN 1            // waves take loop trips from an LDS counter (else static)
 #endif
+#ifndef OA_UJ
+#define OA_UJ 1             // k_stream: join rows per interleaved step
+#endif
 #ifndef OA_HMAX
 #define OA_HMAX 32
 #endif
@@ -154,11 +157,14 @@ constexpr int STAMP_MAX_WG = 1 << 16, STAMP_N = 6 + 2 * (OA_WG / 64);
 __device__ uint64_t g_stamps[STAMP_MAX_WG * STAMP_N];
 #define STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < STAMP_MAX_WG) \
     g_stamps[blockIdx.x * STAMP_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define STAMPI(item, k) do { if (threadIdx.x == 0 && (item) < STAMP_MAX_WG) \
+    g_stamps[(item) * STAMP_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define WSTAMP(k) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < STAMP_MAX_WG) \
     g_stamps[blockIdx.x * STAMP_N + 6 + 2 * (threadIdx.x >> 6) + (k)] = \
         __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define STAMP(k) do { } while (0)
+#define STAMPI(item, k) do { } while (0)
 #define WSTAMP(k) do { } while (0)
 #endif
 
@@ -268,6 +274,8 @@ struct ItemHdr {
     uint32_t nh, nseg, n_span, n_pv;
     uint32_t chunk_total, nsl, nstash, npend;
     uint32_t ctr1, ctr2, pad1, pad2;    // trip counters of phases 1 and 2
+    int32_t item, h0, h1, next;         // k_stream: the item, its halos, the next item
+    int64_t scratch_off;
     uint64_t stash[STASH];          // cuckoo entries whose eviction chain ran out
     uint32_t lstart[HMAX + 1];      // local start of each item halo's current block
     uint32_t vstart[HMAX + 1];      // virtual start of each progenitor segment
@@ -541,6 +549,7 @@ __device__ void rbs_i32(int32_t, i32x4, int32_t, int32_t, int32_t) __asm("llvm.a
 __device__ void rbs_v3f32(f32x3, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.v3f32");
 __device__ void rbs_v2f64(f64x2, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.v2f64");
 __device__ void rbs_f64(double, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.f64");
+__device__ void rbs_i64(int64_t, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.i64");
 constexpr int AUX_NT = 2;      // nt: streamed-once inputs (keeps L2 for the r̂ gathers)
 
 // raw buffer resource (stride 0): 48-bit base, num_records in bytes, 32-bit data format
@@ -1086,6 +1095,470 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     STAMP(5);
 }
 
+// ------------------------------------------------------------------ persistent join
+// k_stream: the compare step as a persistent kernel.  n_wg work-groups (one per CU:
+// the LDS table) take packed items from a device counter.  For item k a work-group
+//   1. inserts the item's staged keys into its LDS table (the keys were written by
+//      the frame pass of the previous iteration: L2-resident),
+//   2. runs the join of item k (phase 2 of k_step) INTERLEAVED with the frame of the
+//      next item k1 -- every wave alternates a join trip (LDS lookups, r̂ gathers:
+//      memory-pipeline bound) with a frame trip (float math: VALU bound), so the two
+//      overlap instead of running as separate phases,
+//   3. writes item k's state words (phase 3 of k_step).
+// The frame pass stores r̂ and the non-joined particles' state words as k_step does,
+// and for joined particles the 8-byte table entry into the work-group's staging ring
+// (two item slots).  The first item's frame runs alone (prologue).
+
+// Phase 0 of one item: its halo table into header Hd.  The caller synchronises.
+template <int IDB>
+__device__ __forceinline__ void stage_item(ItemHdr &Hd, const oa_step_args &a, int32_t item,
+                                           int tid) {
+    const oa_item it = a.items[item];
+    const int nh = it.h1 - it.h0;
+    if (tid < nh) {
+        const oa_halo &h = a.halos[it.h0 + tid];
+        const oa_halo &h0 = a.halos[it.h0];
+        Hd.lstart[tid] = (uint32_t)(h.cur_off - h0.cur_off);
+        Hd.has_prev[tid] = h.prev_cnt > 0;
+        Hd.halo_cnt[tid] = 0;
+        for (int d = 0; d < 3; ++d) { Hd.cb[tid][d] = h.centre[d]; Hd.cb[tid][3 + d] = h.bulk[d]; }
+        for (int d = 0; d < 3; ++d) { Hd.cf[tid][d] = (float)h.centre[d]; Hd.cf[tid][3 + d] = (float)h.bulk[d]; }
+        if (tid == nh - 1) {
+            Hd.lstart[nh] = (uint32_t)(h.cur_off + h.cur_cnt - h0.cur_off);
+            Hd.n_span = Hd.lstart[nh];
+            Hd.cur_base = h0.cur_off;
+        }
+    }
+    if (tid == 0) {
+        Hd.item = item; Hd.h0 = it.h0; Hd.h1 = it.h1; Hd.scratch_off = it.scratch_off;
+        Hd.nonuniform = 0; Hd.overflow = 0; Hd.nh = nh; Hd.chunk_total = 0; Hd.nstash = 0;
+        Hd.npend = 0;
+        Hd.ctr1 = NWAVE; Hd.ctr2 = 2 * NWAVE;   // static first trips (frame 1, join 2)
+        uint32_t ns = 0, vp = 0, nj = 0;
+        for (int k = 0; k < nh; ++k) {
+            const oa_halo &h = a.halos[it.h0 + k];
+            if (h.prev_cnt > 0) {
+                nj += (uint32_t)h.cur_cnt;
+                Hd.seg_halo[ns] = k; Hd.seg_prev_off[ns] = h.prev_off; Hd.vstart[ns] = vp;
+                Hd.seg_cnt[ns] = (uint32_t)h.prev_cnt;
+                vp += ((uint32_t)h.prev_cnt + 63u) & ~63u; ++ns;
+            }
+        }
+        Hd.vstart[ns] = vp; Hd.nseg = ns; Hd.n_pv = vp;
+        const uint32_t ns_eff = nj * OA_SLOT_X2 / 2 + 64;
+        Hd.nsl = ns_eff > (uint32_t)a.lds_slots ? (uint32_t)a.lds_slots : ns_eff;
+        const oa_halo &h0 = a.halos[it.h0], &hl1 = a.halos[it.h1 - 1];
+        Hd.hi0 = 0;
+        if (IDB == 8 && hl1.cur_off + hl1.cur_cnt > h0.cur_off)
+            Hd.hi0 = (uint32_t)(static_cast<const uint64_t *>(a.ids)[h0.cur_off] >> 32);
+    }
+}
+
+template <typename TX, typename TV, typename TD, int IDB, bool OTF>
+__global__ __launch_bounds__(WG) void k_stream(const oa_step_args a, const FrameK fk) {
+    typedef typename IdT<IDB>::T ID;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    ItemHdr *HH = reinterpret_cast<ItemHdr *>(smem);          // two headers
+    const uint32_t nslots_max = (uint32_t)a.lds_slots;
+    uint64_t *slots = reinterpret_cast<uint64_t *>(smem + 2 * HDR_BYTES);
+    uint64_t *pend = slots + nslots_max;
+    const uint32_t pend_cap = (uint32_t)a.lds_entries / 4u;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const ID *ids = reinterpret_cast<const ID *>(a.ids);
+    const ID *ids_prev = reinterpret_cast<const ID *>(a.ids_prev);
+    TD *rhat_out = reinterpret_cast<TD *>(a.rhat_out);
+    const TD *rhat_prev = reinterpret_cast<const TD *>(a.rhat_prev);
+    constexpr uint32_t SX = 3 * sizeof(TX), SV = 3 * sizeof(TV), SD = 3 * sizeof(TD);
+    constexpr int UNR = OA_UJ;                 // join rows per interleaved step
+    constexpr int UF = 1;                      // frame rows per interleaved step
+    constexpr uint32_t T1 = 64 * UF, T2 = 64 * UNR;
+    const uint64_t lanemask_lt = (1ull << lane) - 1ull;
+    ID *scr_ids = reinterpret_cast<ID *>(a.scratch_ids);
+    char *stage_wg = static_cast<char *>(a.stage) + (int64_t)blockIdx.x * 2 * a.lds_entries * 8;
+
+    // ---- frame of one trip of an item's current rows (header Hd, staging slot sl):
+    // r̂ and the non-joined state words to global memory, joined particles' table
+    // entries to the staging ring
+    // uniform scalars of the item whose frame runs (base, span, halos, ID high word)
+    struct FItem { int64_t b; uint32_t ns, nh, hi0; };
+    auto fitem = [&](const ItemHdr &Hd) __attribute__((always_inline)) {
+        return FItem{uni64(Hd.cur_base), uni(Hd.n_span), uni(Hd.nh), uni(Hd.hi0)};
+    };
+    auto frame_loads = [&](const FItem &F, uint32_t T, ID (&idv)[UF], V3<TX> (&xv)[UF],
+                           V3<TV> (&vv)[UF]) __attribute__((always_inline)) {
+        const int64_t b = F.b;
+        const uint32_t ns = F.ns;
+        const Rsrc r_id = make_rsrc(ids + b, ns * IDB);
+        const Rsrc r_x = make_rsrc(reinterpret_cast<const TX *>(a.coords) + 3 * b, ns * SX);
+        const Rsrc r_v = make_rsrc(reinterpret_cast<const TV *>(a.vels) + 3 * b, ns * SV);
+#pragma unroll
+        for (int u = 0; u < UF; ++u) {
+            const uint32_t li = T * T1 + u * 64 + lane;
+            idv[u] = bld<ID, AUX_NT>(r_id, li * IDB);
+            xv[u] = bld3<TX, AUX_NT>(r_x, li * SX);
+            vv[u] = bld3<TV, AUX_NT>(r_v, li * SV);
+        }
+    };
+    auto frame_rows = [&](ItemHdr &Hd, const FItem &F, uint32_t sl, uint32_t T, const ID (&idv)[UF],
+                          const V3<TX> (&xv)[UF], const V3<TV> (&vv)[UF]) __attribute__((always_inline)) {
+        const int64_t b = F.b;
+        const uint32_t ns = F.ns, nhu = F.nh, h0w = F.hi0;
+        const Rsrc r_rh = make_rsrc(rhat_out + 3 * b, ns * SD);
+        const Rsrc r_mt = make_rsrc(a.meta_out + b, ns * 4u);
+        const Rsrc r_st = make_rsrc(stage_wg + (int64_t)sl * a.lds_entries * 8, ns * 8u);
+#pragma unroll
+        for (int u = 0; u < UF; ++u) {
+            const uint32_t r0 = T * T1 + u * 64;
+            if (r0 >= ns) continue;
+            const uint32_t li = r0 + lane;
+            uint32_t hl = 0;
+            if (nhu > 1) {
+                hl = uni(upper_find(Hd.lstart, nhu, r0));
+                if (r0 + 63u >= Hd.lstart[hl + 1])
+                    while (hl + 1 < nhu && li >= Hd.lstart[hl + 1]) ++hl;
+            }
+            uint32_t lo, hi;
+            id_split<IDB>(idv[u], lo, hi);
+            TD r[3];
+            const uint32_t sgn = OTF ? frame_otf<TX, TV, TD>(xv[u], vv[u], Hd.cb[hl], a, fk, r)
+                                     : frame<TX, TV, TD>(xv[u], vv[u], Hd.cb[hl], Hd.cf[hl], a, fk, r);
+            bst3<TD>(r_rh, li * SD, r);
+            const uint32_t meta = sgn << 16;              // angle 0 (calc_angles :348-349)
+            uint64_t e = 0;
+            if (Hd.has_prev[hl]) {
+                e = slot_pack(lo, meta, li);
+                if (IDB == 8 && hi != h0w && li < ns) Hd.nonuniform = 1u;
+            } else {
+                bst32(r_mt, li * 4u, meta);
+            }
+            rbs_i64((int64_t)e, r_st, (int32_t)(li * 8u), 0, 0);
+        }
+    };
+
+    // ---- first item --------------------------------------------------------------
+    if (tid == 0) HH[0].next = (int32_t)atomicAdd(a.work, 1u);
+    __syncthreads();
+    int32_t item = HH[0].next;
+    if (item >= a.n_items) return;
+    stage_item<IDB>(HH[0], a, item, tid);
+    __syncthreads();
+    {   // prologue frame pass (all waves), trips from HH[0].ctr1
+        ItemHdr &Hd = HH[0];
+        const FItem F = fitem(Hd);
+        const uint32_t ntr = (F.ns + T1 - 1) / T1;
+        ID idv[UF]; V3<TX> xv[UF]; V3<TV> vv[UF];
+        uint32_t t = wave, tn = wave + NWAVE;
+        uint32_t f = trip_fetch(&Hd.ctr1, lane);
+        while (t < ntr) {
+            frame_loads(F, t, idv, xv, vv);
+            frame_rows(Hd, F, 0, t, idv, xv, vv);
+            t = tn;
+            tn = trip_take(f, tn);
+            f = trip_fetch(&Hd.ctr1, lane);
+        }
+    }
+    uint32_t cur = 0;
+    for (;;) {
+        ItemHdr &H = HH[cur];
+        ItemHdr &H1 = HH[cur ^ 1];
+        STAMPI(H.item, 0);
+        // ---- clear the table, insert the item's staged keys ------------------------
+        __syncthreads();            // previous item's phase 3 done with the table; frame
+                                    // pass stores (staging, r̂) complete
+        const uint32_t nslots = uni(H.nsl);
+        for (uint32_t w = tid; w < nslots; w += WG) slots[w] = 0ull;
+        if (tid == 0) H.next = (int32_t)atomicAdd(a.work, 1u);
+        __syncthreads();
+        const int32_t item1 = H.next;
+        const bool more = item1 < a.n_items;
+        const int64_t base = uni64(H.cur_base);
+        const uint32_t n_span = uni(H.n_span), hi0 = uni(H.hi0), nhu = uni(H.nh);
+        {
+            const Rsrc r_st = make_rsrc(stage_wg + (int64_t)cur * a.lds_entries * 8, n_span * 8u);
+            constexpr int UI = 4;
+            for (uint32_t l0 = 0; l0 < n_span; l0 += UI * WG) {
+                uint64_t val[UI];
+#pragma unroll
+                for (int u = 0; u < UI; ++u)
+                    val[u] = bld<uint64_t, 0>(r_st, (l0 + u * WG + tid) * 8u);   // beyond: 0
+                uint32_t sl[UI], cs1[UI], cs2[UI];
+                uint64_t c0[UI], c1[UI], c2[UI];
+#pragma unroll
+                for (int u = 0; u < UI; ++u) {
+                    uint32_t cs[3];
+                    cuckoo_slots((uint32_t)val[u], nslots, cs);
+                    sl[u] = cs[0]; cs1[u] = cs[1]; cs2[u] = cs[2];
+                    if (val[u]) { c0[u] = slots[sl[u]]; c1[u] = slots[cs1[u]]; c2[u] = slots[cs2[u]]; }
+                }
+#pragma unroll
+                for (int u = 0; u < UI; ++u) {
+                    if (!val[u]) continue;
+                    const uint32_t t = c0[u] == 0ull ? sl[u] : (c1[u] == 0ull ? cs1[u]
+                                                              : (c2[u] == 0ull ? cs2[u] : 0xFFFFFFFFu));
+                    bool placed = false;
+                    if (t != 0xFFFFFFFFu)
+                        placed = atomicCAS(reinterpret_cast<unsigned long long *>(&slots[t]), 0ull,
+                                           (unsigned long long)val[u]) == 0ull;
+                    if (!placed) {
+                        const uint32_t e = atomicAdd(&H.npend, 1u);
+                        if (e < pend_cap) pend[e] = val[u];
+                        else H.overflow = 2u;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        STAMPI(H.item, 1);
+        // ---- deferred cuckoo walks; the next item's header ----------------------------
+        {
+            const uint32_t np = min(H.npend, pend_cap);
+            for (uint32_t e = tid; e < np; e += WG) {
+                uint64_t v = pend[e];
+                uint32_t cs[3];
+                cuckoo_slots((uint32_t)v, nslots, cs);
+                uint32_t t = cs[0];
+                for (int it_ = 0;; ++it_) {
+                    const uint64_t old = atomicExch(reinterpret_cast<unsigned long long *>(&slots[t]),
+                                                    (unsigned long long)v);
+                    if (old == 0ull) break;
+                    if (it_ == MAX_EVICT) {
+                        const uint32_t k = atomicAdd(&H.nstash, 1u);
+                        if (k < (uint32_t)STASH) H.stash[k] = old;
+                        else H.overflow = 2u;
+                        break;
+                    }
+                    cuckoo_slots((uint32_t)old, nslots, cs);
+                    t = cs[cs[0] == t ? 1 : (cs[1] == t ? 2 : 0)];
+                    v = old;
+                }
+            }
+        }
+        if (more) stage_item<IDB>(H1, a, item1, tid);
+
+        // ---- join of this item interleaved with the frame of the next -----------------
+        const uint32_t n_pv = uni(H.n_pv), nseg = uni(H.nseg);
+        const uint32_t ntr2 = (n_pv + T2 - 1) / T2;
+        const uint32_t cnt0 = uni(H.seg_cnt[0]), hal0 = uni((uint32_t)H.seg_halo[0]);
+        const int64_t off0 = uni64(H.seg_prev_off[0]);
+        const Rsrc r_rh = make_rsrc(rhat_out + 3 * base, n_span * SD);
+        struct Rows {
+            ID pid[UNR];
+            V3<TD> prh[UNR];
+            uint32_t pmeta[UNR], hlv[UNR], nv[UNR];
+            int64_t kb[UNR];
+        };
+        auto load_rows = [&](Rows &S, uint32_t T) __attribute__((always_inline)) {
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const uint32_t r0 = T * T2 + u * 64;
+                uint32_t ro = r0, cnt = cnt0, hs = hal0;
+                int64_t off = off0;
+                if (nseg > 1) {
+                    const uint32_t s = uni(upper_find(H.vstart, nseg, min(r0, n_pv - 1u)));
+                    ro = r0 - uni(H.vstart[s]);
+                    cnt = uni(H.seg_cnt[s]);
+                    hs = uni((uint32_t)H.seg_halo[s]);
+                    off = uni64(H.seg_prev_off[s]);
+                }
+                S.nv[u] = (r0 < n_pv && ro < cnt) ? min(cnt - ro, 64u) : 0u;
+                S.hlv[u] = hs;
+                S.kb[u] = off + ro;
+                S.pid[u] = bld<ID, AUX_NT>(make_rsrc(ids_prev + S.kb[u], S.nv[u] * IDB), lane * IDB);
+                S.prh[u] = bld3<TD, AUX_NT>(make_rsrc(rhat_prev + 3 * S.kb[u], S.nv[u] * SD), lane * SD);
+                S.pmeta[u] = bld<uint32_t, AUX_NT>(make_rsrc(a.meta_prev + S.kb[u], S.nv[u] * 4u), lane * 4u);
+            }
+        };
+        Rows SA, SB;
+        __builtin_amdgcn_sched_barrier(0);
+        load_rows(SA, (uint32_t)wave);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(3 * UNR) : "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        STAMPI(H.item, 2);
+        if (H.overflow) {       // host re-plans with smaller items (work-group uniform)
+            if (tid == 0) atomicOr(a.status, OA_STATUS_TABLE_OVERFLOW);
+            return;
+        }
+        const bool nonuniform = IDB == 8 && uni(H.nonuniform) != 0;
+        const uint32_t nstash = min(uni(H.nstash), (uint32_t)STASH);
+        const FItem F1 = more ? fitem(H1) : FItem{0, 0u, 1u, 0u};
+        const uint32_t ntrf = (F1.ns + T1 - 1) / T1;
+        uint32_t running = 0;
+        struct FRows { ID id[UF]; V3<TX> x[UF]; V3<TV> v[UF]; };
+        FRows FA, FB;
+        // frame trips: wave, wave + NWAVE static, then the counter (one fetched ahead)
+        uint32_t tf = wave, tfn = wave + NWAVE, ff = 0;
+        if (more) {
+            ff = trip_fetch(&H1.ctr1, lane);
+            frame_loads(F1, tf, FA.id, FA.x, FA.v);
+        }
+        uint32_t t2 = wave, t2n = wave + NWAVE;
+        uint32_t f2 = trip_fetch(&H.ctr2, lane);
+        auto step = [&](Rows &S, Rows &Sn, FRows &FC, FRows &FN) __attribute__((always_inline)) {
+            const bool dof = tf < ntrf, doj = t2 < ntr2;
+            if (tfn < ntrf) frame_loads(F1, tfn, FN.id, FN.x, FN.v);     // next frame trip
+            uint64_t hit[UNR];
+            uint32_t hs[UNR];
+            V3<TD> cr[UNR];
+            if (doj) {
+#pragma unroll
+                for (int u = 0; u < UNR; ++u) {
+                    uint32_t lo, hi;
+                    id_split<IDB>(S.pid[u], lo, hi);
+                    const bool can = ((uint32_t)lane < S.nv[u]) & (IDB != 8 || nonuniform || hi == hi0);
+                    uint32_t lmin = 0, lmax = n_span;
+                    if (nhu > 1) {
+                        lmin = uni(H.lstart[S.hlv[u]]);
+                        lmax = uni(H.lstart[S.hlv[u] + 1]) - lmin;
+                    }
+                    uint32_t cs[3];
+                    cuckoo_slots(lo, nslots, cs);
+                    const uint64_t c0 = slots[cs[0]], c1 = slots[cs[1]], c2 = slots[cs[2]];
+                    auto m = [&](uint64_t v) { return ((uint32_t)v == lo) & (slot_pos(v) - lmin < lmax); };
+                    const bool m0 = can & m(c0), m1 = can & m(c1), m2 = can & m(c2);
+                    if (IDB == 8 && nonuniform) {
+                        hit[u] = 0ull; hs[u] = 0u;
+                        if (m0 && ids[base + slot_pos(c0)] == S.pid[u]) { hit[u] = c0; hs[u] = cs[0]; }
+                        else if (m1 && ids[base + slot_pos(c1)] == S.pid[u]) { hit[u] = c1; hs[u] = cs[1]; }
+                        else if (m2 && ids[base + slot_pos(c2)] == S.pid[u]) { hit[u] = c2; hs[u] = cs[2]; }
+                    } else {
+                        hit[u] = m0 ? c0 : (m1 ? c1 : (m2 ? c2 : 0ull));
+                        hs[u] = m0 ? cs[0] : (m1 ? cs[1] : cs[2]);
+                    }
+                    if (nstash) {
+                        if (can && !hit[u]) {
+                            for (uint32_t e = 0; e < nstash; ++e) {
+                                const uint64_t v = H.stash[e];
+                                if (m(v) && (!(IDB == 8 && nonuniform) || ids[base + slot_pos(v)] == S.pid[u])) {
+                                    hit[u] = v; hs[u] = nslots + e;
+                                    break;
+                                }
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < UNR; ++u) {
+                    const uint32_t p = hit[u] ? slot_pos(hit[u]) : 0u;
+                    cr[u] = bld3<TD, 0>(r_rh, p * SD);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                load_rows(Sn, t2n);                     // out of range: zeros
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            // the next item's frame rows while this trip's gathers are in flight
+            if (dof) {
+                frame_rows(H1, F1, cur ^ 1, tf, FC.id, FC.x, FC.v);
+                tf = tfn;
+                tfn = trip_take(ff, tfn);
+                ff = trip_fetch(&H1.ctr1, lane);
+            }
+            if (doj) {
+                bool flag[UNR];
+                uint16_t a16[UNR];
+#pragma unroll
+                for (int u = 0; u < UNR; ++u) {
+                    flag[u] = false;
+                    a16[u] = 0xFFFFu;
+                    if (!hit[u]) continue;
+                    const uint32_t sc = slot_meta(hit[u]) >> 16, sp = S.pmeta[u] >> 16;
+                    // strict sign test (:311-314): zeros and NaNs never flag
+                    const bool cond = a.mode == OA_MODE_PERICENTRIC ? (sp == 2u && sc == 1u)
+                                                                    : (sp == 1u && sc == 2u);
+                    // angle change = arccos(dot(r̂_prev, r̂_match)), no clamp (:324-325)
+                    TD dt = dot3(S.prh[u].x, S.prh[u].y, S.prh[u].z, cr[u].x, cr[u].y, cr[u].z);
+                    const TD change = acos_td(dt);
+                    const uint16_t acc = angle_add((uint16_t)(S.pmeta[u] & 0xFFFFu), change);
+                    if (OTF) {
+                        static_cast<TD *>(a.angle_out)[S.kb[u] + lane] = change;
+                        a.matched_cur[base + slot_pos(hit[u])] = 1;
+                    }
+                    // calc_angles (:342-349): apsis angle emitted, then reset to 0
+                    uint64_t *sp_ = hs[u] < nslots ? &slots[hs[u]] : &H.stash[hs[u] - nslots];
+                    reinterpret_cast<uint16_t *>(sp_)[2] = cond ? (uint16_t)0 : acc;
+                    flag[u] = cond;
+                    a16[u] = acc;
+                }
+                if (OTF) {
+#pragma unroll
+                    for (int u = 0; u < UNR; ++u)
+                        if ((uint32_t)lane < S.nv[u]) a.matched_prev[S.kb[u] + lane] = hit[u] ? 1 : 0;
+                }
+                // apsis records in previous-block order (:315-316)
+#pragma unroll
+                for (int u = 0; u < UNR; ++u) {
+                    const uint32_t r0 = t2 * T2 + u * 64;
+                    if (r0 < n_pv) {
+                        const uint64_t mk = __ballot(flag[u]);
+                        const uint32_t c = (uint32_t)__popcll(mk);
+                        const int64_t sb = H.scratch_off + r0;
+                        if (flag[u]) {
+                            const uint32_t q = (uint32_t)__popcll(mk & lanemask_lt);
+                            scr_ids[sb + q] = S.pid[u];
+                            a.scratch_ang[sb + q] = a16[u];
+                        }
+                        if (lane == 0) {
+                            a.seg_count[sb >> 6] = (uint8_t)c;
+                            if (c) atomicAdd(&H.halo_cnt[S.hlv[u]], (int)c);
+                        }
+                        running += c;
+                    }
+                }
+                t2 = t2n;
+                t2n = trip_take(f2, t2n);
+                f2 = trip_fetch(&H.ctr2, lane);
+            }
+        };
+        while (t2 < ntr2 || tf < ntrf) {
+            step(SA, SB, FA, FB);
+            if (!(t2 < ntr2 || tf < ntrf)) break;
+            step(SB, SA, FB, FA);
+        }
+        if (lane == 0) atomicAdd(&H.chunk_total, running);
+        STAMPI(H.item, 3);
+        __syncthreads();
+        STAMPI(H.item, 4);
+
+        // ---- phase 3: this item's state words, in position order ---------------------
+        {
+            uint32_t *pm = reinterpret_cast<uint32_t *>(slots);
+            const uint32_t nst = min(H.nstash, (uint32_t)STASH);
+            const uint32_t nlow = min((n_span + 1) / 2, nslots);
+            uint64_t keep[P3R];
+#pragma unroll
+            for (int r = 0; r < P3R; ++r) {
+                const uint32_t w = tid + r * WG;
+                keep[r] = w < nlow ? slots[w] : 0ull;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < P3R; ++r)
+                if (keep[r]) pm[slot_pos(keep[r])] = slot_meta(keep[r]);
+            for (uint32_t w = nlow + tid; w < nslots + nst; w += WG) {
+                const uint64_t v = w < nslots ? slots[w] : H.stash[w - nslots];
+                if (v) pm[slot_pos(v)] = slot_meta(v);
+            }
+            __syncthreads();
+            const int nh = (int)nhu;
+            for (uint32_t k = 0; k < (uint32_t)nh; ++k) {
+                if (!H.has_prev[k]) continue;
+                const uint32_t e = H.lstart[k + 1];
+                for (uint32_t li = H.lstart[k] + tid; li < e; li += WG) a.meta_out[base + li] = pm[li];
+            }
+            if (tid < nh) {
+                const oa_halo &h = a.halos[H.h0 + tid];
+                if (h.out_slot >= 0) a.halo_count[h.out_slot] = H.halo_cnt[tid];
+            }
+            if (tid == 0) a.item_count[H.item] = (int32_t)H.chunk_total;
+        }
+        STAMPI(H.item, 5);
+        if (!more) break;
+        cur ^= 1;
+    }
+}
+
 // ------------------------------------------------------------------ compaction
 __global__ __launch_bounds__(1024) void k_scan_slots(const int32_t *cnt, int32_t n,
                                                      int64_t *off, int64_t *total) {
@@ -1296,8 +1769,26 @@ int set_lds(K kernel, int64_t bytes) {
 template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
 int launch_big(const oa_step_args &a, hipStream_t st);
 
+int cu_count() {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 1;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1;
+    return n > 0 ? n : 1;
+}
+
 template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
 int launch_step_c(const oa_step_args &a, hipStream_t st) {
+    if (COMPARE && a.n_items > 0 && a.stage) {
+        // persistent join: one work-group per CU (the LDS table), items from a.work
+        const int64_t lds = 2 * HDR_BYTES + table_bytes(a.lds_entries, a.lds_slots);
+        auto k = k_stream<TX, TV, TD, IDB, OTF>;
+        if (int rc = set_lds(k, lds)) return rc;
+        int nwg = a.n_wg > 0 ? a.n_wg : cu_count();
+        if (nwg > a.n_items) nwg = a.n_items;
+        hipLaunchKernelGGL(k, dim3(nwg), dim3(WG), (size_t)lds, st, a, make_frame_k(a));
+        if (int rc = check_launch("k_stream")) return rc;
+        return launch_big<TX, TV, TD, IDB, COMPARE, OTF>(a, st);
+    }
     if (a.n_items > 0) {
         int64_t lds = HDR_BYTES + table_bytes(a.lds_entries, a.lds_slots);
         auto k = k_step<TX, TV, TD, IDB, COMPARE, OTF>;
@@ -1583,8 +2074,10 @@ int64_t oa_struct_size(int32_t which) {
 const char *oa_last_error(void) { return g_err; }
 
 int64_t oa_step_lds_bytes(int32_t entries, int32_t slots) {
-    return HDR_BYTES + table_bytes(entries, slots);
+    return 2 * HDR_BYTES + table_bytes(entries, slots);     // k_stream: two item headers
 }
+
+int32_t oa_device_units(void) { return cu_count(); }
 
 // Diagnostic builds (-DOA_STAMPS=1): copy the per-work-group phase stamps of the last
 // oa_step launch (s_memrealtime, 100 MHz) to host memory; returns count or -1.
@@ -1632,6 +2125,8 @@ int oa_step(const oa_step_args *args, void *stream) {
         return fail(OA_E_ARG, "null previous-state / scratch pointer");
     if (a.onthefly && a.compare && (!a.angle_out || !a.matched_prev || !a.matched_cur))
         return fail(OA_E_ARG, "null on-the-fly output pointer");
+    if (a.compare && a.stage && !a.work)
+        return fail(OA_E_ARG, "persistent join: null work counter");
     if (a.n_gchunk1 > 0 && (!a.gchunk1 || !a.gtab || (a.compare && !a.gkeys)))
         return fail(OA_E_ARG, "null large-halo table pointer");
     if (a.compare && a.n_gchunk2 > 0 && !a.gchunk2)

@@ -23,8 +23,8 @@ import torch
 from . import _native as N
 
 F32, F64 = np.dtype(np.float32), np.dtype(np.float64)
-DEFAULT_ENTRIES = 14336        # current particles per work-group item
-DEFAULT_SLOTS = 16128          # 8-byte LDS cuckoo slots per item (126 KB) + 2 B/entry map
+DEFAULT_ENTRIES = 12288        # current particles per work-group item (2 B/entry insert list)
+DEFAULT_SLOTS = 16128          # 8-byte LDS cuckoo slots per item (126 KB); + two 4 KB headers
 
 _TORCH_FROM_NP = {
     np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
@@ -265,11 +265,18 @@ class PreparedStep:
 
 
 class Workspace:
-    """Reusable scratch for compare steps (sized for the largest step it serves)."""
+    """Reusable scratch for compare steps (sized for the largest step it serves).
 
-    def __init__(self, device, id_torch_dtype, scratch, n_prev, n_slots, n_items):
+    ``stage`` is the persistent join's staging ring (k_stream: two item slots of
+    ``entries`` 8-byte table entries per work-group) and ``work`` its item counter."""
+
+    def __init__(self, device, id_torch_dtype, scratch, n_prev, n_slots, n_items,
+                 entries=None, n_wg=0):
         def e(n, dt):
             return torch.empty(max(int(n), 1), dtype=dt, device=device)
+        self.n_wg = int(n_wg)
+        self.stage = e(self.n_wg * 2 * int(entries), torch.int64) if self.n_wg and entries else None
+        self.work = e(2, torch.int32)
         self.scratch_ids = e(scratch, id_torch_dtype)
         self.scratch_ang = e(scratch, torch.int16)
         self.seg_count = e(scratch // 64 + 1, torch.uint8)
@@ -283,13 +290,15 @@ class Workspace:
         self.status.zero_()
 
     @classmethod
-    def for_step(cls, pr, device):
+    def for_step(cls, pr, device, entries=None, n_wg=0):
         dt = torch.int64 if pr.plan.ids.itemsize == 8 else torch.int32
-        return cls(device, dt, pr.scratch, pr.n_prev, int(pr.has_prog.sum()), len(pr.items))
+        return cls(device, dt, pr.scratch, pr.n_prev, int(pr.has_prog.sum()), len(pr.items),
+                   entries, n_wg)
 
     def reset(self, n_slots):
         """Per-launch zeroing (the status word accumulates: callers clear it)."""
         self.halo_count[:max(n_slots, 1)].zero_()
+        self.work.zero_()
 
 
 class OrbitEngine:
@@ -310,6 +319,10 @@ class OrbitEngine:
         self.slots = int(lds_slots or env('ORBIT_LDS_SLOTS', 0) or
                          max(DEFAULT_SLOTS, self.entries + 1))
         self.hmax = min(int(hmax or env('ORBIT_HMAX', 1 << 30)), self.lib.oa_build_info(1))
+        # experimental persistent join (k_stream, one work-group per CU) with
+        # ORBIT_PERSISTENT=1; the default launches one work-group per item (k_step),
+        # measured faster (2.11 vs 2.43-2.52 ms per 1e8-particle step)
+        self.n_wg = int(self.lib.oa_device_units()) if env('ORBIT_PERSISTENT', '0') == '1' else 0
         max_lds = self.lib.oa_max_lds_bytes()
         need = self.lib.oa_step_lds_bytes(self.entries, self.slots)
         if need > max_lds:
@@ -369,7 +382,7 @@ class OrbitEngine:
             prep = self.prepare(snap, centres, bulk_cat, H, z, exists, compare,
                                 angles_in=angles_in, plan_src=snapshot,
                                 entries=entries)
-            ws = Workspace.for_step(prep, dev)
+            ws = Workspace.for_step(prep, dev, self.entries, self.n_wg)
             ws.status.zero_()
             res = self.launch(prep, ws)
             st = int(ws.status.item()) if compare else 0
@@ -485,6 +498,9 @@ class OrbitEngine:
             a.seg_count = ws.seg_count.data_ptr()
             a.halo_count, a.item_count, a.status = (ws.halo_count.data_ptr(),
                                                    ws.item_count.data_ptr(), ws.status.data_ptr())
+            use_p = ws.stage is not None and ws.stage.numel() >= ws.n_wg * 2 * a.lds_entries
+            a.stage = ws.stage.data_ptr() if use_p else None
+            a.work, a.n_wg = ws.work.data_ptr(), ws.n_wg
         if step_events is not None:
             step_events[0].record()
         N.check(lib.oa_step(a, st), 'oa_step')

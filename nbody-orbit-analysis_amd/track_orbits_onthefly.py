@@ -127,7 +127,7 @@ class OnTheFly:
             a.angle_out, a.matched_prev, a.matched_cur = (angle_out.data_ptr(),
                                                           matched_prev.data_ptr(),
                                                           matched_cur.data_ptr())
-            ws = Workspace.for_step(pc, eng.device)
+            ws = Workspace.for_step(pc, eng.device, eng.entries, eng.n_wg)
             ws.status.zero_()
             res = eng.launch(pc, ws, prev=prev)
             st = int(ws.status.item())

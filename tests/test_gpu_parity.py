@@ -97,6 +97,20 @@ def test_global_and_packed_paths_match(name):
         compare_groups(out.groups, groups(fix), {})
 
 
+@pytest.mark.parametrize('name', ['g1_config1', 'g3_apo_periodic', 'g8_many_small_halos'])
+def test_persistent_join_matches(name, monkeypatch):
+    """The opt-in persistent kernel (k_stream, ORBIT_PERSISTENT=1) gives the same outputs."""
+    from orbitanalysis_amd.engine import OrbitEngine
+    monkeypatch.setenv('ORBIT_PERSISTENT', '1')
+    fix = load(name)
+    u, meta = universe(fix)
+    for entries in (None, 700):
+        eng = OrbitEngine(mode=meta['run']['mode'], lds_entries=entries)
+        assert eng.n_wg > 0
+        out = run_driver(u, meta['run'], engine=eng)
+        compare_groups(out.groups, groups(fix), {})
+
+
 def _oracle_run(u, mode):
     from oracle import orbit_oracle as O
     return O.track_orbits(u.snapshot_numbers, u.main_branches(), u.regions,

@@ -26,7 +26,7 @@ p0 = eng.prepare(s0, c0[0], c0[2], H, z, ex, False)
 eng.launch(p0, None)
 p1 = eng.prepare(s1, c1[0], c1[2], H, z, ex, True,
                  prev_layout=(p0.starts, p0.counts, ex, p0.plan, p0.n))
-ws = Workspace.for_step(p1, eng.device)
+ws = Workspace.for_step(p1, eng.device, eng.entries, eng.n_wg)
 St = namedtuple('St', 'ids rhat meta')
 for rep in range(3):
     eng.launch(p1, ws, St(s0['ids'], p0.rhat, p0.meta))
@@ -40,6 +40,17 @@ assert got > 0, 'not a stamps build'
 tw = buf.reshape(ni, sn).astype(np.float64) * 10.0 / 1000.0   # 100 MHz -> us
 tw -= tw[:, 0].min()
 t = tw[:, :6]
+if eng.n_wg > 0:      # persistent k_stream: per-item stamps 0..5
+    for name, a_, b_ in (('insert', 0, 1), ('walks+hdr', 1, 2), ('interleave', 2, 3),
+                         ('barrier', 3, 4), ('phase3', 4, 5), ('total', 0, 5)):
+        d = t[:, b_] - t[:, a_]
+        print('%-11s mean %7.2f  p10 %7.2f  p50 %7.2f  p90 %7.2f  max %7.2f us'
+              % (name, d.mean(), *np.percentile(d, [10, 50, 90]), d.max()))
+    span = t[:, 5].max() - t[:, 0].min()
+    busy = (t[:, 5] - t[:, 0]).sum() / eng.n_wg
+    print('items', ni, 'wgs', eng.n_wg, 'span %.1f us, busy per wg %.1f us (gaps %.1f)'
+          % (span, busy, span - busy))
+    sys.exit(0)
 w1, w2 = tw[:, 6::2], tw[:, 7::2]                  # per-wave ends of the phase-1 / 2 loops
 for name, w in (('wave skew phase1 end', w1), ('wave skew phase2 end', w2)):
     d = w.max(1) - w.min(1)
