@@ -310,11 +310,153 @@ def run_functions(T, U):
     return out
 
 
+# ------------------------------------------------- §8(f) rows f3 (collate) and f4 (progenitors)
+COLLATE_CASES = {
+    # name: (batch case, [(tag, collate kwargs, final-counts kwargs or None)])
+    'g1_config1': [('default', {}, {}), ('cut0', dict(angle_cut=0.0), None)],
+    'g2_overlap_birth_massarray': [('default', {}, {}),
+                                   ('np64cut', dict(angle_cut=np.float64(0.3), data_type=np.int64), {})],
+    'g3_apo_periodic': [('default', {}, {})],
+    'g8_many_small_halos': [('default', {}, {}),
+                            ('subset', dict(halo_subset=11, snapshot_index=-2, angle_cut=0.5), None),
+                            ('snaps', dict(angle_cut=np.float32(1.0)), dict(snapshot_numbers='first'))],
+}
+
+
+def run_collate(syn, T, P):
+    out = {}
+    meta = {}
+    rng = np.random.default_rng(99)
+    for name, runs in COLLATE_CASES.items():
+        case = BATCH_CASES[name]
+        u = syn.PlummerSnapshots(**gen_kwargs(case['gen']))
+        path = '/mem/collate_in_%s.hdf5' % name
+        T.track_orbits(u.snapshot_numbers, u.main_branches(), u.regions, u.load_snapshot_data,
+                       path, npool=None, verbose=False, **case['run'])
+        f = FILES[path]
+        out['%s/in/attr/mode' % name] = np.array(f.attrs['mode'])
+        for gname in f.keys():
+            for dname, arr in f[gname].items():
+                out['%s/in/%s/%s' % (name, gname, dname)] = arr
+        for tag, kw, fkw in runs:
+            kw = dict(kw)
+            ap = P.Apsides(path)
+            rec = {'tag': tag}
+            if 'halo_subset' in kw:
+                hs = rng.permutation(ap.final_halo_ids)[:kw.pop('halo_subset')]
+                kw['halo_ids'] = hs
+                out['%s/%s/halo_ids' % (name, tag)] = hs
+            if 'snapshot_index' in kw:
+                kw['snapshot_number'] = int(ap.snapshot_numbers[kw.pop('snapshot_index')])
+                rec['snapshot_number'] = kw['snapshot_number']
+            for k in ('angle_cut', 'data_type'):
+                if k in kw:
+                    rec[k] = repr(kw[k])
+            opath = '/mem/collate_out_%s_%s.hdf5' % (name, tag)
+            ap.collate_apsides(savefile=opath, verbose=False, **kw)
+            if fkw is not None:
+                fk = dict(fkw)
+                if fk.get('snapshot_numbers') == 'first':
+                    fk['snapshot_numbers'] = [int(ap.snapshot_numbers[0])]
+                    rec['final_snapshot_numbers'] = fk['snapshot_numbers']
+                ap.save_final_apsis_counts(opath, verbose=False, **fk)
+                rec['final_counts'] = True
+            g = FILES[opath]
+            for gname in g.keys():
+                for dname, arr in g[gname].items():
+                    out['%s/%s/out/%s/%s' % (name, tag, gname, dname)] = arr
+            meta.setdefault(name, []).append(rec)
+    out['meta_json'] = np.array(json.dumps(meta))
+    return out
+
+
+CENTRAL_CASES = {
+    'f64_nobox': dict(gen=dict(n_halos=3, n_per_halo=[900, 400, 1300], n_snapshots=2, seed=31,
+                               dt=0.5), n=100),
+    'f64_box': dict(gen=dict(n_halos=3, n_per_halo=[800, 600, 700], n_snapshots=2, seed=32,
+                             dt=0.5, box_size=30.0,
+                             centres=[[0.2, 29.9, 15.0], [29.5, 0.3, 0.1], [15.0, 15.0, 29.8]]),
+                    n=50),
+    'f32_c32_listbox': dict(gen=dict(n_halos=2, n_per_halo=[1000, 500], n_snapshots=2, seed=33,
+                                     dt=0.5, dtype='float32', centre_dtype='float32',
+                                     box_size=[20.0, 25.0, 30.0],
+                                     centres=[[19.8, 0.5, 10.0], [1.0, 24.0, 29.5]]), n=600),
+    'f32_c64': dict(gen=dict(n_halos=3, n_per_halo=[700, 300, 500], n_snapshots=2, seed=34,
+                             dt=0.5, dtype='float32', centre_dtype='float64', box_size=40.0,
+                             centres=[[39.9, 20.0, 0.1], [5.0, 5.0, 5.0], [20.0, 39.5, 20.0]]),
+                    n=7),
+}
+
+
+def run_progenitors(syn, P):
+    out = {}
+    meta = {}
+    for name, case in CENTRAL_CASES.items():
+        u = syn.PlummerSnapshots(**gen_kwargs(case['gen']))
+        s = int(u.snapshot_numbers[-1])
+        hids = np.arange(len(u.main_branches()[-1]))
+        pos, rad = u.regions(s, hids)[:2]
+        snap = u.load_snapshot_data(s, pos, rad)
+        ids, offs = P.get_central_particle_ids(snap, pos, n=case['n'])
+        pre = 'central/%s/' % name
+        for k in ('ids', 'coordinates', 'region_offsets'):
+            out[pre + k] = np.asarray(snap[k])
+        if 'box_size' in snap:
+            out[pre + 'box_size'] = np.asarray(snap['box_size'])
+            meta[name + '/box_is_list'] = isinstance(snap['box_size'], list)
+        out[pre + 'halo_positions'] = np.asarray(pos)
+        out[pre + 'out_ids'], out[pre + 'out_offsets'] = ids, offs
+        meta[name + '/n'] = case['n']
+    # find_main_progenitors: disjoint halo blocks (some empty), tracked blocks drawing on a
+    # majority halo, a tied pair, absent IDs, duplicates across blocks and an empty block
+    rng = np.random.default_rng(35)
+    for name, id_dtype in (('i64', np.int64), ('i32', np.int32)):
+        sizes = rng.integers(0, 400, 30)
+        sizes[[4, 17]] = 0
+        pool = rng.permutation(60000)[:int(sizes.sum()) + 2000].astype(id_dtype)
+        halo_pids = pool[:int(sizes.sum())]
+        absent = pool[int(sizes.sum()):]
+        halo_offsets = np.cumsum(np.concatenate([[0], sizes[:-1]]))
+        blocks_ = [halo_pids[a:a + n] for a, n in zip(halo_offsets, sizes)]
+        tracked = []
+        for b in range(40):
+            if b == 7:
+                tracked.append(np.array([], dtype=id_dtype))
+                continue
+            if b == 9:
+                tracked.append(rng.choice(absent, 20, replace=False))
+                continue
+            parts = []
+            for h in rng.choice(30, rng.integers(1, 4), replace=False):
+                if len(blocks_[h]):
+                    parts.append(rng.choice(blocks_[h], min(len(blocks_[h]), int(rng.integers(1, 60))),
+                                            replace=False))
+            if b == 11:     # exact tie between two halos: the lower halo number wins
+                nz = [h for h in range(30) if len(blocks_[h]) >= 10]
+                parts = [blocks_[nz[5]][:10], blocks_[nz[2]][:10]]
+            parts.append(rng.choice(absent, int(rng.integers(0, 5)), replace=False))
+            tracked.append(rng.permutation(np.concatenate(parts)).astype(id_dtype))
+        # duplicates: later blocks re-track IDs of earlier ones
+        tracked[20] = np.concatenate([tracked[20], tracked[3][:15]])
+        tracked[25] = np.concatenate([tracked[1][:40], tracked[25]])
+        tracked_offsets = np.cumsum([0] + [len(t) for t in tracked])[:-1]
+        tracked_pids = np.concatenate(tracked)
+        res = P.find_main_progenitors(halo_pids, halo_offsets, tracked_pids, tracked_offsets)
+        pre = 'mainprog/%s/' % name
+        out[pre + 'halo_pids'], out[pre + 'halo_offsets'] = halo_pids, halo_offsets
+        out[pre + 'tracked_pids'], out[pre + 'tracked_offsets'] = tracked_pids, tracked_offsets
+        out[pre + 'out'] = np.array([int(v) for v in res], dtype=np.int64)
+    out['meta_json'] = np.array(json.dumps(meta))
+    return out
+
+
 def main():
     install_stubs()
     import orbitanalysis.track_orbits as T
     import orbitanalysis.track_orbits_onthefly as O
     import orbitanalysis.utils as U
+    import orbitanalysis.postprocessing as P
+    import orbitanalysis.progenitors as G
     syn = load_synthetic()
     os.makedirs(OUT, exist_ok=True)
     only = set(sys.argv[1:])          # optional: regenerate just the named fixtures
@@ -332,6 +474,12 @@ def main():
     if not only or 'g7_functions' in only:
         np.savez_compressed(os.path.join(OUT, 'g7_functions.npz'), **run_functions(T, U))
         print('wrote g7_functions')
+    if not only or 'g9_collate' in only:
+        np.savez_compressed(os.path.join(OUT, 'g9_collate.npz'), **run_collate(syn, T, P))
+        print('wrote g9_collate')
+    if not only or 'g10_progenitors' in only:
+        np.savez_compressed(os.path.join(OUT, 'g10_progenitors.npz'), **run_progenitors(syn, G))
+        print('wrote g10_progenitors')
 
 
 if __name__ == '__main__':
