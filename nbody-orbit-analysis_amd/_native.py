@@ -13,7 +13,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.abspath(__file__))
 # ORBIT_HIP_LIB selects an alternative build (kernel variants for tuning sweeps)
 LIB_PATH = os.environ.get('ORBIT_HIP_LIB') or os.path.join(PKG, 'liborbit_hip.so')
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -56,7 +56,39 @@ class CompactArgs(ctypes.Structure):
                 ('total_out', c_vp)]
 
 
-# every symbol include/orbit_hip.h declares: name -> (restype, argtypes)
+class CollateArgs(ctypes.Structure):
+    _fields_ = [('n_halos', c_i32), ('in_kind', c_i32), ('key_signed', c_i32),
+                ('chunk_start', c_i32), ('apsis_ids', c_vp), ('angles', c_vp),
+                ('keep_lut', c_vp), ('src_off', c_vp), ('src_cnt', c_vp), ('new_base', c_vp),
+                ('old_keys', c_vp), ('old_cnt', c_vp), ('old_off', c_vp), ('n_old', c_i64),
+                ('n_new_cap', c_i64), ('w_keys', c_vp), ('w_cnt', c_vp), ('w_lb', c_vp),
+                ('w_fp', c_vp), ('w_ulen', c_vp), ('w_found', c_vp), ('new_off', c_vp),
+                ('new_keys', c_vp), ('new_cnt', c_vp)]
+
+
+class CentralArgs(ctypes.Structure):
+    _fields_ = [('coords', c_vp), ('coord_f64', c_i32), ('dx_f64', c_i32),
+                ('positions', c_vp), ('ids', c_vp), ('id_bytes', c_i32), ('n_halos', c_i32),
+                ('offsets', c_vp), ('out_offsets', c_vp), ('n', c_i32), ('n_box_dims', c_i32),
+                ('wrap_f64', c_i32 * 3), ('box', c_dbl * 3), ('half', c_dbl * 3),
+                ('scratch', c_vp), ('out_ids', c_vp)]
+
+
+class MainProgArgs(ctypes.Structure):
+    _fields_ = [('halo_pids', c_vp), ('halo_kind', c_i32), ('n_halo_pids', c_i64),
+                ('halo_offsets', c_vp), ('n_halos', c_i32), ('tracked', c_vp),
+                ('tracked_kind', c_i32), ('n_tracked', c_i64), ('tracked_offsets', c_vp),
+                ('n_blocks', c_i32), ('max_block', c_i32), ('tab_keys', c_vp), ('result', c_vp),
+                ('status', c_vp)]
+
+
+# include/orbit_post.h constants
+ID_KIND = {np.dtype('int64'): 0, np.dtype('uint64'): 1, np.dtype('int32'): 2, np.dtype('uint32'): 3}
+COLLATE_CHUNK = 8192
+CENTRAL_MAX_N = 4096
+POST_MISSING, POST_SENTINEL, POST_OVERFLOW = 1, 2, 4
+
+# every symbol include/orbit_hip.h and include/orbit_post.h declare: name -> (restype, argtypes)
 SYMBOLS = {
     'oa_abi_version': (ctypes.c_int, []),
     'oa_build_info': (c_i32, [c_i32]),
@@ -74,6 +106,15 @@ SYMBOLS = {
     'oa_compare_pairs': (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,
                                         c_vp, c_vp, c_vp]),
     'oa_angle_add': (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    # orbit_post.h
+    'oa_post_struct_size': (c_i64, [c_i32]),
+    'oa_collate_step': (ctypes.c_int, [ctypes.POINTER(CollateArgs), c_vp]),
+    'oa_keys_to_ids': (ctypes.c_int, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
+    'oa_retro_counts': (ctypes.c_int, [c_vp, c_i32, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp,
+                                       c_vp, c_vp, c_vp]),
+    'oa_central_ids': (ctypes.c_int, [ctypes.POINTER(CentralArgs), c_vp]),
+    'oa_mainprog_workspace_bytes': (c_i64, [c_i64, c_i64]),
+    'oa_main_progenitors': (ctypes.c_int, [ctypes.POINTER(MainProgArgs), c_vp]),
 }
 
 
@@ -110,6 +151,12 @@ def load(require_device=False):
             if lib.oa_struct_size(k) != v:
                 raise NativeUnavailable('ABI struct %d size mismatch: C %d, Python %d'
                                         % (k, lib.oa_struct_size(k), v))
+        post = {0: ctypes.sizeof(CollateArgs), 1: ctypes.sizeof(CentralArgs),
+                2: ctypes.sizeof(MainProgArgs)}
+        for k, v in post.items():
+            if lib.oa_post_struct_size(k) != v:
+                raise NativeUnavailable('ABI post struct %d size mismatch: C %d, Python %d'
+                                        % (k, lib.oa_post_struct_size(k), v))
         _LIB = lib
     if require_device:
         import torch

@@ -2047,6 +2047,12 @@ int launch_big(const oa_step_args &a, hipStream_t st) {
 
 }  // namespace
 
+// Error channel shared with the second translation unit (orbit_post.hip):
+// nullptr clears the message, anything else becomes oa_last_error().
+void oa_internal_error(const char *msg) {
+    if (msg) fail(OA_E_ARG, "%s", msg); else g_err[0] = 0;
+}
+
 extern "C" {
 
 int oa_abi_version(void) { return OA_ABI_VERSION; }

@@ -1,0 +1,707 @@
+// orbit_post.hip — MI355X (gfx950) kernels for SURVEY.md §8(f) rows f3 and f4, the
+// consumer and the producer either side of the orbit-tagging path, behind the C ABI
+// of include/orbit_post.h (second translation unit of liborbit_hip.so).
+//
+// Reference (paths under /root/reference/orbitanalysis/):
+//   Apsides.collate_apsides        postprocessing.py:118-142 -> k_collate_new,
+//                                  k_collate_offsets, k_collate_merge
+//   Apsides.save_final_apsis_counts postprocessing.py:215-236 -> k_retro_counts
+//   get_central_particle_ids       progenitors.py:38-56       -> k_central
+//   find_main_progenitors          progenitors.py:82-117      -> k_mp_insert,
+//                                  k_mp_lookup, k_mp_tally
+//
+// Design: no global sort anywhere.
+//  * collate keeps, per collated halo, the cumulative sorted-unique (ID, count) list
+//    the reference rebuilds with np.unique every snapshot; a snapshot's kept apsis IDs
+//    are sorted per halo in LDS (bitonic, <= OA_COLLATE_CHUNK keys), run-length
+//    encoded, located in the old list by binary search, and the merged list is
+//    written by one thread per element at its merge-path rank;
+//  * central IDs: per region block, an MSB-first 8-bit radix select of the n-th
+//    smallest radius (radius keys cached in LDS for blocks <= 8192) and an LDS
+//    bitonic sort of the <= n survivors by (radius, position);
+//  * main progenitors: open-addressing tables in HBM for halo members and for the
+//    first occurrence of every tracked ID, then a per-block LDS tally.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <math.h>
+
+#include "orbit_hip.h"
+#include "orbit_post.h"
+
+void oa_internal_error(const char *msg);   // orbit_hip.hip: owns oa_last_error()'s buffer
+
+namespace {
+
+int fail(int code, const char *msg) {
+    oa_internal_error(msg);
+    return code;
+}
+
+int check_launch(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) return OA_OK;
+    char b[256];
+    snprintf(b, sizeof(b), "%s: %s", what, hipGetErrorString(e));
+    return fail(OA_E_LAUNCH, b);
+}
+
+constexpr uint64_t SIGN = 0x8000000000000000ull;
+constexpr int CH = OA_COLLATE_CHUNK;
+constexpr int KC = 8192;                 // k_central: radius keys cached in LDS
+constexpr int SC = OA_CENTRAL_MAX_N;     // k_central: survivors sorted in LDS
+
+// value of element i as 64-bit two's complement (signed kinds sign-extend)
+__device__ __forceinline__ uint64_t load_val(const void *p, int64_t i, int kind) {
+    switch (kind) {
+        case OA_ID_I64:
+        case OA_ID_U64: return static_cast<const uint64_t *>(p)[i];
+        case OA_ID_I32: return (uint64_t)(int64_t) static_cast<const int32_t *>(p)[i];
+        default: return (uint64_t) static_cast<const uint32_t *>(p)[i];
+    }
+}
+__device__ __forceinline__ uint64_t to_key(uint64_t v, int key_signed) {
+    return key_signed ? v ^ SIGN : v;
+}
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 33; x *= 0xFF51AFD7ED558CCDull; x ^= x >> 33; x *= 0xC4CEB9FE1A85EC53ull;
+    return x ^ (x >> 33);
+}
+// largest j in [0, n) with off[j] <= t  (the segment holding t; empty segments precede it)
+__device__ __forceinline__ int seg_of(const int64_t *off, int n, int64_t t) {
+    int lo = 0, hi = n;                  // invariant: off[lo] <= t (callers guarantee off[0] <= t)
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (off[mid] <= t) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// exclusive work-group scan of one value per thread (NT threads, whole waves)
+template <int NT, typename T>
+__device__ __forceinline__ T block_scan(T v, T *wsum, T &total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    T incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const T y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T acc = 0;
+        for (int k = 0; k < NT / 64; ++k) { const T t = wsum[k]; wsum[k] = acc; acc += t; }
+        wsum[NT / 64] = acc;
+    }
+    __syncthreads();
+    const T r = wsum[w] + incl - v;
+    total = wsum[NT / 64];
+    __syncthreads();
+    return r;
+}
+
+// ascending bitonic sort of P (power of two) keys in LDS, NT threads
+template <int NT>
+__device__ void bitonic_keys(uint64_t *s, int P) {
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P; i += NT) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint64_t a = s[i], b = s[ixj];
+                    if ((a > b) == ((i & k) == 0)) { s[i] = b; s[ixj] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+// ... of (key, index) pairs, lexicographic
+template <int NT>
+__device__ void bitonic_pairs(uint64_t *s, uint32_t *x, int P) {
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P; i += NT) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint64_t a = s[i], b = s[ixj];
+                    const uint32_t ia = x[i], ib = x[ixj];
+                    const bool gt = a > b || (a == b && ia > ib);
+                    if (gt == ((i & k) == 0)) { s[i] = b; s[ixj] = a; x[i] = ib; x[ixj] = ia; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// ------------------------------------------------------------------ f3: collate
+// One work-group per collated halo: this round's kept apsis IDs (angle > cut via the
+// NumPy-evaluated LUT, postprocessing.py:127-128), sorted, run-length encoded
+// (np.unique(return_counts), :135), each unique key located in the halo's old list.
+__global__ __launch_bounds__(1024) void k_collate_new(const oa_collate_args a) {
+    __shared__ uint64_t sk[CH];
+    __shared__ int hp[CH + 1];
+    __shared__ int wsum[17];
+    __shared__ int s_m;
+    const int j = blockIdx.x;
+    const int64_t rem = a.src_cnt[j] - a.chunk_start;
+    if (rem <= 0) {
+        if (threadIdx.x == 0) { a.w_ulen[j] = 0; a.w_found[j] = 0; }
+        return;
+    }
+    const int nraw = rem < CH ? (int)rem : CH;
+    const int64_t s0 = a.src_off[j] + a.chunk_start;
+    const int64_t base = a.new_base[j];
+    const int64_t ob = a.old_off[j], on = a.old_off[j + 1] - ob;
+    if (threadIdx.x == 0) s_m = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < nraw; i += 1024) {
+        if (a.keep_lut[a.angles[s0 + i]]) {
+            const int p = atomicAdd(&s_m, 1);
+            sk[p] = to_key(load_val(a.apsis_ids, s0 + i, a.in_kind), a.key_signed);
+        }
+    }
+    __syncthreads();
+    const int m = s_m;
+    if (m == 0) {
+        if (threadIdx.x == 0) { a.w_ulen[j] = 0; a.w_found[j] = 0; }
+        return;
+    }
+    int P = 1;
+    while (P < m) P <<= 1;
+    for (int i = m + threadIdx.x; i < P; i += 1024) sk[i] = ~0ull;   // ties with a real ~0 key are harmless
+    __syncthreads();
+    bitonic_keys<1024>(sk, P);
+    // run heads: thread t owns positions [t*E, t*E + E)
+    const int E = (m + 1023) / 1024;
+    const int lo = threadIdx.x * E, hi = min(lo + E, m);
+    int nh = 0;
+    for (int i = lo; i < hi; ++i) nh += (i == 0 || sk[i] != sk[i - 1]);
+    int u;
+    int q = block_scan<1024, int>(nh, wsum, u);
+    for (int i = lo; i < hi; ++i)
+        if (i == 0 || sk[i] != sk[i - 1]) hp[q++] = i;
+    if (threadIdx.x == 0) hp[u] = m;
+    __syncthreads();
+    int carry = 0;
+    for (int q0 = 0; q0 < u; q0 += 1024) {
+        const int qq = q0 + threadIdx.x;
+        int f = 0;
+        uint64_t key = 0;
+        int64_t lb = 0;
+        int c = 0;
+        if (qq < u) {
+            key = sk[hp[qq]];
+            c = hp[qq + 1] - hp[qq];
+            int64_t L = 0, R = on;
+            while (L < R) {
+                const int64_t mid = (L + R) >> 1;
+                if (a.old_keys[ob + mid] < key) L = mid + 1; else R = mid;
+            }
+            lb = L;
+            f = (L < on && a.old_keys[ob + L] == key) ? 1 : 0;
+        }
+        int tf;
+        const int ex = block_scan<1024, int>(f, wsum, tf);
+        if (qq < u) {
+            a.w_keys[base + qq] = key;
+            a.w_cnt[base + qq] = c;
+            a.w_lb[base + qq] = lb;
+            a.w_fp[base + qq] = carry + ex;
+        }
+        carry += tf;
+    }
+    if (threadIdx.x == 0) { a.w_ulen[j] = u; a.w_found[j] = carry; }
+}
+
+// merged lengths -> offsets (one work-group; n_halos is a catalogue size)
+__global__ __launch_bounds__(1024) void k_collate_offsets(const oa_collate_args a) {
+    __shared__ int64_t wsum[17];
+    int64_t carry = 0;
+    for (int j0 = 0; j0 < a.n_halos; j0 += 1024) {
+        const int j = j0 + threadIdx.x;
+        int64_t v = 0;
+        if (j < a.n_halos) v = (a.old_off[j + 1] - a.old_off[j]) + a.w_ulen[j] - a.w_found[j];
+        int64_t tot;
+        const int64_t ex = block_scan<1024, int64_t>(v, wsum, tot);
+        if (j < a.n_halos) a.new_off[j] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) a.new_off[a.n_halos] = carry;
+}
+
+// one thread per old element (rank i + #new keys below it not already present) and per
+// new unique key absent from the old list (rank lb + #such new keys before it)
+__global__ __launch_bounds__(256) void k_collate_merge(const oa_collate_args a) {
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (t < a.n_old) {
+        const int j = seg_of(a.old_off, a.n_halos, t);
+        const int64_t i = t - a.old_off[j];
+        const uint64_t key = a.old_keys[t];
+        const int u = a.w_ulen[j];
+        const int64_t base = a.new_base[j];
+        int L = 0, R = u;
+        while (L < R) {
+            const int mid = (L + R) >> 1;
+            if (a.w_keys[base + mid] < key) L = mid + 1; else R = mid;
+        }
+        const bool eq = L < u && a.w_keys[base + L] == key;
+        const int fl = L < u ? a.w_fp[base + L] : a.w_found[j];
+        const int64_t pos = a.new_off[j] + i + L - fl;
+        a.new_keys[pos] = key;
+        a.new_cnt[pos] = a.old_cnt[t] + (eq ? a.w_cnt[base + L] : 0);
+        return;
+    }
+    const int64_t e = t - a.n_old;
+    if (e >= a.n_new_cap) return;
+    const int j = seg_of(a.new_base, a.n_halos, e);
+    const int64_t base = a.new_base[j];
+    const int q = (int)(e - base);
+    const int u = a.w_ulen[j];
+    if (q >= u) return;
+    const int fp = a.w_fp[base + q];
+    const int fn = q + 1 < u ? a.w_fp[base + q + 1] : a.w_found[j];
+    if (fn != fp) return;                       // already in the old list: counted above
+    const int64_t pos = a.new_off[j] + a.w_lb[base + q] + (q - fp);
+    a.new_keys[pos] = a.w_keys[base + q];
+    a.new_cnt[pos] = a.w_cnt[base + q];
+}
+
+__global__ __launch_bounds__(256) void k_keys_to_ids(const uint64_t *keys, int64_t n, int key_signed,
+                                                     int out_kind, void *out) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t v = key_signed ? keys[i] ^ SIGN : keys[i];
+    if (out_kind == OA_ID_I64 || out_kind == OA_ID_U64) static_cast<uint64_t *>(out)[i] = v;
+    else static_cast<uint32_t *>(out)[i] = (uint32_t)v;
+}
+
+// save_final_apsis_counts (:222-236): per element, its count in the final snapshot
+__global__ __launch_bounds__(256) void k_retro_counts(const void *ids, int kind, int64_t n,
+                                                      const int64_t *offs, const int64_t *hinds,
+                                                      int n_seg, const void *ids_final,
+                                                      const int64_t *final_off,
+                                                      const int64_t *counts_final, double *out,
+                                                      int32_t *status) {
+    const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    double r = 0.0;
+    if (n_seg > 0 && e >= offs[0] && e < offs[n_seg]) {
+        const int sg = (kind == OA_ID_I64 || kind == OA_ID_I32) ? 1 : 0;
+        const int h2 = seg_of(offs, n_seg, e);
+        const int64_t h1 = hinds[h2];
+        const uint64_t key = to_key(load_val(ids, e, kind), sg);
+        int64_t L = final_off[h1], R = final_off[h1 + 1];
+        const int64_t end = R;
+        while (L < R) {
+            const int64_t mid = (L + R) >> 1;
+            if (to_key(load_val(ids_final, mid, kind), sg) < key) L = mid + 1; else R = mid;
+        }
+        if (L < end && to_key(load_val(ids_final, L, kind), sg) == key) r = (double)counts_final[L];
+        else atomicOr(status, (int32_t)OA_POST_MISSING);
+    }
+    out[e] = r;
+}
+
+// ------------------------------------------------------------------ f4: central IDs
+// radius key of particle p about the halo centre: dx in the promoted dtype TD,
+// recenter_coordinates (utils.py:24-33) per dim in its comparison dtype, then
+// region_coords (float64, progenitors.py:41) and sqrt(einsum) with the host's f64 tree
+template <typename TX, typename TD>
+__device__ __forceinline__ uint64_t radius_key(const TX *x, int64_t p, const double *c,
+                                               const oa_central_args &a) {
+    TD d[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) d[k] = (TD)x[3 * p + k] - (TD)c[k];
+    for (int k = 0; k < a.n_box_dims; ++k) {
+        if (a.wrap_f64[k]) {
+            double v = (double)d[k];
+            if (v > a.half[k]) d[k] = (TD)(v - a.box[k]);
+            v = (double)d[k];
+            if (v < -a.half[k]) d[k] = (TD)(v + a.box[k]);
+        } else {
+            const TD h = (TD)a.half[k], b = (TD)a.box[k];
+            if (d[k] > h) d[k] = d[k] - b;
+            if (d[k] < -h) d[k] = d[k] + b;
+        }
+    }
+    const double r0 = (double)d[0], r1 = (double)d[1], r2 = (double)d[2];
+    const double p0 = r0 * r0, p1 = r1 * r1, p2 = r2 * r2;
+    const double r = sqrt((p0 + p2) + p1);
+    return (uint64_t)__double_as_longlong(r);   // r >= +0 or NaN: bit order = numeric order, NaN last
+}
+
+template <typename TX, typename TD>
+__global__ __launch_bounds__(1024) void k_central(const oa_central_args a) {
+    __shared__ uint64_t kc[KC];
+    __shared__ uint64_t sk[SC];
+    __shared__ uint32_t si[SC];
+    __shared__ int hist[256];
+    __shared__ int wsum[17];
+    __shared__ uint64_t s_prefix;
+    __shared__ unsigned long long s_min, s_max;
+    __shared__ int s_need, s_cnt, s_done;
+    const int h = blockIdx.x;
+    const int64_t off = a.offsets[h];
+    const int m = (int)(a.offsets[h + 1] - off);
+    const int k = m < a.n ? m : a.n;
+    if (k <= 0) return;
+    const bool cached = m <= KC;
+    const TX *x = static_cast<const TX *>(a.coords);
+    const double *c = a.positions + 3 * (int64_t)h;
+    if (threadIdx.x == 0) { s_min = ~0ull; s_max = 0; s_cnt = 0; s_done = 0; }
+    __syncthreads();
+    uint64_t lmin = ~0ull, lmax = 0;
+    for (int i = threadIdx.x; i < m; i += 1024) {
+        const uint64_t key = radius_key<TX, TD>(x, off + i, c, a);
+        lmin = key < lmin ? key : lmin;
+        lmax = key > lmax ? key : lmax;
+        if (cached) kc[i] = key; else a.scratch[off + i] = key;
+    }
+    if (threadIdx.x < m) { atomicMin(&s_min, lmin); atomicMax(&s_max, lmax); }
+    __syncthreads();
+#define KEY(i) (cached ? kc[i] : a.scratch[off + (i)])
+    if (k == m) {
+        for (int i = threadIdx.x; i < m; i += 1024) { sk[i] = KEY(i); si[i] = i; }
+    } else {
+        // MSB-first radix select of the k-th smallest key.  Bits above the highest bit
+        // where the block's min and max keys differ are common and skipped; each pass
+        // histograms the next <= 8 bits of the keys still matching the fixed prefix.
+        // A pass whose chosen bin is taken whole ends the select early (inclusive bound
+        // hi); otherwise T = the exact k-th key and `need` ties to it are taken by
+        // position.
+        const uint64_t diff = s_min ^ s_max;
+        int lo_fixed = diff ? 64 - __clzll((long long)diff) : 0;    // bits below are free
+        uint64_t prefix = lo_fixed >= 64 ? 0ull : (s_min & ~((1ull << lo_fixed) - 1ull));
+        int need = k;
+        while (lo_fixed > 0) {
+            const int s = lo_fixed > 8 ? lo_fixed - 8 : 0;
+            const int w = lo_fixed - s;
+            for (int d = threadIdx.x; d < 256; d += 1024) hist[d] = 0;
+            __syncthreads();
+            for (int i = threadIdx.x; i < m; i += 1024) {
+                const uint64_t key = KEY(i);
+                if (lo_fixed >= 64 || (key >> lo_fixed) == (prefix >> lo_fixed))
+                    atomicAdd(&hist[(key >> s) & ((1u << w) - 1u)], 1);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                int acc = 0, d = 0;
+                for (; d < (1 << w) - 1; ++d) {
+                    if (acc + hist[d] >= need) break;
+                    acc += hist[d];
+                }
+                s_prefix = prefix | ((uint64_t)d << s);
+                s_need = need - acc;
+                s_done = hist[d] == need - acc;             // the whole bin is selected
+            }
+            __syncthreads();
+            prefix = s_prefix;
+            need = s_need;
+            lo_fixed = s;
+            if (s_done) break;
+        }
+        if (lo_fixed > 0) {                  // early end: every key <= hi, exactly k of them
+            const uint64_t hi = prefix | ((1ull << lo_fixed) - 1ull);
+            for (int i = threadIdx.x; i < m; i += 1024) {
+                const uint64_t key = KEY(i);
+                if (key <= hi) {
+                    const int p = atomicAdd(&s_cnt, 1);
+                    sk[p] = key;
+                    si[p] = (uint32_t)i;
+                }
+            }
+            need = 0;
+        }
+        const uint64_t T = prefix;
+        if (need > 0) {
+            for (int i = threadIdx.x; i < m; i += 1024) {
+                const uint64_t key = KEY(i);
+                if (key < T) {
+                    const int p = atomicAdd(&s_cnt, 1);
+                    sk[p] = key;
+                    si[p] = (uint32_t)i;
+                }
+            }
+        }
+        __syncthreads();
+        const int lt = s_cnt;                      // = k - need
+        int taken = 0;                             // ties to T: lowest positions first
+        for (int i0 = 0; i0 < m && taken < need; i0 += 1024) {
+            const int i = i0 + threadIdx.x;
+            const int f = (i < m && KEY(i) == T) ? 1 : 0;
+            int tot;
+            const int ex = block_scan<1024, int>(f, wsum, tot);
+            if (f && taken + ex < need) { sk[lt + taken + ex] = T; si[lt + taken + ex] = (uint32_t)i; }
+            taken += tot;
+        }
+    }
+#undef KEY
+    __syncthreads();
+    int P = 1;
+    while (P < k) P <<= 1;
+    for (int i = k + threadIdx.x; i < P; i += 1024) { sk[i] = ~0ull; si[i] = 0xFFFFFFFFu; }
+    __syncthreads();
+    bitonic_pairs<1024>(sk, si, P);
+    const int64_t o = a.out_offsets[h];
+    for (int r = threadIdx.x; r < k; r += 1024) {
+        const int64_t src = off + si[r];
+        if (a.id_bytes == 8)
+            static_cast<uint64_t *>(a.out_ids)[o + r] = static_cast<const uint64_t *>(a.ids)[src];
+        else
+            static_cast<uint32_t *>(a.out_ids)[o + r] = static_cast<const uint32_t *>(a.ids)[src];
+    }
+}
+
+// ------------------------------------------------------------------ f4: main progenitors
+// The table is built over the SMALL side (the tracked central IDs, ~n per descendant)
+// and the halo members are streamed past it once.  A slot is {key, first tracked index,
+// smallest member position holding the key}, 16 B; the table stays L2 / MALL resident.
+constexpr uint64_t EMPTY = SIGN;          // INT64_MIN marks a free slot (rejected as an ID)
+struct MpSlot { uint64_t key; uint32_t first; uint32_t hpos; };
+
+__global__ __launch_bounds__(256) void k_mp_fill(MpSlot *tab, uint64_t cap, uint32_t *neg1) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i < cap) { tab[i].key = EMPTY; tab[i].first = 0xFFFFFFFFu; tab[i].hpos = 0xFFFFFFFFu; }
+    if (i == 0) *neg1 = 0xFFFFFFFFu;
+}
+
+// tracked value -> smallest index holding it (np.unique(return_index=True), :82)
+__global__ __launch_bounds__(256) void k_mp_insert(const void *src, int kind, int64_t n,
+                                                   MpSlot *tab, uint64_t cap, int32_t *status) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t v = load_val(src, i, kind);
+    if (v == EMPTY) { atomicOr(status, (int32_t)OA_POST_SENTINEL); return; }
+    uint64_t s = mix64(v) & (cap - 1);
+    for (uint64_t t = 0; t < cap; ++t) {
+        uint64_t cur = tab[s].key;
+        if (cur == EMPTY)
+            cur = atomicCAS((unsigned long long *)&tab[s].key, (unsigned long long)EMPTY,
+                            (unsigned long long)v);
+        if (cur == EMPTY || cur == v) { atomicMin(&tab[s].first, (uint32_t)i); return; }
+        s = (s + 1) & (cap - 1);
+    }
+}
+
+__device__ __forceinline__ int64_t mp_find(const MpSlot *tab, uint64_t cap, uint64_t v) {
+    uint64_t s = mix64(v) & (cap - 1);
+    for (uint64_t t = 0; t < cap; ++t) {
+        const uint64_t cur = tab[s].key;
+        if (cur == v) return (int64_t)s;
+        if (cur == EMPTY) return -1;
+        s = (s + 1) & (cap - 1);
+    }
+    return -1;
+}
+
+// stream the halo members once: a member whose ID is tracked records its position (the
+// in1d(tracked, halo_pids) / myin1d(halo_pids, ...) join, :95-99); the position of a
+// member equal to -1 is kept apart for the de-duplicated tracked entries (:83)
+__global__ __launch_bounds__(256) void k_mp_probe(const void *hp, int kind, int64_t n,
+                                                  MpSlot *tab, uint64_t cap, uint32_t *neg1) {
+    const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint64_t v = load_val(hp, p, kind);
+    if (v == ~0ull) atomicMin(neg1, (uint32_t)p);
+    const int64_t s = mp_find(tab, cap, v);
+    if (s >= 0) atomicMin(&tab[s].hpos, (uint32_t)p);
+}
+
+// per tracked entry: duplicates become -1 (:83-84), then the halo number of the member
+// holding it (halo_number[inds], :92-102), or -1
+__global__ __launch_bounds__(256) void k_mp_lookup(const oa_mainprog_args a, const MpSlot *tab,
+                                                   uint64_t cap, const uint32_t *neg1, int32_t *hn) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= a.n_tracked) return;
+    const uint64_t v = load_val(a.tracked, i, a.tracked_kind);
+    const int64_t s = mp_find(tab, cap, v);
+    uint32_t p = 0xFFFFFFFFu;
+    if (s >= 0) p = tab[s].first == (uint32_t)i ? tab[s].hpos : *neg1;
+    int32_t r = -1;
+    if (p != 0xFFFFFFFFu && a.n_halos > 0 && a.halo_offsets[0] <= (int64_t)p)
+        r = seg_of(a.halo_offsets, a.n_halos, (int64_t)p);
+    hn[i] = r;
+}
+
+// per tracked block: plurality halo number, ties to the lowest (np.unique + argmax, :107-115)
+__global__ __launch_bounds__(256) void k_mp_tally(const oa_mainprog_args a, const int32_t *hn,
+                                                  int ts) {
+    extern __shared__ uint32_t tab[];           // [ts] halo numbers, [ts] counts
+    __shared__ unsigned long long best;
+    uint32_t *tk = tab, *tc = tab + ts;
+    const int b = blockIdx.x;
+    for (int s = threadIdx.x; s < ts; s += 256) { tk[s] = 0xFFFFFFFFu; tc[s] = 0; }
+    if (threadIdx.x == 0) best = 0;
+    __syncthreads();
+    const int64_t lo = a.tracked_offsets[b], hi = a.tracked_offsets[b + 1];
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+        const int32_t h = hn[i];
+        if (h < 0) continue;
+        uint32_t s = (uint32_t)(mix64((uint64_t)h) & (uint64_t)(ts - 1));
+        int t = 0;
+        for (; t < ts; ++t) {
+            uint32_t cur = tk[s];
+            if (cur == 0xFFFFFFFFu) cur = atomicCAS(&tk[s], 0xFFFFFFFFu, (uint32_t)h);
+            if (cur == 0xFFFFFFFFu || cur == (uint32_t)h) { atomicAdd(&tc[s], 1u); break; }
+            s = (s + 1) & (uint32_t)(ts - 1);
+        }
+        if (t == ts) atomicOr(a.status, (int32_t)OA_POST_OVERFLOW);
+    }
+    __syncthreads();
+    unsigned long long mine = 0;
+    for (int s = threadIdx.x; s < ts; s += 256)
+        if (tc[s]) {
+            const unsigned long long v = ((unsigned long long)tc[s] << 32) | (0xFFFFFFFFull - tk[s]);
+            mine = v > mine ? v : mine;
+        }
+    if (mine) atomicMax(&best, mine);
+    __syncthreads();
+    if (threadIdx.x == 0)
+        a.result[b] = best ? (int64_t)(0xFFFFFFFFull - (best & 0xFFFFFFFFull)) : -1;
+}
+
+uint64_t pow2_at_least(uint64_t v, uint64_t lo) {
+    uint64_t c = lo;
+    while (c < v) c <<= 1;
+    return c;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t oa_post_struct_size(int32_t which) {
+    switch (which) {
+        case 0: return sizeof(oa_collate_args);
+        case 1: return sizeof(oa_central_args);
+        case 2: return sizeof(oa_mainprog_args);
+        default: return -1;
+    }
+}
+
+int oa_collate_step(const oa_collate_args *args, void *stream) {
+    oa_internal_error(nullptr);
+    if (!args) return fail(OA_E_ARG, "oa_collate_step: null args");
+    const oa_collate_args &a = *args;
+    if (a.n_halos <= 0) return OA_OK;
+    if (a.in_kind < 0 || a.in_kind > 3) return fail(OA_E_ARG, "oa_collate_step: bad id kind");
+    if (!a.src_off || !a.src_cnt || !a.new_base || !a.old_off || !a.new_off || !a.w_ulen ||
+        !a.w_found || (a.n_new_cap > 0 && (!a.apsis_ids || !a.angles || !a.keep_lut || !a.w_keys ||
+                                            !a.w_cnt || !a.w_lb || !a.w_fp)) ||
+        (a.n_old > 0 && (!a.old_keys || !a.old_cnt)) ||
+        (a.n_old + a.n_new_cap > 0 && (!a.new_keys || !a.new_cnt)))
+        return fail(OA_E_ARG, "oa_collate_step: null pointer");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(k_collate_new, dim3(a.n_halos), dim3(1024), 0, st, a);
+    if (int rc = check_launch("k_collate_new")) return rc;
+    hipLaunchKernelGGL(k_collate_offsets, dim3(1), dim3(1024), 0, st, a);
+    if (int rc = check_launch("k_collate_offsets")) return rc;
+    const int64_t n = a.n_old + a.n_new_cap;
+    if (n > 0) {
+        hipLaunchKernelGGL(k_collate_merge, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
+        if (int rc = check_launch("k_collate_merge")) return rc;
+    }
+    return OA_OK;
+}
+
+int oa_keys_to_ids(const uint64_t *keys, int64_t n, int32_t key_signed, int32_t out_kind,
+                   void *out, void *stream) {
+    oa_internal_error(nullptr);
+    if (n <= 0) return OA_OK;
+    if (!keys || !out || out_kind < 0 || out_kind > 3) return fail(OA_E_ARG, "oa_keys_to_ids: bad args");
+    hipLaunchKernelGGL(k_keys_to_ids, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), keys, n, key_signed, out_kind, out);
+    return check_launch("k_keys_to_ids");
+}
+
+int oa_retro_counts(const void *ids, int32_t kind, int64_t n, const int64_t *offs,
+                    const int64_t *hinds, int32_t n_seg, const void *ids_final,
+                    const int64_t *final_off, const int64_t *counts_final,
+                    double *out, int32_t *status, void *stream) {
+    oa_internal_error(nullptr);
+    if (n <= 0) return OA_OK;
+    if (kind < 0 || kind > 3) return fail(OA_E_ARG, "oa_retro_counts: bad id kind");
+    if (!ids || !out || !status || (n_seg > 0 && (!offs || !hinds || !final_off || !counts_final ||
+                                                  !ids_final)))
+        return fail(OA_E_ARG, "oa_retro_counts: null pointer");
+    hipLaunchKernelGGL(k_retro_counts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), ids, kind, n, offs, hinds, n_seg,
+                       ids_final, final_off, counts_final, out, status);
+    return check_launch("k_retro_counts");
+}
+
+int oa_central_ids(const oa_central_args *args, void *stream) {
+    oa_internal_error(nullptr);
+    if (!args) return fail(OA_E_ARG, "oa_central_ids: null args");
+    const oa_central_args &a = *args;
+    if (a.n_halos <= 0 || a.n <= 0) return OA_OK;
+    if (a.n > SC) return fail(OA_E_ARG, "oa_central_ids: n exceeds OA_CENTRAL_MAX_N");
+    if (a.id_bytes != 4 && a.id_bytes != 8) return fail(OA_E_ARG, "oa_central_ids: id_bytes");
+    if (a.n_box_dims < 0 || a.n_box_dims > 3) return fail(OA_E_ARG, "oa_central_ids: box dims");
+    if (a.coord_f64 && !a.dx_f64) return fail(OA_E_ARG, "oa_central_ids: dx narrower than coordinates");
+    if (!a.coords || !a.positions || !a.ids || !a.offsets || !a.out_offsets || !a.out_ids)
+        return fail(OA_E_ARG, "oa_central_ids: null pointer");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (a.coord_f64)
+        hipLaunchKernelGGL((k_central<double, double>), dim3(a.n_halos), dim3(1024), 0, st, a);
+    else if (a.dx_f64)
+        hipLaunchKernelGGL((k_central<float, double>), dim3(a.n_halos), dim3(1024), 0, st, a);
+    else
+        hipLaunchKernelGGL((k_central<float, float>), dim3(a.n_halos), dim3(1024), 0, st, a);
+    return check_launch("k_central");
+}
+
+int64_t oa_mainprog_workspace_bytes(int64_t n_halo_pids, int64_t n_tracked) {
+    (void)n_halo_pids;                     // the halo members are streamed, not tabled
+    const uint64_t ct = pow2_at_least(2 * (uint64_t)(n_tracked > 0 ? n_tracked : 1), 64);
+    return (int64_t)(ct * sizeof(MpSlot) + 4 * (uint64_t)(n_tracked > 0 ? n_tracked : 1) + 64);
+}
+
+int oa_main_progenitors(const oa_mainprog_args *args, void *stream) {
+    oa_internal_error(nullptr);
+    if (!args) return fail(OA_E_ARG, "oa_main_progenitors: null args");
+    const oa_mainprog_args &a = *args;
+    if (a.n_blocks <= 0) return OA_OK;
+    for (int k : {a.halo_kind, a.tracked_kind})
+        if (k != OA_ID_I64 && k != OA_ID_I32 && k != OA_ID_U32)
+            return fail(OA_E_ARG, "oa_main_progenitors: IDs must be int64, int32 or uint32");
+    if (a.n_halo_pids >= 0xFFFFFFFFll || a.n_tracked >= 0xFFFFFFFFll)
+        return fail(OA_E_ARG, "oa_main_progenitors: more than 2^32-1 IDs");
+    if (!a.tab_keys || !a.result || !a.status || !a.tracked_offsets ||
+        (a.n_tracked > 0 && !a.tracked) || (a.n_halo_pids > 0 && (!a.halo_pids || !a.halo_offsets)))
+        return fail(OA_E_ARG, "oa_main_progenitors: null pointer");
+    if (reinterpret_cast<uintptr_t>(a.tab_keys) & 15)
+        return fail(OA_E_ARG, "oa_main_progenitors: workspace must be 16-byte aligned");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const uint64_t ct = pow2_at_least(2 * (uint64_t)(a.n_tracked > 0 ? a.n_tracked : 1), 64);
+    MpSlot *tab = reinterpret_cast<MpSlot *>(a.tab_keys);
+    uint32_t *neg1 = reinterpret_cast<uint32_t *>(tab + ct);
+    int32_t *hn = reinterpret_cast<int32_t *>(neg1 + 16);
+    hipLaunchKernelGGL(k_mp_fill, dim3((unsigned)((ct + 255) / 256)), dim3(256), 0, st, tab, ct, neg1);
+    if (int rc = check_launch("k_mp_fill")) return rc;
+    if (a.n_tracked > 0) {
+        hipLaunchKernelGGL(k_mp_insert, dim3((unsigned)((a.n_tracked + 255) / 256)), dim3(256), 0,
+                           st, a.tracked, a.tracked_kind, a.n_tracked, tab, ct, a.status);
+        if (int rc = check_launch("k_mp_insert")) return rc;
+        if (a.n_halo_pids > 0) {
+            hipLaunchKernelGGL(k_mp_probe, dim3((unsigned)((a.n_halo_pids + 255) / 256)), dim3(256),
+                               0, st, a.halo_pids, a.halo_kind, a.n_halo_pids, tab, ct, neg1);
+            if (int rc = check_launch("k_mp_probe")) return rc;
+        }
+        hipLaunchKernelGGL(k_mp_lookup, dim3((unsigned)((a.n_tracked + 255) / 256)), dim3(256), 0,
+                           st, a, tab, ct, neg1, hn);
+        if (int rc = check_launch("k_mp_lookup")) return rc;
+    }
+    int ts = 64;
+    while (ts < 2 * a.max_block && ts < 16384) ts <<= 1;
+    if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_mp_tally),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, ts * 8) != hipSuccess)
+        return fail(OA_E_LAUNCH, "oa_main_progenitors: hipFuncSetAttribute");
+    hipLaunchKernelGGL(k_mp_tally, dim3(a.n_blocks), dim3(256), (size_t)ts * 8, st, a, hn, ts);
+    return check_launch("k_mp_tally");
+}
+
+}  // extern "C"

@@ -1,0 +1,167 @@
+"""SURVEY §8(f) rows f3/f4 on the device vs the reference's golden vectors
+(g9_collate, g10_progenitors) and the pinned oracle (needs a GPU).
+
+Bar: collated particle IDs, counts, offsets and halo tables, final counts, central
+IDs and main-progenitor numbers bit-exact (integer work)."""
+import numpy as np
+import pytest
+
+from golden_util import assert_same
+from post_golden import collate_runs, central_cases, mainprog_cases
+from oracle import post_oracle as PO
+
+pytestmark = pytest.mark.gpu
+
+RUNS = collate_runs()
+
+
+class _Mem:
+    def __init__(self, groups=None, attrs=None):
+        self.groups = groups if groups is not None else {}
+        self.attrs = attrs if attrs is not None else {}
+
+    def write_group(self, name, datasets):
+        if name in self.groups:
+            raise ValueError(name)
+        self.groups[name] = {k: np.asarray(v) for k, v in datasets.items()}
+
+
+def _collate(groups, attrs, kw, fkw):
+    from orbitanalysis_amd.postprocessing import Apsides
+    src = _Mem({g: dict(d) for g, d in groups.items()}, dict(attrs))
+    dst = _Mem()
+    ap = Apsides(src)
+    ap.collate_apsides(savefile=dst, verbose=False, **kw)
+    if fkw is not None:
+        ap.save_final_apsis_counts(dst, verbose=False, **fkw)
+    return dst.groups
+
+
+@pytest.mark.parametrize('run', RUNS, ids=['%s-%s' % r[:2] for r in RUNS])
+def test_collate_matches_reference(run):
+    case, tag, groups, attrs, kw, fkw, want = run
+    got = _collate(groups, attrs, kw, fkw)
+    assert sorted(got) == sorted(want)
+    for g in want:
+        assert list(got[g]) == list(want[g]), (g, list(got[g]), list(want[g]))
+        for d in want[g]:
+            assert_same(got[g][d], want[g][d], '%s/%s/%s' % (tag, g, d))
+
+
+def _random_track_file(rng, n_halos, n_snap, per_halo, id_dtype, id_hi, mode='pericentric'):
+    """Synthetic track_orbits output: per snapshot, apsis IDs drawn (with repeats
+    across snapshots) from per-halo pools, f16 angles, a halo that appears late."""
+    pools = [rng.choice(id_hi, size=per_halo * 3, replace=False).astype(id_dtype)
+             for _ in range(n_halos)]
+    groups = {}
+    tag = '{}er'.format(mode[:-3])
+    for s in range(1, n_snap + 1):
+        present = np.arange(n_halos) if s > 1 else np.arange(n_halos - 1)
+        lens = rng.integers(0, per_halo, len(present))
+        if s == 2:
+            lens[0] = 0
+        ids = [rng.choice(pools[h], size=l, replace=False) for h, l in zip(present, lens)]
+        g = {'region_offsets': np.cumsum([0] + [len(x) for x in ids]),
+             tag + '_IDs': np.concatenate(ids).astype(id_dtype) if ids else np.zeros(0, id_dtype),
+             'angles': rng.uniform(0, 3, int(lens.sum())).astype(np.float16),
+             'halo_IDs': present + 100}
+        if s != n_snap:
+            g['final_descendant_IDs'] = present + 100
+        g['region_radii'] = rng.uniform(1, 2, len(present))
+        g['region_positions'] = rng.uniform(0, 9, (len(present), 3))
+        g['bulk_velocities'] = rng.normal(0, 1, (len(present), 3))
+        groups['snapshot_%03d' % s] = g
+    return groups, {'mode': mode}
+
+
+@pytest.mark.parametrize('id_dtype,id_hi,per_halo', [
+    (np.int64, 2 ** 62, 3000),          # signed keys, large values
+    (np.int32, 2 ** 31 - 1, 500),
+    (np.uint32, 2 ** 32 - 1, 500),
+    (np.uint64, 2 ** 62, 500),          # values past 2^63 after the offset below
+    (np.int64, 100000, 20000),          # > OA_COLLATE_CHUNK records per halo: several rounds
+])
+def test_collate_random_vs_oracle(id_dtype, id_hi, per_halo):
+    rng = np.random.default_rng(per_halo + np.dtype(id_dtype).itemsize)
+    groups, attrs = _random_track_file(rng, 5, 4, per_halo, id_dtype, id_hi)
+    if id_dtype == np.uint64:
+        for g in groups.values():
+            g['pericenter_IDs'] = g['pericenter_IDs'] + np.uint64(2 ** 63)
+    for kw in ({}, {'angle_cut': 1.5, 'halo_ids': np.array([103, 101, 104])}):
+        want = PO.collate_apsides(groups, attrs, **kw)
+        fin = PO.save_final_apsis_counts(want, 'pericentric')
+        for g, v in fin.items():
+            want[g]['pericenter_counts_final'] = v
+        got = _collate(groups, attrs, kw, {})
+        assert sorted(got) == sorted(want)
+        for g in want:
+            for d in want[g]:
+                assert_same(got[g][d], want[g][d], '%s/%s' % (g, d))
+
+
+def test_retro_counts_missing_id_raises():
+    from orbitanalysis_amd.postprocessing import Apsides
+    rng = np.random.default_rng(3)
+    groups, attrs = _random_track_file(rng, 3, 3, 200, np.int64, 10 ** 6)
+    dst = _Mem()
+    ap = Apsides(_Mem(groups, attrs))
+    ap.collate_apsides(savefile=dst, verbose=False)
+    first = sorted(dst.groups)[0]
+    dst.groups[first]['particle_IDs'] = dst.groups[first]['particle_IDs'].copy()
+    dst.groups[first]['particle_IDs'][0] = -5
+    with pytest.raises(ValueError):
+        ap.save_final_apsis_counts(dst, verbose=False)
+
+
+@pytest.mark.parametrize('case', central_cases(), ids=lambda c: c[0])
+def test_central_ids_match_reference(case):
+    from orbitanalysis_amd.progenitors import get_central_particle_ids
+    name, snap, pos, n, want_ids, want_off = case
+    ids, off = get_central_particle_ids(snap, pos, n=n)
+    assert_same(ids, want_ids, name + '/ids')
+    assert_same(off, want_off, name + '/offsets')
+
+
+@pytest.mark.parametrize('n,sizes,dtype,box', [
+    (100, [20000, 9000, 50, 0, 8192], np.float32, 40.0),    # LDS cache and global-scratch blocks
+    (4096, [5000, 4096, 100], np.float64, None),
+    (1, [300, 1], np.float64, [10.0, 11.0, 12.0]),
+])
+def test_central_ids_random_vs_oracle(n, sizes, dtype, box):
+    from orbitanalysis_amd.progenitors import get_central_particle_ids
+    rng = np.random.default_rng(sum(sizes))
+    x = rng.uniform(0, 40, (sum(sizes), 3)).astype(dtype)
+    snap = {'ids': rng.permutation(10 ** 7)[:sum(sizes)].astype(np.int64), 'coordinates': x,
+            'region_offsets': np.cumsum([0] + sizes[:-1])}
+    if box is not None:
+        snap['box_size'] = box
+    pos = rng.uniform(0, 40, (len(sizes), 3)).astype(dtype)
+    want = PO.get_central_particle_ids(snap, pos, n=n)
+    got = get_central_particle_ids(snap, pos, n=n)
+    assert_same(got[0], want[0], 'ids')
+    assert_same(got[1], want[1], 'offsets')
+
+
+@pytest.mark.parametrize('case', mainprog_cases(), ids=lambda c: c[0])
+def test_main_progenitors_match_reference(case):
+    from orbitanalysis_amd.progenitors import find_main_progenitors
+    name, hp, ho, tp, to, want = case
+    got = find_main_progenitors(hp, ho, tp, to)
+    assert np.array_equal(np.array([int(v) for v in got]), want), name
+    assert all(v == -1 or isinstance(v, np.int64) for v in got)
+
+
+def test_main_progenitors_random_vs_oracle():
+    from orbitanalysis_amd.progenitors import find_main_progenitors
+    rng = np.random.default_rng(11)
+    sizes = rng.integers(0, 3000, 400)
+    hp = rng.choice(2 ** 50, int(sizes.sum()), replace=False).astype(np.int64)
+    ho = np.cumsum(np.concatenate([[0], sizes[:-1]]))
+    blocks = [rng.choice(hp, int(rng.integers(0, 300)), replace=False) for _ in range(500)]
+    blocks[7] = np.concatenate([blocks[7], blocks[3][:50]])            # duplicates
+    blocks.append(rng.choice(hp, 20000, replace=False))                   # one long block
+    to = np.cumsum([0] + [len(b) for b in blocks])[:-1]
+    tp = np.concatenate(blocks)
+    want = PO.find_main_progenitors(hp, ho, tp, to)
+    got = find_main_progenitors(hp, ho, tp, to)
+    assert [int(v) for v in got] == [int(v) for v in want]

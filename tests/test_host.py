@@ -14,7 +14,8 @@ from conftest import ROOT
 def test_library_exports_every_declared_symbol():
     from orbitanalysis_amd import _native as N
     lib = N.load()
-    hdr = open(os.path.join(ROOT, 'include', 'orbit_hip.h')).read()
+    hdr = ''.join(open(os.path.join(ROOT, 'include', h)).read()
+                  for h in ('orbit_hip.h', 'orbit_post.h'))
     declared = set(re.findall(r'\b(oa_[a-z_0-9]+)\s*\(', hdr))
     assert declared, 'no declarations parsed'
     raw = ctypes.CDLL(N.LIB_PATH)
@@ -26,6 +27,9 @@ def test_library_exports_every_declared_symbol():
     from orbitanalysis_amd import engine as E
     assert lib.oa_step_lds_bytes(E.DEFAULT_ENTRIES, E.DEFAULT_SLOTS) <= 160 * 1024
     assert lib.oa_build_info(0) % 64 == 0 and lib.oa_build_info(1) >= 1
+    post = open(os.path.join(ROOT, 'include', 'orbit_post.h')).read()
+    assert int(re.search(r'OA_COLLATE_CHUNK (\d+)', post).group(1)) == N.COLLATE_CHUNK
+    assert int(re.search(r'OA_CENTRAL_MAX_N (\d+)', post).group(1)) == N.CENTRAL_MAX_N
 
 
 def test_no_silent_cpu_fallback():
@@ -36,6 +40,34 @@ def test_no_silent_cpu_fallback():
     from orbitanalysis_amd.engine import OrbitEngine
     with pytest.raises(N.NativeUnavailable):
         OrbitEngine()
+
+
+def test_post_calls_reject_bad_args_without_device():
+    from orbitanalysis_amd import _native as N
+    lib = N.load()
+    a = N.CentralArgs()
+    a.n_halos, a.n, a.id_bytes = 1, N.CENTRAL_MAX_N + 1, 8
+    assert lib.oa_central_ids(a, None) == -1
+    assert b'OA_CENTRAL_MAX_N' in lib.oa_last_error()
+    m = N.MainProgArgs()
+    m.n_blocks, m.halo_kind, m.tracked_kind = 1, 1, 0
+    assert lib.oa_main_progenitors(m, None) == -1
+    assert lib.oa_retro_counts(None, 7, 5, None, None, 0, None, None, None, None, None, None) == -1
+    assert lib.oa_mainprog_workspace_bytes(10 ** 8, 10) >= 16 * 64 + 40   # tracked-side table only
+
+
+def test_box_plan_follows_numpy_promotion():
+    from orbitanalysis_amd.progenitors import _box_plan
+    f32, f64 = np.dtype(np.float32), np.dtype(np.float64)
+    # scalar box -> float64 array (utils.py:28-29): strong float64 comparisons
+    assert [p[0] for p in _box_plan(30.0, f32)] == [True] * 3
+    # list of Python floats: weak, compared and subtracted in the dx dtype
+    p = _box_plan([20.0, 25.1, 30.0], f32)
+    assert [q[0] for q in p] == [False] * 3
+    assert p[1][2] == float(np.float32(25.1 / 2))
+    # float32 array box: float32; 1-element float64 array: x only
+    assert [q[0] for q in _box_plan(np.array([10.0, 12.0, 14.0], np.float32), f32)] == [False] * 3
+    assert len(_box_plan(np.array([10.0]), f32)) == 1
 
 
 def test_null_args_rejected_without_device():
