@@ -40,7 +40,7 @@ extern "C" {
 /* Raw apsis records of one collated chunk per halo: at most this many per halo per
  * oa_collate_step call (the LDS sort capacity); the host splits larger slices into
  * rounds (postprocessing.py:123-128 appends are order-free under np.unique). */
-#define OA_COLLATE_CHUNK 8192
+#define OA_COLLATE_CHUNK 4096
 /* Largest n of get_central_particle_ids handled by oa_central_ids. */
 #define OA_CENTRAL_MAX_N 4096
 

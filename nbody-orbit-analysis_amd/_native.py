@@ -84,7 +84,7 @@ class MainProgArgs(ctypes.Structure):
 
 # include/orbit_post.h constants
 ID_KIND = {np.dtype('int64'): 0, np.dtype('uint64'): 1, np.dtype('int32'): 2, np.dtype('uint32'): 3}
-COLLATE_CHUNK = 8192
+COLLATE_CHUNK = 4096
 CENTRAL_MAX_N = 4096
 POST_MISSING, POST_SENTINEL, POST_OVERFLOW = 1, 2, 4
 

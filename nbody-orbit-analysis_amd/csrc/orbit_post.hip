@@ -8,19 +8,21 @@
 //   Apsides.save_final_apsis_counts postprocessing.py:215-236 -> k_retro_counts
 //   get_central_particle_ids       progenitors.py:38-56       -> k_central
 //   find_main_progenitors          progenitors.py:82-117      -> k_mp_insert,
-//                                  k_mp_lookup, k_mp_tally
+//                                  k_mp_probe, k_mp_lookup, k_mp_tally
 //
 // Design: no global sort anywhere.
 //  * collate keeps, per collated halo, the cumulative sorted-unique (ID, count) list
 //    the reference rebuilds with np.unique every snapshot; a snapshot's kept apsis IDs
 //    are sorted per halo in LDS (bitonic, <= OA_COLLATE_CHUNK keys), run-length
-//    encoded, located in the old list by binary search, and the merged list is
-//    written by one thread per element at its merge-path rank;
-//  * central IDs: per region block, an MSB-first 8-bit radix select of the n-th
-//    smallest radius (radius keys cached in LDS for blocks <= 8192) and an LDS
-//    bitonic sort of the <= n survivors by (radius, position);
-//  * main progenitors: open-addressing tables in HBM for halo members and for the
-//    first occurrence of every tracked ID, then a per-block LDS tally.
+//    encoded and located in the halo's old list (LDS-cached up to 12288 keys) by
+//    binary search; a second per-halo pass writes every element at its merge rank;
+//  * central IDs: per region block, an MSB-first radix select of the n-th smallest
+//    radius (common high bits skipped, early exit when a bin is taken whole; keys
+//    cached in LDS for blocks <= 12288) and an LDS bitonic sort of the <= n
+//    survivors by (radius, position);
+//  * main progenitors: an open-addressing table over the tracked IDs (first
+//    occurrence) behind an L2-resident bit filter; the halo members are streamed past
+//    it once, then a per-block LDS tally.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -48,7 +50,8 @@ int check_launch(const char *what) {
 
 constexpr uint64_t SIGN = 0x8000000000000000ull;
 constexpr int CH = OA_COLLATE_CHUNK;
-constexpr int KC = 8192;                 // k_central: radius keys cached in LDS
+constexpr int KC = 12288;                // k_central: radius keys cached in LDS
+constexpr int OC = 12288;                // k_collate_new: old keys cached in LDS
 constexpr int SC = OA_CENTRAL_MAX_N;     // k_central: survivors sorted in LDS
 
 // value of element i as 64-bit two's complement (signed kinds sign-extend)
@@ -143,6 +146,7 @@ __device__ void bitonic_pairs(uint64_t *s, uint32_t *x, int P) {
 __global__ __launch_bounds__(1024) void k_collate_new(const oa_collate_args a) {
     __shared__ uint64_t sk[CH];
     __shared__ int hp[CH + 1];
+    __shared__ uint64_t ok[OC];          // the halo's old keys, when they fit
     __shared__ int wsum[17];
     __shared__ int s_m;
     const int j = blockIdx.x;
@@ -157,6 +161,8 @@ __global__ __launch_bounds__(1024) void k_collate_new(const oa_collate_args a) {
     const int64_t ob = a.old_off[j], on = a.old_off[j + 1] - ob;
     if (threadIdx.x == 0) s_m = 0;
     __syncthreads();
+    if (on <= OC)
+        for (int i = threadIdx.x; i < on; i += 1024) ok[i] = a.old_keys[ob + i];
     for (int i = threadIdx.x; i < nraw; i += 1024) {
         if (a.keep_lut[a.angles[s0 + i]]) {
             const int p = atomicAdd(&s_m, 1);
@@ -196,12 +202,20 @@ __global__ __launch_bounds__(1024) void k_collate_new(const oa_collate_args a) {
             key = sk[hp[qq]];
             c = hp[qq + 1] - hp[qq];
             int64_t L = 0, R = on;
-            while (L < R) {
-                const int64_t mid = (L + R) >> 1;
-                if (a.old_keys[ob + mid] < key) L = mid + 1; else R = mid;
+            if (on <= OC) {
+                while (L < R) {
+                    const int64_t mid = (L + R) >> 1;
+                    if (ok[mid] < key) L = mid + 1; else R = mid;
+                }
+                f = (L < on && ok[L] == key) ? 1 : 0;
+            } else {
+                while (L < R) {
+                    const int64_t mid = (L + R) >> 1;
+                    if (a.old_keys[ob + mid] < key) L = mid + 1; else R = mid;
+                }
+                f = (L < on && a.old_keys[ob + L] == key) ? 1 : 0;
             }
             lb = L;
-            f = (L < on && a.old_keys[ob + L] == key) ? 1 : 0;
         }
         int tf;
         const int ex = block_scan<1024, int>(f, wsum, tf);
@@ -232,41 +246,39 @@ __global__ __launch_bounds__(1024) void k_collate_offsets(const oa_collate_args 
     if (threadIdx.x == 0) a.new_off[a.n_halos] = carry;
 }
 
-// one thread per old element (rank i + #new keys below it not already present) and per
-// new unique key absent from the old list (rank lb + #such new keys before it)
+// one work-group per halo: the halo's new unique keys and their "already present"
+// prefix in LDS; every old element goes to rank i + #new keys below it not already
+// present (adding the new count on a match), every new key absent from the old list to
+// rank lb + #such new keys before it
 __global__ __launch_bounds__(256) void k_collate_merge(const oa_collate_args a) {
-    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (t < a.n_old) {
-        const int j = seg_of(a.old_off, a.n_halos, t);
-        const int64_t i = t - a.old_off[j];
-        const uint64_t key = a.old_keys[t];
-        const int u = a.w_ulen[j];
-        const int64_t base = a.new_base[j];
+    __shared__ uint64_t nk[CH];
+    __shared__ int nfp[CH + 1];
+    const int j = blockIdx.x;
+    const int u = a.w_ulen[j];
+    const int64_t base = a.new_base[j];
+    const int64_t ob = a.old_off[j], on = a.old_off[j + 1] - ob;
+    const int64_t no = a.new_off[j];
+    for (int q = threadIdx.x; q < u; q += 256) { nk[q] = a.w_keys[base + q]; nfp[q] = a.w_fp[base + q]; }
+    if (threadIdx.x == 0) nfp[u] = a.w_found[j];
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < on; i += 256) {
+        const uint64_t key = a.old_keys[ob + i];
         int L = 0, R = u;
         while (L < R) {
             const int mid = (L + R) >> 1;
-            if (a.w_keys[base + mid] < key) L = mid + 1; else R = mid;
+            if (nk[mid] < key) L = mid + 1; else R = mid;
         }
-        const bool eq = L < u && a.w_keys[base + L] == key;
-        const int fl = L < u ? a.w_fp[base + L] : a.w_found[j];
-        const int64_t pos = a.new_off[j] + i + L - fl;
+        const bool eq = L < u && nk[L] == key;
+        const int64_t pos = no + i + L - nfp[L];
         a.new_keys[pos] = key;
-        a.new_cnt[pos] = a.old_cnt[t] + (eq ? a.w_cnt[base + L] : 0);
-        return;
+        a.new_cnt[pos] = a.old_cnt[ob + i] + (eq ? a.w_cnt[base + L] : 0);
     }
-    const int64_t e = t - a.n_old;
-    if (e >= a.n_new_cap) return;
-    const int j = seg_of(a.new_base, a.n_halos, e);
-    const int64_t base = a.new_base[j];
-    const int q = (int)(e - base);
-    const int u = a.w_ulen[j];
-    if (q >= u) return;
-    const int fp = a.w_fp[base + q];
-    const int fn = q + 1 < u ? a.w_fp[base + q + 1] : a.w_found[j];
-    if (fn != fp) return;                       // already in the old list: counted above
-    const int64_t pos = a.new_off[j] + a.w_lb[base + q] + (q - fp);
-    a.new_keys[pos] = a.w_keys[base + q];
-    a.new_cnt[pos] = a.w_cnt[base + q];
+    for (int q = threadIdx.x; q < u; q += 256) {
+        if (nfp[q + 1] != nfp[q]) continue;               // already in the old list
+        const int64_t pos = no + a.w_lb[base + q] + (q - nfp[q]);
+        a.new_keys[pos] = nk[q];
+        a.new_cnt[pos] = a.w_cnt[base + q];
+    }
 }
 
 __global__ __launch_bounds__(256) void k_keys_to_ids(const uint64_t *keys, int64_t n, int key_signed,
@@ -462,20 +474,31 @@ __global__ __launch_bounds__(1024) void k_central(const oa_central_args a) {
 constexpr uint64_t EMPTY = SIGN;          // INT64_MIN marks a free slot (rejected as an ID)
 struct MpSlot { uint64_t key; uint32_t first; uint32_t hpos; };
 
-__global__ __launch_bounds__(256) void k_mp_fill(MpSlot *tab, uint64_t cap, uint32_t *neg1) {
+__global__ __launch_bounds__(256) void k_mp_fill(MpSlot *tab, uint64_t cap, uint32_t *neg1,
+                                                 uint32_t *filt, uint64_t fwords) {
     const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i < cap) { tab[i].key = EMPTY; tab[i].first = 0xFFFFFFFFu; tab[i].hpos = 0xFFFFFFFFu; }
+    if (i < fwords) filt[i] = 0u;
     if (i == 0) *neg1 = 0xFFFFFFFFu;
+}
+// one bit per tracked ID (high hash bits), L2-resident: most halo members are not
+// tracked and skip the table probe
+__device__ __forceinline__ uint32_t filt_bit(uint64_t h, uint64_t fbits) {
+    return (uint32_t)((h >> 32) & (fbits - 1));
 }
 
 // tracked value -> smallest index holding it (np.unique(return_index=True), :82)
 __global__ __launch_bounds__(256) void k_mp_insert(const void *src, int kind, int64_t n,
-                                                   MpSlot *tab, uint64_t cap, int32_t *status) {
+                                                   MpSlot *tab, uint64_t cap, int32_t *status,
+                                                   uint32_t *filt, uint64_t fbits) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t v = load_val(src, i, kind);
     if (v == EMPTY) { atomicOr(status, (int32_t)OA_POST_SENTINEL); return; }
-    uint64_t s = mix64(v) & (cap - 1);
+    const uint64_t h = mix64(v);
+    const uint32_t b = filt_bit(h, fbits);
+    atomicOr(&filt[b >> 5], 1u << (b & 31));
+    uint64_t s = h & (cap - 1);
     for (uint64_t t = 0; t < cap; ++t) {
         uint64_t cur = tab[s].key;
         if (cur == EMPTY)
@@ -501,11 +524,14 @@ __device__ __forceinline__ int64_t mp_find(const MpSlot *tab, uint64_t cap, uint
 // in1d(tracked, halo_pids) / myin1d(halo_pids, ...) join, :95-99); the position of a
 // member equal to -1 is kept apart for the de-duplicated tracked entries (:83)
 __global__ __launch_bounds__(256) void k_mp_probe(const void *hp, int kind, int64_t n,
-                                                  MpSlot *tab, uint64_t cap, uint32_t *neg1) {
+                                                  MpSlot *tab, uint64_t cap, uint32_t *neg1,
+                                                  const uint32_t *filt, uint64_t fbits) {
     const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (p >= n) return;
     const uint64_t v = load_val(hp, p, kind);
     if (v == ~0ull) atomicMin(neg1, (uint32_t)p);
+    const uint32_t b = filt_bit(mix64(v), fbits);
+    if (!((filt[b >> 5] >> (b & 31)) & 1u)) return;
     const int64_t s = mp_find(tab, cap, v);
     if (s >= 0) atomicMin(&tab[s].hpos, (uint32_t)p);
 }
@@ -568,6 +594,11 @@ uint64_t pow2_at_least(uint64_t v, uint64_t lo) {
     while (c < v) c <<= 1;
     return c;
 }
+// filter: >= 16 bits per tracked ID (~6 % false positives), 4 KiB .. 4 MiB
+uint64_t mp_filter_bits(uint64_t n_tracked) {
+    uint64_t b = pow2_at_least(16 * n_tracked, 1ull << 15);
+    return b > (1ull << 25) ? (1ull << 25) : b;
+}
 
 }  // namespace
 
@@ -599,9 +630,8 @@ int oa_collate_step(const oa_collate_args *args, void *stream) {
     if (int rc = check_launch("k_collate_new")) return rc;
     hipLaunchKernelGGL(k_collate_offsets, dim3(1), dim3(1024), 0, st, a);
     if (int rc = check_launch("k_collate_offsets")) return rc;
-    const int64_t n = a.n_old + a.n_new_cap;
-    if (n > 0) {
-        hipLaunchKernelGGL(k_collate_merge, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
+    if (a.n_old + a.n_new_cap > 0) {
+        hipLaunchKernelGGL(k_collate_merge, dim3(a.n_halos), dim3(256), 0, st, a);
         if (int rc = check_launch("k_collate_merge")) return rc;
     }
     return OA_OK;
@@ -656,8 +686,9 @@ int oa_central_ids(const oa_central_args *args, void *stream) {
 
 int64_t oa_mainprog_workspace_bytes(int64_t n_halo_pids, int64_t n_tracked) {
     (void)n_halo_pids;                     // the halo members are streamed, not tabled
-    const uint64_t ct = pow2_at_least(2 * (uint64_t)(n_tracked > 0 ? n_tracked : 1), 64);
-    return (int64_t)(ct * sizeof(MpSlot) + 4 * (uint64_t)(n_tracked > 0 ? n_tracked : 1) + 64);
+    const uint64_t nt = (uint64_t)(n_tracked > 0 ? n_tracked : 1);
+    const uint64_t ct = pow2_at_least(2 * nt, 64);
+    return (int64_t)(ct * sizeof(MpSlot) + 64 + 4 * nt + 4 + mp_filter_bits(nt) / 8);
 }
 
 int oa_main_progenitors(const oa_mainprog_args *args, void *stream) {
@@ -677,18 +708,24 @@ int oa_main_progenitors(const oa_mainprog_args *args, void *stream) {
         return fail(OA_E_ARG, "oa_main_progenitors: workspace must be 16-byte aligned");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const uint64_t ct = pow2_at_least(2 * (uint64_t)(a.n_tracked > 0 ? a.n_tracked : 1), 64);
+    const uint64_t nt = (uint64_t)(a.n_tracked > 0 ? a.n_tracked : 1);
+    const uint64_t fbits = mp_filter_bits(nt), fwords = fbits / 32;
     MpSlot *tab = reinterpret_cast<MpSlot *>(a.tab_keys);
     uint32_t *neg1 = reinterpret_cast<uint32_t *>(tab + ct);
     int32_t *hn = reinterpret_cast<int32_t *>(neg1 + 16);
-    hipLaunchKernelGGL(k_mp_fill, dim3((unsigned)((ct + 255) / 256)), dim3(256), 0, st, tab, ct, neg1);
+    uint32_t *filt = reinterpret_cast<uint32_t *>(hn + nt + 1);
+    const uint64_t nfill = ct > fwords ? ct : fwords;
+    hipLaunchKernelGGL(k_mp_fill, dim3((unsigned)((nfill + 255) / 256)), dim3(256), 0, st, tab, ct,
+                       neg1, filt, fwords);
     if (int rc = check_launch("k_mp_fill")) return rc;
     if (a.n_tracked > 0) {
         hipLaunchKernelGGL(k_mp_insert, dim3((unsigned)((a.n_tracked + 255) / 256)), dim3(256), 0,
-                           st, a.tracked, a.tracked_kind, a.n_tracked, tab, ct, a.status);
+                           st, a.tracked, a.tracked_kind, a.n_tracked, tab, ct, a.status, filt, fbits);
         if (int rc = check_launch("k_mp_insert")) return rc;
         if (a.n_halo_pids > 0) {
             hipLaunchKernelGGL(k_mp_probe, dim3((unsigned)((a.n_halo_pids + 255) / 256)), dim3(256),
-                               0, st, a.halo_pids, a.halo_kind, a.n_halo_pids, tab, ct, neg1);
+                               0, st, a.halo_pids, a.halo_kind, a.n_halo_pids, tab, ct, neg1, filt,
+                               fbits);
             if (int rc = check_launch("k_mp_probe")) return rc;
         }
         hipLaunchKernelGGL(k_mp_lookup, dim3((unsigned)((a.n_tracked + 255) / 256)), dim3(256), 0,
