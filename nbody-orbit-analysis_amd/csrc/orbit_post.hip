@@ -322,11 +322,11 @@ __global__ __launch_bounds__(256) void k_retro_counts(const void *ids, int kind,
 // recenter_coordinates (utils.py:24-33) per dim in its comparison dtype, then
 // region_coords (float64, progenitors.py:41) and sqrt(einsum) with the host's f64 tree
 template <typename TX, typename TD>
-__device__ __forceinline__ uint64_t radius_key(const TX *x, int64_t p, const double *c,
+__device__ __forceinline__ uint64_t radius_key(const TX (&x)[3], const double *c,
                                                const oa_central_args &a) {
     TD d[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) d[k] = (TD)x[3 * p + k] - (TD)c[k];
+    for (int k = 0; k < 3; ++k) d[k] = (TD)x[k] - (TD)c[k];
     for (int k = 0; k < a.n_box_dims; ++k) {
         if (a.wrap_f64[k]) {
             double v = (double)d[k];
@@ -366,11 +366,27 @@ __global__ __launch_bounds__(1024) void k_central(const oa_central_args a) {
     if (threadIdx.x == 0) { s_min = ~0ull; s_max = 0; s_cnt = 0; s_done = 0; }
     __syncthreads();
     uint64_t lmin = ~0ull, lmax = 0;
-    for (int i = threadIdx.x; i < m; i += 1024) {
-        const uint64_t key = radius_key<TX, TD>(x, off + i, c, a);
-        lmin = key < lmin ? key : lmin;
-        lmax = key > lmax ? key : lmax;
-        if (cached) kc[i] = key; else a.scratch[off + i] = key;
+    // four particles per thread per trip: their coordinate loads are all in flight
+    // before the first radius is computed
+    constexpr int RU = 4;
+    for (int i0 = threadIdx.x; i0 < m; i0 += 1024 * RU) {
+        TX xs[RU][3];
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            const int i = i0 + u * 1024;
+            const int64_t p = off + (i < m ? i : 0);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) xs[u][d] = x[3 * p + d];
+        }
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            const int i = i0 + u * 1024;
+            if (i >= m) break;
+            const uint64_t key = radius_key<TX, TD>(xs[u], c, a);
+            lmin = key < lmin ? key : lmin;
+            lmax = key > lmax ? key : lmax;
+            if (cached) kc[i] = key; else a.scratch[off + i] = key;
+        }
     }
     if (threadIdx.x < m) { atomicMin(&s_min, lmin); atomicMax(&s_max, lmax); }
     __syncthreads();
@@ -399,15 +415,31 @@ __global__ __launch_bounds__(1024) void k_central(const oa_central_args a) {
                     atomicAdd(&hist[(key >> s) & ((1u << w) - 1u)], 1);
             }
             __syncthreads();
-            if (threadIdx.x == 0) {
-                int acc = 0, d = 0;
-                for (; d < (1 << w) - 1; ++d) {
-                    if (acc + hist[d] >= need) break;
-                    acc += hist[d];
+            if (threadIdx.x < 64) {
+                // wave 0 finds the bin holding the need-th key: 4 bins per lane, a wave
+                // prefix sum, the first lane whose running count reaches `need`
+                const int l = threadIdx.x;
+                const int h0 = hist[4 * l], h1 = hist[4 * l + 1], h2 = hist[4 * l + 2],
+                          h3 = hist[4 * l + 3];
+                const int sum = h0 + h1 + h2 + h3;
+                int incl = sum;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int y = __shfl_up(incl, o);
+                    if (l >= o) incl += y;
                 }
-                s_prefix = prefix | ((uint64_t)d << s);
-                s_need = need - acc;
-                s_done = hist[d] == need - acc;             // the whole bin is selected
+                const uint64_t hitm = __ballot(incl >= need);
+                if (l == __ffsll((unsigned long long)hitm) - 1) {
+                    int acc = incl - sum, q = 0;
+                    const int hs[4] = {h0, h1, h2, h3};
+                    for (; q < 3; ++q) {
+                        if (acc + hs[q] >= need) break;
+                        acc += hs[q];
+                    }
+                    s_prefix = prefix | ((uint64_t)(4 * l + q) << s);
+                    s_need = need - acc;
+                    s_done = hs[q] == need - acc;          // the whole bin is selected
+                }
             }
             __syncthreads();
             prefix = s_prefix;
