@@ -75,6 +75,12 @@ namespace {
 #ifndef OA_ABL_SLOTW
 #define OA_ABL_SLOTW 0
 #endif
+#ifndef OA_NTST
+#define OA_NTST 1           // phase-3 state words and apsis records stored non-temporal
+#endif
+#ifndef OA_TOUCH
+#define OA_TOUCH 0          // re-touch the item's r̂ lines (L2 LRU refresh) before phase 2
+#endif
 #ifndef OA_ABL_GATHER
 #define OA_ABL_GATHER 0
 #endif
@@ -869,6 +875,14 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         if (tid == 0) a.item_count[blockIdx.x] = 0;
         return;
     }
+    uint32_t touch = 0;
+    if (OA_TOUCH) {
+        // one dword per 128-B line of the r̂ block written in phase 1: the lines become
+        // most-recently-used in L2 while the walks run, so phase 2's gathers hit
+        const uint32_t nb = n_span * SD;
+        for (uint32_t o = (uint32_t)tid * 128u; o < nb; o += WG * 128u)
+            touch ^= bld<uint32_t, 0>(r_rh, o);
+    }
     if (!OA_IMMEDIATE_WALK) {
         __syncthreads();
         const uint32_t np = min(H.npend, pend_cap);
@@ -1011,8 +1025,13 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                 const int64_t sb = it.scratch_off + r0;
                 if (flag[u] && !OA_ABL_EMIT) {
                     const uint32_t q = (uint32_t)__popcll(m & lanemask_lt);
-                    scr_ids[sb + q] = S.pid[u];
-                    a.scratch_ang[sb + q] = a16[u];
+                    if (OA_NTST) {
+                        __builtin_nontemporal_store(S.pid[u], &scr_ids[sb + q]);
+                        __builtin_nontemporal_store(a16[u], &a.scratch_ang[sb + q]);
+                    } else {
+                        scr_ids[sb + q] = S.pid[u];
+                        a.scratch_ang[sb + q] = a16[u];
+                    }
                 }
                 if (lane == 0) {
                     a.seg_count[sb >> 6] = (uint8_t)c;
@@ -1050,6 +1069,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         stage(SC, LB, SA, LA, SB);
     }
     WSTAMP(1);
+    if (OA_TOUCH) asm volatile("" :: "v"(touch));
     if (lane == 0) atomicAdd(&H.chunk_total, running);
     STAMP(4);
     __syncthreads();
@@ -1084,7 +1104,12 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             if (!H.has_prev[k]) continue;
             const uint32_t e = H.lstart[k + 1];
             for (uint32_t li = H.lstart[k] + tid; li < e; li += WG)
-                if (!OA_ABL_PHASE3) a.meta_out[base + li] = pm[li];
+                if (!OA_ABL_PHASE3) {
+                    // not re-read by this launch: a streaming store leaves the L2 to
+                    // the r̂ lines phase 2 gathers
+                    if (OA_NTST) __builtin_nontemporal_store(pm[li], &a.meta_out[base + li]);
+                    else a.meta_out[base + li] = pm[li];
+                }
         }
     }
     if (tid < nh) {
