@@ -17,13 +17,14 @@ r̂ in the coordinate dtype, no Hubble term, v_r in promote(velocity, coordinate
 track_orbits_onthefly.py:71-120).  The per-halo entered / departed lists are
 compacted and sorted on the device from the kernel's match flags.
 """
+import os
 import time
 
 import numpy as np
 import torch
 
 from . import _native as N
-from .engine import OrbitEngine, SnapshotState, Workspace, to_device, F64
+from .engine import OrbitEngine, SnapshotState, Workspace, to_device, F64, np_dtype
 
 _TORCH = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64}
 
@@ -104,17 +105,28 @@ class OnTheFly:
         a.vr_f64 = int(np.result_type(plan.vel, coord) == F64)
         return pr
 
-    def run(self, snaps, slices, centres):
-        """snaps / slices / centres: [current, previous].  Returns host outputs."""
+    def run(self, snaps, slices, centres, carried=None):
+        """snaps / slices / centres: [current, previous].  Returns host outputs.
+
+        ``carried``: the (state, bulk velocities) a previous call left for its current
+        snapshot (``self.carry``), when that snapshot is this call's previous one with
+        the same regions; its frame is then not recomputed (``snaps[1]`` unused)."""
         eng = self.eng
         cur, prv = snaps
-        if np.dtype(cur['coordinates'].dtype) != np.dtype(prv['coordinates'].dtype):
-            raise NotImplementedError('coordinate dtype differs between the two snapshots')
-        # previous snapshot: frame only
-        pp = self._prepare(prv, slices[1], centres[1], False)
-        eng.launch(pp, None)
-        prev = SnapshotState(ids=pp.snap['ids'], rhat=pp.rhat, meta=pp.meta, starts=pp.starts,
-                             counts=pp.counts, exists=np.arange(len(slices[1])), plan=pp.plan)
+        if carried is None:
+            if np_dtype(cur['coordinates']) != np_dtype(prv['coordinates']):
+                raise NotImplementedError('coordinate dtype differs between the two snapshots')
+            # previous snapshot: frame only
+            pp = self._prepare(prv, slices[1], centres[1], False)
+            eng.launch(pp, None)
+            prev = SnapshotState(ids=pp.snap['ids'], rhat=pp.rhat, meta=pp.meta,
+                                 starts=pp.starts, counts=pp.counts,
+                                 exists=np.arange(len(slices[1])), plan=pp.plan)
+            bulk_p = None
+        else:
+            prev, bulk_p = carried
+            if np_dtype(cur['coordinates']) != np.dtype(prev.plan.coord):
+                raise NotImplementedError('coordinate dtype differs between the two snapshots')
         n_prev = prev.ids.numel()
         entries = None
         for _ in range(8):
@@ -138,29 +150,36 @@ class OnTheFly:
         else:
             raise RuntimeError('LDS hash tables kept overflowing (adversarial IDs?)')
         nh = len(slices[0])
-        ids_dtype = np.dtype(cur['ids'].dtype)
+        ids_dtype = np_dtype(cur['ids'])
         unsigned = ids_dtype.kind == 'u'
         # apsis records per halo, previous-block order (:154-166)
         offsets, apsis_ids, _ = eng.fetch(res, ids_dtype)
-        # angle changes of every matched particle, previous-block order (:173-174)
+        # angle changes of every matched particle, previous-block order (:173-174):
+        # N values, brought back through pinned memory
         mp = matched_prev[:n_prev].bool()
-        angles = angle_out[:n_prev][mp].cpu().numpy()
+        sel = angle_out[:n_prev][mp]
+        angles_h = torch.empty(sel.shape, dtype=sel.dtype, pin_memory=True)
+        angles_h.copy_(sel)
+        angles = angles_h.numpy()
         p_has = pc.halos.cpu().numpy().view(N.HALO_DTYPE)['prev_cnt'] > 0
+
+        def halo_of(pos, starts):
+            # block of each selected position (blocks tile [0, n) in halo order)
+            st = torch.from_numpy(np.asarray(starts, dtype=np.int64)).to(eng.device)
+            return torch.searchsorted(st, pos, right=True) - 1
         # departed: previous particles without a match, sorted per halo (:145)
-        pcnt = torch.from_numpy(prev.counts).to(eng.device)
-        ph = torch.repeat_interleave(torch.arange(nh, device=eng.device), pcnt)
         dsel = torch.nonzero(~mp).squeeze(1)
         d_ids = prev.ids[dsel]
-        departed, d_off = _grouped(d_ids, ph[dsel], _sort_key(d_ids, unsigned), nh)
+        departed, d_off = _grouped(d_ids, halo_of(dsel, prev.starts), _sort_key(d_ids, unsigned),
+                                   nh)
         # entered: current particles without a match, sorted per halo (:168); all of
         # a halo's particles, in loader order, when its progenitor block is empty (:178)
-        ccnt = torch.from_numpy(pc.counts).to(eng.device)
-        ch = torch.repeat_interleave(torch.arange(nh, device=eng.device), ccnt)
         esel = torch.nonzero(matched_cur[:pc.n] == 0).squeeze(1)
         e_ids = pc.snap['ids'][esel]
-        sorted_h = torch.from_numpy(p_has).to(eng.device)[ch[esel]]
+        eh = halo_of(esel, pc.starts)
+        sorted_h = torch.from_numpy(p_has).to(eng.device)[eh]
         key = torch.where(sorted_h, _sort_key(e_ids, unsigned), esel.to(torch.int64))
-        entered, e_off = _grouped(e_ids, ch[esel], key, nh)
+        entered, e_off = _grouped(e_ids, eh, key, nh)
         # concatenation dtype of the reference's per-halo lists (:183, :203): an empty
         # halo contributes np.array([], dtype=ids.dtype)
         parts = [np.zeros(0, np.dtype(pc.plan.coord))] * int(p_has.sum()) + \
@@ -171,12 +190,39 @@ class OnTheFly:
             return t.cpu().numpy().view(ids_dtype) if t.numel() else np.zeros(0, ids_dtype)
 
         bulk_c = pc.halos.cpu().numpy().view(N.HALO_DTYPE)['bulk'].astype(pc.plan.bulk)
-        bulk_p = pp.halos.cpu().numpy().view(N.HALO_DTYPE)['bulk'].astype(pp.plan.bulk)
+        if bulk_p is None:
+            bulk_p = pp.halos.cpu().numpy().view(N.HALO_DTYPE)['bulk'].astype(pp.plan.bulk)
+        # this snapshot's frame state (r̂ in the coordinate dtype, sign bits) is exactly
+        # what the next call needs for its previous snapshot
+        self.carry = (SnapshotState(ids=pc.snap['ids'], rhat=pc.rhat, meta=pc.meta,
+                                    starts=pc.starts, counts=pc.counts, exists=np.arange(nh),
+                                    plan=pc.plan), bulk_c)
         return {'apsis_offsets': offsets, 'apsis_ids': apsis_ids,
-                'angles': angles.astype(adt),
+                'angles': angles.astype(adt, copy=False),
                 'entered_offsets': e_off, 'entered_ids': host_ids(entered),
                 'departed_offsets': d_off, 'departed_ids': host_ids(departed),
                 'bulk_velocities': [bulk_c, bulk_p]}
+
+
+# Frame state of the last call's current snapshot, keyed by the loader callable
+# (SURVEY §8(f) f1): a stream of calls s, s+1, ... whose progenitor row and regions at
+# s-1 equal the previous call's current ones loads and frames each snapshot once
+# instead of twice.  ORBIT_OTF_CARRY=0 disables it; clear_carry() drops it.
+_CARRY = {}
+
+
+def _carry_enabled():
+    return os.environ.get('ORBIT_OTF_CARRY', '1') != '0'
+
+
+def _same(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return a.dtype == b.dtype and a.shape == b.shape and np.array_equal(a, b, equal_nan=True)
+
+
+def clear_carry():
+    """Release the device state kept between on-the-fly calls."""
+    _CARRY.clear()
 
 
 def track_orbits(snapshot_number, progenitor_links, regions, load_snapshot_data,
@@ -190,25 +236,50 @@ def track_orbits(snapshot_number, progenitor_links, regions, load_snapshot_data,
     progenitor_links = np.asarray(progenitor_links)
     snaps, slices, positions, radii = [], [], [], []
     box_size = None
+    key = load_snapshot_data              # bound methods compare by (instance, function)
+    try:
+        entry = _CARRY.get(key) if _carry_enabled() else None
+    except TypeError:                     # an unhashable callable: no carry
+        key, entry = None, None
+    carried = None
     for s, halo_ids_ in zip([snapshot_number, snapshot_number - 1], progenitor_links):
         halo_exists = np.argwhere(halo_ids_ != -1).flatten()
         halo_ids = halo_ids_[halo_exists]
         region_pos, region_rad = regions(s, halo_ids)
         positions.append(repack(region_pos, len(halo_ids_), halo_exists))
         radii.append(repack(region_rad, len(halo_ids_), halo_exists))
+        if s == snapshot_number - 1 and entry is not None and entry['s'] == s and \
+                np.array_equal(entry['row'], halo_ids_) and \
+                _same(entry['pos'], region_pos) and _same(entry['rad'], region_rad):
+            # the previous call's current snapshot, same regions: its device frame state
+            # is reused and the snapshot is not loaded again
+            snaps.append(None)
+            slices.append(entry['slices'])
+            box_size = entry['box_size']
+            carried = entry['carry']
+            continue
         snapshot = load_snapshot_data(s, region_pos, region_rad)
         snaps.append(snapshot)
         offsets = list(snapshot['region_offsets']) + [len(snapshot['ids'])]
         sl = np.array(list(zip(offsets[:-1], offsets[1:])))
         slices.append(repack(sl, len(halo_ids_), halo_exists))
         box_size = snapshot['box_size'] if 'box_size' in snapshot else None
+        if s == snapshot_number:
+            cur_meta = dict(s=s, row=halo_ids_.copy(), pos=np.array(region_pos, copy=True),
+                            rad=np.array(region_rad, copy=True), slices=slices[-1],
+                            box_size=box_size)
     if verbose:
         print('Identifying {}ers...'.format(mode[:8]))
         t0 = time.time()
     otf = OnTheFly(engine, mode)
     if otf.mode != mode:
         raise ValueError('engine mode %r != mode %r' % (otf.mode, mode))
-    out = otf.run(snaps, slices, positions)
+    if key is not None:
+        _CARRY.pop(key, None)             # a failing call leaves nothing stale behind
+    out = otf.run(snaps, slices, positions, carried=carried)
+    if key is not None and _carry_enabled():
+        _CARRY.clear()                    # one carried snapshot at a time (device memory)
+        _CARRY[key] = dict(cur_meta, carry=otf.carry)
     if verbose:
         print('Identified {}ers in {} s\n'.format(mode[:8], time.time() - t0))
     tag = mode[:8] + 'er'

@@ -271,3 +271,40 @@ def test_module_functions_match_reference_golden():
             a, aa = calc_angles(len(ins['ids']), ins['angles_prev'], dref)
             assert np.array_equal(a, fix[key + '/angles'], equal_nan=True), key
             assert np.array_equal(aa, fix[key + '/apsis_angles'], equal_nan=True), key
+
+
+def test_onthefly_stream_carry_matches_fresh_calls(monkeypatch):
+    """A stream of on-the-fly calls s = 2, 3, 4 with chained progenitor links reuses the
+    previous call's device frame state (the snapshot s-1 is neither loaded nor framed
+    again) and writes exactly the files of independent calls."""
+    from orbitanalysis_amd import track_orbits_onthefly as T
+    from orbitanalysis_amd.synthetic import PlummerSnapshots
+    from orbitanalysis_amd.savefile import MemorySavefile
+    u = PlummerSnapshots(n_halos=3, n_per_halo=[900, 700, 500], n_snapshots=5, seed=41, dt=0.5,
+                         box_size=40.0, region_returns=2)
+    links = np.array([[0, 1, 2], [0, 1, 2]])
+    loads = []
+
+    class Loader:
+        def __call__(self, s, pos, rad):
+            loads.append(s)
+            return u.load_snapshot_data(s, pos, rad)
+    results = {}
+    for carry in ('1', '0'):
+        monkeypatch.setenv('ORBIT_OTF_CARRY', carry)
+        T.clear_carry()
+        loads.clear()
+        out = MemorySavefile()
+        load = Loader()
+        for s in (2, 3, 4):
+            for mode in ('pericentric',):
+                T.track_orbits(s, links, u.regions, load, out, mode=mode, verbose=False)
+        results[carry] = (out.files, list(loads))
+    T.clear_carry()
+    assert results['1'][1] == [2, 1, 3, 4], results['1'][1]          # s-1 loaded once
+    assert results['0'][1] == [2, 1, 3, 2, 4, 3]
+    for s in (2, 3, 4):
+        a, b = results['1'][0][s][0], results['0'][0][s][0]
+        assert sorted(a) == sorted(b)
+        for k in a:
+            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=True), (s, k)

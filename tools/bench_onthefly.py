@@ -1,0 +1,195 @@
+"""BASELINE.json configs[4] on one GPU: the track_orbits_onthefly stream with
+double-buffered H2D.
+
+Config 5 is 1e9 particles over 8 GPUs and 200 snapshots; one GPU's share is 1.25e8
+particles per snapshot (float32, int64 IDs, periodic box).  Snapshots sit in pinned
+host memory, as a loader that fills pinned buffers would leave them.  Each step
+compares snapshot k with k-1:
+
+  * a copy stream runs the H2D of snapshot k+1 (ids, coordinates, velocities:
+    32 B/particle) into one of three device slots (k-1's IDs stay alive as the
+    previous state);
+  * the compute stream waits for snapshot k's copy, then runs the on-the-fly compare
+    (`OnTheFly.run` with the carried frame state of k-1: one frame per snapshot) and
+    brings every output to the host (apsis CSR, angle changes, entered/departed CSR).
+
+value = particles of the timed steps / wall time (PCIe-inclusive, end to end).
+Also reported: compute-only ms per step (HIP events), the H2D rate alone, and the
+CPU oracle (the reference's per-call algorithm: both frames + compare) on a bounded
+sample of halos with its apsis IDs checked against the GPU's.
+
+  python tools/bench_onthefly.py [--particles 1.25e8] [--steps 6]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PCIE_PEAK = 64.0        # GB/s per direction, PCIe 5.0 x16 (spec)
+
+
+def log(*a):
+    print('[bench_onthefly]', *a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--particles', type=float, default=1.25e8)
+    ap.add_argument('--per-halo', type=int, default=10000)
+    ap.add_argument('--steps', type=int, default=6)
+    ap.add_argument('--snapshots', type=int, default=3, help='distinct host snapshots (cycled)')
+    ap.add_argument('--cpu-halos', type=int, default=150)
+    ap.add_argument('--mode', default='pericentric')
+    args = ap.parse_args()
+    import torch
+    import orbitanalysis_amd  # noqa: F401
+    from orbitanalysis_amd.synthetic_device import DevicePlummer
+    from orbitanalysis_amd.track_orbits_onthefly import OnTheFly
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    nh = max(1, int(args.particles) // args.per_halo)
+    gen = DevicePlummer(n_halos=nh, n_particles=int(args.particles), seed=5, device=dev)
+    S = args.snapshots
+    host, cats, offs = [], [], []
+    t0 = time.perf_counter()
+    for s in range(S):
+        sn = gen.snapshot(s)
+        h = {k: torch.empty(sn[k].shape, dtype=sn[k].dtype, pin_memory=True)
+             for k in ('ids', 'coordinates', 'velocities')}
+        for k in h:
+            h[k].copy_(sn[k])
+        host.append(h)
+        offs.append(np.asarray(sn['region_offsets'], dtype=np.int64))
+        cats.append(gen.catalogue(s)[0])
+        del sn
+    box = gen.box
+    del gen
+    torch.cuda.empty_cache()
+    log('setup %.1f s: %d halos, %s particles per snapshot, %d pinned host snapshots'
+        % (time.perf_counter() - t0, nh, [int(h['ids'].numel()) for h in host], S))
+
+    nmax = max(int(h['ids'].numel()) for h in host)
+    slots = [{k: torch.empty((nmax,) + tuple(host[0][k].shape[1:]), dtype=host[0][k].dtype,
+                             device=dev) for k in host[0]} for _ in range(3)]
+    cs = torch.cuda.Stream(device=dev)
+    evs = {}
+
+    def h2d(k):
+        """Snapshot k (host copy k % S) into slot k % 3 on the copy stream."""
+        src, dst = host[k % S], slots[k % 3]
+        with torch.cuda.stream(cs):
+            for key in src:
+                n = src[key].shape[0]
+                dst[key][:n].copy_(src[key], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(cs)
+        evs[k] = ev
+
+    def snap_dict(k):
+        n = int(host[k % S]['ids'].numel())
+        d = {key: slots[k % 3][key][:n] for key in host[0]}
+        d.update(masses=1.0, box_size=box)
+        o = offs[k % S]
+        sl = np.stack([o, np.append(o[1:], n)], axis=1)
+        return d, sl
+
+    otf = OnTheFly(mode=args.mode)
+    # H2D alone (copy-engine rate) on one snapshot
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    h2d(0)
+    evs[0].synchronize()
+    h2d_s = time.perf_counter() - t
+    h2d_bytes = sum(v.numel() * v.element_size() for v in host[0].values())
+    log('H2D alone: %.1f ms for %.2f GB (%.1f GB/s)' % (h2d_s * 1e3, h2d_bytes / 1e9,
+                                                     h2d_bytes / h2d_s / 1e9))
+    # snapshot 0: frame only (its state is carried into step 1)
+    h2d(1)
+    torch.cuda.current_stream().wait_event(evs[0])
+    d0, sl0 = snap_dict(0)
+    pp = otf._prepare(d0, sl0, cats[0], False)
+    otf.eng.launch(pp, None)
+    from orbitanalysis_amd.engine import SnapshotState
+    from orbitanalysis_amd import _native as N
+    bulk0 = pp.halos.cpu().numpy().view(N.HALO_DTYPE)['bulk'].astype(pp.plan.bulk)
+    carried = (SnapshotState(ids=pp.snap['ids'], rhat=pp.rhat, meta=pp.meta, starts=pp.starts,
+                             counts=pp.counts, exists=np.arange(nh), plan=pp.plan), bulk0)
+    total_steps = 1 + args.steps              # 1 warm-up step
+    comp_ms, units, outs = [], 0, None
+    t_start = None
+    for k in range(1, total_steps + 1):
+        if k == 2:
+            torch.cuda.synchronize()
+            t_start = time.perf_counter()
+        if k + 1 <= total_steps:
+            h2d(k + 1)                         # overlaps this step's compare
+        torch.cuda.current_stream().wait_event(evs[k])
+        dk, slk = snap_dict(k)
+        dp, slp = snap_dict(k - 1)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        outs = otf.run([dk, None], [slk, slp], [cats[k % S], cats[(k - 1) % S]], carried=carried)
+        e1.record()
+        carried = otf.carry
+        if k >= 2:
+            e1.synchronize()
+            comp_ms.append(e0.elapsed_time(e1))
+            units += int(dk['ids'].numel())
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t_start
+    n_apsis = int(outs['apsis_offsets'][-1])
+
+    # CPU oracle: the reference per-call algorithm (frames of both snapshots + compare)
+    # on the first cpu_halos halos of the last step's pair
+    from oracle import orbit_oracle as O
+    k = total_steps
+    ch = min(args.cpu_halos, nh)
+
+    def host_snap(j):
+        o = offs[j % S]
+        e = int(o[ch]) if ch < nh else int(host[j % S]['ids'].numel())
+        d = {key: host[j % S][key][:e].numpy() for key in host[0]}
+        d.update(masses=1.0, box_size=box)
+        sl = np.stack([o[:ch], np.append(o[1:ch], e)], axis=1)
+        return d, sl
+    hc, slc = host_snap(k)
+    hp, slp = host_snap(k - 1)
+    t = time.perf_counter()
+    rc, vc, _ = O.onthefly_region_frame(hc, slc, cats[k % S][:ch])
+    rp, vp, _ = O.onthefly_region_frame(hp, slp, cats[(k - 1) % S][:ch])
+    want = O.onthefly_compare(hc['ids'], hp['ids'], vc, vp, rc, rp, slc, slp, args.mode)
+    cdt = time.perf_counter() - t
+    tag = args.mode[:8] + 'er'
+    got = outs['apsis_ids'][:int(outs['apsis_offsets'][ch])]
+    ok = bool(np.array_equal(want[tag + '_ids'], got))
+    cpu_units = int(slc[-1][1])
+
+    res = {
+        'metric': 'particle-snapshots/s (track_orbits_onthefly stream, H2D inclusive)',
+        'value': units / wall, 'unit': 'particle-snapshots/s', 'n_gpus': 1,
+        'steps': args.steps, 'warmup': 1, 'ms_per_step': wall / args.steps * 1e3,
+        'higher_is_better': True, 'dtype': 'f32', 'data': 'synthetic Plummer spheres, pinned host',
+        'config': {'workload': 'BASELINE configs[4] per-GPU share: %d particles/snapshot, %d '
+                               'halos, f32, box, double-buffered H2D on a copy stream, frame '
+                               'state carried between snapshots' % (units // args.steps, nh)},
+        'compute_ms_per_step': float(np.mean(comp_ms)),
+        'compute_only_rate': units / (sum(comp_ms) * 1e-3),
+        'apsis_last_step': n_apsis,
+        'roofline': {'bound': 'pcie', 'achieved': h2d_bytes / h2d_s / 1e9, 'peak': PCIE_PEAK,
+                     'unit': 'GB/s', 'frac': h2d_bytes / h2d_s / 1e9 / PCIE_PEAK,
+                     'traffic': h2d_bytes, 'note': 'H2D of one snapshot alone, pinned host'},
+        'cpu_baseline': {'value': cpu_units / cdt, 'unit': 'particle-snapshots/s', 'cores': 1,
+                         'kind': 'port', 'sample': '%d of %d halos of the last pair, both '
+                         'frames + compare, %.1f s; apsis IDs identical to the GPU: %s'
+                         % (ch, nh, cdt, ok)},
+    }
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == '__main__':
+    main()
