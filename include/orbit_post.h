@@ -56,6 +56,10 @@ typedef struct oa_collate_args {
     int32_t in_kind;            /* dtype of apsis_ids                                      */
     int32_t key_signed;         /* order keys as signed (output kind signed)               */
     int32_t chunk_start;        /* round r: records [r*CHUNK, (r+1)*CHUNK) of each slice   */
+    int32_t lds_keys;           /* sort slots: power of two in [64, CHUNK], >= every halo's
+                                   record count this round                                */
+    int32_t lds_old;            /* old keys cached in LDS per halo (<= 12288); halos with
+                                   more are searched in global memory                     */
     const void *apsis_ids;      /* this snapshot's {peri|apo}center_IDs                    */
     const uint16_t *angles;     /* this snapshot's angles (float16 bits)                   */
     const uint8_t *keep_lut;    /* [65536]: 1 if (float16 value > angle_cut) in NumPy      */

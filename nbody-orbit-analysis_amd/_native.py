@@ -58,7 +58,7 @@ class CompactArgs(ctypes.Structure):
 
 class CollateArgs(ctypes.Structure):
     _fields_ = [('n_halos', c_i32), ('in_kind', c_i32), ('key_signed', c_i32),
-                ('chunk_start', c_i32), ('apsis_ids', c_vp), ('angles', c_vp),
+                ('chunk_start', c_i32), ('lds_keys', c_i32), ('lds_old', c_i32), ('apsis_ids', c_vp), ('angles', c_vp),
                 ('keep_lut', c_vp), ('src_off', c_vp), ('src_cnt', c_vp), ('new_base', c_vp),
                 ('old_keys', c_vp), ('old_cnt', c_vp), ('old_off', c_vp), ('n_old', c_i64),
                 ('n_new_cap', c_i64), ('w_keys', c_vp), ('w_cnt', c_vp), ('w_lb', c_vp),

@@ -51,7 +51,6 @@ int check_launch(const char *what) {
 constexpr uint64_t SIGN = 0x8000000000000000ull;
 constexpr int CH = OA_COLLATE_CHUNK;
 constexpr int KC = 12288;                // k_central: radius keys cached in LDS
-constexpr int OC = 12288;                // k_collate_new: old keys cached in LDS
 constexpr int SC = OA_CENTRAL_MAX_N;     // k_central: survivors sorted in LDS
 
 // value of element i as 64-bit two's complement (signed kinds sign-extend)
@@ -140,14 +139,19 @@ __device__ void bitonic_pairs(uint64_t *s, uint32_t *x, int P) {
 }
 
 // ------------------------------------------------------------------ f3: collate
-// One work-group per collated halo: this round's kept apsis IDs (angle > cut via the
-// NumPy-evaluated LUT, postprocessing.py:127-128), sorted, run-length encoded
+// One 256-thread work-group per collated halo: this round's kept apsis IDs (angle > cut
+// via the NumPy-evaluated LUT, postprocessing.py:127-128), sorted, run-length encoded
 // (np.unique(return_counts), :135), each unique key located in the halo's old list.
-__global__ __launch_bounds__(1024) void k_collate_new(const oa_collate_args a) {
-    __shared__ uint64_t sk[CH];
-    __shared__ int hp[CH + 1];
-    __shared__ uint64_t ok[OC];          // the halo's old keys, when they fit
-    __shared__ int wsum[17];
+// Dynamic LDS sized by the host for this round: a.lds_keys sort slots (power of two,
+// >= every halo's kept count) and a.lds_old cached old keys (halos with more search
+// the old list in global memory), so several work-groups share a CU.
+constexpr int CT = 256;
+__global__ __launch_bounds__(CT) void k_collate_new(const oa_collate_args a) {
+    extern __shared__ __attribute__((aligned(16))) char cl_smem[];
+    uint64_t *sk = reinterpret_cast<uint64_t *>(cl_smem);
+    uint64_t *ok = sk + a.lds_keys;                       // the halo's old keys, when they fit
+    int *hp = reinterpret_cast<int *>(ok + a.lds_old);
+    __shared__ int wsum[CT / 64 + 1];
     __shared__ int s_m;
     const int j = blockIdx.x;
     const int64_t rem = a.src_cnt[j] - a.chunk_start;
@@ -159,11 +163,12 @@ __global__ __launch_bounds__(1024) void k_collate_new(const oa_collate_args a) {
     const int64_t s0 = a.src_off[j] + a.chunk_start;
     const int64_t base = a.new_base[j];
     const int64_t ob = a.old_off[j], on = a.old_off[j + 1] - ob;
+    const bool cached = on <= a.lds_old;
     if (threadIdx.x == 0) s_m = 0;
     __syncthreads();
-    if (on <= OC)
-        for (int i = threadIdx.x; i < on; i += 1024) ok[i] = a.old_keys[ob + i];
-    for (int i = threadIdx.x; i < nraw; i += 1024) {
+    if (cached)
+        for (int i = threadIdx.x; i < on; i += CT) ok[i] = a.old_keys[ob + i];
+    for (int i = threadIdx.x; i < nraw; i += CT) {
         if (a.keep_lut[a.angles[s0 + i]]) {
             const int p = atomicAdd(&s_m, 1);
             sk[p] = to_key(load_val(a.apsis_ids, s0 + i, a.in_kind), a.key_signed);
@@ -177,22 +182,22 @@ __global__ __launch_bounds__(1024) void k_collate_new(const oa_collate_args a) {
     }
     int P = 1;
     while (P < m) P <<= 1;
-    for (int i = m + threadIdx.x; i < P; i += 1024) sk[i] = ~0ull;   // ties with a real ~0 key are harmless
+    for (int i = m + threadIdx.x; i < P; i += CT) sk[i] = ~0ull;   // ties with a real ~0 key are harmless
     __syncthreads();
-    bitonic_keys<1024>(sk, P);
+    bitonic_keys<CT>(sk, P);
     // run heads: thread t owns positions [t*E, t*E + E)
-    const int E = (m + 1023) / 1024;
+    const int E = (m + CT - 1) / CT;
     const int lo = threadIdx.x * E, hi = min(lo + E, m);
     int nh = 0;
     for (int i = lo; i < hi; ++i) nh += (i == 0 || sk[i] != sk[i - 1]);
     int u;
-    int q = block_scan<1024, int>(nh, wsum, u);
+    int q = block_scan<CT, int>(nh, wsum, u);
     for (int i = lo; i < hi; ++i)
         if (i == 0 || sk[i] != sk[i - 1]) hp[q++] = i;
     if (threadIdx.x == 0) hp[u] = m;
     __syncthreads();
     int carry = 0;
-    for (int q0 = 0; q0 < u; q0 += 1024) {
+    for (int q0 = 0; q0 < u; q0 += CT) {
         const int qq = q0 + threadIdx.x;
         int f = 0;
         uint64_t key = 0;
@@ -202,7 +207,7 @@ __global__ __launch_bounds__(1024) void k_collate_new(const oa_collate_args a) {
             key = sk[hp[qq]];
             c = hp[qq + 1] - hp[qq];
             int64_t L = 0, R = on;
-            if (on <= OC) {
+            if (cached) {
                 while (L < R) {
                     const int64_t mid = (L + R) >> 1;
                     if (ok[mid] < key) L = mid + 1; else R = mid;
@@ -218,7 +223,7 @@ __global__ __launch_bounds__(1024) void k_collate_new(const oa_collate_args a) {
             lb = L;
         }
         int tf;
-        const int ex = block_scan<1024, int>(f, wsum, tf);
+        const int ex = block_scan<CT, int>(f, wsum, tf);
         if (qq < u) {
             a.w_keys[base + qq] = key;
             a.w_cnt[base + qq] = c;
@@ -247,21 +252,22 @@ __global__ __launch_bounds__(1024) void k_collate_offsets(const oa_collate_args 
 }
 
 // one work-group per halo: the halo's new unique keys and their "already present"
-// prefix in LDS; every old element goes to rank i + #new keys below it not already
-// present (adding the new count on a match), every new key absent from the old list to
-// rank lb + #such new keys before it
-__global__ __launch_bounds__(256) void k_collate_merge(const oa_collate_args a) {
-    __shared__ uint64_t nk[CH];
-    __shared__ int nfp[CH + 1];
+// prefix in LDS (a.lds_keys slots); every old element goes to rank i + #new keys below
+// it not already present (adding the new count on a match), every new key absent
+// from the old list to rank lb + #such new keys before it
+__global__ __launch_bounds__(CT) void k_collate_merge(const oa_collate_args a) {
+    extern __shared__ __attribute__((aligned(16))) char cl_smem[];
+    uint64_t *nk = reinterpret_cast<uint64_t *>(cl_smem);
+    int *nfp = reinterpret_cast<int *>(nk + a.lds_keys);
     const int j = blockIdx.x;
     const int u = a.w_ulen[j];
     const int64_t base = a.new_base[j];
     const int64_t ob = a.old_off[j], on = a.old_off[j + 1] - ob;
     const int64_t no = a.new_off[j];
-    for (int q = threadIdx.x; q < u; q += 256) { nk[q] = a.w_keys[base + q]; nfp[q] = a.w_fp[base + q]; }
+    for (int q = threadIdx.x; q < u; q += CT) { nk[q] = a.w_keys[base + q]; nfp[q] = a.w_fp[base + q]; }
     if (threadIdx.x == 0) nfp[u] = a.w_found[j];
     __syncthreads();
-    for (int64_t i = threadIdx.x; i < on; i += 256) {
+    for (int64_t i = threadIdx.x; i < on; i += CT) {
         const uint64_t key = a.old_keys[ob + i];
         int L = 0, R = u;
         while (L < R) {
@@ -273,7 +279,7 @@ __global__ __launch_bounds__(256) void k_collate_merge(const oa_collate_args a) 
         a.new_keys[pos] = key;
         a.new_cnt[pos] = a.old_cnt[ob + i] + (eq ? a.w_cnt[base + L] : 0);
     }
-    for (int q = threadIdx.x; q < u; q += 256) {
+    for (int q = threadIdx.x; q < u; q += CT) {
         if (nfp[q + 1] != nfp[q]) continue;               // already in the old list
         const int64_t pos = no + a.w_lb[base + q] + (q - nfp[q]);
         a.new_keys[pos] = nk[q];
@@ -658,12 +664,22 @@ int oa_collate_step(const oa_collate_args *args, void *stream) {
         (a.n_old + a.n_new_cap > 0 && (!a.new_keys || !a.new_cnt)))
         return fail(OA_E_ARG, "oa_collate_step: null pointer");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(k_collate_new, dim3(a.n_halos), dim3(1024), 0, st, a);
+    if (a.lds_keys < 64 || a.lds_keys > CH || (a.lds_keys & (a.lds_keys - 1)) || a.lds_old < 0)
+        return fail(OA_E_ARG, "oa_collate_step: lds_keys must be a power of two in [64, CHUNK]");
+    const int64_t lds1 = (int64_t)a.lds_keys * 12 + 4 + (int64_t)a.lds_old * 8;
+    const int64_t lds2 = (int64_t)a.lds_keys * 12 + 4;
+    if (lds1 > 150 * 1024) return fail(OA_E_ARG, "oa_collate_step: LDS request too large");
+    if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_collate_new),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void *>(k_collate_merge),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2) != hipSuccess)
+        return fail(OA_E_LAUNCH, "oa_collate_step: hipFuncSetAttribute");
+    hipLaunchKernelGGL(k_collate_new, dim3(a.n_halos), dim3(CT), (size_t)lds1, st, a);
     if (int rc = check_launch("k_collate_new")) return rc;
     hipLaunchKernelGGL(k_collate_offsets, dim3(1), dim3(1024), 0, st, a);
     if (int rc = check_launch("k_collate_offsets")) return rc;
     if (a.n_old + a.n_new_cap > 0) {
-        hipLaunchKernelGGL(k_collate_merge, dim3(a.n_halos), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(k_collate_merge, dim3(a.n_halos), dim3(CT), (size_t)lds2, st, a);
         if (int rc = check_launch("k_collate_merge")) return rc;
     }
     return OA_OK;

@@ -130,6 +130,9 @@ def _id_kind(dt, what):
     return N.ID_KIND[dt]
 
 
+OLD_CACHE = 12288        # old keys per halo cached in LDS by k_collate_new (a.lds_old cap)
+
+
 class _CollateState:
     """Cumulative per-halo sorted-unique (key, count) lists in HBM (CSR)."""
 
@@ -139,6 +142,7 @@ class _CollateState:
         self.device = device
         self.n = n_halos
         self.off = torch.zeros(n_halos + 1, dtype=torch.int64, device=device)
+        self.off_h = np.zeros(n_halos + 1, dtype=np.int64)
         self.keys = torch.empty(1, dtype=torch.int64, device=device)
         self.cnt = torch.empty(1, dtype=torch.int64, device=device)
         self.total = 0
@@ -157,6 +161,12 @@ class _CollateState:
         st = torch.cuda.current_stream(dev).cuda_stream
         for r in range(rounds):
             chunk = np.clip(src_cnt - r * ch, 0, ch).astype(np.int64)
+            # LDS sized to this round: sort slots for the largest chunk, old keys for the
+            # largest cached list (several work-groups then share a CU)
+            lds_keys = 64
+            while lds_keys < int(chunk.max(initial=0)):
+                lds_keys <<= 1
+            lds_old = int(min(np.diff(self.off_h).max(initial=0), OLD_CACHE))
             base = np.concatenate([[0], np.cumsum(chunk)[:-1]]).astype(np.int64)
             cap = int(chunk.sum())
             i64 = dict(dtype=torch.int64, device=dev)
@@ -172,6 +182,7 @@ class _CollateState:
             base_d = _dev(base, dev)
             a = N.CollateArgs(
                 n_halos=self.n, in_kind=in_kind, key_signed=key_signed, chunk_start=r * ch,
+                lds_keys=lds_keys, lds_old=lds_old,
                 apsis_ids=_ptr(ids_d), angles=_ptr(angles_d), keep_lut=_ptr(lut_d),
                 src_off=_ptr(src_off_d), src_cnt=_ptr(src_cnt_d), new_base=_ptr(base_d),
                 old_keys=_ptr(self.keys), old_cnt=_ptr(self.cnt), old_off=_ptr(self.off),
@@ -186,11 +197,11 @@ class _CollateState:
                 e1.record()
                 events.append((e0, e1))
             self.off, self.keys, self.cnt = new_off, new_keys, new_cnt
-            self.total = int(new_off[self.n].item())
+            self.off_h = new_off.cpu().numpy()
+            self.total = int(self.off_h[-1])
 
     def lengths(self):
-        off = self.off.cpu().numpy()
-        return np.diff(off)
+        return np.diff(self.off_h)
 
     def export(self, lib, key_signed, out_dtype):
         torch = self.torch
