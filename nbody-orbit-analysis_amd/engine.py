@@ -324,7 +324,9 @@ class OrbitEngine:
         # measured faster (2.11 vs 2.43-2.52 ms per 1e8-particle step)
         self.n_wg = int(self.lib.oa_device_units()) if env('ORBIT_PERSISTENT', '0') == '1' else 0
         max_lds = self.lib.oa_max_lds_bytes()
-        need = self.lib.oa_step_lds_bytes(self.entries, self.slots)
+        need = self.lib.oa_step_lds_bytes(self.entries, self.slots)   # k_stream: 2 headers
+        if not self.n_wg:
+            need -= self.lib.oa_step_lds_bytes(0, 0) // 2                  # k_step: one
         if need > max_lds:
             raise ValueError('LDS table needs %d bytes > device limit %d' % (need, max_lds))
         self.prev: Optional[SnapshotState] = None
