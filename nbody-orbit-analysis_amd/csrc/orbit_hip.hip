@@ -1925,6 +1925,15 @@ __global__ __launch_bounds__(256) void k_angle_add(const uint16_t *prev, const T
 // Chunks are (item, start, count) triples built by the host (engine.plan_items).
 constexpr int BIG_WG = 256;
 
+// large-halo table slot of a hash: range reduction onto any capacity (the host sizes
+// tables to a ~0.7 load so they stay Infinity-Cache resident), linear probing
+__device__ __forceinline__ uint64_t big_slot(uint64_t h, uint64_t cap) {
+    return __umul64hi(h, cap);
+}
+__device__ __forceinline__ uint64_t big_next(uint64_t s, uint64_t cap) {
+    return s + 1 == cap ? 0 : s + 1;
+}
+
 template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
 __global__ __launch_bounds__(BIG_WG) void k_big_frame(const oa_step_args a, const FrameK fk) {
     typedef typename IdT<IDB>::T ID;
@@ -1963,14 +1972,14 @@ __global__ __launch_bounds__(BIG_WG) void k_big_frame(const oa_step_args a, cons
         if (!COMPARE && a.angles_in) ang = a.angles_in[i];
         a.meta_out[i] = ang | (sgn << 16);
         if (ins) {
-            uint64_t sl = id_hash64((uint64_t)id) & (cap - 1);
+            uint64_t sl = big_slot(id_hash64((uint64_t)id), cap);
             for (uint64_t t = 0; t < cap; ++t) {
                 uint32_t *val = reinterpret_cast<uint32_t *>(tab + 2 * sl + 1);
                 if (atomicCAS(val, 0u, (uint32_t)(p + 1)) == 0u) {
                     tab[2 * sl] = (uint64_t)id;
                     break;
                 }
-                sl = (sl + 1) & (cap - 1);
+                sl = big_next(sl, cap);
             }
         }
     }
@@ -2004,13 +2013,13 @@ __global__ __launch_bounds__(BIG_WG) void k_big_join(const oa_step_args a) {
             pid = lds_nt(&ids_prev[k]);
             const V3<TD> prh = ld3_nt(rhat_prev, k);
             const uint32_t pmeta = lds_nt(&a.meta_prev[k]);
-            uint64_t sl = id_hash64((uint64_t)pid) & (cap - 1);
+            uint64_t sl = big_slot(id_hash64((uint64_t)pid), cap);
             int64_t j = -1;
             for (uint64_t t = 0; t < cap; ++t) {
                 const uint4 e = *reinterpret_cast<const uint4 *>(tab + 2 * sl);
                 if (e.z == 0u) break;
                 if ((((uint64_t)e.y << 32) | e.x) == (uint64_t)pid) { j = (int64_t)e.z - 1; break; }
-                sl = (sl + 1) & (cap - 1);
+                sl = big_next(sl, cap);
             }
             if (j >= 0) {
                 hit = true;

@@ -175,6 +175,9 @@ def plan_global(glob, cur_cnt, prev_cnt, first_index, compare):
         n = int(cur_cnt[h])
         for st in range(0, n, GCHUNK):
             ch1.append((gi, st, min(GCHUNK, n - st)))
+        # linear probing at load <= 0.5 (the kernels range-reduce the hash onto any
+        # capacity; a 0.7 load, small enough for the Infinity Cache, measured slower:
+        # 2.26 vs 1.65 ms for configs[1])
         cap = 64
         while cap < 2 * n:
             cap <<= 1
