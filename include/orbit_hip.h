@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OA_ABI_VERSION 6
+#define OA_ABI_VERSION 7
 
 #define OA_OK 0
 #define OA_E_ARG (-1)       /* invalid argument / unsupported dtype plan */
@@ -62,7 +62,9 @@ typedef struct oa_halo {
  * Global items (large halos, items[n_items ..]): the single halo h0 = h1 - 1.   */
 typedef struct oa_item {
     int32_t h0, h1;
-    int32_t reserved0, reserved1; /* 0, 1 */
+    int32_t slot0;              /* first output slot (oa_halo.out_slot) among [h0,h1),
+                                   or -1 (set by the host planner)                    */
+    int32_t reserved1;          /* 1 */
     int64_t scratch_off;        /* first apsis-scratch slot of this item (a multiple
                                    of 64; one slot per progenitor particle)           */
     int64_t n_pv;               /* progenitor particles of the item                  */

@@ -13,7 +13,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.abspath(__file__))
 # ORBIT_HIP_LIB selects an alternative build (kernel variants for tuning sweeps)
 LIB_PATH = os.environ.get('ORBIT_HIP_LIB') or os.path.join(PKG, 'liborbit_hip.so')
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -21,7 +21,7 @@ c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, cty
 HALO_DTYPE = np.dtype([('cur_off', '<i8'), ('cur_cnt', '<i8'), ('prev_off', '<i8'),
                        ('prev_cnt', '<i8'), ('centre', '<f8', (3,)), ('bulk', '<f8', (3,)),
                        ('out_slot', '<i8'), ('reserved', '<i8')])
-ITEM_DTYPE = np.dtype([('h0', '<i4'), ('h1', '<i4'), ('reserved0', '<i4'), ('reserved1', '<i4'),
+ITEM_DTYPE = np.dtype([('h0', '<i4'), ('h1', '<i4'), ('slot0', '<i4'), ('reserved1', '<i4'),
                        ('scratch_off', '<i8'), ('n_pv', '<i8')])
 
 MODE = {'pericentric': 0, 'apocentric': 1}

@@ -1623,10 +1623,8 @@ __global__ __launch_bounds__(256) void k_gather_items(const oa_compact_args a) {
     __shared__ uint32_t roff[257];
     const oa_item it = a.items[blockIdx.x];
     const int32_t n = a.item_count[blockIdx.x];
-    if (n <= 0) return;
-    int64_t slot = -1;
-    for (int h = it.h0; h < it.h1 && slot < 0; ++h) slot = a.halos[h].out_slot;
-    if (slot < 0) return;
+    const int64_t slot = it.slot0;               // planned on the host: no halo walk
+    if (n <= 0 || slot < 0) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t dst = a.offsets_out[slot];
     const ID *src = reinterpret_cast<const ID *>(a.scratch_ids);

@@ -190,6 +190,21 @@ def plan_global(glob, cur_cnt, prev_cnt, first_index, compare):
     return as3(ch1), as3(ch2), np.array(tab, dtype=np.int64).reshape(-1, 2), off
 
 
+def set_item_slots(items, out_slot):
+    """items['slot0'] = the first output slot among each item's halos [h0, h1), or -1
+    (k_gather_items then needs no serial walk over the halo table)."""
+    if len(items) == 0:
+        return
+    nh = len(out_slot)
+    has = np.asarray(out_slot) >= 0
+    # next halo index >= j with a slot (nh if none)
+    nxt = np.full(nh + 1, nh, dtype=np.int64)
+    idx = np.where(has, np.arange(nh), nh)
+    nxt[:nh] = np.minimum.accumulate(idx[::-1])[::-1]
+    first = nxt[items['h0']]
+    items['slot0'] = np.where(first < items['h1'], np.asarray(out_slot)[np.minimum(first, nh - 1)], -1)
+
+
 def to_device(x, device, dtype=None):
     """numpy/torch array -> contiguous device tensor (bit-preserving for uint)."""
     if isinstance(x, torch.Tensor):
@@ -368,6 +383,8 @@ class OrbitEngine:
             halos['out_slot'][has_prog] = np.arange(int(has_prog.sum()))
         items, glob, scratch = plan_items(counts, halos['prev_cnt'], entries or self.entries,
                                           self.hmax)
+        set_item_slots(items, halos['out_slot'])
+        set_item_slots(glob, halos['out_slot'])
         return halos, items, glob, scratch, starts, counts, has_prog
 
     # ------------------------------------------------------------------ step
