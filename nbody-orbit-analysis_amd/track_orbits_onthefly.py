@@ -54,22 +54,36 @@ def _block_starts(slices, n):
     return starts
 
 
-def _sort_key(ids_t, unsigned):
-    k = ids_t.to(torch.int64)
-    if unsigned:
-        k = (k & 0xFFFFFFFF) if ids_t.dtype == torch.int32 else k ^ (-(1 << 63))
-    return k
+def _sorted_unique_per_halo(lib, device, ids_t, counts, ids_dtype):
+    """np.unique of each halo's rows (``ids_t``: device IDs grouped by halo, ``counts``
+    rows per halo) on the device with the collation kernels (k_collate_new / _merge:
+    per-halo LDS sort, run-length encoding, merge into an empty state).  Returns host
+    (ids, offsets[nh + 1])."""
+    from .postprocessing import _CollateState, _id_kind
+    nh = len(counts)
+    state = _CollateState(nh, device)
+    n = int(ids_t.numel())
+    signed = 1 if np.dtype(ids_dtype).kind == 'i' else 0
+    if n:
+        cnt = np.asarray(counts, dtype=np.int64)
+        off = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.int64)
+        zeros = torch.zeros(n, dtype=torch.int16, device=device)          # f16 0.0 angles
+        keep = torch.ones(65536, dtype=torch.uint8, device=device)        # every row kept
+        state.merge(lib, ids_t.contiguous(), _id_kind(ids_dtype, 'particle ID'), signed,
+                    zeros, keep, off, cnt)
+    ids, _ = state.export(lib, signed, np.dtype(ids_dtype))
+    return ids, np.concatenate([[0], np.cumsum(state.lengths())]).astype(np.int64)
 
 
-def _grouped(values, halo, key, n):
-    """Stable (halo, key) ordering of the rows; returns (values, offsets)."""
-    if values.numel() == 0:
-        return values, np.zeros(n + 1, dtype=np.int64)
-    o1 = torch.argsort(key, stable=True)
-    o2 = torch.argsort(halo[o1], stable=True)
-    order = o1[o2]
-    counts = torch.bincount(halo, minlength=n).cpu().numpy()
-    return values[order], np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+def _interleave_halos(take_a, a, a_off, b, b_off):
+    """Per halo j: a[a_off[j]:a_off[j+1]] if take_a[j] else b[b_off[j]:b_off[j+1]],
+    concatenated in halo order.  Returns (values, offsets)."""
+    lens = np.where(take_a, np.diff(a_off), np.diff(b_off)).astype(np.int64)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    comb = np.concatenate([a, b]) if len(b) else a
+    start = np.where(take_a, a_off[:-1], len(a) + b_off[:-1]).astype(np.int64)
+    src = np.repeat(start - off[:-1], lens) + np.arange(off[-1], dtype=np.int64)
+    return comb[src], off
 
 
 class OnTheFly:
@@ -163,31 +177,38 @@ class OnTheFly:
         angles = angles_h.numpy()
         p_has = pc.halos.cpu().numpy().view(N.HALO_DTYPE)['prev_cnt'] > 0
 
+        def host_ids(t):
+            return t.cpu().numpy().view(ids_dtype) if t.numel() else np.zeros(0, ids_dtype)
+
         def halo_of(pos, starts):
             # block of each selected position (blocks tile [0, n) in halo order)
             st = torch.from_numpy(np.asarray(starts, dtype=np.int64)).to(eng.device)
             return torch.searchsorted(st, pos, right=True) - 1
-        # departed: previous particles without a match, sorted per halo (:145)
+        # departed: setdiff1d(previous, current) per halo (:145), i.e. the sorted unique
+        # IDs of the unmatched previous rows (which already sit in halo order)
         dsel = torch.nonzero(~mp).squeeze(1)
-        d_ids = prev.ids[dsel]
-        departed, d_off = _grouped(d_ids, halo_of(dsel, prev.starts), _sort_key(d_ids, unsigned),
-                                   nh)
-        # entered: current particles without a match, sorted per halo (:168); all of
-        # a halo's particles, in loader order, when its progenitor block is empty (:178)
+        dh = halo_of(dsel, prev.starts)
+        departed, d_off = _sorted_unique_per_halo(
+            eng.lib, eng.device, prev.ids[dsel],
+            torch.bincount(dh, minlength=nh).cpu().numpy(), ids_dtype)
+        # entered: setdiff1d(current, previous) per halo (:168); all of a halo's
+        # particles, in loader order, when its progenitor block is empty (:178)
         esel = torch.nonzero(matched_cur[:pc.n] == 0).squeeze(1)
         e_ids = pc.snap['ids'][esel]
         eh = halo_of(esel, pc.starts)
         sorted_h = torch.from_numpy(p_has).to(eng.device)[eh]
-        key = torch.where(sorted_h, _sort_key(e_ids, unsigned), esel.to(torch.int64))
-        entered, e_off = _grouped(e_ids, eh, key, nh)
+        srt, s_off = _sorted_unique_per_halo(
+            eng.lib, eng.device, e_ids[sorted_h],
+            torch.bincount(eh[sorted_h], minlength=nh).cpu().numpy(), ids_dtype)
+        raw = host_ids(e_ids[~sorted_h])
+        r_off = np.concatenate([[0], np.cumsum(torch.bincount(eh[~sorted_h], minlength=nh)
+                                                .cpu().numpy())]).astype(np.int64)
+        entered, e_off = _interleave_halos(p_has, srt, s_off, raw, r_off)
         # concatenation dtype of the reference's per-halo lists (:183, :203): an empty
         # halo contributes np.array([], dtype=ids.dtype)
         parts = [np.zeros(0, np.dtype(pc.plan.coord))] * int(p_has.sum()) + \
                 [np.zeros(0, ids_dtype)] * int((~p_has).sum())
         adt = np.concatenate(parts).dtype if parts else np.dtype(np.float64)
-
-        def host_ids(t):
-            return t.cpu().numpy().view(ids_dtype) if t.numel() else np.zeros(0, ids_dtype)
 
         bulk_c = pc.halos.cpu().numpy().view(N.HALO_DTYPE)['bulk'].astype(pc.plan.bulk)
         if bulk_p is None:
@@ -199,8 +220,8 @@ class OnTheFly:
                                     plan=pc.plan), bulk_c)
         return {'apsis_offsets': offsets, 'apsis_ids': apsis_ids,
                 'angles': angles.astype(adt, copy=False),
-                'entered_offsets': e_off, 'entered_ids': host_ids(entered),
-                'departed_offsets': d_off, 'departed_ids': host_ids(departed),
+                'entered_offsets': e_off, 'entered_ids': entered,
+                'departed_offsets': d_off, 'departed_ids': departed,
                 'bulk_velocities': [bulk_c, bulk_p]}
 
 
