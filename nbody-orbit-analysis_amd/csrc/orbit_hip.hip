@@ -78,6 +78,9 @@ namespace {
 #ifndef OA_NTST
 #define OA_NTST 1           // phase-3 state words and apsis records stored non-temporal
 #endif
+#ifndef OA_P2META
+#define OA_P2META 0         // phase 1 stores every state word, phase 2 overwrites the
+#endif                      // joined ones in place (L2 merges the lines): no phase 3
 #ifndef OA_TOUCH
 #define OA_TOUCH 0          // re-touch the item's r̂ lines (L2 LRU refresh) before phase 2
 #endif
@@ -769,7 +772,11 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                 if (a.angles_in && ok) ang = a.angles_in[base + li];
             }
             const uint32_t meta = ang | (sgn << 16);
-            if (!COMPARE || !H.has_prev[hl]) { bst32(r_mt, li * 4u, meta); continue; }
+            if (OA_P2META && COMPARE) bst32(r_mt, li * 4u, meta);     // entered: final
+            if (!COMPARE || !H.has_prev[hl]) {
+                if (!(OA_P2META && COMPARE)) bst32(r_mt, li * 4u, meta);
+                continue;
+            }
             if (!ok) continue;
             if (IDB == 8 && hi != hi0) H.nonuniform = 1u;     // benign race: all write 1
             val[u] = slot_pack(lo, meta, li);
@@ -1001,7 +1008,10 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                 a.matched_cur[base + slot_pos(L.hit[u])] = 1;
             }
             // calc_angles (:342-349): apsis angle emitted, then reset to 0
-            if (!OA_ABL_SLOTW) {
+            if (OA_P2META) {
+                // the joined particle's state word, in place over phase 1's
+                bst32(r_mt, slot_pos(L.hit[u]) * 4u, (cond ? 0u : (uint32_t)acc) | (sc << 16));
+            } else if (!OA_ABL_SLOTW) {
                 uint64_t *sp_ = L.hs[u] < nslots ? &slots[L.hs[u]] : &H.stash[L.hs[u] - nslots];
                 reinterpret_cast<uint16_t *>(sp_)[2] = cond ? (uint16_t)0 : acc;
             }
@@ -1079,7 +1089,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // the first ceil(n_span / 2) slots (4 B per position): those slots are read into
     // registers first (<= P3R per thread), the others and the stash are read after
     // the barrier (pm never reaches them), then pm is stored out coalesced.
-    {
+    if (!OA_P2META) {
         uint32_t *pm = reinterpret_cast<uint32_t *>(slots);
         const uint32_t nst = min(H.nstash, (uint32_t)STASH);
         const uint32_t nlow = min((n_span + 1) / 2, nslots);
