@@ -81,6 +81,9 @@ namespace {
 #ifndef OA_P2META
 #define OA_P2META 0         // phase 1 stores every state word, phase 2 overwrites the
 #endif                      // joined ones in place (L2 merges the lines): no phase 3
+#ifndef OA_PF2E
+#define OA_PF2E 0           // issue both static phase-2 trips' loads before the walks
+#endif
 #ifndef OA_TOUCH
 #define OA_TOUCH 0          // re-touch the item's r̂ lines (L2 LRU refresh) before phase 2
 #endif
@@ -890,8 +893,22 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         for (uint32_t o = (uint32_t)tid * 128u; o < nb; o += WG * 128u)
             touch ^= bld<uint32_t, 0>(r_rh, o);
     }
+    Rows SA, SB, SC;
+    Look LA, LB;
+    if (OA_PF2E) {
+        // both static trips' loads go out before the walks, so their HBM latency hides
+        // behind the walks and the barrier; a counted vmcnt retires only the phase-1
+        // stores (other waves gather them) and leaves the loads in flight
+        __builtin_amdgcn_sched_barrier(0);
+        load_rows(SA, (uint32_t)wave);
+        load_rows(SB, (uint32_t)(wave + NWAVE));
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(6 * UNR) : "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    }
     if (!OA_IMMEDIATE_WALK) {
-        __syncthreads();
+        if (!OA_PF2E) __syncthreads();
         const uint32_t np = min(H.npend, pend_cap);
         for (uint32_t e = tid; e < np; e += WG) {
             uint64_t v = pend[e];
@@ -914,16 +931,18 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
         }
     }
-    Rows SA, SB, SC;
-    Look LA, LB;
     // The first trip's loads are issued BEFORE the phase-1/2 barrier.  The barrier
     // then retires only this wave's older VMEM ops with a counted vmcnt that leaves
     // the prefetch loads in flight, plus every LDS insert (lgkmcnt), then a raw
     // s_barrier (a __syncthreads() would drain vmcnt to 0).
-    __builtin_amdgcn_sched_barrier(0);
-    load_rows(SA, (uint32_t)wave);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(3 * UNR) : "memory");
+    if (!OA_PF2E) {
+        __builtin_amdgcn_sched_barrier(0);
+        load_rows(SA, (uint32_t)wave);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(3 * UNR) : "memory");
+    } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     STAMP(3);
@@ -1054,7 +1073,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // pipeline: trips t (compute), t1 (lookup), t2 (loads); every wave starts with
     // trips wave, wave + NWAVE, wave + 2 NWAVE, later ones come from the counter
     uint32_t tc = wave, tl = wave + NWAVE, tp = wave + 2 * NWAVE;
-    load_rows(SB, tl);
+    if (!OA_PF2E) load_rows(SB, tl);
     lookup(SA, LA);
     auto stage = [&](Rows &S0, Look &L0, Rows &S1, Look &L1, Rows &S2) __attribute__((always_inline)) {
         const uint32_t f = trip_fetch(&H.ctr2, lane);
