@@ -165,3 +165,22 @@ def test_main_progenitors_random_vs_oracle():
     want = PO.find_main_progenitors(hp, ho, tp, to)
     got = find_main_progenitors(hp, ho, tp, to)
     assert [int(v) for v in got] == [int(v) for v in want]
+
+
+def test_post_calls_raise_like_the_reference():
+    from orbitanalysis_amd.progenitors import get_central_particle_ids, find_main_progenitors
+    from orbitanalysis_amd.postprocessing import Apsides
+    rng = np.random.default_rng(5)
+    snap = {'ids': np.arange(20000, dtype=np.int64), 'coordinates': rng.uniform(0, 1, (20000, 3)),
+            'region_offsets': np.array([0])}
+    with pytest.raises(NotImplementedError):          # n beyond the LDS survivor sort
+        get_central_particle_ids(snap, np.zeros((1, 3)), n=5000)
+    ids, off = get_central_particle_ids(snap, np.zeros((1, 3)), n=0)
+    assert ids.size == 0 and list(off) == [0]
+    with pytest.raises(NotImplementedError):          # in1d would compare uint64 as float
+        find_main_progenitors(np.arange(10, dtype=np.uint64), np.array([0]),
+                              np.arange(3, dtype=np.uint64), np.array([0]))
+    groups, attrs = _random_track_file(rng, 2, 3, 50, np.int64, 10 ** 6)
+    with pytest.raises(ValueError):
+        Apsides(_Mem(groups, attrs)).collate_apsides(halo_ids=np.array([999]), savefile=_Mem(),
+                                                     verbose=False)

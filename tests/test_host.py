@@ -164,3 +164,41 @@ def test_synthetic_generator_is_deterministic():
     a = PlummerSnapshots(n_halos=2, n_per_halo=300, n_snapshots=3, seed=5).input_digest()
     b = PlummerSnapshots(n_halos=2, n_per_halo=300, n_snapshots=3, seed=5).input_digest()
     assert a == b
+
+
+def test_set_item_slots_first_output_slot():
+    from orbitanalysis_amd import _native as N
+    from orbitanalysis_amd.engine import set_item_slots
+    out_slot = np.array([-1, 0, -1, -1, 1, 2, -1])
+    items = np.zeros(4, dtype=N.ITEM_DTYPE)
+    items['h0'] = [0, 2, 4, 6]
+    items['h1'] = [2, 4, 6, 7]
+    set_item_slots(items, out_slot)
+    assert list(items['slot0']) == [0, -1, 1, -1]
+
+
+def test_interleave_halos_matches_per_halo_concat():
+    from orbitanalysis_amd.track_orbits_onthefly import _interleave_halos
+    rng = np.random.default_rng(3)
+    nh = 50
+    take = rng.uniform(size=nh) < 0.6
+    la, lb = rng.integers(0, 6, nh), rng.integers(0, 6, nh)
+    a_off = np.concatenate([[0], np.cumsum(la)])
+    b_off = np.concatenate([[0], np.cumsum(lb)])
+    a, b = rng.integers(0, 100, a_off[-1]), rng.integers(100, 200, b_off[-1])
+    got, off = _interleave_halos(take, a, a_off, b, b_off)
+    want = [a[a_off[j]:a_off[j + 1]] if take[j] else b[b_off[j]:b_off[j + 1]] for j in range(nh)]
+    assert np.array_equal(got, np.concatenate(want))
+    assert np.array_equal(off, np.concatenate([[0], np.cumsum([len(w) for w in want])]))
+
+
+def test_onthefly_carry_key_and_switch(monkeypatch):
+    from orbitanalysis_amd import track_orbits_onthefly as T
+    monkeypatch.setenv('ORBIT_OTF_CARRY', '0')
+    assert not T._carry_enabled()
+    monkeypatch.setenv('ORBIT_OTF_CARRY', '1')
+    assert T._carry_enabled()
+    assert T._same(np.array([1.0, np.nan]), np.array([1.0, np.nan]))
+    assert not T._same(np.array([1.0], np.float32), np.array([1.0]))
+    T.clear_carry()
+    assert T._CARRY == {}
