@@ -1,0 +1,108 @@
+"""End to end through the public batch API (SURVEY.md §8(d) "end-to-end"): BASELINE
+configs[2] shape (1e8 f32 particles in 1e4 halos per snapshot) fed by a host NumPy
+loader to ``orbitanalysis_amd.track_orbits.track_orbits``, the reference's call
+(track_orbits.py:9-244), with an in-memory savefile (the HDF5 write is excluded, as
+§8(d) says).
+
+Each snapshot pays what a drop-in user pays: the loader's host arrays go to the
+device (ids, coordinates, velocities: 32 B/particle, pageable NumPy memory), the
+per-snapshot plan is built on the host, the kernels run, and the apsis CSR comes
+back and is written to the savefile.  The loader hands back prebuilt arrays (S
+distinct snapshots, cycled), so its own cost is ~0.
+
+value = particles of the timed snapshots / wall time of those snapshots (the first
+snapshot, which only frames, and one warm-up comparison are excluded).
+
+  python tools/bench_e2e.py [--particles 1e8] [--halos 10000] [--snapshots 6]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def log(*a):
+    print('[bench_e2e]', *a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--particles', type=float, default=1e8)
+    ap.add_argument('--halos', type=int, default=10000)
+    ap.add_argument('--snapshots', type=int, default=6, help='snapshots in the run')
+    ap.add_argument('--distinct', type=int, default=3, help='distinct host snapshots (cycled)')
+    ap.add_argument('--mode', default='pericentric')
+    args = ap.parse_args()
+    import torch
+    import orbitanalysis_amd  # noqa: F401
+    from orbitanalysis_amd.synthetic_device import DevicePlummer
+    from orbitanalysis_amd.track_orbits import track_orbits
+    from orbitanalysis_amd.savefile import MemorySavefile
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    gen = DevicePlummer(n_halos=args.halos, n_particles=int(args.particles), seed=0,
+                        device=dev)
+    S = args.distinct
+    host, cats = [], []
+    t0 = time.perf_counter()
+    for s in range(S):
+        sn = gen.snapshot(s)
+        h = {k: (v.cpu().numpy() if isinstance(v, torch.Tensor) else v) for k, v in sn.items()}
+        host.append(h)
+        cats.append(gen.catalogue(s))
+        del sn
+    del gen
+    torch.cuda.empty_cache()
+    log('setup %.1f s: %d host snapshots of %s particles' % (
+        time.perf_counter() - t0, S, [len(h['ids']) for h in host]))
+
+    stamps = {}
+
+    def regions(snapshot_number, halo_ids):
+        c, r, bv = cats[snapshot_number % S]
+        return c[halo_ids], r[halo_ids], bv[halo_ids]
+
+    def load_snapshot_data(snapshot_number, positions, radii):
+        stamps[snapshot_number] = time.perf_counter()
+        return dict(host[snapshot_number % S])
+
+    n = args.snapshots
+    sink = MemorySavefile()
+    branches = np.tile(np.arange(args.halos), (n, 1))
+    t_start = time.perf_counter()
+    track_orbits(np.arange(n), branches, regions, load_snapshot_data, sink, mode=args.mode,
+                 verbose=False)
+    torch.cuda.synchronize()
+    t_end = time.perf_counter()
+    # timed: snapshots 2 .. n-1 (from the loader call of snapshot 2 to the end)
+    timed = list(range(2, n))
+    wall = t_end - stamps[2]
+    units = sum(len(host[s % S]['ids']) for s in timed)
+    n_apsis = sum(len(g['pericenter_IDs' if args.mode == 'pericentric' else 'apocenter_IDs'])
+                  for g in sink.groups.values()) if hasattr(sink, 'groups') else None
+    per = [stamps[s + 1] - stamps[s] for s in range(2, n - 1)] + [t_end - stamps[n - 1]]
+    b = 32.0 * units / len(timed)
+    res = {
+        'metric': 'particle-snapshots/s (track_orbits end to end, host NumPy loader)',
+        'value': units / wall, 'unit': 'particle-snapshots/s', 'n_gpus': 1,
+        'steps': len(timed), 'warmup': 2, 'ms_per_step': wall / len(timed) * 1e3,
+        'higher_is_better': True, 'dtype': 'f32', 'data': 'synthetic Plummer spheres, host NumPy',
+        'config': {'workload': 'BASELINE configs[2] shape: %d particles/snapshot, %d halos, f32, '
+                               'public track_orbits, in-memory savefile' % (units // len(timed),
+                                                                          args.halos)},
+        'ms_per_snapshot': [round(p * 1e3, 2) for p in per],
+        'h2d_bytes_per_snapshot': b,
+        'apsis_records': n_apsis,
+        'total_wall_s': t_end - t_start,
+    }
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == '__main__':
+    main()
