@@ -65,7 +65,7 @@ class PlummerSnapshots:
                  halo_velocity=0.3, dtype=np.float64, centre_dtype=None,
                  masses='scalar', bulk='computed', cosmology=None,
                  births=None, id_offset=0, id_dtype=np.int64, first_snapshot=0,
-                 shuffle=True, region_returns=3):
+                 shuffle=True, region_returns=3, absent=None, empty=None):
         self.n_halos = int(n_halos)
         sizes = np.broadcast_to(np.asarray(n_per_halo, dtype=np.int64), (self.n_halos,))
         self.sizes = sizes.copy()
@@ -112,6 +112,11 @@ class PlummerSnapshots:
         if births is None:
             births = np.zeros(self.n_halos, dtype=np.int64)
         self.births = np.asarray(births, dtype=np.int64)
+        # edge cases: (snapshot index, halo) pairs that are -1 in main_branches
+        # (gaps, deaths, all-absent rows) / whose region radius is 0 (empty blocks; a
+        # snapshot whose every region is empty loads 0 particles)
+        self.absent = [tuple(int(v) for v in p) for p in (absent or [])]
+        self.empty = {tuple(int(v) for v in p) for p in (empty or [])}
 
         # integrate all snapshots once (relative coordinates about each halo centre)
         self._rel_pos, self._rel_vel = [], []
@@ -151,6 +156,8 @@ class PlummerSnapshots:
         mb = np.tile(np.arange(self.n_halos, dtype=np.int64), (self.n_snapshots, 1))
         for h in range(self.n_halos):
             mb[:self.births[h], h] = -1
+        for s, h in self.absent:
+            mb[s, h] = -1
         return mb
 
     # --------------------------------------------------------------- callbacks
@@ -158,6 +165,9 @@ class PlummerSnapshots:
         halo_ids = np.atleast_1d(np.asarray(halo_ids, dtype=np.int64))
         c = self.halo_centres(snapshot_number)[halo_ids].astype(self.centre_dtype)
         radii = np.full(halo_ids.size, self.r_cut, dtype=self.centre_dtype)
+        if self.empty:
+            s = self._index(snapshot_number)
+            radii[[(s, int(h)) in self.empty for h in halo_ids]] = 0
         if self.region_returns == 2:
             return c, radii
         bulk = None

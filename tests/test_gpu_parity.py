@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 
 BATCH = ['g1_config1', 'g2_overlap_birth_massarray', 'g3_apo_periodic',
          'g4_hubble_catalogue', 'g5_fp32_centre32', 'g5_fp32_centre64',
-         'g5_fp32_catalogue32', 'g8_many_small_halos']
+         'g5_fp32_catalogue32', 'g8_many_small_halos', 'g11_edges']
 
 ANGLE_MISMATCH_MAX = 0.01      # fraction of apsis angles allowed to differ by 1 f16 ulp
 
@@ -66,7 +66,7 @@ def test_driver_matches_reference_golden(name):
     print(name, rep)
 
 
-@pytest.mark.parametrize('name', ['g1_config1', 'g3_apo_periodic'])
+@pytest.mark.parametrize('name', ['g1_config1', 'g3_apo_periodic', 'g11_edges'])
 def test_resume_matches_reference_golden(name):
     from orbitanalysis_amd.savefile import MemorySavefile
     fix = load(name)
@@ -82,7 +82,7 @@ def test_resume_matches_reference_golden(name):
 
 
 @pytest.mark.parametrize('name', ['g1_config1', 'g2_overlap_birth_massarray', 'g3_apo_periodic',
-                                  'g5_fp32_centre32', 'g8_many_small_halos'])
+                                  'g5_fp32_centre32', 'g8_many_small_halos', 'g11_edges'])
 def test_global_and_packed_paths_match(name):
     """Tiny LDS tables push every larger halo through the global-table path
     (k_big_frame / k_big_join) and pack many small halos per item: same outputs."""

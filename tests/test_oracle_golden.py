@@ -10,7 +10,7 @@ from oracle import orbit_oracle as O
 
 BATCH = ['g1_config1', 'g2_overlap_birth_massarray', 'g3_apo_periodic',
          'g4_hubble_catalogue', 'g5_fp32_centre32', 'g5_fp32_centre64',
-         'g5_fp32_catalogue32', 'g8_many_small_halos']
+         'g5_fp32_catalogue32', 'g8_many_small_halos', 'g11_edges']
 
 
 @pytest.mark.parametrize('name', BATCH)
@@ -25,7 +25,7 @@ def test_batch_driver_matches_reference(name):
         assert_same(rec.checkpoint, fix['checkpoint/angles'], 'checkpoint')
 
 
-@pytest.mark.parametrize('name', ['g1_config1', 'g3_apo_periodic'])
+@pytest.mark.parametrize('name', ['g1_config1', 'g3_apo_periodic', 'g11_edges'])
 def test_resume_matches_reference(name):
     fix = load(name)
     u, meta = universe(fix)

@@ -88,6 +88,7 @@ def _groups(flat):
     ('g3_apo_periodic', 2, 'range'),              # apocentric, periodic box, checkpoint
     ('g5_fp32_centre32', 3, 'hash'),              # float32 path, computed f32 bulk, 3 ranks
     ('g8_many_small_halos', 2, 'hash'),           # 40 halos, IDs offset past 2^40
+    ('g11_edges', 2, 'range'),                    # gaps, death, empty blocks / snapshot
 ])
 def test_sharded_driver_matches_reference(name, world, owner):
     fix = load(name)

@@ -139,6 +139,16 @@ BATCH_CASES = {
         gen=dict(n_halos=40, n_per_halo=list(range(20, 420, 10)), n_snapshots=4, seed=8,
                  dt=0.4, id_offset=2 ** 40, bulk='catalogue'),
         run=dict(mode='pericentric')),
+    # a1 edges: a birth, a gap (halo 1 absent at s3), a death (halo 3 from s5), an
+    # empty block (halo 0 at s2, so s3 compares against an empty block), a snapshot
+    # that loads 0 particles (s4: every region empty), an all-absent row (s6): s5
+    # compares against s3 and s7 against s5 (track_orbits.py:111-126, :160-164)
+    'g11_edges': dict(
+        gen=dict(n_halos=4, n_per_halo=[600, 500, 400, 300], n_snapshots=8, seed=11, dt=0.5,
+                 births=[0, 0, 2, 0],
+                 absent=[[3, 1], [5, 3], [6, 0], [6, 1], [6, 2], [6, 3], [7, 3]],
+                 empty=[[2, 0], [4, 0], [4, 1], [4, 2], [4, 3]]),
+        run=dict(mode='pericentric', checkpoint=True)),
 }
 
 
