@@ -190,7 +190,7 @@ def test_frame_state_bits_match_oracle(dtype, centre_dtype):
         assert np.array_equal(sgn[sl[0]:sl[1]], want), j
 
 
-@pytest.mark.parametrize('name', ['g6_onthefly', 'g6b_onthefly_f32', 'g6c_onthefly_f32_c64'])
+@pytest.mark.parametrize('name', ['g6_onthefly', 'g6b_onthefly_f32', 'g6c_onthefly_f32_c64', 'g6d_onthefly_empty'])
 @pytest.mark.parametrize('mode', ['pericentric', 'apocentric'])
 def test_onthefly_matches_reference_golden(name, mode):
     """On-the-fly driver (track_orbits_onthefly.py) on the device vs the reference's

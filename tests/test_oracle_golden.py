@@ -38,7 +38,7 @@ def test_resume_matches_reference(name):
     assert_groups_equal(rec.groups, groups(fix, 'resume/'))
 
 
-ONTHEFLY = ['g6_onthefly', 'g6b_onthefly_f32', 'g6c_onthefly_f32_c64']
+ONTHEFLY = ['g6_onthefly', 'g6b_onthefly_f32', 'g6c_onthefly_f32_c64', 'g6d_onthefly_empty']
 
 
 @pytest.mark.parametrize('name', ONTHEFLY)

@@ -216,6 +216,12 @@ ONTHEFLY_CASES = {
                  centres=[[1.0, 1.0, 1.0], [30.0, 69.0, 40.0], [59.5, 35.0, 79.0]],
                  region_returns=2),
         links=[[0, 1, 2], [0, 1, 2]], snapshot=3),
+    # empty blocks: halo 1's current block and halo 2's progenitor block (all of halo
+    # 2's particles are entered, halo 1's progenitors all departed; NaN bulk)
+    'g6d_onthefly_empty': dict(
+        gen=dict(n_halos=4, n_per_halo=[700, 600, 500, 400], n_snapshots=4, seed=37, dt=0.5,
+                 empty=[[3, 1], [2, 2]], region_returns=2),
+        links=[[0, 1, 2, 3], [0, 1, 2, -1]], snapshot=3),
 }
 
 
