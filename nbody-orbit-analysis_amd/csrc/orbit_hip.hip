@@ -81,6 +81,9 @@ namespace {
 #ifndef OA_P2META
 #define OA_P2META 0         // phase 1 stores every state word, phase 2 overwrites the
 #endif                      // joined ones in place (L2 merges the lines): no phase 3
+#ifndef OA_HIMM
+#define OA_HIMM 0           // k_step: high ID words as a min/max reduction (no hi0 load)
+#endif
 #ifndef OA_PF2E
 #define OA_PF2E 0           // issue both static phase-2 trips' loads before the walks
 #endif
@@ -693,9 +696,12 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         uint32_t ns_eff = nj * OA_SLOT_X2 / 2 + 64;
         H.nsl = ns_eff > nslots_max ? nslots_max : ns_eff;
         // reference high word for the 32-bit LDS keys: the item's first particle
+        // (OA_HIMM: phase 1 reduces the min / max high word of the inserted IDs
+        // instead, so phase 0 has no dependent load of ids[])
         const oa_halo &h0 = a.halos[it.h0], &hl1 = a.halos[it.h1 - 1];
-        H.hi0 = 0;
-        if (IDB == 8 && hl1.cur_off + hl1.cur_cnt > h0.cur_off)
+        H.hi0 = OA_HIMM ? 0xFFFFFFFFu : 0u;
+        H.pad0 = 0;
+        if (!OA_HIMM && IDB == 8 && hl1.cur_off + hl1.cur_cnt > h0.cur_off)
             H.hi0 = (uint32_t)((uint64_t)ids[h0.cur_off] >> 32);
     }
     __syncthreads();
@@ -707,7 +713,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
 
     const int64_t base = uni64(H.cur_base);
     const uint32_t n_span = uni(H.n_span);
-    const uint32_t hi0 = uni(H.hi0);
+    uint32_t hi0 = OA_HIMM ? 0u : uni(H.hi0);
+    uint32_t hmn = 0xFFFFFFFFu, hmx = 0u;           // OA_HIMM: this lane's high words
     const uint32_t nhu = uni(H.nh);
     const Rsrc r_id = make_rsrc(ids + base, n_span * IDB);
     const Rsrc r_x = make_rsrc(reinterpret_cast<const TX *>(a.coords) + 3 * base, n_span * SX);
@@ -781,7 +788,10 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                 continue;
             }
             if (!ok) continue;
-            if (IDB == 8 && hi != hi0) H.nonuniform = 1u;     // benign race: all write 1
+            if (IDB == 8) {
+                if (OA_HIMM) { hmn = min(hmn, hi); hmx = max(hmx, hi); }
+                else if (hi != hi0) H.nonuniform = 1u;     // benign race: all write 1
+            }
             val[u] = slot_pack(lo, meta, li);
             uint32_t cs[3];
             cuckoo_slots(lo, nslots, cs);
@@ -824,6 +834,14 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         t1n = trip_take(f1, t1n);
     }
 #undef OA_LOAD1
+    if (OA_HIMM && IDB == 8 && COMPARE) {
+#pragma unroll
+        for (int o = 32; o; o >>= 1) {
+            hmn = min(hmn, (uint32_t)__shfl_xor((int)hmn, o));
+            hmx = max(hmx, (uint32_t)__shfl_xor((int)hmx, o));
+        }
+        if (lane == 0) { atomicMin(&H.hi0, hmn); atomicMax(&H.pad0, hmx); }
+    }
     WSTAMP(0);
     STAMP(2);
     if constexpr (!COMPARE) return;
@@ -950,7 +968,10 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         if (tid == 0) atomicOr(a.status, OA_STATUS_TABLE_OVERFLOW);
         return;
     }
-    const bool nonuniform = IDB == 8 && uni(H.nonuniform) != 0;
+    // OA_HIMM: an item without entries has min 0xFFFFFFFF > max 0 (uniform; every
+    // lookup misses on the empty slots' position check)
+    const bool nonuniform = IDB == 8 && (OA_HIMM ? uni(H.hi0) < uni(H.pad0) : uni(H.nonuniform) != 0);
+    if (OA_HIMM) hi0 = uni(H.hi0);
     const uint32_t nstash = min(uni(H.nstash), (uint32_t)STASH);
     // cuckoo lookup of (halo, id) for one trip of rows, then the gather of the matched
     // current r̂ rows (written in phase 1: L2).  The three candidate slots are read
