@@ -47,42 +47,44 @@ def step_bytes(pr, n_prev, n_apsis):
 
 
 def cpu_baseline(snap_cur, snap_prev, cat_cur, cat_prev, H, z, gpu_prev_angles,
-                 gpu_ids, gpu_offs, n_halos, mode):
-    """Time the oracle's per-halo path (track_orbits.py:147-185 for a compared
-    snapshot) on the first n_halos blocks; return rate + parity vs the GPU."""
-    from oracle import orbit_oracle as O
+                 gpu_ids, gpu_offs, n_halos, mode, workers):
+    """Time the reference's per-halo path on the CPU (oracle/cpu_baseline.py, a child
+    process that never touches the GPU) on the first ``n_halos`` blocks of the last
+    timed snapshot pair: the reference's own join (setdiff1d/in1d/myin1d) on 1 core and
+    over ``workers`` processes, and the oracle's searchsorted join on 1 core.  Returns
+    the child's JSON plus whether its apsis IDs equal the GPU's for the sample."""
+    import subprocess
+    import tempfile
 
     def host(snap, k):
         offs = snap['region_offsets']
         end = int(offs[k]) if k < len(offs) else int(snap['ids'].numel())
-        d = {key: snap[key][:end].cpu().numpy() for key in ('ids', 'coordinates', 'velocities')}
-        d.update({key: snap[key] for key in ('masses', 'box_size', 'redshift')})
-        d['region_offsets'] = offs[:k]
-        return d, np.append(offs[:k], end)
+        return ({key: snap[key][:end].cpu().numpy() for key in ('ids', 'coordinates', 'velocities')},
+                np.append(offs[:k], end).astype(np.int64))
 
     cur, cb = host(snap_cur, n_halos)
     prv, pb = host(snap_prev, n_halos)
-    ang_prev = gpu_prev_angles[:pb[-1]]
-    # previous-snapshot frame (state input of the step, untimed)
-    prev_rh, prev_vr = [], []
-    for j in range(n_halos):
-        rh, vr, _ = O.region_frame(prv, (pb[j], pb[j + 1]), cat_prev[0][j], cat_prev[2][j], H)
-        prev_rh.append(rh)
-        prev_vr.append(vr)
-    t0 = time.perf_counter()
-    ids_out = []
-    for j in range(n_halos):
-        sl = (cb[j], cb[j + 1])
-        rh, vr, _ = O.region_frame(cur, sl, cat_cur[0][j], cat_cur[2][j], H)
-        d = O.compare_radial_velocities(cur['ids'][sl[0]:sl[1]], prv['ids'][pb[j]:pb[j + 1]],
-                                        vr, prev_vr[j], rh, prev_rh[j], mode)
-        O.calc_angles(sl[1] - sl[0], ang_prev[pb[j]:pb[j + 1]], d)
-        ids_out.append(d['apsis_ids'])
-    dt = time.perf_counter() - t0
-    units = int(cb[-1])
-    want = np.concatenate(ids_out)
+    tmp = '/dev/shm' if os.path.isdir('/dev/shm') else None
+    with tempfile.TemporaryDirectory(dir=tmp) as td:
+        path = os.path.join(td, 'sample.npz')
+        np.savez(path, c_ids=cur['ids'], c_x=cur['coordinates'], c_v=cur['velocities'],
+                 p_ids=prv['ids'], p_x=prv['coordinates'], p_v=prv['velocities'],
+                 c_off=cb, p_off=pb, c_centre=cat_cur[0][:n_halos], c_bulk=cat_cur[2][:n_halos],
+                 p_centre=cat_prev[0][:n_halos], p_bulk=cat_prev[2][:n_halos],
+                 angles_prev=gpu_prev_angles[:pb[-1]], H=H, z=z, mode=mode,
+                 mass=float(snap_cur['masses']), box=float(snap_cur['box_size']))
+        ids_out = os.path.join(td, 'ids.npy')
+        env = dict(os.environ, OMP_NUM_THREADS='1', OPENBLAS_NUM_THREADS='1', MKL_NUM_THREADS='1')
+        r = subprocess.run([sys.executable, os.path.join(ROOT, 'oracle', 'cpu_baseline.py'), path,
+                            '--workers', str(workers), '--ids-out', ids_out],
+                           capture_output=True, text=True, env=env, timeout=900)
+        if r.returncode != 0:
+            raise RuntimeError('cpu baseline failed: %s' % r.stderr[-2000:])
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+        want = np.load(ids_out)
     got = gpu_ids[:int(gpu_offs[n_halos])]
-    return units / dt, dt, units, bool(np.array_equal(want, got))
+    out['identical'] = bool(np.array_equal(want, got))
+    return out
 
 
 def main():
@@ -95,8 +97,12 @@ def main():
     ap.add_argument('--mode', default='pericentric')
     ap.add_argument('--dtype', default='float32', choices=['float32', 'float64'],
                     help='coordinates / velocities / catalogue dtype (configs[1] is float64)')
-    ap.add_argument('--max-snapshots', type=int, default=16)
+    ap.add_argument('--max-snapshots', type=int, default=40,
+                    help='device memory guard: snapshots generated (steps + warmup + 1)')
     ap.add_argument('--cpu-halos', type=int, default=1500)
+    ap.add_argument('--cpu-workers', type=int, default=0,
+                    help='processes of the P-core CPU baseline (0: min(16, cpu_count): the '
+                         'GPU box gives one GPU 16 host cores)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--backend', default='nccl',
                     help="collective backend for N > 1 ('gloo': rehearsal with several "
@@ -128,7 +134,7 @@ def main():
 
     import orbitanalysis_amd  # noqa: F401
     from orbitanalysis_amd import _native
-    from orbitanalysis_amd.engine import OrbitEngine, Workspace, meta_angles
+    from orbitanalysis_amd.engine import OrbitEngine, meta_angles
     from collections import namedtuple
     State = namedtuple('State', 'ids rhat meta')
     from orbitanalysis_amd.synthetic_device import DevicePlummer
@@ -137,7 +143,11 @@ def main():
     t_setup = time.perf_counter()
     gen = DevicePlummer(n_halos=args.halos, n_particles=int(args.particles), seed=0,
                         rank=rank, world=world, device=dev, dtype=args.dtype)
-    S = min(args.steps + args.warmup + 1, args.max_snapshots)
+    # one snapshot per step, none reused: every timed pair is (s - 1, s) of one orbit
+    S = args.steps + args.warmup + 1
+    if S > args.max_snapshots:
+        raise SystemExit('--steps + --warmup + 1 = %d snapshots > --max-snapshots %d'
+                         % (S, args.max_snapshots))
     snaps, cats = [], []
     for s in range(S):
         snaps.append(gen.snapshot(s))
@@ -155,15 +165,13 @@ def main():
     chain = [(prep0, 0)]
     layout = (prep0.starts, prep0.counts, exists, prep0.plan, prep0.n)
     for t in range(1, args.warmup + args.steps + 1):
-        s = t % S
+        s = t
         pr = eng.prepare(snaps[s], cats[s][0], cats[s][2], H, z, exists, True, prev_layout=layout)
         chain.append((pr, s))
         layout = (pr.starts, pr.counts, exists, pr.plan, pr.n)
     preps = [c[0] for c in chain[1:]]
-    ws = Workspace(dev, torch.int64 if preps[0].plan.ids.itemsize == 8 else torch.int32,
-                   max(p.scratch for p in preps), max(p.n_prev for p in preps),
-                   max(int(p.has_prog.sum()) for p in preps), max(len(p.items) for p in preps),
-                   eng.entries, eng.n_wg)
+    for p in preps:
+        ws = eng.workspace(p)                 # grown to the largest step
     # catalogue exchange (N > 1): rank r holds catalogue rows [r*nl, (r+1)*nl)
     nl = -(-args.halos // world)
     cat_local, cat_all = [], None
@@ -244,13 +252,26 @@ def main():
         offs = ws.offsets[:int(last.has_prog.sum()) + 1].cpu().numpy()
         gids = ws.out_ids[:n_apsis].cpu().numpy()
         nh = min(args.cpu_halos, args.halos)
-        rate, dt, cu, ok = cpu_baseline(snaps[s_last], snaps[s_prev], cats[s_last], cats[s_prev],
-                                        H, z, ang_prev, gids, offs, nh, args.mode)
-        cpu = {'value': rate, 'unit': 'particle-snapshots/s', 'cores': 1, 'kind': 'port',
-               'sample': '%d of %d halos (%d particles) of the last timed snapshot, oracle '
-                         'region_frame+compare_radial_velocities+calc_angles per halo, %.1f s; '
-                         'apsis IDs identical to the GPU: %s' % (nh, args.halos, cu, dt, ok)}
-        log('cpu baseline %.3e particle-snapshots/s over %.1f s, parity %s' % (rate, dt, ok))
+        ncpu = os.cpu_count() or 1
+        workers = args.cpu_workers or min(16, ncpu)
+        cb = cpu_baseline(snaps[s_last], snaps[s_prev], cats[s_last], cats[s_prev],
+                          H, z, ang_prev, gids, offs, nh, args.mode, workers)
+        pc, r1, p1 = cb['ref_pcore'], cb['ref_1core'], cb['port_1core']
+        cpu = {'value': pc['rate'], 'unit': 'particle-snapshots/s', 'cores': workers,
+               'kind': 'port',
+               'sample': '%d of %d halos (%d particles) of the last timed snapshot pair; the '
+                         "reference's per-halo path restated (region_frame, setdiff1d/in1d/"
+                         'myin1d join, calc_angles) with the halos split over %d processes '
+                         '(host has %d CPUs; the box allots one GPU 16), %.2f s; apsis IDs '
+                         'identical to the GPU: %s' % (nh, args.halos, cb['particles'], workers,
+                                                       ncpu, pc['seconds'], cb['identical']),
+               'single_core': {'value': r1['rate'], 'seconds': r1['seconds'],
+                               'algorithm': 'reference join (setdiff1d + in1d + myin1d)'},
+               'single_core_searchsorted': {'value': p1['rate'], 'seconds': p1['seconds'],
+                                            'algorithm': 'oracle join (argsort + searchsorted)'},
+               'host_cpus': ncpu}
+        log('cpu baseline: %d procs %.3e/s, 1 core %.3e/s (searchsorted join %.3e/s), parity %s'
+            % (workers, pc['rate'], r1['rate'], p1['rate'], cb['identical']))
 
     if rank == 0:
         out = {

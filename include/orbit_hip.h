@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OA_ABI_VERSION 7
+#define OA_ABI_VERSION 8
 
 #define OA_OK 0
 #define OA_E_ARG (-1)       /* invalid argument / unsupported dtype plan */
@@ -39,6 +39,10 @@ extern "C" {
 /* Run-time flags reported by the step kernel in `status` (bit mask). */
 #define OA_STATUS_TABLE_OVERFLOW 2u   /* the LDS cuckoo table could not place every
                                          entry (stash full): re-plan smaller items */
+#define OA_STATUS_PLAN 4u             /* an item exceeds the kernel's limits (more than
+                                         oa_build_info(3) * work-group progenitor
+                                         positions): the plan did not come from
+                                         oa_plan_items                               */
 
 #define OA_MODE_PERICENTRIC 0
 #define OA_MODE_APOCENTRIC 1
@@ -140,15 +144,6 @@ typedef struct oa_step_args {
                                    (0 = empty), u32 pad}; zeroed by oa_step          */
     uint32_t *gvals;            /* unused (NULL)                                      */
     int64_t gtab_total;         /* slots over all global items                        */
-    /* persistent join (compare != 0, ABI >= 5): n_wg work-groups each process packed
-     * items in turn, taking them from *work, the frame of the next item interleaved
-     * with the join of the current one.  stage: n_wg * 2 * lds_entries * 8 bytes of
-     * device scratch; work: device counter, zero on entry.  stage == NULL: one
-     * work-group per packed item (no interleaving). */
-    uint32_t *work;
-    void *stage;
-    int32_t n_wg;               /* 0: one per compute unit                            */
-    int32_t reserved_p;
 } oa_step_args;
 
 /* Arguments of oa_compact: gather the per-item apsis records into the reference's
@@ -180,7 +175,7 @@ int oa_abi_version(void);
 int64_t oa_struct_size(int32_t which);
 
 /* Compile-time configuration: 0 work-group size, 1 max halos per item,
- * 2 phase-1 unroll, 3 phase-2 unroll; -1 otherwise. */
+ * 2 phase-1 unroll, 3 progenitor rows (64 positions) per wave of an item; -1 otherwise. */
 int32_t oa_build_info(int32_t which);
 
 /* Message of the last failing call on this thread ("" if none). */
@@ -201,11 +196,25 @@ int oa_bulk_velocity(const void *vels, int32_t vel_f64, const void *masses, int3
  * (:293-351), emitting apsis records in previous-block order. */
 int oa_step(const oa_step_args *args, void *stream);
 
-/* Dynamic LDS bytes a join work-group needs for the given table sizes. */
-int64_t oa_step_lds_bytes(int32_t entries, int32_t slots);
+/* Dynamic LDS bytes a join work-group needs for the given table sizes and r̂ dtype
+ * (dx_f64: 1 = float64): max(8 * slots + 2 * entries, 3 * entries * sizeof(r̂)) +
+ * entries + the item header. */
+int64_t oa_step_lds_bytes(int32_t entries, int32_t slots, int32_t dx_f64);
 
-/* Compute units of the current device (the persistent join's default n_wg). */
-int32_t oa_device_units(void);
+/* HOST function (no device needed): the work-group plan of one snapshot.
+ * Replaces the per-halo dispatch of track_orbits.py:147-194 (the `track(j)` closure
+ * mapped over halos): consecutive halos whose current blocks fit one LDS table
+ * (<= entries particles, <= hmax halos, <= max_pv padded progenitor positions) are
+ * packed greedily into items (k_step); a halo beyond any of those limits becomes a
+ * single-halo global item (k_big_*), listed after every packed item.
+ *   cur_cnt[n_halos], prev_cnt[n_halos] (< 0: no progenitor), out_slot[n_halos]
+ *   (-1: none) are host arrays; items[cap] receives the plan (oa_item.slot0 set).
+ * Returns the number of items written (packed + global), or a negative OA_E*;
+ * *n_small = packed items, *scratch = apsis-scratch slots (one per padded
+ * progenitor position). */
+int64_t oa_plan_items(const int64_t *cur_cnt, const int64_t *prev_cnt, const int64_t *out_slot,
+                      int64_t n_halos, int64_t entries, int64_t hmax, int64_t max_pv,
+                      oa_item *items, int64_t cap, int64_t *n_small, int64_t *scratch);
 
 /* Diagnostic builds only (-DOA_STAMPS=1): copy the per-work-group phase timestamps
  * (s_memrealtime, 100 MHz; 6 per work-group) of the last oa_step to host memory.

@@ -13,7 +13,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.abspath(__file__))
 # ORBIT_HIP_LIB selects an alternative build (kernel variants for tuning sweeps)
 LIB_PATH = os.environ.get('ORBIT_HIP_LIB') or os.path.join(PKG, 'liborbit_hip.so')
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -26,6 +26,7 @@ ITEM_DTYPE = np.dtype([('h0', '<i4'), ('h1', '<i4'), ('slot0', '<i4'), ('reserve
 
 MODE = {'pericentric': 0, 'apocentric': 1}
 STATUS_TABLE_OVERFLOW = 2
+STATUS_PLAN = 4
 
 
 class StepArgs(ctypes.Structure):
@@ -43,8 +44,7 @@ class StepArgs(ctypes.Structure):
                 ('matched_prev', c_vp), ('matched_cur', c_vp), ('vr_out', c_vp),
                 ('n_global_items', c_i32), ('n_gchunk1', c_i32), ('n_gchunk2', c_i32),
                 ('gchunk1', c_vp), ('gchunk2', c_vp), ('gtab', c_vp), ('gkeys', c_vp),
-                ('gvals', c_vp), ('gtab_total', c_i64),
-                ('work', c_vp), ('stage', c_vp), ('n_wg', c_i32), ('reserved_p', c_i32)]
+                ('gvals', c_vp), ('gtab_total', c_i64)]
 
 
 class CompactArgs(ctypes.Structure):
@@ -96,8 +96,8 @@ SYMBOLS = {
     'oa_last_error': (ctypes.c_char_p, []),
     'oa_bulk_velocity': (ctypes.c_int, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
     'oa_step': (ctypes.c_int, [ctypes.POINTER(StepArgs), c_vp]),
-    'oa_step_lds_bytes': (c_i64, [c_i32, c_i32]),
-    'oa_device_units': (c_i32, []),
+    'oa_step_lds_bytes': (c_i64, [c_i32, c_i32, c_i32]),
+    'oa_plan_items': (c_i64, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp]),
     'oa_max_lds_bytes': (c_i64, []),
     'oa_debug_stamps': (c_i64, [c_vp, c_i64]),
     'oa_compact': (ctypes.c_int, [ctypes.POINTER(CompactArgs), c_vp]),

@@ -14,13 +14,14 @@
 //
 // Design: one work-group per *item* (a run of consecutive halos whose
 // current blocks fit the LDS hash table; larger halos go through per-halo tables in
-// global memory, k_big_*).  Phase 1 streams the item's current blocks (ids, AoS x, AoS v) once,
-// computes the frame in registers, writes the particle record {r̂, meta} and inserts
-// (halo, id) -> local index into an LDS open-addressing table.  Phase 2 streams the
-// progenitor blocks (ids, records), probes the table, gathers the just-written
-// current record from L2, applies the strict sign test and the arccos angle update
-// and compacts apsis records in previous-block order with wave ballots.  Every
-// input byte is read from HBM once; no sort.
+// global memory, k_big_*).  Phase 1 streams the item's current blocks (ids, AoS x,
+// AoS v) once, computes the frame in registers, writes r̂ and inserts (halo, id) ->
+// position into an LDS cuckoo table.  Phase 2a streams the progenitor blocks' IDs
+// and state words, probes the table and decides the strict sign test; phase 2b
+// stages the item's current r̂ into the LDS the table occupied, streams the
+// progenitor r̂, applies the arccos angle update and compacts apsis records in
+// previous-block order with wave ballots.  Every input byte is read from HBM once;
+// no sort, no per-particle gather from L2.
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (no FMA contraction:
 // the reference's NumPy arithmetic rounds every product and sum).
@@ -40,82 +41,13 @@ namespace {
 #define OA_WG 1024
 #endif
 #ifndef OA_UNR1
-#define OA_UNR1 2
+#define OA_UNR1 2           // phase 1: rows per wave trip
 #endif
-#ifndef OA_UNR2
-#define OA_UNR2 2
+#ifndef OA_KROWS
+#define OA_KROWS 12         // phase 2: progenitor rows held per wave (n_pv <= KROWS * WG)
 #endif
-// Ablation switches for diagnostic builds only (wrong results by design):
-//   OA_ABL_GATHER  phase 2 uses the previous r̂ instead of gathering the current one
-//   OA_ABL_INSERT  phase 1 skips the LDS hash inserts (phase 2 then misses)
-//   OA_ABL_FRAME   phase 1 skips the frame arithmetic (r̂ = dx)
-//   OA_ABL_STORE1  phase 1 skips its r̂ stores
-//   OA_ABL_PHASE3  phase 3 skips its meta stores
-//   OA_ABL_ACOS    phase 2 skips arccos
-//   OA_ABL_EMIT    phase 2 skips apsis record stores / counters
-//   OA_ABL_SLOTW   phase 2 skips the angle write-back into the slot
-#ifndef OA_ABL_CAS
-#define OA_ABL_CAS 0
-#endif
-#ifndef OA_ABL_WALK
-#define OA_ABL_WALK 0
-#endif
-#ifndef OA_IMMEDIATE_WALK
-#define OA_IMMEDIATE_WALK 0
-#endif
-#ifndef OA_HASH
-#define OA_HASH 1
-#endif
-#ifndef OA_ABL_ACOS
-#define OA_ABL_ACOS 0
-#endif
-#ifndef OA_ABL_EMIT
-#define OA_ABL_EMIT 0
-#endif
-#ifndef OA_ABL_SLOTW
-#define OA_ABL_SLOTW 0
-#endif
-#ifndef OA_NTST
-#define OA_NTST 1           // phase-3 state words and apsis records stored non-temporal
-#endif
-#ifndef OA_P2META
-#define OA_P2META 0         // phase 1 stores every state word, phase 2 overwrites the
-#endif                      // joined ones in place (L2 merges the lines): no phase 3
-#ifndef OA_HIMM
-#define OA_HIMM 0           // k_step: high ID words as a min/max reduction (no hi0 load)
-#endif
-#ifndef OA_PF2E
-#define OA_PF2E 0           // issue both static phase-2 trips' loads before the walks
-#endif
-#ifndef OA_TOUCH
-#define OA_TOUCH 0          // re-touch the item's r̂ lines (L2 LRU refresh) before phase 2
-#endif
-#ifndef OA_ABL_GATHER
-#define OA_ABL_GATHER 0
-#endif
-#ifndef OA_ABL_INSERT
-#define OA_ABL_INSERT 0
-#endif
-#ifndef OA_ABL_FRAME
-#define OA_ABL_FRAME 0
-#endif
-#ifndef OA_ABL_STORE1
-#define OA_ABL_STORE1 0
-#endif
-#ifndef OA_ABL_PHASE3
-#define OA_ABL_PHASE3 0
-#endif
-#ifndef OA_SLOT_X2
-#define OA_SLOT_X2 4        // per-item table: slots = entries * OA_SLOT_X2 / 2 (+64)
-#endif
-#ifndef OA_PF1D
-#define OA_PF1D 1           // phase-1 loop trips of loads in flight ahead (1 or 2)
-#endif
-#ifndef OA_DYN
-#define OA_DYN 1            // waves take loop trips from an LDS counter (else static)
-#endif
-#ifndef OA_UJ
-#define OA_UJ 1             // k_stream: join rows per interleaved step
+#ifndef OA_PF2
+#define OA_PF2 3            // phase 2b: rows of previous r̂ loads in flight ahead
 #endif
 #ifndef OA_HMAX
 #define OA_HMAX 32
@@ -124,12 +56,11 @@ constexpr int WG = OA_WG;           // k_step work-group
 constexpr int NWAVE = WG / 64;
 constexpr int HMAX = OA_HMAX;       // halos per item
 constexpr int UNR1 = OA_UNR1;       // phase-1 particles per thread per loop trip
-constexpr int UNR2 = OA_UNR2;       // phase-2 particles per thread per loop trip
+constexpr int KROWS = OA_KROWS;
+constexpr int PF2 = OA_PF2;
 constexpr int BULK_CHUNK = 8192;    // numpy pairwise-sum buffer chunk
 constexpr int STASH = 64;           // cuckoo stash entries per item
 constexpr int MAX_EVICT = 48;       // eviction-chain length before an entry is stashed
-constexpr int P3R = 7;              // phase 3: overlaid slots held per thread, so an
-                                    // item spans <= 2 * P3R * WG positions
 static_assert(WG % 64 == 0 && WG <= 1024, "work-group must be whole waves");
 static_assert(HMAX < WG, "halo table is staged by one thread per halo");
 
@@ -150,36 +81,26 @@ int check_launch(const char *what) {
 }
 
 // ------------------------------------------------------------------ loads
-#ifndef OA_NT
-#define OA_NT 1
-#endif
-// streamed-once inputs: non-temporal loads keep L2 for the phase-2 r̂ gathers
+// streamed-once inputs: non-temporal loads leave L2 to the lines that are re-read
 template <typename T> __device__ __forceinline__ T lds_nt(const T *p) {
-#if OA_NT
     return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
 }
 
 #ifndef OA_STAMPS
 #define OA_STAMPS 0
 #endif
 #if OA_STAMPS
-// diagnostic build only: per-work-group s_memrealtime (100 MHz) at phase boundaries
-// plus, per wave, the ends of its phase-1 and phase-2 loops (WSTAMP 0/1)
-constexpr int STAMP_MAX_WG = 1 << 16, STAMP_N = 6 + 2 * (OA_WG / 64);
+// diagnostic build only: per-work-group s_memrealtime (100 MHz) at the 8 phase
+// boundaries plus, per wave, the ends of its phase-1, 2a and 2b loops (WSTAMP 0/1/2)
+constexpr int STAMP_MAX_WG = 1 << 16, STAMP_NP = 8, STAMP_N = STAMP_NP + 3 * (OA_WG / 64);
 __device__ uint64_t g_stamps[STAMP_MAX_WG * STAMP_N];
 #define STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < STAMP_MAX_WG) \
     g_stamps[blockIdx.x * STAMP_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define STAMPI(item, k) do { if (threadIdx.x == 0 && (item) < STAMP_MAX_WG) \
-    g_stamps[(item) * STAMP_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define WSTAMP(k) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < STAMP_MAX_WG) \
-    g_stamps[blockIdx.x * STAMP_N + 6 + 2 * (threadIdx.x >> 6) + (k)] = \
+    g_stamps[blockIdx.x * STAMP_N + STAMP_NP + 3 * (threadIdx.x >> 6) + (k)] = \
         __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define STAMP(k) do { } while (0)
-#define STAMPI(item, k) do { } while (0)
 #define WSTAMP(k) do { } while (0)
 #endif
 
@@ -249,10 +170,8 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
     h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
     return h;
 }
-// Three cuckoo candidate slots of a key (low 32 bits of the ID) in a table of n slots:
-// one 64-bit mix, three 21-bit fields scaled to [0, n).
+// Three cuckoo candidate slots of a key (low 32 bits of the ID) in a table of n slots.
 __device__ __forceinline__ void cuckoo_slots(uint32_t lo, uint32_t n, uint32_t s[3]) {
-#if OA_HASH == 1
     // two 32-bit multiplicative mixes; 16-bit fields scaled by 24-bit (full-rate) products
     const uint32_t a = lo ^ (lo >> 16);
     uint32_t h1 = a * 0x9E3779B1u, h2 = (a ^ 0x5BD1E995u) * 0x85EBCA6Bu;
@@ -261,15 +180,6 @@ __device__ __forceinline__ void cuckoo_slots(uint32_t lo, uint32_t n, uint32_t s
     s[0] = __umul24(h1 >> 16, n) >> 16;
     s[1] = __umul24(h1 & 0xFFFFu, n) >> 16;
     s[2] = __umul24(h2 >> 16, n) >> 16;
-    return;
-#endif
-    uint64_t x = ((uint64_t)lo + 0x632BE59BD9B4E019ull) * 0x9E3779B97F4A7C15ull;
-    x ^= x >> 29;
-    x *= 0xBF58476D1CE4E5B9ull;
-    x ^= x >> 32;
-    s[0] = (uint32_t)(((x & 0x1FFFFFull) * n) >> 21);
-    s[1] = (uint32_t)((((x >> 21) & 0x1FFFFFull) * n) >> 21);
-    s[2] = (uint32_t)((((x >> 42) & 0x1FFFFFull) * n) >> 21);
 }
 
 template <int IDB> struct IdT;
@@ -288,9 +198,7 @@ struct ItemHdr {
     uint32_t nonuniform, hi0, pad0, overflow;
     uint32_t nh, nseg, n_span, n_pv;
     uint32_t chunk_total, nsl, nstash, npend;
-    uint32_t ctr1, ctr2, pad1, pad2;    // trip counters of phases 1 and 2
-    int32_t item, h0, h1, next;         // k_stream: the item, its halos, the next item
-    int64_t scratch_off;
+    uint32_t ctr1, pad1, pad2, pad3;    // phase-1 trip counter
     uint64_t stash[STASH];          // cuckoo entries whose eviction chain ran out
     uint32_t lstart[HMAX + 1];      // local start of each item halo's current block
     uint32_t vstart[HMAX + 1];      // virtual start of each progenitor segment
@@ -524,14 +432,22 @@ __device__ __forceinline__ uint32_t frame_otf(const V3<TX> &x, const V3<TV> &v, 
 }
 
 // ------------------------------------------------------------------ step kernel
-// LDS image of one item (after the ItemHdr):
-//   slots[S]  u64  open-addressing table of the item's current particles that have a
-//                  progenitor: lo32(ID) | (angle16 | sign2 << 16 | (pos+1) << 18) << 32,
-//                  0 = empty.  pos = position in the item span.  One ds_read_b64 per
-//                  probe returns key, sign, angle and position; the angle is updated in
-//                  place.
-//   pend[E/4] u64 phase 1: the deferred-insert list
-//   phase 3 overlays slots[0 .. E/2) with a position-indexed u32 array of state words
+// LDS image of one item after the ItemHdr (two overlays of region A in time):
+//   phases 1-2a  slots[S] u64  3-way cuckoo table of the item's current particles that
+//                              have a progenitor block:
+//                              lo32(ID) | (sign2 << 16 | (pos+1) << 18) << 32, 0 = empty;
+//                pend[E/4] u64 phase 1's deferred inserts (walked before phase 2a)
+//   phases 2b-3  rc[3][E] TD   the item's current r̂ as three component arrays (SoA),
+//                              staged from the rows phase 1 wrote; after phase 2b reads
+//                              rc_x[c] of the matched particle c it overwrites that word
+//                              with c's new float16 angle
+//   always       sgn[E] u8     sign(v_r) of every current position (bits 0-1) and, from
+//                              phase 2a on, bit 2 = matched (the particle has its angle
+//                              in rc_x[c]); phase 3 turns it into the state word
+// The table side (phase 2a) and the r̂ side (phase 2b) of the join never need LDS at
+// the same time, so the current r̂ a previous particle pairs with is read from LDS, not
+// gathered from L2: a gathered 12-byte r̂ moves a whole L2 line to the CU, and those
+// lines were what bounded phase 2.
 constexpr uint32_t POS_BITS = 14, POS_SHIFT = 18, MAX_POS = (1u << POS_BITS) - 2;
 
 __device__ __forceinline__ uint64_t slot_pack(uint32_t lo, uint32_t meta, uint32_t pos) {
@@ -542,6 +458,16 @@ __device__ __forceinline__ uint32_t slot_pos(uint64_t v) {
 }
 __device__ __forceinline__ uint32_t slot_meta(uint64_t v) {
     return (uint32_t)(v >> 32) & ((1u << POS_SHIFT) - 1u);
+}
+
+// Region A: max(table + deferral list, three r̂ component arrays), 16-B aligned.
+__host__ __device__ inline int64_t region_a_bytes(int entries, int slots, int td_bytes) {
+    const int64_t t = table_bytes(entries, slots);
+    const int64_t r = ((int64_t)3 * td_bytes * entries + 15) & ~int64_t(15);
+    return t > r ? t : r;
+}
+__host__ __device__ inline int64_t step_lds_bytes(int entries, int slots, int td_bytes) {
+    return HDR_BYTES + region_a_bytes(entries, slots, td_bytes) + (((int64_t)entries + 15) & ~int64_t(15));
 }
 
 // ---- buffer resources --------------------------------------------------------------
@@ -564,8 +490,7 @@ __device__ void rbs_i32(int32_t, i32x4, int32_t, int32_t, int32_t) __asm("llvm.a
 __device__ void rbs_v3f32(f32x3, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.v3f32");
 __device__ void rbs_v2f64(f64x2, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.v2f64");
 __device__ void rbs_f64(double, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.f64");
-__device__ void rbs_i64(int64_t, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.i64");
-constexpr int AUX_NT = 2;      // nt: streamed-once inputs (keeps L2 for the r̂ gathers)
+constexpr int AUX_NT = 2;      // nt: streamed-once inputs and outputs
 
 // raw buffer resource (stride 0): 48-bit base, num_records in bytes, 32-bit data format
 __device__ __forceinline__ Rsrc make_rsrc(const void *p, uint32_t bytes) {
@@ -591,8 +516,8 @@ template <typename T, int AUX> __device__ __forceinline__ V3<T> bld3(Rsrc r, uin
         return V3<T>{v.x, v.y, w};
     }
 }
-__device__ __forceinline__ void bst32(Rsrc r, uint32_t o, uint32_t v) {
-    rbs_i32((int32_t)v, r, (int32_t)o, 0, 0);
+template <int AUX> __device__ __forceinline__ void bst32(Rsrc r, uint32_t o, uint32_t v) {
+    rbs_i32((int32_t)v, r, (int32_t)o, 0, AUX);
 }
 template <typename T> __device__ __forceinline__ void bst3(Rsrc r, uint32_t o, const T v[3]) {
     if constexpr (sizeof(T) == 4) {
@@ -611,32 +536,38 @@ __device__ __forceinline__ int64_t uni64(int64_t x) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-// Trip counters: trips are runs of 64 * UNR consecutive (virtual) positions.  Every
+// Trip counters of phase 1: trips are runs of 64 * UNR1 consecutive positions.  Every
 // wave starts on trips `wave` and `wave + NWAVE`; later trips come from an LDS counter
-// (a wave that gets ahead takes more, so all waves end a phase within about one trip
-// of each other).  The counter is read one trip ahead, so its LDS round trip overlaps
-// a trip's work.
+// (a wave that gets ahead takes more, so all waves end the phase within about one
+// trip of each other).  The counter is read one trip ahead, so its LDS round trip
+// overlaps a trip's work.
 __device__ __forceinline__ uint32_t trip_fetch(uint32_t *ctr, int lane) {
     uint32_t v = 0;
-    if (OA_DYN) {
-        if (lane == 0) v = atomicAdd(ctr, 1u);
-    }
+    if (lane == 0) v = atomicAdd(ctr, 1u);
     return v;
 }
-__device__ __forceinline__ uint32_t trip_take(uint32_t fetched, uint32_t t_prev) {
-    return OA_DYN ? __builtin_amdgcn_readfirstlane(fetched) : t_prev + NWAVE;
+__device__ __forceinline__ uint32_t trip_take(uint32_t fetched) {
+    return __builtin_amdgcn_readfirstlane(fetched);
 }
+
+// Phase-2 packed link of one previous particle (a register per row, phases 2a -> 2b):
+//   bits 0-13 current position c of the match, bit 14 matched, bit 15 apsis flag,
+//   bits 16-31 the previous float16 angle
+constexpr uint32_t PK_HIT = 1u << 14, PK_FLAG = 1u << 15;
 
 template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
 __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK fk) {
     typedef typename IdT<IDB>::T ID;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     ItemHdr &H = *reinterpret_cast<ItemHdr *>(smem);
-    const uint32_t nslots_max = (uint32_t)a.lds_slots;
+    const uint32_t nslots_max = (uint32_t)a.lds_slots, E = (uint32_t)a.lds_entries;
     uint64_t *slots = reinterpret_cast<uint64_t *>(smem + HDR_BYTES);
-    // phase 1: the list of deferred cuckoo inserts
-    uint64_t *pend = slots + nslots_max;
-    const uint32_t pend_cap = (uint32_t)a.lds_entries / 4u;
+    uint64_t *pend = slots + nslots_max;              // phase 1: deferred cuckoo inserts
+    const uint32_t pend_cap = E / 4u;
+    TD *rcx = reinterpret_cast<TD *>(smem + HDR_BYTES);   // phases 2b-3 (over the table)
+    TD *rcy = rcx + E, *rcz = rcy + E;
+    uint8_t *sgn8 = reinterpret_cast<uint8_t *>(
+        smem + HDR_BYTES + region_a_bytes((int)E, (int)nslots_max, (int)sizeof(TD)));
 
     const oa_item it = a.items[blockIdx.x];
     // the wave index is uniform: readfirstlane lets every trip / row quantity derived
@@ -648,8 +579,6 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     TD *rhat_out = reinterpret_cast<TD *>(a.rhat_out);
     const TD *rhat_prev = reinterpret_cast<const TD *>(a.rhat_prev);
     constexpr uint32_t SX = 3 * sizeof(TX), SV = 3 * sizeof(TV), SD = 3 * sizeof(TD);
-    // phase-2 unroll: float64 r̂ trips hold twice the registers (no spills)
-    constexpr int UNR = sizeof(TD) == 8 ? 1 : UNR2;
     STAMP(0);
 
     // ---- phase 0: stage the item's halo table in LDS -------------------------
@@ -659,7 +588,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         const oa_halo &h0 = a.halos[it.h0];
         H.lstart[tid] = (uint32_t)(h.cur_off - h0.cur_off);
         // joined halos: those with a non-empty progenitor block (an empty one matches
-        // nothing: its particles keep angle 0, written in phase 1)
+        // nothing: its particles keep angle 0)
         H.has_prev[tid] = COMPARE && h.prev_cnt > 0;
         H.halo_cnt[tid] = 0;
         for (int d = 0; d < 3; ++d) { H.cb[tid][d] = h.centre[d]; H.cb[tid][3 + d] = h.bulk[d]; }
@@ -673,35 +602,27 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     if (tid == 0) {
         H.nonuniform = 0; H.overflow = 0; H.nh = nh; H.chunk_total = 0; H.nstash = 0;
         H.npend = 0;
-        // static first trips: phase 1 wave, wave + NWAVE; phase 2 also wave + 2 NWAVE
-        H.ctr1 = 2 * NWAVE; H.ctr2 = 3 * NWAVE;
+        H.ctr1 = 2 * NWAVE;                 // phase 1: static first trips wave, wave + NWAVE
         // progenitor segments in halo order (serial: nh <= HMAX); each starts on a
         // 64-position row of the virtual (padded) progenitor space
-        uint32_t ns = 0, vp = 0;
+        uint32_t ns = 0, vp = 0, nj = 0;
         for (int k = 0; k < nh; ++k) {
             const oa_halo &h = a.halos[it.h0 + k];
             if (COMPARE && h.prev_cnt > 0) {
                 H.seg_halo[ns] = k; H.seg_prev_off[ns] = h.prev_off; H.vstart[ns] = vp;
                 H.seg_cnt[ns] = (uint32_t)h.prev_cnt;
                 vp += ((uint32_t)h.prev_cnt + 63u) & ~63u; ++ns;
+                nj += (uint32_t)h.cur_cnt;
             }
         }
         H.vstart[ns] = vp; H.nseg = ns; H.n_pv = vp;
-        // table size for this item: load factor <= 2 / OA_SLOT_X2
-        uint32_t nj = 0;
-        for (int k = 0; k < nh; ++k) {
-            const oa_halo &h = a.halos[it.h0 + k];
-            if (COMPARE && h.prev_cnt > 0) nj += (uint32_t)h.cur_cnt;
-        }
-        uint32_t ns_eff = nj * OA_SLOT_X2 / 2 + 64;
+        // table size for this item: load <= 1/2 where the LDS budget allows
+        const uint32_t ns_eff = 2 * nj + 64;
         H.nsl = ns_eff > nslots_max ? nslots_max : ns_eff;
         // reference high word for the 32-bit LDS keys: the item's first particle
-        // (OA_HIMM: phase 1 reduces the min / max high word of the inserted IDs
-        // instead, so phase 0 has no dependent load of ids[])
         const oa_halo &h0 = a.halos[it.h0], &hl1 = a.halos[it.h1 - 1];
-        H.hi0 = OA_HIMM ? 0xFFFFFFFFu : 0u;
-        H.pad0 = 0;
-        if (!OA_HIMM && IDB == 8 && hl1.cur_off + hl1.cur_cnt > h0.cur_off)
+        H.hi0 = 0u;
+        if (IDB == 8 && hl1.cur_off + hl1.cur_cnt > h0.cur_off)
             H.hi0 = (uint32_t)((uint64_t)ids[h0.cur_off] >> 32);
     }
     __syncthreads();
@@ -713,13 +634,12 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
 
     const int64_t base = uni64(H.cur_base);
     const uint32_t n_span = uni(H.n_span);
-    uint32_t hi0 = OA_HIMM ? 0u : uni(H.hi0);
-    uint32_t hmn = 0xFFFFFFFFu, hmx = 0u;           // OA_HIMM: this lane's high words
+    const uint32_t hi0 = uni(H.hi0);
     const uint32_t nhu = uni(H.nh);
     const Rsrc r_id = make_rsrc(ids + base, n_span * IDB);
     const Rsrc r_x = make_rsrc(reinterpret_cast<const TX *>(a.coords) + 3 * base, n_span * SX);
     const Rsrc r_v = make_rsrc(reinterpret_cast<const TV *>(a.vels) + 3 * base, n_span * SV);
-    const Rsrc r_rh = make_rsrc(rhat_out + 3 * base, n_span * SD);   // phase 1 stores, phase 2 gathers
+    const Rsrc r_rh = make_rsrc(rhat_out + 3 * base, n_span * SD);   // phase 1 stores, 2b stages
     const Rsrc r_mt = make_rsrc(a.meta_out + base, n_span * 4u);
     STAMP(1);
 
@@ -760,14 +680,9 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                 if (r0 + 63u >= H.lstart[hl + 1])
                     while (hl + 1 < nhu && li >= H.lstart[hl + 1]) ++hl;
             }
-            uint32_t lo, hi;
-            id_split<IDB>(idv[u], lo, hi);
             TD r[3];
             uint32_t sgn;
-            if (OA_ABL_FRAME) {
-                r[0] = (TD)xv[u].x - (TD)H.cb[hl][0]; r[1] = (TD)xv[u].y; r[2] = (TD)vv[u].z;
-                sgn = 1u;
-            } else if (!COMPARE && !OTF && a.vr_out) {
+            if (!COMPARE && !OTF && a.vr_out) {
                 double vr;
                 sgn = frame<TX, TV, TD>(xv[u], vv[u], H.cb[hl], H.cf[hl], a, fk, r, &vr);
                 if (ok) a.vr_out[base + li] = vr;
@@ -775,31 +690,27 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                 sgn = OTF ? frame_otf<TX, TV, TD>(xv[u], vv[u], H.cb[hl], a, fk, r)
                           : frame<TX, TV, TD>(xv[u], vv[u], H.cb[hl], H.cf[hl], a, fk, r);
             }
-            if (!OA_ABL_STORE1) bst3<TD>(r_rh, li * SD, r);
-            else asm volatile("" :: "v"(r[0]), "v"(r[1]), "v"(r[2]));
-            uint32_t ang = 0;
+            bst3<TD>(r_rh, li * SD, r);
             if constexpr (!COMPARE) {
+                uint32_t ang = 0;
                 if (a.angles_in && ok) ang = a.angles_in[base + li];
-            }
-            const uint32_t meta = ang | (sgn << 16);
-            if (OA_P2META && COMPARE) bst32(r_mt, li * 4u, meta);     // entered: final
-            if (!COMPARE || !H.has_prev[hl]) {
-                if (!(OA_P2META && COMPARE)) bst32(r_mt, li * 4u, meta);
+                bst32<AUX_NT>(r_mt, li * 4u, ang | (sgn << 16));
                 continue;
+            } else {
+                // every state word is written by phase 3, from this sign
+                if (ok) sgn8[li] = (uint8_t)sgn;
+                if (!ok || !H.has_prev[hl]) continue;
+                uint32_t lo, hi;
+                id_split<IDB>(idv[u], lo, hi);
+                if (IDB == 8 && hi != hi0) H.nonuniform = 1u;     // benign race: all write 1
+                val[u] = slot_pack(lo, sgn << 16, li);
+                uint32_t cs[3];
+                cuckoo_slots(lo, nslots, cs);
+                sl[u] = cs[0];
+                cs1[u] = cs[1];
+                cs2[u] = cs[2];
+                ins[u] = true;
             }
-            if (!ok) continue;
-            if (IDB == 8) {
-                if (OA_HIMM) { hmn = min(hmn, hi); hmx = max(hmx, hi); }
-                else if (hi != hi0) H.nonuniform = 1u;     // benign race: all write 1
-            }
-            val[u] = slot_pack(lo, meta, li);
-            uint32_t cs[3];
-            cuckoo_slots(lo, nslots, cs);
-            sl[u] = cs[0];
-            cs1[u] = cs[1];
-            cs2[u] = cs[2];
-            ins[u] = !OA_ABL_INSERT;
-            if (OA_ABL_INSERT) asm volatile("" :: "v"(val[u]), "v"(sl[u]));
         }
         if (COMPARE) {
             // first try: claim an EMPTY candidate with a CAS (at load <= 1/2 one of the
@@ -831,102 +742,66 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
 #pragma unroll
         for (int u = 0; u < UNR1; ++u) { idv[u] = idn[u]; xv[u] = xn[u]; vv[u] = vn[u]; }
         t1 = t1n;
-        t1n = trip_take(f1, t1n);
+        t1n = trip_take(f1);
     }
 #undef OA_LOAD1
-    if (OA_HIMM && IDB == 8 && COMPARE) {
-#pragma unroll
-        for (int o = 32; o; o >>= 1) {
-            hmn = min(hmn, (uint32_t)__shfl_xor((int)hmn, o));
-            hmx = max(hmx, (uint32_t)__shfl_xor((int)hmx, o));
-        }
-        if (lane == 0) { atomicMin(&H.hi0, hmn); atomicMax(&H.pad0, hmx); }
-    }
     WSTAMP(0);
     STAMP(2);
     if constexpr (!COMPARE) return;
 
-    // ---- phase 2: stream progenitor blocks, join, flag, angle, emit ---------
+    // ---- phase 2: the join, in two halves -------------------------------------
     // Rows are 64 virtual positions; progenitor segment s occupies
     // [vstart[s], vstart[s] + seg_cnt[s]) and starts on a row, so a row lies in one
-    // segment: its halo, block offset and resources are uniform.
+    // segment: its halo, block offset and resources are uniform.  Rows are dealt
+    // statically: wave w takes rows w, w + NWAVE, ... (<= KROWS of them, the host
+    // planner caps n_pv), and keeps each row's IDs and packed link in registers from
+    // phase 2a to phase 2b.
     const uint32_t n_pv = uni(H.n_pv), nseg = uni(H.nseg);
-    constexpr uint32_t T2 = 64 * UNR;                 // positions per wave trip
-    const uint32_t ntr2 = (n_pv + T2 - 1) / T2;
-    const uint64_t lanemask_lt = (1ull << lane) - 1ull;
-    uint32_t running = 0;
-    ID *scr_ids = reinterpret_cast<ID *>(a.scratch_ids);
-
-    // three register sets of streamed rows (ids, r̂, meta and the row's uniform
-    // segment data) and two of lookup results rotate through a 3-stage pipeline:
-    // trip t+2 loads, trip t+1 looks up and gathers, trip t computes and emits
-    struct Rows {
-        ID pid[UNR];
-        V3<TD> prh[UNR];
-        uint32_t pmeta[UNR], hlv[UNR], nv[UNR];
-        int64_t kb[UNR];
-    };
-    struct Look {
-        uint64_t hit[UNR];
-        uint32_t hs[UNR];
-        V3<TD> cr[UNR];
-    };
-    // segment 0 in SGPRs: single-segment items (one joined halo) never touch LDS for
-    // their row set-up
-    const uint32_t cnt0 = uni(H.seg_cnt[0]), hal0 = uni((uint32_t)H.seg_halo[0]);
-    const int64_t off0 = uni64(H.seg_prev_off[0]);
-    auto load_rows = [&](Rows &S, uint32_t T) __attribute__((always_inline)) {
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            const uint32_t r0 = T * T2 + u * 64;
-            uint32_t ro = r0, cnt = cnt0, hs = hal0;
-            int64_t off = off0;
-            if (nseg > 1) {
-                const uint32_t s = uni(upper_find(H.vstart, nseg, min(r0, n_pv - 1u)));
-                ro = r0 - uni(H.vstart[s]);
-                cnt = uni(H.seg_cnt[s]);
-                hs = uni((uint32_t)H.seg_halo[s]);
-                off = uni64(H.seg_prev_off[s]);
-            }
-            S.nv[u] = (r0 < n_pv && ro < cnt) ? min(cnt - ro, 64u) : 0u;
-            S.hlv[u] = hs;
-            S.kb[u] = off + ro;
-            S.pid[u] = bld<ID, AUX_NT>(make_rsrc(ids_prev + S.kb[u], S.nv[u] * IDB), lane * IDB);
-            S.prh[u] = bld3<TD, AUX_NT>(make_rsrc(rhat_prev + 3 * S.kb[u], S.nv[u] * SD), lane * SD);
-            S.pmeta[u] = bld<uint32_t, AUX_NT>(make_rsrc(a.meta_prev + S.kb[u], S.nv[u] * 4u), lane * 4u);
-        }
-    };
-    // An item none of whose halos has a progenitor block has nothing to join (the
-    // work-group-uniform exit keeps the prefetch below unconditional: a predicated
-    // one makes the compiler copy the loaded registers and wait on them here).
-    if (n_pv == 0) {
+    const uint32_t nrow = (n_pv + 63) / 64;
+    if (n_pv == 0) {                                 // nothing to join: state words only
+        __syncthreads();
+        for (uint32_t li = tid; li < n_span; li += WG)
+            bst32<AUX_NT>(r_mt, li * 4u, (uint32_t)(sgn8[li] & 3u) << 16);
         if (tid == 0) a.item_count[blockIdx.x] = 0;
         return;
     }
-    uint32_t touch = 0;
-    if (OA_TOUCH) {
-        // one dword per 128-B line of the r̂ block written in phase 1: the lines become
-        // most-recently-used in L2 while the walks run, so phase 2's gathers hit
-        const uint32_t nb = n_span * SD;
-        for (uint32_t o = (uint32_t)tid * 128u; o < nb; o += WG * 128u)
-            touch ^= bld<uint32_t, 0>(r_rh, o);
+    const uint32_t cnt0 = uni(H.seg_cnt[0]), hal0 = uni((uint32_t)H.seg_halo[0]);
+    const int64_t off0 = uni64(H.seg_prev_off[0]);
+    // a row's segment data: valid lanes nv, item-local halo hs, first previous index kb
+    auto row_of = [&](uint32_t r, uint32_t &nv, uint32_t &hs, int64_t &kb) __attribute__((always_inline)) {
+        const uint32_t r0 = r * 64u;
+        uint32_t ro = r0, cnt = cnt0;
+        hs = hal0;
+        int64_t off = off0;
+        if (nseg > 1) {
+            const uint32_t s = uni(upper_find(H.vstart, nseg, min(r0, n_pv - 1u)));
+            ro = r0 - uni(H.vstart[s]);
+            cnt = uni(H.seg_cnt[s]);
+            hs = uni((uint32_t)H.seg_halo[s]);
+            off = uni64(H.seg_prev_off[s]);
+        }
+        nv = (r < nrow && ro < cnt) ? min(cnt - ro, 64u) : 0u;
+        kb = off + ro;
+    };
+    // Every row's 2a loads (IDs, state words) go out before the walks and the barrier:
+    // up to 2 * KROWS loads in flight per wave hide the HBM latency behind them.
+    ID pid[KROWS];
+    uint32_t pk[KROWS];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < KROWS; ++k) {
+        uint32_t nv, hs;
+        int64_t kb;
+        row_of(wave + NWAVE * k, nv, hs, kb);
+        pid[k] = bld<ID, AUX_NT>(make_rsrc(ids_prev + kb, nv * IDB), lane * IDB);
+        pk[k] = bld<uint32_t, AUX_NT>(make_rsrc(a.meta_prev + kb, nv * 4u), lane * 4u);
     }
-    Rows SA, SB, SC;
-    Look LA, LB;
-    if (OA_PF2E) {
-        // both static trips' loads go out before the walks, so their HBM latency hides
-        // behind the walks and the barrier; a counted vmcnt retires only the phase-1
-        // stores (other waves gather them) and leaves the loads in flight
-        __builtin_amdgcn_sched_barrier(0);
-        load_rows(SA, (uint32_t)wave);
-        load_rows(SB, (uint32_t)(wave + NWAVE));
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(6 * UNR) : "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    if (!OA_IMMEDIATE_WALK) {
-        if (!OA_PF2E) __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+    // barrier without a vmcnt drain: the loads above stay in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    {
         const uint32_t np = min(H.npend, pend_cap);
         for (uint32_t e = tid; e < np; e += WG) {
             uint64_t v = pend[e];
@@ -949,689 +824,187 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
         }
     }
-    // The first trip's loads are issued BEFORE the phase-1/2 barrier.  The barrier
-    // then retires only this wave's older VMEM ops with a counted vmcnt that leaves
-    // the prefetch loads in flight, plus every LDS insert (lgkmcnt), then a raw
-    // s_barrier (a __syncthreads() would drain vmcnt to 0).
-    if (!OA_PF2E) {
-        __builtin_amdgcn_sched_barrier(0);
-        load_rows(SA, (uint32_t)wave);
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(3 * UNR) : "memory");
-    } else {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     STAMP(3);
-    if (H.overflow) {
-        if (tid == 0) atomicOr(a.status, OA_STATUS_TABLE_OVERFLOW);
+    if (H.overflow || nrow > (uint32_t)(KROWS * NWAVE)) {
+        if (tid == 0) atomicOr(a.status, H.overflow ? OA_STATUS_TABLE_OVERFLOW : OA_STATUS_PLAN);
         return;
     }
-    // OA_HIMM: an item without entries has min 0xFFFFFFFF > max 0 (uniform; every
-    // lookup misses on the empty slots' position check)
-    const bool nonuniform = IDB == 8 && (OA_HIMM ? uni(H.hi0) < uni(H.pad0) : uni(H.nonuniform) != 0);
-    if (OA_HIMM) hi0 = uni(H.hi0);
+    const bool nonuniform = IDB == 8 && uni(H.nonuniform) != 0;
     const uint32_t nstash = min(uni(H.nstash), (uint32_t)STASH);
-    // cuckoo lookup of (halo, id) for one trip of rows, then the gather of the matched
-    // current r̂ rows (written in phase 1: L2).  The three candidate slots are read
-    // together (one LDS round trip) and the match is selected without branches;
-    // departed particles miss (setdiff1d/in1d, :300-304).  The halo's position range
-    // tells copies of one ID in overlapping regions apart and rejects empty slots.
-    // The gather is unconditional (a miss re-reads row 0).
-    auto lookup = [&](const Rows &S, Look &L) __attribute__((always_inline)) {
+
+    // ---- phase 2a: cuckoo lookup of every previous particle -----------------
+    // Three candidate slots read together (one LDS round trip), the match selected
+    // without branches; departed particles miss (setdiff1d / in1d, :300-304).  The
+    // halo's position range tells copies of one ID in overlapping regions apart and
+    // rejects empty slots.  The strict sign test (:311-314) needs only the two sign
+    // fields, so the apsis flag is decided here.
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            uint32_t lo, hi;
-            id_split<IDB>(S.pid[u], lo, hi);
-            const bool can = ((uint32_t)lane < S.nv[u]) & (IDB != 8 || nonuniform || hi == hi0);
-            uint32_t lmin = 0, lmax = n_span;                 // the halo's position span
-            if (nhu > 1) {
-                lmin = uni(H.lstart[S.hlv[u]]);
-                lmax = uni(H.lstart[S.hlv[u] + 1]) - lmin;
-            }
-            uint32_t cs[3];
-            cuckoo_slots(lo, nslots, cs);
-            const uint64_t c0 = slots[cs[0]], c1 = slots[cs[1]], c2 = slots[cs[2]];
-            auto m = [&](uint64_t v) { return ((uint32_t)v == lo) & (slot_pos(v) - lmin < lmax); };
-            const bool m0 = can & m(c0), m1 = can & m(c1), m2 = can & m(c2);
-            if (IDB == 8 && nonuniform) {
-                // rare: candidates whose low word matches are confirmed on the full ID
-                L.hit[u] = 0ull; L.hs[u] = 0u;
-                if (m0 && ids[base + slot_pos(c0)] == S.pid[u]) { L.hit[u] = c0; L.hs[u] = cs[0]; }
-                else if (m1 && ids[base + slot_pos(c1)] == S.pid[u]) { L.hit[u] = c1; L.hs[u] = cs[1]; }
-                else if (m2 && ids[base + slot_pos(c2)] == S.pid[u]) { L.hit[u] = c2; L.hs[u] = cs[2]; }
-            } else {
-                L.hit[u] = m0 ? c0 : (m1 ? c1 : (m2 ? c2 : 0ull));
-                L.hs[u] = m0 ? cs[0] : (m1 ? cs[1] : cs[2]);
-            }
-            if (nstash) {
-                if (can && !L.hit[u]) {
-                    for (uint32_t e = 0; e < nstash; ++e) {
-                        const uint64_t v = H.stash[e];
-                        if (m(v) && (!(IDB == 8 && nonuniform) || ids[base + slot_pos(v)] == S.pid[u])) {
-                            L.hit[u] = v; L.hs[u] = nslots + e;
-                            break;
-                        }
-                    }
+    for (int k = 0; k < KROWS; ++k) {
+        const uint32_t r = wave + NWAVE * k;
+        uint32_t nv, hs;
+        int64_t kb;
+        row_of(r, nv, hs, kb);
+        const uint32_t pmeta = pk[k];
+        uint32_t lo, hi;
+        id_split<IDB>(pid[k], lo, hi);
+        const bool can = ((uint32_t)lane < nv) & (IDB != 8 || nonuniform || hi == hi0);
+        uint32_t lmin = 0, lmax = n_span;                 // the halo's position span
+        if (nhu > 1) {
+            lmin = uni(H.lstart[hs]);
+            lmax = uni(H.lstart[hs + 1]) - lmin;
+        }
+        uint32_t cs[3];
+        cuckoo_slots(lo, nslots, cs);
+        const uint64_t c0 = slots[cs[0]], c1 = slots[cs[1]], c2 = slots[cs[2]];
+        auto m = [&](uint64_t v) { return ((uint32_t)v == lo) & (slot_pos(v) - lmin < lmax); };
+        const bool m0 = can & m(c0), m1 = can & m(c1), m2 = can & m(c2);
+        uint64_t hit;
+        if (IDB == 8 && nonuniform) {
+            // rare: candidates whose low word matches are confirmed on the full ID
+            hit = 0ull;
+            if (m0 && ids[base + slot_pos(c0)] == pid[k]) hit = c0;
+            else if (m1 && ids[base + slot_pos(c1)] == pid[k]) hit = c1;
+            else if (m2 && ids[base + slot_pos(c2)] == pid[k]) hit = c2;
+        } else {
+            hit = m0 ? c0 : (m1 ? c1 : (m2 ? c2 : 0ull));
+        }
+        if (nstash && can && !hit) {
+            for (uint32_t e = 0; e < nstash; ++e) {
+                const uint64_t v = H.stash[e];
+                if (m(v) && (!(IDB == 8 && nonuniform) || ids[base + slot_pos(v)] == pid[k])) {
+                    hit = v;
+                    break;
                 }
             }
         }
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            const uint32_t p = (L.hit[u] && !OA_ABL_GATHER) ? slot_pos(L.hit[u]) : 0u;
-            L.cr[u] = bld3<TD, 0>(r_rh, p * SD);
-        }
-    };
-    // flag, angle and apsis records of one trip
-    auto compute = [&](const Rows &S, const Look &L, uint32_t t) __attribute__((always_inline)) {
-        bool flag[UNR];
-        uint16_t a16[UNR];
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            flag[u] = false;
-            a16[u] = 0xFFFFu;
-            if (!L.hit[u]) continue;
-            const uint32_t sc = slot_meta(L.hit[u]) >> 16, sp = S.pmeta[u] >> 16;
-            // strict sign test (:311-314): zeros and NaNs never flag
+        uint32_t p = 0;
+        if (hit) {
+            const uint32_t c = slot_pos(hit), sc = slot_meta(hit) >> 16, sp = pmeta >> 16;
             const bool cond = a.mode == OA_MODE_PERICENTRIC ? (sp == 2u && sc == 1u)
                                                             : (sp == 1u && sc == 2u);
+            p = c | PK_HIT | (cond ? PK_FLAG : 0u) | (pmeta << 16);
+            sgn8[c] = (uint8_t)(sc | 4u);
+        }
+        pk[k] = p;
+        if (OTF && r < nrow && (uint32_t)lane < nv) a.matched_prev[kb + lane] = hit ? 1 : 0;
+    }
+    WSTAMP(1);
+    STAMP(4);
+
+    // ---- phase 2b: angles from the current r̂ staged in LDS, apsis records ------
+    // The first PF2 rows' previous r̂ loads go out before the staging (HBM latency
+    // behind it); the barrier after phase 2a retires everything older with a counted
+    // vmcnt, so phase 1's r̂ stores are visible to the staging reads of other waves.
+    V3<TD> prh[KROWS];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < PF2 && k < KROWS; ++k) {
+        uint32_t nv, hs;
+        int64_t kb;
+        row_of(wave + NWAVE * k, nv, hs, kb);
+        prh[k] = bld3<TD, AUX_NT>(make_rsrc(rhat_prev + 3 * kb, nv * SD), lane * SD);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"((sizeof(TD) == 4 ? 1 : 2) * PF2) : "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    {
+        // the item's current r̂ rows, written by phase 1 (L2), as SoA into region A
+        constexpr int SU = 4;
+        for (uint32_t l0 = tid; l0 < n_span; l0 += SU * WG) {
+            V3<TD> v[SU];
+#pragma unroll
+            for (int u = 0; u < SU; ++u) v[u] = bld3<TD, 0>(r_rh, (l0 + u * WG) * SD);
+#pragma unroll
+            for (int u = 0; u < SU; ++u) {
+                const uint32_t li = l0 + u * WG;
+                if (li < n_span) { rcx[li] = v[u].x; rcy[li] = v[u].y; rcz[li] = v[u].z; }
+            }
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    STAMP(5);
+
+    const uint64_t lanemask_lt = (1ull << lane) - 1ull;
+    uint32_t running = 0;
+    ID *scr_ids = reinterpret_cast<ID *>(a.scratch_ids);
+    uint32_t *rcw = reinterpret_cast<uint32_t *>(rcx);        // new angles over rc_x
+    constexpr uint32_t RCW = sizeof(TD) / 4;
+#pragma unroll
+    for (int k = 0; k < KROWS; ++k) {
+        if (k + PF2 < KROWS) {
+            uint32_t nv, hs;
+            int64_t kb;
+            row_of(wave + NWAVE * (k + PF2), nv, hs, kb);
+            prh[k + PF2] = bld3<TD, AUX_NT>(make_rsrc(rhat_prev + 3 * kb, nv * SD), lane * SD);
+        }
+        const uint32_t r = wave + NWAVE * k;
+        if (r >= nrow) continue;
+        uint32_t nv, hs;
+        int64_t kb;
+        row_of(r, nv, hs, kb);
+        const uint32_t p = pk[k];
+        bool flag = false;
+        uint16_t a16 = 0;
+        if (p & PK_HIT) {
+            const uint32_t c = p & (PK_HIT - 1u);
             // angle change = arccos(dot(r̂_prev, r̂_match)), no clamp (:324-325)
-            const V3<TD> cr = OA_ABL_GATHER ? S.prh[u] : L.cr[u];
-            TD dt = dot3(S.prh[u].x, S.prh[u].y, S.prh[u].z, cr.x, cr.y, cr.z);
-            const TD change = OA_ABL_ACOS ? dt : acos_td(dt);
-            uint16_t acc = angle_add((uint16_t)(S.pmeta[u] & 0xFFFFu), change);
+            const TD dt = dot3(prh[k].x, prh[k].y, prh[k].z, rcx[c], rcy[c], rcz[c]);
+            const TD change = acos_td(dt);
+            // calc_angles (:342-349): f16 + change, rounded once; reset at an apsis
+            const uint16_t acc = angle_add((uint16_t)(p >> 16), change);
+            flag = (p & PK_FLAG) != 0u;
+            a16 = acc;
+            rcw[RCW * c] = flag ? 0u : (uint32_t)acc;
             if (OTF) {
                 // on-the-fly outputs (track_orbits_onthefly.py:145-174): the angle
                 // change of every matched particle, and which current ones matched
-                static_cast<TD *>(a.angle_out)[S.kb[u] + lane] = change;
-                a.matched_cur[base + slot_pos(L.hit[u])] = 1;
+                static_cast<TD *>(a.angle_out)[kb + lane] = change;
+                a.matched_cur[base + c] = 1;
             }
-            // calc_angles (:342-349): apsis angle emitted, then reset to 0
-            if (OA_P2META) {
-                // the joined particle's state word, in place over phase 1's
-                bst32(r_mt, slot_pos(L.hit[u]) * 4u, (cond ? 0u : (uint32_t)acc) | (sc << 16));
-            } else if (!OA_ABL_SLOTW) {
-                uint64_t *sp_ = L.hs[u] < nslots ? &slots[L.hs[u]] : &H.stash[L.hs[u] - nslots];
-                reinterpret_cast<uint16_t *>(sp_)[2] = cond ? (uint16_t)0 : acc;
-            }
-            flag[u] = cond;
-            a16[u] = acc;
-        }
-        if (OTF) {
-#pragma unroll
-            for (int u = 0; u < UNR; ++u)
-                if ((uint32_t)lane < S.nv[u]) a.matched_prev[S.kb[u] + lane] = L.hit[u] ? 1 : 0;
         }
         // apsis records in previous-block order (:315-316): wave ballot + prefix
         // popcount packs each 64-position row's records at its own scratch base;
         // k_gather_items orders the rows (no work-group barrier here)
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            const uint32_t r0 = t * T2 + u * 64;                // multiple of 64
-            if (r0 < n_pv) {
-                const uint64_t m = __ballot(flag[u]);
-                const uint32_t c = (uint32_t)__popcll(m);
-                const int64_t sb = it.scratch_off + r0;
-                if (flag[u] && !OA_ABL_EMIT) {
-                    const uint32_t q = (uint32_t)__popcll(m & lanemask_lt);
-                    if (OA_NTST) {
-                        __builtin_nontemporal_store(S.pid[u], &scr_ids[sb + q]);
-                        __builtin_nontemporal_store(a16[u], &a.scratch_ang[sb + q]);
-                    } else {
-                        scr_ids[sb + q] = S.pid[u];
-                        a.scratch_ang[sb + q] = a16[u];
-                    }
-                }
-                if (lane == 0) {
-                    a.seg_count[sb >> 6] = (uint8_t)c;
-                    if (c && !OA_ABL_EMIT) atomicAdd(&H.halo_cnt[S.hlv[u]], (int)c);
-                }
-                running += c;
-            }
+        const uint64_t mk = __ballot(flag);
+        const uint32_t cnt = (uint32_t)__popcll(mk);
+        const int64_t sb = it.scratch_off + (int64_t)r * 64;
+        if (flag) {
+            const uint32_t q = (uint32_t)__popcll(mk & lanemask_lt);
+            __builtin_nontemporal_store(pid[k], &scr_ids[sb + q]);
+            __builtin_nontemporal_store(a16, &a.scratch_ang[sb + q]);
         }
-    };
-    // pipeline: trips t (compute), t1 (lookup), t2 (loads); every wave starts with
-    // trips wave, wave + NWAVE, wave + 2 NWAVE, later ones come from the counter
-    uint32_t tc = wave, tl = wave + NWAVE, tp = wave + 2 * NWAVE;
-    if (!OA_PF2E) load_rows(SB, tl);
-    lookup(SA, LA);
-    auto stage = [&](Rows &S0, Look &L0, Rows &S1, Look &L1, Rows &S2) __attribute__((always_inline)) {
-        const uint32_t f = trip_fetch(&H.ctr2, lane);
-        __builtin_amdgcn_sched_barrier(0);
-        load_rows(S2, tp);            // out of range: zeros
-        __builtin_amdgcn_sched_barrier(0);
-        lookup(S1, L1);               // its rows were loaded a stage ago
-        compute(S0, L0, tc);           // its gathers were issued a stage ago
-        tc = tl; tl = tp; tp = trip_take(f, tp);
-    };
-    while (tc < ntr2) {
-        stage(SA, LA, SB, LB, SC);
-        if (tc >= ntr2) break;
-        stage(SB, LB, SC, LA, SA);
-        if (tc >= ntr2) break;
-        stage(SC, LA, SA, LB, SB);
-        if (tc >= ntr2) break;
-        stage(SA, LB, SB, LA, SC);
-        if (tc >= ntr2) break;
-        stage(SB, LA, SC, LB, SA);
-        if (tc >= ntr2) break;
-        stage(SC, LB, SA, LA, SB);
+        if (lane == 0) {
+            a.seg_count[sb >> 6] = (uint8_t)cnt;
+            if (cnt) atomicAdd(&H.halo_cnt[hs], (int)cnt);
+        }
+        running += cnt;
     }
-    WSTAMP(1);
-    if (OA_TOUCH) asm volatile("" :: "v"(touch));
+    WSTAMP(2);
     if (lane == 0) atomicAdd(&H.chunk_total, running);
-    STAMP(4);
+    STAMP(6);
     __syncthreads();
 
-    // ---- phase 3: state words of the joined particles, in position order ----------
-    // Every table entry's word goes to pm[pos], a position-indexed array that overlays
-    // the first ceil(n_span / 2) slots (4 B per position): those slots are read into
-    // registers first (<= P3R per thread), the others and the stash are read after
-    // the barrier (pm never reaches them), then pm is stored out coalesced.
-    if (!OA_P2META) {
-        uint32_t *pm = reinterpret_cast<uint32_t *>(slots);
-        const uint32_t nst = min(H.nstash, (uint32_t)STASH);
-        const uint32_t nlow = min((n_span + 1) / 2, nslots);
-        uint64_t keep[P3R];
-#pragma unroll
-        for (int r = 0; r < P3R; ++r) {
-            const uint32_t w = tid + r * WG;
-            keep[r] = w < nlow ? slots[w] : 0ull;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < P3R; ++r)
-            if (keep[r]) pm[slot_pos(keep[r])] = slot_meta(keep[r]);
-        for (uint32_t w = nlow + tid; w < nslots + nst; w += WG) {
-            const uint64_t v = w < nslots ? slots[w] : H.stash[w - nslots];
-            if (v) pm[slot_pos(v)] = slot_meta(v);
-        }
-        __syncthreads();
-        // halos without a progenitor block are not in the table: their words were
-        // stored in phase 1
-        for (uint32_t k = 0; k < (uint32_t)nh; ++k) {
-            if (!H.has_prev[k]) continue;
-            const uint32_t e = H.lstart[k + 1];
-            for (uint32_t li = H.lstart[k] + tid; li < e; li += WG)
-                if (!OA_ABL_PHASE3) {
-                    // not re-read by this launch: a streaming store leaves the L2 to
-                    // the r̂ lines phase 2 gathers
-                    if (OA_NTST) __builtin_nontemporal_store(pm[li], &a.meta_out[base + li]);
-                    else a.meta_out[base + li] = pm[li];
-                }
-        }
+    // ---- phase 3: every state word of the item, in position order ---------------
+    // matched: the new angle phase 2b left in rc_x; entered or in a halo without a
+    // progenitor block: angle 0 (calc_angles :348-349).  Nothing in this launch reads
+    // them again, so the stores are non-temporal.
+    for (uint32_t li = tid; li < n_span; li += WG) {
+        const uint32_t s = sgn8[li];
+        const uint32_t ang = (s & 4u) ? (rcw[RCW * li] & 0xFFFFu) : 0u;
+        bst32<AUX_NT>(r_mt, li * 4u, ang | ((s & 3u) << 16));
     }
     if (tid < nh) {
         const oa_halo &h = a.halos[it.h0 + tid];
         if (h.out_slot >= 0) a.halo_count[h.out_slot] = H.halo_cnt[tid];
     }
     if (tid == 0) a.item_count[blockIdx.x] = (int32_t)H.chunk_total;
-    STAMP(5);
-}
-
-// ------------------------------------------------------------------ persistent join
-// k_stream: the compare step as a persistent kernel.  n_wg work-groups (one per CU:
-// the LDS table) take packed items from a device counter.  For item k a work-group
-//   1. inserts the item's staged keys into its LDS table (the keys were written by
-//      the frame pass of the previous iteration: L2-resident),
-//   2. runs the join of item k (phase 2 of k_step) INTERLEAVED with the frame of the
-//      next item k1 -- every wave alternates a join trip (LDS lookups, r̂ gathers:
-//      memory-pipeline bound) with a frame trip (float math: VALU bound), so the two
-//      overlap instead of running as separate phases,
-//   3. writes item k's state words (phase 3 of k_step).
-// The frame pass stores r̂ and the non-joined particles' state words as k_step does,
-// and for joined particles the 8-byte table entry into the work-group's staging ring
-// (two item slots).  The first item's frame runs alone (prologue).
-
-// Phase 0 of one item: its halo table into header Hd.  The caller synchronises.
-template <int IDB>
-__device__ __forceinline__ void stage_item(ItemHdr &Hd, const oa_step_args &a, int32_t item,
-                                           int tid) {
-    const oa_item it = a.items[item];
-    const int nh = it.h1 - it.h0;
-    if (tid < nh) {
-        const oa_halo &h = a.halos[it.h0 + tid];
-        const oa_halo &h0 = a.halos[it.h0];
-        Hd.lstart[tid] = (uint32_t)(h.cur_off - h0.cur_off);
-        Hd.has_prev[tid] = h.prev_cnt > 0;
-        Hd.halo_cnt[tid] = 0;
-        for (int d = 0; d < 3; ++d) { Hd.cb[tid][d] = h.centre[d]; Hd.cb[tid][3 + d] = h.bulk[d]; }
-        for (int d = 0; d < 3; ++d) { Hd.cf[tid][d] = (float)h.centre[d]; Hd.cf[tid][3 + d] = (float)h.bulk[d]; }
-        if (tid == nh - 1) {
-            Hd.lstart[nh] = (uint32_t)(h.cur_off + h.cur_cnt - h0.cur_off);
-            Hd.n_span = Hd.lstart[nh];
-            Hd.cur_base = h0.cur_off;
-        }
-    }
-    if (tid == 0) {
-        Hd.item = item; Hd.h0 = it.h0; Hd.h1 = it.h1; Hd.scratch_off = it.scratch_off;
-        Hd.nonuniform = 0; Hd.overflow = 0; Hd.nh = nh; Hd.chunk_total = 0; Hd.nstash = 0;
-        Hd.npend = 0;
-        Hd.ctr1 = NWAVE; Hd.ctr2 = 2 * NWAVE;   // static first trips (frame 1, join 2)
-        uint32_t ns = 0, vp = 0, nj = 0;
-        for (int k = 0; k < nh; ++k) {
-            const oa_halo &h = a.halos[it.h0 + k];
-            if (h.prev_cnt > 0) {
-                nj += (uint32_t)h.cur_cnt;
-                Hd.seg_halo[ns] = k; Hd.seg_prev_off[ns] = h.prev_off; Hd.vstart[ns] = vp;
-                Hd.seg_cnt[ns] = (uint32_t)h.prev_cnt;
-                vp += ((uint32_t)h.prev_cnt + 63u) & ~63u; ++ns;
-            }
-        }
-        Hd.vstart[ns] = vp; Hd.nseg = ns; Hd.n_pv = vp;
-        const uint32_t ns_eff = nj * OA_SLOT_X2 / 2 + 64;
-        Hd.nsl = ns_eff > (uint32_t)a.lds_slots ? (uint32_t)a.lds_slots : ns_eff;
-        const oa_halo &h0 = a.halos[it.h0], &hl1 = a.halos[it.h1 - 1];
-        Hd.hi0 = 0;
-        if (IDB == 8 && hl1.cur_off + hl1.cur_cnt > h0.cur_off)
-            Hd.hi0 = (uint32_t)(static_cast<const uint64_t *>(a.ids)[h0.cur_off] >> 32);
-    }
-}
-
-template <typename TX, typename TV, typename TD, int IDB, bool OTF>
-__global__ __launch_bounds__(WG) void k_stream(const oa_step_args a, const FrameK fk) {
-    typedef typename IdT<IDB>::T ID;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    ItemHdr *HH = reinterpret_cast<ItemHdr *>(smem);          // two headers
-    const uint32_t nslots_max = (uint32_t)a.lds_slots;
-    uint64_t *slots = reinterpret_cast<uint64_t *>(smem + 2 * HDR_BYTES);
-    uint64_t *pend = slots + nslots_max;
-    const uint32_t pend_cap = (uint32_t)a.lds_entries / 4u;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const ID *ids = reinterpret_cast<const ID *>(a.ids);
-    const ID *ids_prev = reinterpret_cast<const ID *>(a.ids_prev);
-    TD *rhat_out = reinterpret_cast<TD *>(a.rhat_out);
-    const TD *rhat_prev = reinterpret_cast<const TD *>(a.rhat_prev);
-    constexpr uint32_t SX = 3 * sizeof(TX), SV = 3 * sizeof(TV), SD = 3 * sizeof(TD);
-    constexpr int UNR = OA_UJ;                 // join rows per interleaved step
-    constexpr int UF = 1;                      // frame rows per interleaved step
-    constexpr uint32_t T1 = 64 * UF, T2 = 64 * UNR;
-    const uint64_t lanemask_lt = (1ull << lane) - 1ull;
-    ID *scr_ids = reinterpret_cast<ID *>(a.scratch_ids);
-    char *stage_wg = static_cast<char *>(a.stage) + (int64_t)blockIdx.x * 2 * a.lds_entries * 8;
-
-    // ---- frame of one trip of an item's current rows (header Hd, staging slot sl):
-    // r̂ and the non-joined state words to global memory, joined particles' table
-    // entries to the staging ring
-    // uniform scalars of the item whose frame runs (base, span, halos, ID high word)
-    struct FItem { int64_t b; uint32_t ns, nh, hi0; };
-    auto fitem = [&](const ItemHdr &Hd) __attribute__((always_inline)) {
-        return FItem{uni64(Hd.cur_base), uni(Hd.n_span), uni(Hd.nh), uni(Hd.hi0)};
-    };
-    auto frame_loads = [&](const FItem &F, uint32_t T, ID (&idv)[UF], V3<TX> (&xv)[UF],
-                           V3<TV> (&vv)[UF]) __attribute__((always_inline)) {
-        const int64_t b = F.b;
-        const uint32_t ns = F.ns;
-        const Rsrc r_id = make_rsrc(ids + b, ns * IDB);
-        const Rsrc r_x = make_rsrc(reinterpret_cast<const TX *>(a.coords) + 3 * b, ns * SX);
-        const Rsrc r_v = make_rsrc(reinterpret_cast<const TV *>(a.vels) + 3 * b, ns * SV);
-#pragma unroll
-        for (int u = 0; u < UF; ++u) {
-            const uint32_t li = T * T1 + u * 64 + lane;
-            idv[u] = bld<ID, AUX_NT>(r_id, li * IDB);
-            xv[u] = bld3<TX, AUX_NT>(r_x, li * SX);
-            vv[u] = bld3<TV, AUX_NT>(r_v, li * SV);
-        }
-    };
-    auto frame_rows = [&](ItemHdr &Hd, const FItem &F, uint32_t sl, uint32_t T, const ID (&idv)[UF],
-                          const V3<TX> (&xv)[UF], const V3<TV> (&vv)[UF]) __attribute__((always_inline)) {
-        const int64_t b = F.b;
-        const uint32_t ns = F.ns, nhu = F.nh, h0w = F.hi0;
-        const Rsrc r_rh = make_rsrc(rhat_out + 3 * b, ns * SD);
-        const Rsrc r_mt = make_rsrc(a.meta_out + b, ns * 4u);
-        const Rsrc r_st = make_rsrc(stage_wg + (int64_t)sl * a.lds_entries * 8, ns * 8u);
-#pragma unroll
-        for (int u = 0; u < UF; ++u) {
-            const uint32_t r0 = T * T1 + u * 64;
-            if (r0 >= ns) continue;
-            const uint32_t li = r0 + lane;
-            uint32_t hl = 0;
-            if (nhu > 1) {
-                hl = uni(upper_find(Hd.lstart, nhu, r0));
-                if (r0 + 63u >= Hd.lstart[hl + 1])
-                    while (hl + 1 < nhu && li >= Hd.lstart[hl + 1]) ++hl;
-            }
-            uint32_t lo, hi;
-            id_split<IDB>(idv[u], lo, hi);
-            TD r[3];
-            const uint32_t sgn = OTF ? frame_otf<TX, TV, TD>(xv[u], vv[u], Hd.cb[hl], a, fk, r)
-                                     : frame<TX, TV, TD>(xv[u], vv[u], Hd.cb[hl], Hd.cf[hl], a, fk, r);
-            bst3<TD>(r_rh, li * SD, r);
-            const uint32_t meta = sgn << 16;              // angle 0 (calc_angles :348-349)
-            uint64_t e = 0;
-            if (Hd.has_prev[hl]) {
-                e = slot_pack(lo, meta, li);
-                if (IDB == 8 && hi != h0w && li < ns) Hd.nonuniform = 1u;
-            } else {
-                bst32(r_mt, li * 4u, meta);
-            }
-            rbs_i64((int64_t)e, r_st, (int32_t)(li * 8u), 0, 0);
-        }
-    };
-
-    // ---- first item --------------------------------------------------------------
-    if (tid == 0) HH[0].next = (int32_t)atomicAdd(a.work, 1u);
-    __syncthreads();
-    int32_t item = HH[0].next;
-    if (item >= a.n_items) return;
-    stage_item<IDB>(HH[0], a, item, tid);
-    __syncthreads();
-    {   // prologue frame pass (all waves), trips from HH[0].ctr1
-        ItemHdr &Hd = HH[0];
-        const FItem F = fitem(Hd);
-        const uint32_t ntr = (F.ns + T1 - 1) / T1;
-        ID idv[UF]; V3<TX> xv[UF]; V3<TV> vv[UF];
-        uint32_t t = wave, tn = wave + NWAVE;
-        uint32_t f = trip_fetch(&Hd.ctr1, lane);
-        while (t < ntr) {
-            frame_loads(F, t, idv, xv, vv);
-            frame_rows(Hd, F, 0, t, idv, xv, vv);
-            t = tn;
-            tn = trip_take(f, tn);
-            f = trip_fetch(&Hd.ctr1, lane);
-        }
-    }
-    uint32_t cur = 0;
-    for (;;) {
-        ItemHdr &H = HH[cur];
-        ItemHdr &H1 = HH[cur ^ 1];
-        STAMPI(H.item, 0);
-        // ---- clear the table, insert the item's staged keys ------------------------
-        __syncthreads();            // previous item's phase 3 done with the table; frame
-                                    // pass stores (staging, r̂) complete
-        const uint32_t nslots = uni(H.nsl);
-        for (uint32_t w = tid; w < nslots; w += WG) slots[w] = 0ull;
-        if (tid == 0) H.next = (int32_t)atomicAdd(a.work, 1u);
-        __syncthreads();
-        const int32_t item1 = H.next;
-        const bool more = item1 < a.n_items;
-        const int64_t base = uni64(H.cur_base);
-        const uint32_t n_span = uni(H.n_span), hi0 = uni(H.hi0), nhu = uni(H.nh);
-        {
-            const Rsrc r_st = make_rsrc(stage_wg + (int64_t)cur * a.lds_entries * 8, n_span * 8u);
-            constexpr int UI = 4;
-            for (uint32_t l0 = 0; l0 < n_span; l0 += UI * WG) {
-                uint64_t val[UI];
-#pragma unroll
-                for (int u = 0; u < UI; ++u)
-                    val[u] = bld<uint64_t, 0>(r_st, (l0 + u * WG + tid) * 8u);   // beyond: 0
-                uint32_t sl[UI], cs1[UI], cs2[UI];
-                uint64_t c0[UI], c1[UI], c2[UI];
-#pragma unroll
-                for (int u = 0; u < UI; ++u) {
-                    uint32_t cs[3];
-                    cuckoo_slots((uint32_t)val[u], nslots, cs);
-                    sl[u] = cs[0]; cs1[u] = cs[1]; cs2[u] = cs[2];
-                    if (val[u]) { c0[u] = slots[sl[u]]; c1[u] = slots[cs1[u]]; c2[u] = slots[cs2[u]]; }
-                }
-#pragma unroll
-                for (int u = 0; u < UI; ++u) {
-                    if (!val[u]) continue;
-                    const uint32_t t = c0[u] == 0ull ? sl[u] : (c1[u] == 0ull ? cs1[u]
-                                                              : (c2[u] == 0ull ? cs2[u] : 0xFFFFFFFFu));
-                    bool placed = false;
-                    if (t != 0xFFFFFFFFu)
-                        placed = atomicCAS(reinterpret_cast<unsigned long long *>(&slots[t]), 0ull,
-                                           (unsigned long long)val[u]) == 0ull;
-                    if (!placed) {
-                        const uint32_t e = atomicAdd(&H.npend, 1u);
-                        if (e < pend_cap) pend[e] = val[u];
-                        else H.overflow = 2u;
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        STAMPI(H.item, 1);
-        // ---- deferred cuckoo walks; the next item's header ----------------------------
-        {
-            const uint32_t np = min(H.npend, pend_cap);
-            for (uint32_t e = tid; e < np; e += WG) {
-                uint64_t v = pend[e];
-                uint32_t cs[3];
-                cuckoo_slots((uint32_t)v, nslots, cs);
-                uint32_t t = cs[0];
-                for (int it_ = 0;; ++it_) {
-                    const uint64_t old = atomicExch(reinterpret_cast<unsigned long long *>(&slots[t]),
-                                                    (unsigned long long)v);
-                    if (old == 0ull) break;
-                    if (it_ == MAX_EVICT) {
-                        const uint32_t k = atomicAdd(&H.nstash, 1u);
-                        if (k < (uint32_t)STASH) H.stash[k] = old;
-                        else H.overflow = 2u;
-                        break;
-                    }
-                    cuckoo_slots((uint32_t)old, nslots, cs);
-                    t = cs[cs[0] == t ? 1 : (cs[1] == t ? 2 : 0)];
-                    v = old;
-                }
-            }
-        }
-        if (more) stage_item<IDB>(H1, a, item1, tid);
-
-        // ---- join of this item interleaved with the frame of the next -----------------
-        const uint32_t n_pv = uni(H.n_pv), nseg = uni(H.nseg);
-        const uint32_t ntr2 = (n_pv + T2 - 1) / T2;
-        const uint32_t cnt0 = uni(H.seg_cnt[0]), hal0 = uni((uint32_t)H.seg_halo[0]);
-        const int64_t off0 = uni64(H.seg_prev_off[0]);
-        const Rsrc r_rh = make_rsrc(rhat_out + 3 * base, n_span * SD);
-        struct Rows {
-            ID pid[UNR];
-            V3<TD> prh[UNR];
-            uint32_t pmeta[UNR], hlv[UNR], nv[UNR];
-            int64_t kb[UNR];
-        };
-        auto load_rows = [&](Rows &S, uint32_t T) __attribute__((always_inline)) {
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                const uint32_t r0 = T * T2 + u * 64;
-                uint32_t ro = r0, cnt = cnt0, hs = hal0;
-                int64_t off = off0;
-                if (nseg > 1) {
-                    const uint32_t s = uni(upper_find(H.vstart, nseg, min(r0, n_pv - 1u)));
-                    ro = r0 - uni(H.vstart[s]);
-                    cnt = uni(H.seg_cnt[s]);
-                    hs = uni((uint32_t)H.seg_halo[s]);
-                    off = uni64(H.seg_prev_off[s]);
-                }
-                S.nv[u] = (r0 < n_pv && ro < cnt) ? min(cnt - ro, 64u) : 0u;
-                S.hlv[u] = hs;
-                S.kb[u] = off + ro;
-                S.pid[u] = bld<ID, AUX_NT>(make_rsrc(ids_prev + S.kb[u], S.nv[u] * IDB), lane * IDB);
-                S.prh[u] = bld3<TD, AUX_NT>(make_rsrc(rhat_prev + 3 * S.kb[u], S.nv[u] * SD), lane * SD);
-                S.pmeta[u] = bld<uint32_t, AUX_NT>(make_rsrc(a.meta_prev + S.kb[u], S.nv[u] * 4u), lane * 4u);
-            }
-        };
-        Rows SA, SB;
-        __builtin_amdgcn_sched_barrier(0);
-        load_rows(SA, (uint32_t)wave);
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(3 * UNR) : "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        STAMPI(H.item, 2);
-        if (H.overflow) {       // host re-plans with smaller items (work-group uniform)
-            if (tid == 0) atomicOr(a.status, OA_STATUS_TABLE_OVERFLOW);
-            return;
-        }
-        const bool nonuniform = IDB == 8 && uni(H.nonuniform) != 0;
-        const uint32_t nstash = min(uni(H.nstash), (uint32_t)STASH);
-        const FItem F1 = more ? fitem(H1) : FItem{0, 0u, 1u, 0u};
-        const uint32_t ntrf = (F1.ns + T1 - 1) / T1;
-        uint32_t running = 0;
-        struct FRows { ID id[UF]; V3<TX> x[UF]; V3<TV> v[UF]; };
-        FRows FA, FB;
-        // frame trips: wave, wave + NWAVE static, then the counter (one fetched ahead)
-        uint32_t tf = wave, tfn = wave + NWAVE, ff = 0;
-        if (more) {
-            ff = trip_fetch(&H1.ctr1, lane);
-            frame_loads(F1, tf, FA.id, FA.x, FA.v);
-        }
-        uint32_t t2 = wave, t2n = wave + NWAVE;
-        uint32_t f2 = trip_fetch(&H.ctr2, lane);
-        auto step = [&](Rows &S, Rows &Sn, FRows &FC, FRows &FN) __attribute__((always_inline)) {
-            const bool dof = tf < ntrf, doj = t2 < ntr2;
-            if (tfn < ntrf) frame_loads(F1, tfn, FN.id, FN.x, FN.v);     // next frame trip
-            uint64_t hit[UNR];
-            uint32_t hs[UNR];
-            V3<TD> cr[UNR];
-            if (doj) {
-#pragma unroll
-                for (int u = 0; u < UNR; ++u) {
-                    uint32_t lo, hi;
-                    id_split<IDB>(S.pid[u], lo, hi);
-                    const bool can = ((uint32_t)lane < S.nv[u]) & (IDB != 8 || nonuniform || hi == hi0);
-                    uint32_t lmin = 0, lmax = n_span;
-                    if (nhu > 1) {
-                        lmin = uni(H.lstart[S.hlv[u]]);
-                        lmax = uni(H.lstart[S.hlv[u] + 1]) - lmin;
-                    }
-                    uint32_t cs[3];
-                    cuckoo_slots(lo, nslots, cs);
-                    const uint64_t c0 = slots[cs[0]], c1 = slots[cs[1]], c2 = slots[cs[2]];
-                    auto m = [&](uint64_t v) { return ((uint32_t)v == lo) & (slot_pos(v) - lmin < lmax); };
-                    const bool m0 = can & m(c0), m1 = can & m(c1), m2 = can & m(c2);
-                    if (IDB == 8 && nonuniform) {
-                        hit[u] = 0ull; hs[u] = 0u;
-                        if (m0 && ids[base + slot_pos(c0)] == S.pid[u]) { hit[u] = c0; hs[u] = cs[0]; }
-                        else if (m1 && ids[base + slot_pos(c1)] == S.pid[u]) { hit[u] = c1; hs[u] = cs[1]; }
-                        else if (m2 && ids[base + slot_pos(c2)] == S.pid[u]) { hit[u] = c2; hs[u] = cs[2]; }
-                    } else {
-                        hit[u] = m0 ? c0 : (m1 ? c1 : (m2 ? c2 : 0ull));
-                        hs[u] = m0 ? cs[0] : (m1 ? cs[1] : cs[2]);
-                    }
-                    if (nstash) {
-                        if (can && !hit[u]) {
-                            for (uint32_t e = 0; e < nstash; ++e) {
-                                const uint64_t v = H.stash[e];
-                                if (m(v) && (!(IDB == 8 && nonuniform) || ids[base + slot_pos(v)] == S.pid[u])) {
-                                    hit[u] = v; hs[u] = nslots + e;
-                                    break;
-                                }
-                            }
-                        }
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < UNR; ++u) {
-                    const uint32_t p = hit[u] ? slot_pos(hit[u]) : 0u;
-                    cr[u] = bld3<TD, 0>(r_rh, p * SD);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                load_rows(Sn, t2n);                     // out of range: zeros
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            // the next item's frame rows while this trip's gathers are in flight
-            if (dof) {
-                frame_rows(H1, F1, cur ^ 1, tf, FC.id, FC.x, FC.v);
-                tf = tfn;
-                tfn = trip_take(ff, tfn);
-                ff = trip_fetch(&H1.ctr1, lane);
-            }
-            if (doj) {
-                bool flag[UNR];
-                uint16_t a16[UNR];
-#pragma unroll
-                for (int u = 0; u < UNR; ++u) {
-                    flag[u] = false;
-                    a16[u] = 0xFFFFu;
-                    if (!hit[u]) continue;
-                    const uint32_t sc = slot_meta(hit[u]) >> 16, sp = S.pmeta[u] >> 16;
-                    // strict sign test (:311-314): zeros and NaNs never flag
-                    const bool cond = a.mode == OA_MODE_PERICENTRIC ? (sp == 2u && sc == 1u)
-                                                                    : (sp == 1u && sc == 2u);
-                    // angle change = arccos(dot(r̂_prev, r̂_match)), no clamp (:324-325)
-                    TD dt = dot3(S.prh[u].x, S.prh[u].y, S.prh[u].z, cr[u].x, cr[u].y, cr[u].z);
-                    const TD change = acos_td(dt);
-                    const uint16_t acc = angle_add((uint16_t)(S.pmeta[u] & 0xFFFFu), change);
-                    if (OTF) {
-                        static_cast<TD *>(a.angle_out)[S.kb[u] + lane] = change;
-                        a.matched_cur[base + slot_pos(hit[u])] = 1;
-                    }
-                    // calc_angles (:342-349): apsis angle emitted, then reset to 0
-                    uint64_t *sp_ = hs[u] < nslots ? &slots[hs[u]] : &H.stash[hs[u] - nslots];
-                    reinterpret_cast<uint16_t *>(sp_)[2] = cond ? (uint16_t)0 : acc;
-                    flag[u] = cond;
-                    a16[u] = acc;
-                }
-                if (OTF) {
-#pragma unroll
-                    for (int u = 0; u < UNR; ++u)
-                        if ((uint32_t)lane < S.nv[u]) a.matched_prev[S.kb[u] + lane] = hit[u] ? 1 : 0;
-                }
-                // apsis records in previous-block order (:315-316)
-#pragma unroll
-                for (int u = 0; u < UNR; ++u) {
-                    const uint32_t r0 = t2 * T2 + u * 64;
-                    if (r0 < n_pv) {
-                        const uint64_t mk = __ballot(flag[u]);
-                        const uint32_t c = (uint32_t)__popcll(mk);
-                        const int64_t sb = H.scratch_off + r0;
-                        if (flag[u]) {
-                            const uint32_t q = (uint32_t)__popcll(mk & lanemask_lt);
-                            scr_ids[sb + q] = S.pid[u];
-                            a.scratch_ang[sb + q] = a16[u];
-                        }
-                        if (lane == 0) {
-                            a.seg_count[sb >> 6] = (uint8_t)c;
-                            if (c) atomicAdd(&H.halo_cnt[S.hlv[u]], (int)c);
-                        }
-                        running += c;
-                    }
-                }
-                t2 = t2n;
-                t2n = trip_take(f2, t2n);
-                f2 = trip_fetch(&H.ctr2, lane);
-            }
-        };
-        while (t2 < ntr2 || tf < ntrf) {
-            step(SA, SB, FA, FB);
-            if (!(t2 < ntr2 || tf < ntrf)) break;
-            step(SB, SA, FB, FA);
-        }
-        if (lane == 0) atomicAdd(&H.chunk_total, running);
-        STAMPI(H.item, 3);
-        __syncthreads();
-        STAMPI(H.item, 4);
-
-        // ---- phase 3: this item's state words, in position order ---------------------
-        {
-            uint32_t *pm = reinterpret_cast<uint32_t *>(slots);
-            const uint32_t nst = min(H.nstash, (uint32_t)STASH);
-            const uint32_t nlow = min((n_span + 1) / 2, nslots);
-            uint64_t keep[P3R];
-#pragma unroll
-            for (int r = 0; r < P3R; ++r) {
-                const uint32_t w = tid + r * WG;
-                keep[r] = w < nlow ? slots[w] : 0ull;
-            }
-            __syncthreads();
-#pragma unroll
-            for (int r = 0; r < P3R; ++r)
-                if (keep[r]) pm[slot_pos(keep[r])] = slot_meta(keep[r]);
-            for (uint32_t w = nlow + tid; w < nslots + nst; w += WG) {
-                const uint64_t v = w < nslots ? slots[w] : H.stash[w - nslots];
-                if (v) pm[slot_pos(v)] = slot_meta(v);
-            }
-            __syncthreads();
-            const int nh = (int)nhu;
-            for (uint32_t k = 0; k < (uint32_t)nh; ++k) {
-                if (!H.has_prev[k]) continue;
-                const uint32_t e = H.lstart[k + 1];
-                for (uint32_t li = H.lstart[k] + tid; li < e; li += WG) a.meta_out[base + li] = pm[li];
-            }
-            if (tid < nh) {
-                const oa_halo &h = a.halos[H.h0 + tid];
-                if (h.out_slot >= 0) a.halo_count[h.out_slot] = H.halo_cnt[tid];
-            }
-            if (tid == 0) a.item_count[H.item] = (int32_t)H.chunk_total;
-        }
-        STAMPI(H.item, 5);
-        if (!more) break;
-        cur ^= 1;
-    }
+    STAMP(7);
 }
 
 // ------------------------------------------------------------------ compaction
@@ -1851,19 +1224,10 @@ int cu_count() {
 
 template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
 int launch_step_c(const oa_step_args &a, hipStream_t st) {
-    if (COMPARE && a.n_items > 0 && a.stage) {
-        // persistent join: one work-group per CU (the LDS table), items from a.work
-        const int64_t lds = 2 * HDR_BYTES + table_bytes(a.lds_entries, a.lds_slots);
-        auto k = k_stream<TX, TV, TD, IDB, OTF>;
-        if (int rc = set_lds(k, lds)) return rc;
-        int nwg = a.n_wg > 0 ? a.n_wg : cu_count();
-        if (nwg > a.n_items) nwg = a.n_items;
-        hipLaunchKernelGGL(k, dim3(nwg), dim3(WG), (size_t)lds, st, a, make_frame_k(a));
-        if (int rc = check_launch("k_stream")) return rc;
-        return launch_big<TX, TV, TD, IDB, COMPARE, OTF>(a, st);
-    }
     if (a.n_items > 0) {
-        int64_t lds = HDR_BYTES + table_bytes(a.lds_entries, a.lds_slots);
+        // a frame-only launch needs no table: several work-groups share a CU
+        const int64_t lds = COMPARE ? step_lds_bytes(a.lds_entries, a.lds_slots, (int)sizeof(TD))
+                                    : HDR_BYTES;
         auto k = k_step<TX, TV, TD, IDB, COMPARE, OTF>;
         if (int rc = set_lds(k, lds)) return rc;
         hipLaunchKernelGGL(k, dim3(a.n_items), dim3(WG), (size_t)lds, st, a, make_frame_k(a));
@@ -2144,7 +1508,7 @@ int32_t oa_build_info(int32_t which) {
         case 0: return WG;
         case 1: return HMAX;
         case 2: return UNR1;
-        case 3: return UNR2;
+        case 3: return KROWS;
         default: return -1;
     }
 }
@@ -2161,11 +1525,54 @@ int64_t oa_struct_size(int32_t which) {
 
 const char *oa_last_error(void) { return g_err; }
 
-int64_t oa_step_lds_bytes(int32_t entries, int32_t slots) {
-    return 2 * HDR_BYTES + table_bytes(entries, slots);     // k_stream: two item headers
+int64_t oa_step_lds_bytes(int32_t entries, int32_t slots, int32_t dx_f64) {
+    return step_lds_bytes(entries, slots, dx_f64 ? 8 : 4);
 }
 
-int32_t oa_device_units(void) { return cu_count(); }
+// Host-side item plan: greedy packing of consecutive halos, O(n_halos).
+int64_t oa_plan_items(const int64_t *cur_cnt, const int64_t *prev_cnt, const int64_t *out_slot,
+                      int64_t n_halos, int64_t entries, int64_t hmax, int64_t max_pv,
+                      oa_item *items, int64_t cap, int64_t *n_small, int64_t *scratch) {
+    g_err[0] = 0;
+    if (n_halos < 0 || entries < 0 || hmax < 1 || max_pv < 0 || !n_small || !scratch ||
+        (n_halos > 0 && (!cur_cnt || !prev_cnt || !items)))
+        return fail(OA_E_ARG, "oa_plan_items: bad arguments");
+    if (n_halos > INT32_MAX) return fail(OA_E_ARG, "oa_plan_items: more than 2^31 halos");
+    auto pv = [&](int64_t j) { const int64_t p = prev_cnt[j] > 0 ? prev_cnt[j] : 0; return (p + 63) / 64 * 64; };
+    auto big = [&](int64_t j) { return cur_cnt[j] > entries || pv(j) > max_pv; };
+    auto slot0 = [&](int64_t h0, int64_t h1) -> int32_t {
+        if (out_slot)
+            for (int64_t j = h0; j < h1; ++j)
+                if (out_slot[j] >= 0) return (int32_t)out_slot[j];
+        return -1;
+    };
+    int64_t n = 0, sc = 0, ng = 0;
+    for (int64_t j = 0; j < n_halos;) {                 // packed items
+        if (cur_cnt[j] < 0) return fail(OA_E_ARG, "oa_plan_items: negative block size");
+        if (big(j)) { ++j; ++ng; continue; }
+        const int64_t h0 = j;
+        int64_t tot = 0, ptot = 0;
+        while (j < n_halos && j - h0 < hmax && !big(j) && tot + cur_cnt[j] <= entries &&
+               ptot + pv(j) <= max_pv) {
+            tot += cur_cnt[j];
+            ptot += pv(j);
+            ++j;
+        }
+        if (n >= cap) return fail(OA_E_ARG, "oa_plan_items: more than cap items");
+        items[n] = oa_item{(int32_t)h0, (int32_t)j, slot0(h0, j), 1, sc, ptot};
+        sc += ptot;                                    // one 64-slot segment per row
+        ++n;
+    }
+    *n_small = n;
+    if (n + ng > cap) return fail(OA_E_ARG, "oa_plan_items: more than cap items");
+    for (int64_t j = 0; j < n_halos; ++j) {             // global (large-halo) items
+        if (!big(j)) continue;
+        items[n++] = oa_item{(int32_t)j, (int32_t)(j + 1), slot0(j, j + 1), 1, sc, pv(j)};
+        sc += pv(j);
+    }
+    *scratch = sc;
+    return n;
+}
 
 // Diagnostic builds (-DOA_STAMPS=1): copy the per-work-group phase stamps of the last
 // oa_step launch (s_memrealtime, 100 MHz) to host memory; returns count or -1.
@@ -2201,7 +1608,6 @@ int oa_step(const oa_step_args *args, void *stream) {
     if (a.mode != OA_MODE_PERICENTRIC && a.mode != OA_MODE_APOCENTRIC)
         return fail(OA_E_ARG, "bad mode");
     if (a.n_items > 0 && (a.lds_entries <= 0 || a.lds_entries > (int)MAX_POS + 1 ||
-                          a.lds_entries > 2 * P3R * WG ||
                           a.lds_slots <= a.lds_entries))
         return fail(OA_E_ARG, "bad lds_entries/lds_slots (entries <= %u < slots)", MAX_POS + 1);
     if (a.n_items + a.n_global_items > 0 &&
@@ -2213,8 +1619,6 @@ int oa_step(const oa_step_args *args, void *stream) {
         return fail(OA_E_ARG, "null previous-state / scratch pointer");
     if (a.onthefly && a.compare && (!a.angle_out || !a.matched_prev || !a.matched_cur))
         return fail(OA_E_ARG, "null on-the-fly output pointer");
-    if (a.compare && a.stage && !a.work)
-        return fail(OA_E_ARG, "persistent join: null work counter");
     if (a.n_gchunk1 > 0 && (!a.gchunk1 || !a.gtab || (a.compare && !a.gkeys)))
         return fail(OA_E_ARG, "null large-halo table pointer");
     if (a.compare && a.n_gchunk2 > 0 && !a.gchunk2)

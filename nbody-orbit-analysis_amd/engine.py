@@ -12,6 +12,7 @@ Host work per snapshot is O(n_halos) table building (no per-particle Python).
 Reference behaviour mirrored: track_orbits.py:104-240 (per-snapshot body),
 :247-290 (frame), :293-327 (compare), :330-351 (angles), :199-227 (assembly).
 """
+import ctypes
 import math
 import os
 from dataclasses import dataclass, field
@@ -23,8 +24,13 @@ import torch
 from . import _native as N
 
 F32, F64 = np.dtype(np.float32), np.dtype(np.float64)
-DEFAULT_ENTRIES = 12288        # current particles per work-group item (2 B/entry insert list)
-DEFAULT_SLOTS = 16128          # 8-byte LDS cuckoo slots per item (126 KB); + two 4 KB headers
+# LDS table sizes per work-group item, by r̂ dtype.  One item's LDS is
+# the header + max(8-byte cuckoo slots + 2 B/entry insert list, 3 r̂ components per
+# entry) + 1 B/entry of signs, within the CU's 160 KB:
+#   float32 r̂: 11776 entries, 15456 slots (load <= 0.76)   -> 163,072 B
+#   float64 r̂:  6144 entries, 12288 slots (load <= 0.5)    -> 157,696 B
+DEFAULT_ENTRIES = {False: 11776, True: 6144}
+DEFAULT_SLOTS = {False: 15456, True: 12288}
 
 _TORCH_FROM_NP = {
     np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
@@ -128,66 +134,62 @@ def plan_dtypes(snapshot, centre, bulk_cat, H, z):
 GCHUNK = 4096                  # particles per work-group chunk of a large halo
 
 
-def plan_items(cur_cnt, prev_cnt, entries, hmax=128):
-    """Work-group items of one snapshot.
+def plan_items(cur_cnt, prev_cnt, entries, hmax=128, out_slot=None, max_pv=None):
+    """Work-group items of one snapshot, planned by the library's host
+    function ``oa_plan_items`` (O(n_halos) C++; no per-halo Python).
 
     Consecutive halos whose current blocks fit one LDS table (<= ``entries``
-    particles, <= ``hmax`` halos) are packed greedily into *items* (k_step).  A halo
-    larger than that becomes a *global* item: joined through its own table in global
-    memory by as many work-groups as it has chunks (k_big_frame / k_big_join).
+    particles, <= ``hmax`` halos, <= ``max_pv`` padded progenitor positions) are
+    packed greedily into *items* (k_step).  A halo beyond those limits becomes a
+    *global* item: joined through its own table in global memory by as many
+    work-groups as it has chunks (k_big_frame / k_big_join).
 
-    Returns (items, global_items, scratch): ITEM_DTYPE arrays and the apsis-scratch
-    size (64-slot segments per item, global items after the packed ones).  An item's
-    ``n_pv`` counts its progenitor rows of 64 virtual positions: every progenitor block
-    is padded to whole rows, so a row of k_step's phase 2 lies in one block."""
-    nh = len(cur_cnt)
-    small, glob = [], []
-    scratch = 0
-    j = 0
-    pc = np.maximum(prev_cnt, 0)
-    while j < nh:
-        if cur_cnt[j] > entries:
-            glob.append((j, j + 1, 0, 1, 0, (pc[j] + 63) // 64 * 64))
-            j += 1
-            continue
-        start, tot, ptot = j, 0, 0
-        while j < nh and j - start < hmax and tot + cur_cnt[j] <= entries:
-            tot += cur_cnt[j]
-            ptot += (pc[j] + 63) // 64 * 64      # each progenitor block starts a 64-row
-            j += 1
-        small.append((start, j, 0, 1, scratch, ptot))
-        scratch += ptot                          # one 64-slot scratch segment per row
-    for k, g in enumerate(glob):
-        glob[k] = g[:4] + (scratch, g[5])
-        scratch += g[5]
-    it = np.array(small, dtype=N.ITEM_DTYPE) if small else np.zeros(0, N.ITEM_DTYPE)
-    gt = np.array(glob, dtype=N.ITEM_DTYPE) if glob else np.zeros(0, N.ITEM_DTYPE)
-    return it, gt, scratch
+    Returns (items, global_items, scratch): ITEM_DTYPE arrays (``slot0`` set from
+    ``out_slot`` when given) and the apsis-scratch size (one 64-slot segment per
+    progenitor row, global items after the packed ones).  An item's ``n_pv`` counts
+    its progenitor rows of 64 virtual positions: every progenitor block is padded to
+    whole rows, so a row of k_step's phase 2 lies in one block."""
+    lib = N.load()
+    cur = np.ascontiguousarray(cur_cnt, dtype=np.int64)
+    prev = np.ascontiguousarray(prev_cnt, dtype=np.int64)
+    nh = len(cur)
+    osl = None if out_slot is None else np.ascontiguousarray(out_slot, dtype=np.int64)
+    if max_pv is None:
+        max_pv = lib.oa_build_info(3) * lib.oa_build_info(0)
+    out = np.zeros(max(nh, 1), dtype=N.ITEM_DTYPE)
+    n_small, scratch = ctypes.c_int64(0), ctypes.c_int64(0)
+    n = lib.oa_plan_items(cur.ctypes.data, prev.ctypes.data,
+                          None if osl is None else osl.ctypes.data, nh, int(entries),
+                          int(hmax), int(max_pv), out.ctypes.data, len(out),
+                          ctypes.byref(n_small), ctypes.byref(scratch))
+    if n < 0:
+        raise ValueError(lib.oa_last_error().decode())
+    k = n_small.value
+    return out[:k].copy(), out[k:n].copy(), int(scratch.value)
 
 
 def plan_global(glob, cur_cnt, prev_cnt, first_index, compare):
-    """Chunk lists and table layout of the global items (k_big_frame / k_big_join)."""
-    ch1, ch2, tab = [], [], []
-    off = 0
-    for k, g in enumerate(glob):
-        gi = first_index + k
-        h = int(g['h0'])
-        n = int(cur_cnt[h])
-        for st in range(0, n, GCHUNK):
-            ch1.append((gi, st, min(GCHUNK, n - st)))
-        # linear probing at load <= 0.5 (the kernels range-reduce the hash onto any
-        # capacity; a 0.7 load, small enough for the Infinity Cache, measured slower:
-        # 2.26 vs 1.65 ms for configs[1])
-        cap = 64
-        while cap < 2 * n:
-            cap <<= 1
-        tab.append((off, cap))
-        off += cap
-        m = int(max(prev_cnt[h], 0)) if compare else 0
-        for st in range(0, m, GCHUNK):
-            ch2.append((gi, st, min(GCHUNK, m - st)))
-    as3 = lambda x: np.array(x, dtype=np.int64).reshape(-1, 3)          # noqa: E731
-    return as3(ch1), as3(ch2), np.array(tab, dtype=np.int64).reshape(-1, 2), off
+    """Chunk lists and table layout of the global items (k_big_frame / k_big_join),
+    vectorised: (item, start, count) chunks of GCHUNK particles of every large halo's
+    current block (and, when comparing, of its previous block), and one linear-probing
+    table per halo with a power-of-two capacity >= 2 n (load <= 0.5; a 0.7 load, small
+    enough for the Infinity Cache, measured slower: 2.26 vs 1.65 ms for configs[1])."""
+    h = np.asarray(glob['h0'], dtype=np.int64)
+    gi = first_index + np.arange(len(h), dtype=np.int64)
+
+    def chunks(n):
+        k = (n + GCHUNK - 1) // GCHUNK
+        rep = np.repeat(np.arange(len(n)), k)
+        st = (np.arange(k.sum()) - np.repeat(np.cumsum(k) - k, k)) * GCHUNK
+        return np.stack([gi[rep], st, np.minimum(GCHUNK, n[rep] - st)], axis=1).astype(np.int64)
+
+    n1 = np.asarray(cur_cnt, dtype=np.int64)[h]
+    n2 = np.maximum(np.asarray(prev_cnt, dtype=np.int64)[h], 0) if compare else np.zeros_like(n1)
+    two_n = np.maximum(2 * n1, 1)
+    cap = np.maximum(64, np.left_shift(1, np.ceil(np.log2(two_n)).astype(np.int64)))
+    cap = np.where(cap < two_n, cap * 2, cap)            # guard float rounding
+    tab = np.stack([np.cumsum(cap) - cap, cap], axis=1).astype(np.int64).reshape(-1, 2)
+    return chunks(n1).reshape(-1, 3), chunks(n2).reshape(-1, 3), tab, int(cap.sum())
 
 
 def set_item_slots(items, out_slot):
@@ -203,6 +205,15 @@ def set_item_slots(items, out_slot):
     nxt[:nh] = np.minimum.accumulate(idx[::-1])[::-1]
     first = nxt[items['h0']]
     items['slot0'] = np.where(first < items['h1'], np.asarray(out_slot)[np.minimum(first, nh - 1)], -1)
+
+
+def check_angles_in(angles_in, n):
+    """Checkpoint angles restored on resume must cover the snapshot exactly: the
+    kernels read one per particle, and the reference fails on the mismatch too
+    (track_orbits.py:229-232 -> calc_angles :342)."""
+    if angles_in is not None and len(angles_in) != n:
+        raise ValueError('checkpoint angles have %d entries for a snapshot of %d particles'
+                         % (len(angles_in), n))
 
 
 def to_device(x, device, dtype=None):
@@ -265,6 +276,7 @@ class PreparedStep:
     scratch: int
     compare: bool
     n_prev: int = 0
+    entries: int = 0               # per-item particle budget the plan used
     halos: Optional[torch.Tensor] = None
     d_items: Optional[torch.Tensor] = None
     glob: dict = field(default_factory=dict)       # device chunk lists / tables
@@ -283,18 +295,17 @@ class PreparedStep:
 
 
 class Workspace:
-    """Reusable scratch for compare steps (sized for the largest step it serves).
+    """Scratch of compare steps, kept by the engine and grown on demand (capacities are
+    high-water marks, so a steady stream of snapshots allocates nothing)."""
 
-    ``stage`` is the persistent join's staging ring (k_stream: two item slots of
-    ``entries`` 8-byte table entries per work-group) and ``work`` its item counter."""
+    FIELDS = ('scratch', 'n_prev', 'n_slots', 'n_items')
 
-    def __init__(self, device, id_torch_dtype, scratch, n_prev, n_slots, n_items,
-                 entries=None, n_wg=0):
+    def __init__(self, device, id_torch_dtype, scratch, n_prev, n_slots, n_items):
         def e(n, dt):
             return torch.empty(max(int(n), 1), dtype=dt, device=device)
-        self.n_wg = int(n_wg)
-        self.stage = e(self.n_wg * 2 * int(entries), torch.int64) if self.n_wg and entries else None
-        self.work = e(2, torch.int32)
+        self.device, self.id_dtype = device, id_torch_dtype
+        self.cap = dict(scratch=int(scratch), n_prev=int(n_prev), n_slots=int(n_slots),
+                        n_items=int(n_items))
         self.scratch_ids = e(scratch, id_torch_dtype)
         self.scratch_ang = e(scratch, torch.int16)
         self.seg_count = e(scratch // 64 + 1, torch.uint8)
@@ -307,16 +318,23 @@ class Workspace:
         self.total = e(1, torch.int64)
         self.status.zero_()
 
+    @staticmethod
+    def need(pr):
+        return dict(scratch=pr.scratch, n_prev=pr.n_prev, n_slots=int(pr.has_prog.sum()),
+                    n_items=len(pr.items))
+
     @classmethod
-    def for_step(cls, pr, device, entries=None, n_wg=0):
+    def for_step(cls, pr, device):
         dt = torch.int64 if pr.plan.ids.itemsize == 8 else torch.int32
-        return cls(device, dt, pr.scratch, pr.n_prev, int(pr.has_prog.sum()), len(pr.items),
-                   entries, n_wg)
+        return cls(device, dt, **cls.need(pr))
+
+    def fits(self, pr):
+        dt = torch.int64 if pr.plan.ids.itemsize == 8 else torch.int32
+        return dt == self.id_dtype and all(self.cap[k] >= v for k, v in self.need(pr).items())
 
     def reset(self, n_slots):
         """Per-launch zeroing (the status word accumulates: callers clear it)."""
         self.halo_count[:max(n_slots, 1)].zero_()
-        self.work.zero_()
 
 
 class OrbitEngine:
@@ -331,23 +349,42 @@ class OrbitEngine:
         self.device = torch.device(device if device is not None else 'cuda')
         self.mode = mode
         env = os.environ.get
-        # defaults fill one CU's 160 KB LDS: 8 B per cuckoo slot + 2 B
-        # per entry; halos larger than `entries` take the global-table path
-        self.entries = int(lds_entries or env('ORBIT_LDS_ENTRIES', DEFAULT_ENTRIES))
-        self.slots = int(lds_slots or env('ORBIT_LDS_SLOTS', 0) or
-                         max(DEFAULT_SLOTS, self.entries + 1))
+        # LDS table sizes: one item fills one CU's 160 KB; the defaults
+        # depend on the r̂ dtype, an explicit value applies to both
+        self.entries_cfg = int(lds_entries or env('ORBIT_LDS_ENTRIES', 0)) or None
+        self.slots_cfg = int(lds_slots or env('ORBIT_LDS_SLOTS', 0)) or None
         self.hmax = min(int(hmax or env('ORBIT_HMAX', 1 << 30)), self.lib.oa_build_info(1))
-        # experimental persistent join (k_stream, one work-group per CU) with
-        # ORBIT_PERSISTENT=1; the default launches one work-group per item (k_step),
-        # measured faster (2.11 vs 2.43-2.52 ms per 1e8-particle step)
-        self.n_wg = int(self.lib.oa_device_units()) if env('ORBIT_PERSISTENT', '0') == '1' else 0
-        max_lds = self.lib.oa_max_lds_bytes()
-        need = self.lib.oa_step_lds_bytes(self.entries, self.slots)   # k_stream: 2 headers
-        if not self.n_wg:
-            need -= self.lib.oa_step_lds_bytes(0, 0) // 2                  # k_step: one
-        if need > max_lds:
-            raise ValueError('LDS table needs %d bytes > device limit %d' % (need, max_lds))
+        self.max_pv = self.lib.oa_build_info(3) * self.lib.oa_build_info(0)
+        self.max_lds = self.lib.oa_max_lds_bytes()
+        for f64 in (False, True):
+            self.table_sizes(f64)                   # validates the LDS budget
         self.prev: Optional[SnapshotState] = None
+        self._ws: Optional[Workspace] = None
+
+    def table_sizes(self, dx_f64, entries=None):
+        """(entries, slots) of one k_step item for a float32 / float64 r̂."""
+        e = int(entries or self.entries_cfg or DEFAULT_ENTRIES[bool(dx_f64)])
+        s = int(self.slots_cfg or max(DEFAULT_SLOTS[bool(dx_f64)], e + 1))
+        need = self.lib.oa_step_lds_bytes(e, s, int(bool(dx_f64)))
+        if need > self.max_lds:
+            raise ValueError('LDS table (%d entries, %d slots, %s r̂) needs %d bytes > device '
+                             'limit %d' % (e, s, 'float64' if dx_f64 else 'float32', need,
+                                           self.max_lds))
+        return e, s
+
+    @property
+    def entries(self):
+        return self.table_sizes(False)[0]
+
+    def workspace(self, pr):
+        """The engine's compare-step workspace, grown to fit ``pr``."""
+        if self._ws is None or not self._ws.fits(pr):
+            old = self._ws.cap if self._ws is not None else {}
+            need = Workspace.need(pr)
+            cap = {k: max(need[k], old.get(k, 0)) for k in need}
+            dt = torch.int64 if pr.plan.ids.itemsize == 8 else torch.int32
+            self._ws = Workspace(self.device, dt, **cap)
+        return self._ws
 
     def reset(self):
         self.prev = None
@@ -381,10 +418,8 @@ class OrbitEngine:
             halos['prev_off'][has_prog] = p_starts[p[has_prog]]
             halos['prev_cnt'][has_prog] = p_counts[p[has_prog]]
             halos['out_slot'][has_prog] = np.arange(int(has_prog.sum()))
-        items, glob, scratch = plan_items(counts, halos['prev_cnt'], entries or self.entries,
-                                          self.hmax)
-        set_item_slots(items, halos['out_slot'])
-        set_item_slots(glob, halos['out_slot'])
+        items, glob, scratch = plan_items(counts, halos['prev_cnt'], entries, self.hmax,
+                                          out_slot=halos['out_slot'], max_pv=self.max_pv)
         return halos, items, glob, scratch, starts, counts, has_prog
 
     # ------------------------------------------------------------------ step
@@ -400,21 +435,26 @@ class OrbitEngine:
         if is_array(snapshot['masses']):
             snap['masses'] = to_device(snapshot['masses'], dev)
         entries = None
-        for _ in range(8):
+        for attempt in range(10):
             prep = self.prepare(snap, centres, bulk_cat, H, z, exists, compare,
                                 angles_in=angles_in, plan_src=snapshot,
                                 entries=entries)
-            ws = Workspace.for_step(prep, dev, self.entries, self.n_wg)
-            ws.status.zero_()
+            ws = self.workspace(prep) if compare else None
+            if ws is not None:
+                ws.status.zero_()
             res = self.launch(prep, ws)
+            # one small read-back per snapshot (the driver fetches the results anyway)
             st = int(ws.status.item()) if compare else 0
             if not st:
                 break
-            if st & N.STATUS_TABLE_OVERFLOW:
-                # cuckoo stash full: smaller items (larger halos move to the global path)
-                entries = max(256, (entries or self.entries) // 2)
+            if st & N.STATUS_PLAN:
+                raise RuntimeError('oa_step: an item exceeds the kernel limits (planner bug)')
+            # cuckoo stash full: smaller items; at the floor every halo takes the
+            # global-table path, which keys on the full 64-bit ID
+            e = prep.entries
+            entries = 0 if e <= 256 else max(256, e // 2)
         else:
-            raise RuntimeError('LDS hash tables kept overflowing (adversarial IDs?)')
+            raise RuntimeError('LDS hash tables kept overflowing')
         self.prev = SnapshotState(ids=snap['ids'], rhat=prep.rhat, meta=prep.meta,
                                   starts=prep.starts,
                                   counts=prep.counts, exists=exists, plan=prep.plan)
@@ -425,7 +465,9 @@ class OrbitEngine:
         """Host half of a step: dtype plan, halo/item tables, device uploads.
 
         ``snap`` holds device tensors for ids/coordinates/velocities(/masses);
-        ``prev_layout`` (starts, counts, exists, plan) defaults to the engine state."""
+        ``prev_layout`` (starts, counts, exists, plan) defaults to the engine state.
+        ``entries`` overrides the per-item particle budget of the plan (0: every halo
+        on the global-table path)."""
         dev = self.device
         exists = np.asarray(exists)
         plan = plan_dtypes(plan_src if plan_src is not None else snap,
@@ -444,12 +486,17 @@ class OrbitEngine:
         n = snap['ids'].numel()
         if snap['coordinates'].numel() != 3 * n or snap['velocities'].numel() != 3 * n:
             raise ValueError('coordinates/velocities must be (N, 3) with N = len(ids)')
+        if not compare:
+            check_angles_in(angles_in, n)
+        lds_e, lds_s = self.table_sizes(plan.dx == F64)
+        plan_e = lds_e if entries is None else min(int(entries), lds_e)
         halos, items, glob, scratch, starts, counts, has_prog = self.build_tables(
-            snap, centres, bulk_cat, exists, compare, prev_layout, entries)
+            snap, centres, bulk_cat, exists, compare, prev_layout, plan_e)
         all_items = np.concatenate([items, glob])
         pr = PreparedStep(plan=plan, n=n, starts=starts, counts=counts, has_prog=has_prog,
                           items=all_items, n_small=len(items), scratch=scratch,
-                          compare=bool(compare), n_prev=prev_layout[4] if compare else 0)
+                          compare=bool(compare), n_prev=prev_layout[4] if compare else 0,
+                          entries=plan_e)
         pr.halos = torch.from_numpy(halos.view(np.uint8)).to(dev)
         pr.d_items = torch.from_numpy(all_items.view(np.uint8)).to(dev)
         if len(glob):
@@ -494,7 +541,7 @@ class OrbitEngine:
         a.id_bytes = plan.ids.itemsize
         a.mode = N.MODE[self.mode]
         a.compare = int(bool(compare))
-        a.lds_entries, a.lds_slots = self.entries, self.slots
+        a.lds_entries, a.lds_slots = lds_e, lds_s
         return pr
 
     def launch(self, pr, ws, prev=None, stream=None, step_events=None):
@@ -520,9 +567,6 @@ class OrbitEngine:
             a.seg_count = ws.seg_count.data_ptr()
             a.halo_count, a.item_count, a.status = (ws.halo_count.data_ptr(),
                                                    ws.item_count.data_ptr(), ws.status.data_ptr())
-            use_p = ws.stage is not None and ws.stage.numel() >= ws.n_wg * 2 * a.lds_entries
-            a.stage = ws.stage.data_ptr() if use_p else None
-            a.work, a.n_wg = ws.work.data_ptr(), ws.n_wg
         if step_events is not None:
             step_events[0].record()
         N.check(lib.oa_step(a, st), 'oa_step')

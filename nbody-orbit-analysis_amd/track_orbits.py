@@ -100,14 +100,23 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
                 print('Savefile initialized\n')
 
         compare = i > istart
-        angles_in = out.read_checkpoint() if (resume and not compare) else None
+        angles_in = None
+        if resume and not compare:
+            # the reference opens savefile + '.checkpoint' here (track_orbits.py:229-232)
+            angles_in = out.read_checkpoint()
+            if angles_in is None:
+                raise FileNotFoundError('resume: no checkpoint angles in the savefile '
+                                        '(run with checkpoint=True first)')
+        # apsis IDs are the previous snapshot's IDs (ids_prev_[apsis_inds], :315-316):
+        # they keep that snapshot's dtype
+        ids_dtype_prev = eng.prev.plan.ids if compare else None
 
         if verbose:
             t0 = time.time()
         res = eng.step(snapshot, region_positions, region_bulk_vels, H, snapshot['redshift'],
                        halo_exists, compare, angles_in=angles_in)
         if compare:
-            apsis_offsets, apsis_ids, apsis_angles = eng.fetch(res, eng.prev.plan.ids)
+            apsis_offsets, apsis_ids, apsis_angles = eng.fetch(res, ids_dtype_prev)
         if verbose:
             print('Finished pericenter detection for snapshot {} in {} s\n'.format(
                 '%03d' % snapshot_number, time.time() - t0))

@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from . import _native as N
-from .engine import OrbitEngine, SnapshotState, Workspace, to_device, F64, np_dtype
+from .engine import OrbitEngine, SnapshotState, to_device, F64, np_dtype
 
 _TORCH = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64}
 
@@ -143,7 +143,7 @@ class OnTheFly:
                 raise NotImplementedError('coordinate dtype differs between the two snapshots')
         n_prev = prev.ids.numel()
         entries = None
-        for _ in range(8):
+        for _ in range(10):
             pc = self._prepare(cur, slices[0], centres[0], True, prev=prev, entries=entries)
             coord = _TORCH[np.dtype(pc.plan.coord)]
             angle_out = torch.empty(max(n_prev, 1), dtype=coord, device=eng.device)
@@ -153,16 +153,18 @@ class OnTheFly:
             a.angle_out, a.matched_prev, a.matched_cur = (angle_out.data_ptr(),
                                                           matched_prev.data_ptr(),
                                                           matched_cur.data_ptr())
-            ws = Workspace.for_step(pc, eng.device, eng.entries, eng.n_wg)
+            ws = eng.workspace(pc)
             ws.status.zero_()
             res = eng.launch(pc, ws, prev=prev)
             st = int(ws.status.item())
             if not st:
                 break
-            if st & N.STATUS_TABLE_OVERFLOW:
-                entries = max(256, (entries or eng.entries) // 2)
+            if st & N.STATUS_PLAN:
+                raise RuntimeError('oa_step: an item exceeds the kernel limits (planner bug)')
+            # stash full: smaller items, then every halo on the 64-bit global-table path
+            entries = 0 if pc.entries <= 256 else max(256, pc.entries // 2)
         else:
-            raise RuntimeError('LDS hash tables kept overflowing (adversarial IDs?)')
+            raise RuntimeError('LDS hash tables kept overflowing')
         nh = len(slices[0])
         ids_dtype = np_dtype(cur['ids'])
         unsigned = ids_dtype.kind == 'u'
@@ -263,6 +265,13 @@ def track_orbits(snapshot_number, progenitor_links, regions, load_snapshot_data,
     except TypeError:                     # an unhashable callable: no carry
         key, entry = None, None
     carried = None
+    otf = OnTheFly(engine, mode)
+    if otf.mode != mode:
+        raise ValueError('engine mode %r != mode %r' % (otf.mode, mode))
+    # device tensors of a carry belong to the engine (device, LDS configuration) that
+    # made them: a call with another engine, or on another device, starts afresh
+    if entry is not None and (entry['engine'] is not engine or entry['device'] != otf.eng.device):
+        entry = None
     for s, halo_ids_ in zip([snapshot_number, snapshot_number - 1], progenitor_links):
         halo_exists = np.argwhere(halo_ids_ != -1).flatten()
         halo_ids = halo_ids_[halo_exists]
@@ -292,15 +301,13 @@ def track_orbits(snapshot_number, progenitor_links, regions, load_snapshot_data,
     if verbose:
         print('Identifying {}ers...'.format(mode[:8]))
         t0 = time.time()
-    otf = OnTheFly(engine, mode)
-    if otf.mode != mode:
-        raise ValueError('engine mode %r != mode %r' % (otf.mode, mode))
     if key is not None:
         _CARRY.pop(key, None)             # a failing call leaves nothing stale behind
     out = otf.run(snaps, slices, positions, carried=carried)
     if key is not None and _carry_enabled():
         _CARRY.clear()                    # one carried snapshot at a time (device memory)
-        _CARRY[key] = dict(cur_meta, carry=otf.carry)
+        _CARRY[key] = dict(cur_meta, carry=otf.carry,
+                           engine=engine, device=otf.eng.device)
     if verbose:
         print('Identified {}ers in {} s\n'.format(mode[:8], time.time() - t0))
     tag = mode[:8] + 'er'

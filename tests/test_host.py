@@ -25,7 +25,9 @@ def test_library_exports_every_declared_symbol():
     assert lib.oa_abi_version() == N.ABI_VERSION
     assert lib.oa_struct_size(0) == 96 and lib.oa_struct_size(1) == 32
     from orbitanalysis_amd import engine as E
-    assert lib.oa_step_lds_bytes(E.DEFAULT_ENTRIES, E.DEFAULT_SLOTS) <= 160 * 1024
+    for f64 in (False, True):
+        assert lib.oa_step_lds_bytes(E.DEFAULT_ENTRIES[f64], E.DEFAULT_SLOTS[f64], int(f64)) \
+            <= 160 * 1024
     assert lib.oa_build_info(0) % 64 == 0 and lib.oa_build_info(1) >= 1
     post = open(os.path.join(ROOT, 'include', 'orbit_post.h')).read()
     assert int(re.search(r'OA_COLLATE_CHUNK (\d+)', post).group(1)) == N.COLLATE_CHUNK
@@ -133,15 +135,19 @@ def test_plan_items_invariants():
     cur[::37] = 50000
     prev = cur + rng.integers(-10, 10, 500)
     prev[::11] = -1
-    items, glob, scratch = plan_items(cur, prev, 4096, hmax=16)
+    prev[5] = 9000                                  # a progenitor block beyond max_pv
+    items, glob, scratch = plan_items(cur, prev, 4096, hmax=16, max_pv=8192)
+    pv = (np.maximum(prev, 0) + 63) // 64 * 64
     covered = np.zeros(500, int)
     for it in items:
         assert it['h1'] - it['h0'] <= 16
         assert cur[it['h0']:it['h1']].sum() <= 4096
+        assert pv[it['h0']:it['h1']].sum() <= 8192
         covered[it['h0']:it['h1']] += 1
     for g in glob:                                  # large halos: single-halo global items
-        assert g['h1'] == g['h0'] + 1 and cur[g['h0']] > 4096
+        assert g['h1'] == g['h0'] + 1 and (cur[g['h0']] > 4096 or pv[g['h0']] > 8192)
         covered[g['h0']] += 1
+    assert 5 in glob['h0']
     assert np.all(covered == 1)
     segs = 0
     for it in np.concatenate([items, glob]):
@@ -202,3 +208,57 @@ def test_onthefly_carry_key_and_switch(monkeypatch):
     assert not T._same(np.array([1.0], np.float32), np.array([1.0]))
     T.clear_carry()
     assert T._CARRY == {}
+
+
+def test_plan_items_slots_and_speed():
+    """The host planner (C++) fills slot0 like set_item_slots and plans 1e4 halos in
+    well under a millisecond (the Python loop it replaced took ~43 ms)."""
+    import time
+    from orbitanalysis_amd.engine import plan_items, set_item_slots
+    rng = np.random.default_rng(1)
+    nh = 10000
+    cur = rng.integers(9000, 11000, nh)
+    prev = cur + rng.integers(-50, 50, nh)
+    prev[::7] = -1
+    out_slot = np.where(prev >= 0, np.cumsum(prev >= 0) - 1, -1)
+    items, glob, scratch = plan_items(cur, prev, 11776, 32, out_slot=out_slot)
+    want = items.copy()
+    set_item_slots(want, out_slot)
+    assert np.array_equal(items['slot0'], want['slot0'])
+    t0 = time.perf_counter()
+    for _ in range(20):
+        plan_items(cur, prev, 11776, 32, out_slot=out_slot)
+    assert (time.perf_counter() - t0) / 20 < 2e-3
+
+
+def test_checkpoint_angles_length_checked():
+    from orbitanalysis_amd.engine import check_angles_in
+    check_angles_in(None, 5)
+    check_angles_in(np.zeros(5, np.float16), 5)
+    with pytest.raises(ValueError):
+        check_angles_in(np.zeros(4, np.float16), 5)
+
+
+def test_resume_without_checkpoint_raises():
+    """resume=True re-processes the last saved snapshot from its checkpoint angles
+    (track_orbits.py:229-232); without them the reference fails opening the
+    .checkpoint file, and so does the drop-in (before any device work)."""
+    from orbitanalysis_amd.track_orbits import track_orbits
+    from orbitanalysis_amd.savefile import MemorySavefile
+
+    class StubEngine:
+        mode, prev = 'pericentric', None
+
+        def reset(self):
+            pass
+
+    out = MemorySavefile()
+    out.initialize('pericentric', None)
+    out.write_group('snapshot_001', {})
+    snap = {'ids': np.arange(3), 'coordinates': np.zeros((3, 3)), 'velocities': np.zeros((3, 3)),
+            'masses': 1.0, 'region_offsets': np.array([0]), 'redshift': 0.0, 'H0': 1.0,
+            'Omega_m': 0.3, 'Omega_L': 0.7}
+    with pytest.raises(FileNotFoundError):
+        track_orbits([0, 1, 2], [[0], [0], [0]], lambda s, h: (np.zeros((1, 3)), np.ones(1), None),
+                     lambda s, p, r: dict(snap), out, resume=True, verbose=False,
+                     engine=StubEngine())

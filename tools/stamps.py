@@ -8,7 +8,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import orbitanalysis_amd  # noqa
 from orbitanalysis_amd import _native as N
-from orbitanalysis_amd.engine import OrbitEngine, Workspace
+from orbitanalysis_amd.engine import OrbitEngine
 from orbitanalysis_amd.synthetic_device import DevicePlummer
 from orbitanalysis_amd.utils import hubble_parameter
 from collections import namedtuple
@@ -26,46 +26,35 @@ p0 = eng.prepare(s0, c0[0], c0[2], H, z, ex, False)
 eng.launch(p0, None)
 p1 = eng.prepare(s1, c1[0], c1[2], H, z, ex, True,
                  prev_layout=(p0.starts, p0.counts, ex, p0.plan, p0.n))
-ws = Workspace.for_step(p1, eng.device, eng.entries, eng.n_wg)
+ws = eng.workspace(p1)
 St = namedtuple('St', 'ids rhat meta')
 for rep in range(3):
     eng.launch(p1, ws, St(s0['ids'], p0.rhat, p0.meta))
 torch.cuda.synchronize()
 ni = len(p1.items)
 nw = eng.lib.oa_build_info(0) // 64
-sn = 6 + 2 * nw
+NP = 8                                            # STAMP_NP in orbit_hip.hip
+sn = NP + 3 * nw
 buf = np.zeros(ni * sn, dtype=np.uint64)
 got = eng.lib.oa_debug_stamps(buf.ctypes.data, buf.size)
 assert got > 0, 'not a stamps build'
 tw = buf.reshape(ni, sn).astype(np.float64) * 10.0 / 1000.0   # 100 MHz -> us
 tw -= tw[:, 0].min()
-t = tw[:, :6]
-if eng.n_wg > 0:      # persistent k_stream: per-item stamps 0..5
-    for name, a_, b_ in (('insert', 0, 1), ('walks+hdr', 1, 2), ('interleave', 2, 3),
-                         ('barrier', 3, 4), ('phase3', 4, 5), ('total', 0, 5)):
-        d = t[:, b_] - t[:, a_]
-        print('%-11s mean %7.2f  p10 %7.2f  p50 %7.2f  p90 %7.2f  max %7.2f us'
-              % (name, d.mean(), *np.percentile(d, [10, 50, 90]), d.max()))
-    span = t[:, 5].max() - t[:, 0].min()
-    busy = (t[:, 5] - t[:, 0]).sum() / eng.n_wg
-    print('items', ni, 'wgs', eng.n_wg, 'span %.1f us, busy per wg %.1f us (gaps %.1f)'
-          % (span, busy, span - busy))
-    sys.exit(0)
-w1, w2 = tw[:, 6::2], tw[:, 7::2]                  # per-wave ends of the phase-1 / 2 loops
-for name, w in (('wave skew phase1 end', w1), ('wave skew phase2 end', w2)):
+t = tw[:, :NP]
+w1, w2, w3 = tw[:, NP::3], tw[:, NP + 1::3], tw[:, NP + 2::3]   # per-wave loop ends
+for name, w in (('wave skew phase1 end', w1), ('wave skew phase2a end', w2),
+                ('wave skew phase2b end', w3)):
     d = w.max(1) - w.min(1)
     m = w.max(1) - w.mean(1)
     print('%-22s max-min mean %6.2f p90 %6.2f | max-mean mean %6.2f us'
           % (name, d.mean(), np.percentile(d, 90), m.mean()))
-start, span = t[:, 0], t[:, 5] - t[:, 0]
-print('items', ni, 'kernel span %.1f us' % (t[:, 5].max()))
-for name, a, b in (('phase0', 0, 1), ('phase1(t0)', 1, 2), ('barrier1', 2, 3),
-                   ('phase2(t0)', 3, 4), ('phase3+', 4, 5), ('total', 0, 5)):
+start, end = t[:, 0], t[:, NP - 1]
+print('items', ni, 'kernel span %.1f us' % (end.max()))
+for name, a, b in (('phase0', 0, 1), ('phase1(t0)', 1, 2), ('walks+bar', 2, 3),
+                   ('phase2a(t0)', 3, 4), ('stage+bar', 4, 5), ('phase2b(t0)', 5, 6),
+                   ('phase3+', 6, 7), ('total', 0, 7)):
     d = t[:, b] - t[:, a]
-    print('%-11s mean %7.2f  p10 %7.2f  p50 %7.2f  p90 %7.2f  max %7.2f us'
+    print('%-12s mean %7.2f  p10 %7.2f  p50 %7.2f  p90 %7.2f  max %7.2f us'
           % (name, d.mean(), *np.percentile(d, [10, 50, 90]), d.max()))
-order = np.argsort(start)
-print('start times of first 600 items (us):', np.round(start[order][::40][:15], 1))
-# concurrency: number of items alive at sampled times
-ts = np.linspace(0, t[:, 5].max(), 12)
-print('alive:', [int(((t[:, 0] <= x) & (t[:, 5] > x)).sum()) for x in ts])
+ts = np.linspace(0, end.max(), 12)
+print('alive:', [int(((start <= x) & (end > x)).sum()) for x in ts])
