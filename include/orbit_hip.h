@@ -61,17 +61,24 @@ typedef struct oa_halo {
     int64_t reserved;
 } oa_halo;
 
-/* One work-group's share of a snapshot.  32 bytes, device array.
+/* One work-group's share of a snapshot.  48 bytes, device array, built on the host by
+ * oa_plan_items.
  * Packed items (k_step): halos [h0,h1) whose current blocks total <= lds_entries.
  * Global items (large halos, items[n_items ..]): the single halo h0 = h1 - 1.   */
 typedef struct oa_item {
     int32_t h0, h1;
     int32_t slot0;              /* first output slot (oa_halo.out_slot) among [h0,h1),
-                                   or -1 (set by the host planner)                    */
-    int32_t reserved1;          /* 1 */
+                                   or -1                                               */
+    int32_t n_span;             /* current particles of halos [h0,h1)                  */
     int64_t scratch_off;        /* first apsis-scratch slot of this item (a multiple
-                                   of 64; one slot per progenitor particle)           */
-    int64_t n_pv;               /* progenitor particles of the item                  */
+                                   of 64; one slot per padded progenitor position)    */
+    int64_t n_pv;               /* padded progenitor positions of the item (each block
+                                   with prev_cnt > 0 rounded up to 64)                */
+    int64_t cur_off;            /* halos[h0].cur_off: the item's first current row     */
+    int32_t n_slots;            /* LDS cuckoo slots of a packed item's table:
+                                   min(2 * (current particles with a progenitor) + 64,
+                                   the slots budget); 0 for global items             */
+    int32_t reserved;
 } oa_item;
 
 /* Arguments of oa_step (one snapshot of the batch driver's inner loop). */
@@ -207,14 +214,16 @@ int64_t oa_step_lds_bytes(int32_t entries, int32_t slots, int32_t dx_f64);
  * (<= entries particles, <= hmax halos, <= max_pv padded progenitor positions) are
  * packed greedily into items (k_step); a halo beyond any of those limits becomes a
  * single-halo global item (k_big_*), listed after every packed item.
- *   cur_cnt[n_halos], prev_cnt[n_halos] (< 0: no progenitor), out_slot[n_halos]
- *   (-1: none) are host arrays; items[cap] receives the plan (oa_item.slot0 set).
+ *   cur_off[n_halos], cur_cnt[n_halos] (the current blocks), prev_cnt[n_halos]
+ *   (< 0: no progenitor), out_slot[n_halos] (-1: none) are host arrays; `slots` is
+ *   the LDS table budget (oa_step_args.lds_slots); items[cap] receives the plan.
  * Returns the number of items written (packed + global), or a negative OA_E*;
  * *n_small = packed items, *scratch = apsis-scratch slots (one per padded
  * progenitor position). */
-int64_t oa_plan_items(const int64_t *cur_cnt, const int64_t *prev_cnt, const int64_t *out_slot,
-                      int64_t n_halos, int64_t entries, int64_t hmax, int64_t max_pv,
-                      oa_item *items, int64_t cap, int64_t *n_small, int64_t *scratch);
+int64_t oa_plan_items(const int64_t *cur_off, const int64_t *cur_cnt, const int64_t *prev_cnt,
+                      const int64_t *out_slot, int64_t n_halos, int64_t entries, int64_t slots,
+                      int64_t hmax, int64_t max_pv, oa_item *items, int64_t cap,
+                      int64_t *n_small, int64_t *scratch);
 
 /* Diagnostic builds only (-DOA_STAMPS=1): copy the per-work-group phase timestamps
  * (s_memrealtime, 100 MHz; 6 per work-group) of the last oa_step to host memory.

@@ -21,8 +21,9 @@ c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, cty
 HALO_DTYPE = np.dtype([('cur_off', '<i8'), ('cur_cnt', '<i8'), ('prev_off', '<i8'),
                        ('prev_cnt', '<i8'), ('centre', '<f8', (3,)), ('bulk', '<f8', (3,)),
                        ('out_slot', '<i8'), ('reserved', '<i8')])
-ITEM_DTYPE = np.dtype([('h0', '<i4'), ('h1', '<i4'), ('slot0', '<i4'), ('reserved1', '<i4'),
-                       ('scratch_off', '<i8'), ('n_pv', '<i8')])
+ITEM_DTYPE = np.dtype([('h0', '<i4'), ('h1', '<i4'), ('slot0', '<i4'), ('n_span', '<i4'),
+                       ('scratch_off', '<i8'), ('n_pv', '<i8'), ('cur_off', '<i8'),
+                       ('n_slots', '<i4'), ('reserved', '<i4')])
 
 MODE = {'pericentric': 0, 'apocentric': 1}
 STATUS_TABLE_OVERFLOW = 2
@@ -97,7 +98,8 @@ SYMBOLS = {
     'oa_bulk_velocity': (ctypes.c_int, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
     'oa_step': (ctypes.c_int, [ctypes.POINTER(StepArgs), c_vp]),
     'oa_step_lds_bytes': (c_i64, [c_i32, c_i32, c_i32]),
-    'oa_plan_items': (c_i64, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    'oa_plan_items': (c_i64, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp,
+                              c_i64, c_vp, c_vp]),
     'oa_max_lds_bytes': (c_i64, []),
     'oa_debug_stamps': (c_i64, [c_vp, c_i64]),
     'oa_compact': (ctypes.c_int, [ctypes.POINTER(CompactArgs), c_vp]),

@@ -52,6 +52,9 @@ namespace {
 #ifndef OA_HMAX
 #define OA_HMAX 32
 #endif
+// phase 2b stages an item's current r̂ through registers, STAGE_* rows per thread:
+// lds_entries <= STAGE_* * WG (11776 float32 / 6144 float64 entries fill the LDS)
+constexpr int STAGE_F32 = 12, STAGE_F64 = 6;
 constexpr int WG = OA_WG;           // k_step work-group
 constexpr int NWAVE = WG / 64;
 constexpr int HMAX = OA_HMAX;       // halos per item
@@ -92,7 +95,7 @@ template <typename T> __device__ __forceinline__ T lds_nt(const T *p) {
 #if OA_STAMPS
 // diagnostic build only: per-work-group s_memrealtime (100 MHz) at the 8 phase
 // boundaries plus, per wave, the ends of its phase-1, 2a and 2b loops (WSTAMP 0/1/2)
-constexpr int STAMP_MAX_WG = 1 << 16, STAMP_NP = 8, STAMP_N = STAMP_NP + 3 * (OA_WG / 64);
+constexpr int STAMP_MAX_WG = 1 << 16, STAMP_NP = 9, STAMP_N = STAMP_NP + 3 * (OA_WG / 64);
 __device__ uint64_t g_stamps[STAMP_MAX_WG * STAMP_N];
 #define STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < STAMP_MAX_WG) \
     g_stamps[blockIdx.x * STAMP_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -536,20 +539,6 @@ __device__ __forceinline__ int64_t uni64(int64_t x) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-// Trip counters of phase 1: trips are runs of 64 * UNR1 consecutive positions.  Every
-// wave starts on trips `wave` and `wave + NWAVE`; later trips come from an LDS counter
-// (a wave that gets ahead takes more, so all waves end the phase within about one
-// trip of each other).  The counter is read one trip ahead, so its LDS round trip
-// overlaps a trip's work.
-__device__ __forceinline__ uint32_t trip_fetch(uint32_t *ctr, int lane) {
-    uint32_t v = 0;
-    if (lane == 0) v = atomicAdd(ctr, 1u);
-    return v;
-}
-__device__ __forceinline__ uint32_t trip_take(uint32_t fetched) {
-    return __builtin_amdgcn_readfirstlane(fetched);
-}
-
 // Phase-2 packed link of one previous particle (a register per row, phases 2a -> 2b):
 //   bits 0-13 current position c of the match, bit 14 matched, bit 15 apsis flag,
 //   bits 16-31 the previous float16 angle
@@ -569,7 +558,12 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     uint8_t *sgn8 = reinterpret_cast<uint8_t *>(
         smem + HDR_BYTES + region_a_bytes((int)E, (int)nslots_max, (int)sizeof(TD)));
 
+    // the item (host-planned, oa_plan_items): scalar loads, uniform values
     const oa_item it = a.items[blockIdx.x];
+    const int nh = it.h1 - it.h0;
+    const uint32_t nhu = (uint32_t)nh;
+    const int64_t base = it.cur_off;
+    const uint32_t n_span = (uint32_t)it.n_span, nslots = (uint32_t)it.n_slots;
     // the wave index is uniform: readfirstlane lets every trip / row quantity derived
     // from it live in SGPRs (scalar arithmetic, scalar branches)
     const int tid = threadIdx.x, lane = tid & 63;
@@ -581,94 +575,99 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     constexpr uint32_t SX = 3 * sizeof(TX), SV = 3 * sizeof(TV), SD = 3 * sizeof(TD);
     STAMP(0);
 
-    // ---- phase 0: stage the item's halo table in LDS -------------------------
-    const int nh = it.h1 - it.h0;
-    if (tid < nh) {
-        const oa_halo &h = a.halos[it.h0 + tid];
-        const oa_halo &h0 = a.halos[it.h0];
-        H.lstart[tid] = (uint32_t)(h.cur_off - h0.cur_off);
-        // joined halos: those with a non-empty progenitor block (an empty one matches
-        // nothing: its particles keep angle 0)
-        H.has_prev[tid] = COMPARE && h.prev_cnt > 0;
-        H.halo_cnt[tid] = 0;
-        for (int d = 0; d < 3; ++d) { H.cb[tid][d] = h.centre[d]; H.cb[tid][3 + d] = h.bulk[d]; }
-        for (int d = 0; d < 3; ++d) { H.cf[tid][d] = (float)h.centre[d]; H.cf[tid][3 + d] = (float)h.bulk[d]; }
-        if (tid == nh - 1) {
-            H.lstart[nh] = (uint32_t)(h.cur_off + h.cur_cnt - h0.cur_off);
-            H.n_span = H.lstart[nh];
-            H.cur_base = h0.cur_off;
-        }
-    }
-    if (tid == 0) {
-        H.nonuniform = 0; H.overflow = 0; H.nh = nh; H.chunk_total = 0; H.nstash = 0;
-        H.npend = 0;
-        H.ctr1 = 2 * NWAVE;                 // phase 1: static first trips wave, wave + NWAVE
-        // progenitor segments in halo order (serial: nh <= HMAX); each starts on a
-        // 64-position row of the virtual (padded) progenitor space
-        uint32_t ns = 0, vp = 0, nj = 0;
-        for (int k = 0; k < nh; ++k) {
-            const oa_halo &h = a.halos[it.h0 + k];
-            if (COMPARE && h.prev_cnt > 0) {
-                H.seg_halo[ns] = k; H.seg_prev_off[ns] = h.prev_off; H.vstart[ns] = vp;
-                H.seg_cnt[ns] = (uint32_t)h.prev_cnt;
-                vp += ((uint32_t)h.prev_cnt + 63u) & ~63u; ++ns;
-                nj += (uint32_t)h.cur_cnt;
-            }
-        }
-        H.vstart[ns] = vp; H.nseg = ns; H.n_pv = vp;
-        // table size for this item: load <= 1/2 where the LDS budget allows
-        const uint32_t ns_eff = 2 * nj + 64;
-        H.nsl = ns_eff > nslots_max ? nslots_max : ns_eff;
-        // reference high word for the 32-bit LDS keys: the item's first particle
-        const oa_halo &h0 = a.halos[it.h0], &hl1 = a.halos[it.h1 - 1];
-        H.hi0 = 0u;
-        if (IDB == 8 && hl1.cur_off + hl1.cur_cnt > h0.cur_off)
-            H.hi0 = (uint32_t)((uint64_t)ids[h0.cur_off] >> 32);
-    }
-    __syncthreads();
-    const uint32_t nslots = uni(H.nsl);
-    if (COMPARE) {
-        for (uint32_t w = tid; w < nslots; w += WG) slots[w] = 0ull;
-    }
-    __syncthreads();
-
-    const int64_t base = uni64(H.cur_base);
-    const uint32_t n_span = uni(H.n_span);
-    const uint32_t hi0 = uni(H.hi0);
-    const uint32_t nhu = uni(H.nh);
+    // ---- phase 0: the item's halo table into LDS, the LDS table cleared, the first
+    // phase-1 trip in flight -- all overlapped: wave 0 loads the halo rows first, then
+    // every wave issues its first trip's loads (a later counted vmcnt for the halo
+    // rows leaves them in flight), clears its share of the table, and the only barrier
+    // waits for LDS traffic alone.
+    oa_halo hrow;
+    if (wave == 0 && lane < nh) hrow = a.halos[it.h0 + lane];
+    // reference high word for the 32-bit LDS keys: the item's first particle
+    uint32_t hi0 = 0u;
+    if (IDB == 8 && COMPARE && n_span > 0) hi0 = uni((uint32_t)((uint64_t)ids[base] >> 32));
+    __builtin_amdgcn_sched_barrier(0);
     const Rsrc r_id = make_rsrc(ids + base, n_span * IDB);
     const Rsrc r_x = make_rsrc(reinterpret_cast<const TX *>(a.coords) + 3 * base, n_span * SX);
     const Rsrc r_v = make_rsrc(reinterpret_cast<const TV *>(a.vels) + 3 * base, n_span * SV);
-    const Rsrc r_rh = make_rsrc(rhat_out + 3 * base, n_span * SD);   // phase 1 stores, 2b stages
+    const Rsrc r_rh = make_rsrc(rhat_out + 3 * base, n_span * SD);
     const Rsrc r_mt = make_rsrc(a.meta_out + base, n_span * 4u);
-    STAMP(1);
-
-    // ---- phase 1: frame of every current particle, LDS insert ---------------
-    // software-pipelined: trip t+1's loads are in flight while trip t computes
-#define OA_LOAD1(IDA, XA, VA, T)                                                   \
-    _Pragma("unroll") for (int u = 0; u < UNR1; ++u) {                             \
-        const uint32_t li_ = (T) * T1 + u * 64 + lane;                             \
+    // Phase-1 rows are dealt statically: wave w frames rows w, w + NWAVE, ... (<= SU of
+    // them), two per trip, and keeps each row's r̂ in registers (rr) until phase 2b
+    // writes it into the LDS the table held -- no read-back of the rows it stored.
+    constexpr int SU = sizeof(TD) == 4 ? STAGE_F32 : STAGE_F64;
+    // float64 inputs: one row per trip (register budget of 1024-thread work-groups)
+    constexpr int U1 = (sizeof(TX) == 8 || sizeof(TV) == 8) ? 1 : UNR1;
+    constexpr int NTRIP = SU / U1;
+    static_assert(SU % U1 == 0, "rows per wave must be whole trips");
+    const uint32_t nrow1 = (n_span + 63) / 64;
+#define OA_LOAD1(IDA, XA, VA, KP)                                                  \
+    _Pragma("unroll") for (int u = 0; u < U1; ++u) {                             \
+        const uint32_t li_ = (wave + NWAVE * ((KP) * U1 + u)) * 64 + lane;       \
         IDA[u] = bld<ID, AUX_NT>(r_id, li_ * IDB);                                 \
         XA[u] = bld3<TX, AUX_NT>(r_x, li_ * SX);                                   \
         VA[u] = bld3<TV, AUX_NT>(r_v, li_ * SV);                                   \
     }
-    ID idv[UNR1], idn[UNR1];
-    V3<TX> xv[UNR1], xn[UNR1];
-    V3<TV> vv[UNR1], vn[UNR1];
-    constexpr uint32_t T1 = 64 * UNR1;               // positions per wave trip
-    const uint32_t ntr1 = (n_span + T1 - 1) / T1;
-    uint32_t t1 = wave, t1n = wave + NWAVE;
-    OA_LOAD1(idv, xv, vv, t1)
-    while (t1 < ntr1) {
-        const uint32_t f1 = trip_fetch(&H.ctr1, lane);   // the trip after next
-        OA_LOAD1(idn, xn, vn, t1n)                       // the next trip (out of range: zeros)
-        uint64_t val[UNR1];
-        uint32_t sl[UNR1], cs1[UNR1], cs2[UNR1];
-        bool ins[UNR1];
+    ID idv[U1], idn[U1];
+    V3<TX> xv[U1], xn[U1];
+    V3<TV> vv[U1], vn[U1];
+    V3<TD> rr[SU];
+    OA_LOAD1(idv, xv, vv, 0)
+    __builtin_amdgcn_sched_barrier(0);
+    if (COMPARE) {
+        for (uint32_t w = tid; w < nslots; w += WG) slots[w] = 0ull;
+    }
+    if (wave == 0) {
+        // progenitor segments: every halo with a non-empty progenitor block, in halo
+        // order, each starting on a 64-position row of the padded progenitor space
+        // (lane scans over the item's <= HMAX halos)
+        const bool in = lane < nh;
+        const bool hp = COMPARE && in && hrow.prev_cnt > 0;
+        const uint32_t pv = hp ? (((uint32_t)hrow.prev_cnt + 63u) & ~63u) : 0u;
+        uint32_t vi = pv, si = hp ? 1u : 0u;
 #pragma unroll
-        for (int u = 0; u < UNR1; ++u) {
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(vi, o), z = __shfl_up(si, o);
+            if (lane >= o) { vi += y; si += z; }
+        }
+        if (in) {
+            H.lstart[lane] = (uint32_t)(hrow.cur_off - base);
+            // joined halos: those with a non-empty progenitor block (an empty one
+            // matches nothing: its particles keep angle 0)
+            H.has_prev[lane] = hp;
+            H.halo_cnt[lane] = 0;
+            for (int d = 0; d < 3; ++d) { H.cb[lane][d] = hrow.centre[d]; H.cb[lane][3 + d] = hrow.bulk[d]; }
+            for (int d = 0; d < 3; ++d) { H.cf[lane][d] = (float)hrow.centre[d]; H.cf[lane][3 + d] = (float)hrow.bulk[d]; }
+            if (hp) {
+                const uint32_t sg = si - 1u;
+                H.seg_halo[sg] = lane; H.seg_prev_off[sg] = hrow.prev_off;
+                H.vstart[sg] = vi - pv; H.seg_cnt[sg] = (uint32_t)hrow.prev_cnt;
+            }
+        }
+        const uint32_t n_pv = (uint32_t)__shfl(vi, 63), nseg = (uint32_t)__shfl(si, 63);
+        if (lane == 0) {
+            H.lstart[nh] = n_span;
+            H.vstart[nseg] = n_pv; H.nseg = nseg; H.n_pv = n_pv;
+            H.nonuniform = 0; H.overflow = 0; H.chunk_total = 0; H.nstash = 0; H.npend = 0;
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    STAMP(1);
+
+    // ---- phase 1: frame of every current particle, LDS insert ---------------
+    // software-pipelined: trip t+1's loads are in flight while trip t computes
+#pragma unroll
+    for (int kp = 0; kp < NTRIP; ++kp) {
+        if ((uint32_t)(wave + NWAVE * kp * U1) >= nrow1) break;
+        if (kp + 1 < NTRIP) OA_LOAD1(idn, xn, vn, kp + 1)     // out of range: zeros
+        uint64_t val[U1];
+        uint32_t sl[U1], cs1[U1], cs2[U1];
+        bool ins[U1];
+#pragma unroll
+        for (int u = 0; u < U1; ++u) {
             ins[u] = false;
-            const uint32_t r0 = t1 * T1 + u * 64;       // the row's first position (uniform)
+            const uint32_t r0 = (wave + NWAVE * (kp * U1 + u)) * 64;   // uniform
             if (r0 >= n_span) continue;
             const uint32_t li = r0 + lane;
             const bool ok = li < n_span;
@@ -691,6 +690,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                           : frame<TX, TV, TD>(xv[u], vv[u], H.cb[hl], H.cf[hl], a, fk, r);
             }
             bst3<TD>(r_rh, li * SD, r);
+            rr[kp * U1 + u] = V3<TD>{r[0], r[1], r[2]};
             if constexpr (!COMPARE) {
                 uint32_t ang = 0;
                 if (a.angles_in && ok) ang = a.angles_in[base + li];
@@ -715,12 +715,12 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         if (COMPARE) {
             // first try: claim an EMPTY candidate with a CAS (at load <= 1/2 one of the
             // three almost always is), so eviction chains stay rare
-            uint64_t c0[UNR1], c1[UNR1], c2[UNR1];
+            uint64_t c0[U1], c1[U1], c2[U1];
 #pragma unroll
-            for (int u = 0; u < UNR1; ++u)
+            for (int u = 0; u < U1; ++u)
                 if (ins[u]) { c0[u] = slots[sl[u]]; c1[u] = slots[cs1[u]]; c2[u] = slots[cs2[u]]; }
 #pragma unroll
-            for (int u = 0; u < UNR1; ++u) {
+            for (int u = 0; u < U1; ++u) {
                 if (!ins[u]) continue;
                 const uint32_t t = c0[u] == 0ull ? sl[u] : (c1[u] == 0ull ? cs1[u]
                                                           : (c2[u] == 0ull ? cs2[u] : 0xFFFFFFFFu));
@@ -732,7 +732,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             // an entry whose three candidates are taken is deferred: the walks run after
             // the loop, spread over the whole work-group
 #pragma unroll
-            for (int u = 0; u < UNR1; ++u) {
+            for (int u = 0; u < U1; ++u) {
                 if (!ins[u]) continue;
                 const uint32_t e = atomicAdd(&H.npend, 1u);
                 if (e < pend_cap) pend[e] = val[u];
@@ -740,13 +740,11 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
         }
 #pragma unroll
-        for (int u = 0; u < UNR1; ++u) { idv[u] = idn[u]; xv[u] = xn[u]; vv[u] = vn[u]; }
-        t1 = t1n;
-        t1n = trip_take(f1);
+        for (int u = 0; u < U1; ++u) { idv[u] = idn[u]; xv[u] = xn[u]; vv[u] = vn[u]; }
     }
 #undef OA_LOAD1
     WSTAMP(0);
-    STAMP(2);
+    STAMP(8);
     if constexpr (!COMPARE) return;
 
     // ---- phase 2: the join, in two halves -------------------------------------
@@ -797,10 +795,11 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         pk[k] = bld<uint32_t, AUX_NT>(make_rsrc(a.meta_prev + kb, nv * 4u), lane * 4u);
     }
     __builtin_amdgcn_sched_barrier(0);
-    // barrier without a vmcnt drain: the loads above stay in flight
+    // barrier on LDS traffic only: the loads above and phase 1's r̂ stores stay in flight
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    STAMP(2);
     {
         const uint32_t np = min(H.npend, pend_cap);
         for (uint32_t e = tid; e < np; e += WG) {
@@ -895,9 +894,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     STAMP(4);
 
     // ---- phase 2b: angles from the current r̂ staged in LDS, apsis records ------
-    // The first PF2 rows' previous r̂ loads go out before the staging (HBM latency
-    // behind it); the barrier after phase 2a retires everything older with a counted
-    // vmcnt, so phase 1's r̂ stores are visible to the staging reads of other waves.
+    // The first PF2 rows' previous r̂ loads go out before the barrier (their HBM
+    // latency behind the staging), which waits for LDS traffic only.
     V3<TD> prh[KROWS];
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -908,22 +906,14 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         prh[k] = bld3<TD, AUX_NT>(make_rsrc(rhat_prev + 3 * kb, nv * SD), lane * SD);
     }
     __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"((sizeof(TD) == 4 ? 1 : 2) * PF2) : "memory");
-    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();          // every lookup done: the table is dead
     __builtin_amdgcn_sched_barrier(0);
-    {
-        // the item's current r̂ rows, written by phase 1 (L2), as SoA into region A
-        constexpr int SU = 4;
-        for (uint32_t l0 = tid; l0 < n_span; l0 += SU * WG) {
-            V3<TD> v[SU];
+    // the item's current r̂, from the registers phase 1 left it in
 #pragma unroll
-            for (int u = 0; u < SU; ++u) v[u] = bld3<TD, 0>(r_rh, (l0 + u * WG) * SD);
-#pragma unroll
-            for (int u = 0; u < SU; ++u) {
-                const uint32_t li = l0 + u * WG;
-                if (li < n_span) { rcx[li] = v[u].x; rcy[li] = v[u].y; rcz[li] = v[u].z; }
-            }
-        }
+    for (int k = 0; k < SU; ++k) {
+        const uint32_t li = (wave + NWAVE * k) * 64 + lane;
+        if (li < n_span) { rcx[li] = rr[k].x; rcy[li] = rr[k].y; rcz[li] = rr[k].z; }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -1530,12 +1520,13 @@ int64_t oa_step_lds_bytes(int32_t entries, int32_t slots, int32_t dx_f64) {
 }
 
 // Host-side item plan: greedy packing of consecutive halos, O(n_halos).
-int64_t oa_plan_items(const int64_t *cur_cnt, const int64_t *prev_cnt, const int64_t *out_slot,
-                      int64_t n_halos, int64_t entries, int64_t hmax, int64_t max_pv,
-                      oa_item *items, int64_t cap, int64_t *n_small, int64_t *scratch) {
+int64_t oa_plan_items(const int64_t *cur_off, const int64_t *cur_cnt, const int64_t *prev_cnt,
+                      const int64_t *out_slot, int64_t n_halos, int64_t entries, int64_t slots,
+                      int64_t hmax, int64_t max_pv, oa_item *items, int64_t cap,
+                      int64_t *n_small, int64_t *scratch) {
     g_err[0] = 0;
-    if (n_halos < 0 || entries < 0 || hmax < 1 || max_pv < 0 || !n_small || !scratch ||
-        (n_halos > 0 && (!cur_cnt || !prev_cnt || !items)))
+    if (n_halos < 0 || entries < 0 || slots < 0 || hmax < 1 || max_pv < 0 || !n_small ||
+        !scratch || (n_halos > 0 && (!cur_off || !cur_cnt || !prev_cnt || !items)))
         return fail(OA_E_ARG, "oa_plan_items: bad arguments");
     if (n_halos > INT32_MAX) return fail(OA_E_ARG, "oa_plan_items: more than 2^31 halos");
     auto pv = [&](int64_t j) { const int64_t p = prev_cnt[j] > 0 ? prev_cnt[j] : 0; return (p + 63) / 64 * 64; };
@@ -1551,15 +1542,18 @@ int64_t oa_plan_items(const int64_t *cur_cnt, const int64_t *prev_cnt, const int
         if (cur_cnt[j] < 0) return fail(OA_E_ARG, "oa_plan_items: negative block size");
         if (big(j)) { ++j; ++ng; continue; }
         const int64_t h0 = j;
-        int64_t tot = 0, ptot = 0;
+        int64_t tot = 0, ptot = 0, nj = 0;
         while (j < n_halos && j - h0 < hmax && !big(j) && tot + cur_cnt[j] <= entries &&
                ptot + pv(j) <= max_pv) {
             tot += cur_cnt[j];
             ptot += pv(j);
+            if (prev_cnt[j] > 0) nj += cur_cnt[j];
             ++j;
         }
         if (n >= cap) return fail(OA_E_ARG, "oa_plan_items: more than cap items");
-        items[n] = oa_item{(int32_t)h0, (int32_t)j, slot0(h0, j), 1, sc, ptot};
+        const int64_t nsl = 2 * nj + 64 < slots ? 2 * nj + 64 : slots;   // load <= 1/2 if it fits
+        items[n] = oa_item{(int32_t)h0, (int32_t)j, slot0(h0, j), (int32_t)tot, sc, ptot,
+                           cur_off[h0], (int32_t)nsl, 0};
         sc += ptot;                                    // one 64-slot segment per row
         ++n;
     }
@@ -1567,7 +1561,8 @@ int64_t oa_plan_items(const int64_t *cur_cnt, const int64_t *prev_cnt, const int
     if (n + ng > cap) return fail(OA_E_ARG, "oa_plan_items: more than cap items");
     for (int64_t j = 0; j < n_halos; ++j) {             // global (large-halo) items
         if (!big(j)) continue;
-        items[n++] = oa_item{(int32_t)j, (int32_t)(j + 1), slot0(j, j + 1), 1, sc, pv(j)};
+        items[n++] = oa_item{(int32_t)j, (int32_t)(j + 1), slot0(j, j + 1), 0, sc, pv(j),
+                             cur_off[j], 0, 0};
         sc += pv(j);
     }
     *scratch = sc;
@@ -1608,8 +1603,10 @@ int oa_step(const oa_step_args *args, void *stream) {
     if (a.mode != OA_MODE_PERICENTRIC && a.mode != OA_MODE_APOCENTRIC)
         return fail(OA_E_ARG, "bad mode");
     if (a.n_items > 0 && (a.lds_entries <= 0 || a.lds_entries > (int)MAX_POS + 1 ||
+                          a.lds_entries > (a.dx_f64 || a.onthefly && a.coord_f64 ? STAGE_F64 : STAGE_F32) * WG ||
                           a.lds_slots <= a.lds_entries))
-        return fail(OA_E_ARG, "bad lds_entries/lds_slots (entries <= %u < slots)", MAX_POS + 1);
+        return fail(OA_E_ARG, "bad lds_entries/lds_slots (entries <= %d (r̂ dtype) < slots)",
+                    (a.dx_f64 ? STAGE_F64 : STAGE_F32) * WG);
     if (a.n_items + a.n_global_items > 0 &&
         (!a.halos || !a.ids || !a.coords || !a.vels || !a.rhat_out || !a.meta_out))
         return fail(OA_E_ARG, "null input/output pointer");

@@ -134,7 +134,8 @@ def plan_dtypes(snapshot, centre, bulk_cat, H, z):
 GCHUNK = 4096                  # particles per work-group chunk of a large halo
 
 
-def plan_items(cur_cnt, prev_cnt, entries, hmax=128, out_slot=None, max_pv=None):
+def plan_items(cur_cnt, prev_cnt, entries, hmax=128, out_slot=None, max_pv=None, slots=None,
+               cur_off=None):
     """Work-group items of one snapshot, planned by the library's host
     function ``oa_plan_items`` (O(n_halos) C++; no per-halo Python).
 
@@ -153,14 +154,18 @@ def plan_items(cur_cnt, prev_cnt, entries, hmax=128, out_slot=None, max_pv=None)
     cur = np.ascontiguousarray(cur_cnt, dtype=np.int64)
     prev = np.ascontiguousarray(prev_cnt, dtype=np.int64)
     nh = len(cur)
+    off = np.ascontiguousarray(np.concatenate([[0], np.cumsum(cur)[:-1]]) if cur_off is None
+                               else cur_off, dtype=np.int64)
+    if slots is None:
+        slots = 2 * int(entries) + 64
     osl = None if out_slot is None else np.ascontiguousarray(out_slot, dtype=np.int64)
     if max_pv is None:
         max_pv = lib.oa_build_info(3) * lib.oa_build_info(0)
     out = np.zeros(max(nh, 1), dtype=N.ITEM_DTYPE)
     n_small, scratch = ctypes.c_int64(0), ctypes.c_int64(0)
-    n = lib.oa_plan_items(cur.ctypes.data, prev.ctypes.data,
+    n = lib.oa_plan_items(off.ctypes.data, cur.ctypes.data, prev.ctypes.data,
                           None if osl is None else osl.ctypes.data, nh, int(entries),
-                          int(hmax), int(max_pv), out.ctypes.data, len(out),
+                          int(slots), int(hmax), int(max_pv), out.ctypes.data, len(out),
                           ctypes.byref(n_small), ctypes.byref(scratch))
     if n < 0:
         raise ValueError(lib.oa_last_error().decode())
@@ -391,7 +396,7 @@ class OrbitEngine:
 
     # ------------------------------------------------------------------ tables
     def build_tables(self, snapshot, centres, bulk_cat, exists, compare, prev_layout=None,
-                     entries=None):
+                     entries=None, slots=None):
         n = int(snapshot['ids'].numel()) if isinstance(snapshot['ids'], torch.Tensor) \
             else len(snapshot['ids'])
         starts = np.asarray(snapshot['region_offsets'], dtype=np.int64).reshape(-1)
@@ -419,7 +424,8 @@ class OrbitEngine:
             halos['prev_cnt'][has_prog] = p_counts[p[has_prog]]
             halos['out_slot'][has_prog] = np.arange(int(has_prog.sum()))
         items, glob, scratch = plan_items(counts, halos['prev_cnt'], entries, self.hmax,
-                                          out_slot=halos['out_slot'], max_pv=self.max_pv)
+                                          out_slot=halos['out_slot'], max_pv=self.max_pv,
+                                          slots=slots, cur_off=starts)
         return halos, items, glob, scratch, starts, counts, has_prog
 
     # ------------------------------------------------------------------ step
@@ -491,7 +497,7 @@ class OrbitEngine:
         lds_e, lds_s = self.table_sizes(plan.dx == F64)
         plan_e = lds_e if entries is None else min(int(entries), lds_e)
         halos, items, glob, scratch, starts, counts, has_prog = self.build_tables(
-            snap, centres, bulk_cat, exists, compare, prev_layout, plan_e)
+            snap, centres, bulk_cat, exists, compare, prev_layout, plan_e, lds_s)
         all_items = np.concatenate([items, glob])
         pr = PreparedStep(plan=plan, n=n, starts=starts, counts=counts, has_prog=has_prog,
                           items=all_items, n_small=len(items), scratch=scratch,

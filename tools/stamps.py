@@ -33,14 +33,14 @@ for rep in range(3):
 torch.cuda.synchronize()
 ni = len(p1.items)
 nw = eng.lib.oa_build_info(0) // 64
-NP = 8                                            # STAMP_NP in orbit_hip.hip
+NP = 9                                            # STAMP_NP in orbit_hip.hip
 sn = NP + 3 * nw
 buf = np.zeros(ni * sn, dtype=np.uint64)
 got = eng.lib.oa_debug_stamps(buf.ctypes.data, buf.size)
 assert got > 0, 'not a stamps build'
 tw = buf.reshape(ni, sn).astype(np.float64) * 10.0 / 1000.0   # 100 MHz -> us
 tw -= tw[:, 0].min()
-t = tw[:, :NP]
+t = tw[:, [0, 1, 8, 2, 3, 4, 5, 6, 7]]           # stamps in phase order
 w1, w2, w3 = tw[:, NP::3], tw[:, NP + 1::3], tw[:, NP + 2::3]   # per-wave loop ends
 for name, w in (('wave skew phase1 end', w1), ('wave skew phase2a end', w2),
                 ('wave skew phase2b end', w3)):
@@ -48,11 +48,11 @@ for name, w in (('wave skew phase1 end', w1), ('wave skew phase2a end', w2),
     m = w.max(1) - w.mean(1)
     print('%-22s max-min mean %6.2f p90 %6.2f | max-mean mean %6.2f us'
           % (name, d.mean(), np.percentile(d, 90), m.mean()))
-start, end = t[:, 0], t[:, NP - 1]
+start, end = t[:, 0], t[:, 8]
 print('items', ni, 'kernel span %.1f us' % (end.max()))
-for name, a, b in (('phase0', 0, 1), ('phase1(t0)', 1, 2), ('walks+bar', 2, 3),
-                   ('phase2a(t0)', 3, 4), ('stage+bar', 4, 5), ('phase2b(t0)', 5, 6),
-                   ('phase3+', 6, 7), ('total', 0, 7)):
+for name, a, b in (('phase0', 0, 1), ('phase1(t0)', 1, 2), ('2a-issue+bar', 2, 3),
+                   ('walks+bar', 3, 4), ('phase2a(t0)', 4, 5), ('stage+bar', 5, 6),
+                   ('phase2b(t0)', 6, 7), ('phase3+', 7, 8), ('total', 0, 8)):
     d = t[:, b] - t[:, a]
     print('%-12s mean %7.2f  p10 %7.2f  p50 %7.2f  p90 %7.2f  max %7.2f us'
           % (name, d.mean(), *np.percentile(d, [10, 50, 90]), d.max()))
