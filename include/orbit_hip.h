@@ -151,6 +151,11 @@ typedef struct oa_step_args {
                                    (0 = empty), u32 pad}; zeroed by oa_step          */
     uint32_t *gvals;            /* unused (NULL)                                      */
     int64_t gtab_total;         /* slots over all global items                        */
+    /* optional (NULL = off): per apsis record, the index of its particle in the
+     * previous-state arrays (ids_prev / rhat_prev rows, < 2^31), stored beside
+     * scratch_ids; the sharded driver maps it to the particle's position in the global
+     * previous block, which orders the merged records (sharding.py) */
+    int32_t *scratch_pos;
 } oa_step_args;
 
 /* Arguments of oa_compact: gather the per-item apsis records into the reference's
@@ -172,6 +177,9 @@ typedef struct oa_compact_args {
     void *out_ids;              /* capacity >= total (<= n_prev) */
     uint16_t *out_ang;
     int64_t *total_out;         /* device scalar: number of apsis records */
+    const int32_t *scratch_pos; /* optional: oa_step_args.scratch_pos of the step        */
+    int32_t *out_pos;           /* optional: the records' previous-state indices, in
+                                   output order (with scratch_pos)                     */
 } oa_compact_args;
 
 /* ABI version (OA_ABI_VERSION) — lets the host reject a stale library. */

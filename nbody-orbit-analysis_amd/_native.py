@@ -45,7 +45,7 @@ class StepArgs(ctypes.Structure):
                 ('matched_prev', c_vp), ('matched_cur', c_vp), ('vr_out', c_vp),
                 ('n_global_items', c_i32), ('n_gchunk1', c_i32), ('n_gchunk2', c_i32),
                 ('gchunk1', c_vp), ('gchunk2', c_vp), ('gtab', c_vp), ('gkeys', c_vp),
-                ('gvals', c_vp), ('gtab_total', c_i64)]
+                ('gvals', c_vp), ('gtab_total', c_i64), ('scratch_pos', c_vp)]
 
 
 class CompactArgs(ctypes.Structure):
@@ -54,7 +54,7 @@ class CompactArgs(ctypes.Structure):
                 ('scratch_ids', c_vp), ('scratch_ang', c_vp), ('seg_count', c_vp),
                 ('halo_count', c_vp), ('item_count', c_vp), ('n_slots', c_i32),
                 ('offsets_out', c_vp), ('out_ids', c_vp), ('out_ang', c_vp),
-                ('total_out', c_vp)]
+                ('total_out', c_vp), ('scratch_pos', c_vp), ('out_pos', c_vp)]
 
 
 class CollateArgs(ctypes.Structure):

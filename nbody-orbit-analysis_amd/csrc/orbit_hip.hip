@@ -63,7 +63,17 @@ constexpr int KROWS = OA_KROWS;
 constexpr int PF2 = OA_PF2;
 constexpr int BULK_CHUNK = 8192;    // numpy pairwise-sum buffer chunk
 constexpr int STASH = 64;           // cuckoo stash entries per item
-constexpr int MAX_EVICT = 48;       // eviction-chain length before an entry is stashed
+#ifndef OA_MAXEV
+#define OA_MAXEV 48
+#endif
+#ifndef OA_RWALK
+#define OA_RWALK 0
+#endif
+constexpr int MAX_EVICT = OA_MAXEV; // eviction-chain length before an entry is stashed
+#ifndef OA_NCAND
+#define OA_NCAND 3
+#endif
+constexpr int NCAND = OA_NCAND;     // cuckoo candidate slots per key (3 or 4)
 static_assert(WG % 64 == 0 && WG <= 1024, "work-group must be whole waves");
 static_assert(HMAX < WG, "halo table is staged by one thread per halo");
 
@@ -95,16 +105,20 @@ template <typename T> __device__ __forceinline__ T lds_nt(const T *p) {
 #if OA_STAMPS
 // diagnostic build only: per-work-group s_memrealtime (100 MHz) at the 8 phase
 // boundaries plus, per wave, the ends of its phase-1, 2a and 2b loops (WSTAMP 0/1/2)
-constexpr int STAMP_MAX_WG = 1 << 16, STAMP_NP = 9, STAMP_N = STAMP_NP + 3 * (OA_WG / 64);
+constexpr int STAMP_MAX_WG = 1 << 16, STAMP_NP = 9, STAMP_N = STAMP_NP + 3 * (OA_WG / 64) + 1;
 __device__ uint64_t g_stamps[STAMP_MAX_WG * STAMP_N];
 #define STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < STAMP_MAX_WG) \
     g_stamps[blockIdx.x * STAMP_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// the last word: a diagnostic value of the work-group (table walks)
+#define DIAG(v) do { if (threadIdx.x == 0 && blockIdx.x < STAMP_MAX_WG) \
+    g_stamps[blockIdx.x * STAMP_N + STAMP_N - 1] = (v); } while (0)
 #define WSTAMP(k) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < STAMP_MAX_WG) \
     g_stamps[blockIdx.x * STAMP_N + STAMP_NP + 3 * (threadIdx.x >> 6) + (k)] = \
         __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define STAMP(k) do { } while (0)
 #define WSTAMP(k) do { } while (0)
+#define DIAG(v) do { } while (0)
 #endif
 
 template <typename T> struct V3 { T x, y, z; };
@@ -174,7 +188,7 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
     return h;
 }
 // Three cuckoo candidate slots of a key (low 32 bits of the ID) in a table of n slots.
-__device__ __forceinline__ void cuckoo_slots(uint32_t lo, uint32_t n, uint32_t s[3]) {
+__device__ __forceinline__ void cuckoo_slots(uint32_t lo, uint32_t n, uint32_t s[NCAND]) {
     // two 32-bit multiplicative mixes; 16-bit fields scaled by 24-bit (full-rate) products
     const uint32_t a = lo ^ (lo >> 16);
     uint32_t h1 = a * 0x9E3779B1u, h2 = (a ^ 0x5BD1E995u) * 0x85EBCA6Bu;
@@ -183,6 +197,7 @@ __device__ __forceinline__ void cuckoo_slots(uint32_t lo, uint32_t n, uint32_t s
     s[0] = __umul24(h1 >> 16, n) >> 16;
     s[1] = __umul24(h1 & 0xFFFFu, n) >> 16;
     s[2] = __umul24(h2 >> 16, n) >> 16;
+    if (NCAND > 3) s[3 % NCAND] = __umul24(h2 & 0xFFFFu, n) >> 16;
 }
 
 template <int IDB> struct IdT;
@@ -201,7 +216,7 @@ struct ItemHdr {
     uint32_t nonuniform, hi0, pad0, overflow;
     uint32_t nh, nseg, n_span, n_pv;
     uint32_t chunk_total, nsl, nstash, npend;
-    uint32_t ctr1, pad1, pad2, pad3;    // phase-1 trip counter
+    uint32_t ctr1, pad1, pad2, pad3;    // phase-1 trip counter, walk diagnostics
     uint64_t stash[STASH];          // cuckoo entries whose eviction chain ran out
     uint32_t lstart[HMAX + 1];      // local start of each item halo's current block
     uint32_t vstart[HMAX + 1];      // virtual start of each progenitor segment
@@ -591,18 +606,27 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     const Rsrc r_v = make_rsrc(reinterpret_cast<const TV *>(a.vels) + 3 * base, n_span * SV);
     const Rsrc r_rh = make_rsrc(rhat_out + 3 * base, n_span * SD);
     const Rsrc r_mt = make_rsrc(a.meta_out + base, n_span * 4u);
-    // Phase-1 rows are dealt statically: wave w frames rows w, w + NWAVE, ... (<= SU of
-    // them), two per trip, and keeps each row's r̂ in registers (rr) until phase 2b
-    // writes it into the LDS the table held -- no read-back of the rows it stored.
+    // Phase-1 rows go in trips of U1 consecutive rows; a wave takes at most NTRIP trips
+    // (<= SU rows) and keeps each row's r̂ in registers (rr) until phase 2b writes it
+    // into the LDS the table held -- no read-back of the rows it stored.
     constexpr int SU = sizeof(TD) == 4 ? STAGE_F32 : STAGE_F64;
     // float64 inputs: one row per trip (register budget of 1024-thread work-groups)
     constexpr int U1 = (sizeof(TX) == 8 || sizeof(TV) == 8) ? 1 : UNR1;
     constexpr int NTRIP = SU / U1;
     static_assert(SU % U1 == 0, "rows per wave must be whole trips");
     const uint32_t nrow1 = (n_span + 63) / 64;
-#define OA_LOAD1(IDA, XA, VA, KP)                                                  \
+    const uint32_t ntr1 = (nrow1 + U1 - 1) / U1;     // trips of U1 consecutive rows
+    // the wave's k-th trip: wave, wave + NWAVE, then trips from an LDS counter (read a
+    // trip ahead), at most NTRIP of them, so the rows' r̂ fit the wave's registers
+    // (float64 inputs, one row per trip: rows dealt statically, wave + NWAVE * k)
+    constexpr bool DYN = U1 > 1;
+    uint32_t tp[NTRIP];
+#pragma unroll
+    for (int k = 0; k < NTRIP; ++k) tp[k] = (uint32_t)(wave + NWAVE * k);
+    uint32_t ntrips = NTRIP;
+#define OA_LOAD1(IDA, XA, VA, T)                                                   \
     _Pragma("unroll") for (int u = 0; u < U1; ++u) {                             \
-        const uint32_t li_ = (wave + NWAVE * ((KP) * U1 + u)) * 64 + lane;       \
+        const uint32_t li_ = ((T) * U1 + u) * 64 + lane;                           \
         IDA[u] = bld<ID, AUX_NT>(r_id, li_ * IDB);                                 \
         XA[u] = bld3<TX, AUX_NT>(r_x, li_ * SX);                                   \
         VA[u] = bld3<TV, AUX_NT>(r_v, li_ * SV);                                   \
@@ -611,7 +635,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     V3<TX> xv[U1], xn[U1];
     V3<TV> vv[U1], vn[U1];
     V3<TD> rr[SU];
-    OA_LOAD1(idv, xv, vv, 0)
+    OA_LOAD1(idv, xv, vv, tp[0])
     __builtin_amdgcn_sched_barrier(0);
     if (COMPARE) {
         for (uint32_t w = tid; w < nslots; w += WG) slots[w] = 0ull;
@@ -648,6 +672,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             H.lstart[nh] = n_span;
             H.vstart[nseg] = n_pv; H.nseg = nseg; H.n_pv = n_pv;
             H.nonuniform = 0; H.overflow = 0; H.chunk_total = 0; H.nstash = 0; H.npend = 0;
+            H.pad1 = 0;
+            H.ctr1 = 2 * NWAVE;             // phase 1: the first two trips of every wave are static
         }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -659,15 +685,18 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // software-pipelined: trip t+1's loads are in flight while trip t computes
 #pragma unroll
     for (int kp = 0; kp < NTRIP; ++kp) {
-        if ((uint32_t)(wave + NWAVE * kp * U1) >= nrow1) break;
-        if (kp + 1 < NTRIP) OA_LOAD1(idn, xn, vn, kp + 1)     // out of range: zeros
+        if (tp[kp] >= ntr1) { ntrips = kp; break; }         // trip numbers only grow
+        const uint32_t tcur = DYN ? tp[kp] : (uint32_t)(wave + NWAVE * kp);
+        uint32_t f = 0;
+        if (DYN && kp + 2 < NTRIP && lane == 0) f = atomicAdd(&H.ctr1, 1u);   // trip kp + 2
+        if (kp + 1 < NTRIP) OA_LOAD1(idn, xn, vn, (DYN ? tp[(kp + 1) % NTRIP] : (uint32_t)(wave + NWAVE * (kp + 1))))
         uint64_t val[U1];
-        uint32_t sl[U1], cs1[U1], cs2[U1];
+        uint32_t csu[U1][NCAND];
         bool ins[U1];
 #pragma unroll
         for (int u = 0; u < U1; ++u) {
             ins[u] = false;
-            const uint32_t r0 = (wave + NWAVE * (kp * U1 + u)) * 64;   // uniform
+            const uint32_t r0 = (tcur * U1 + u) * 64;        // uniform
             if (r0 >= n_span) continue;
             const uint32_t li = r0 + lane;
             const bool ok = li < n_span;
@@ -704,26 +733,26 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                 id_split<IDB>(idv[u], lo, hi);
                 if (IDB == 8 && hi != hi0) H.nonuniform = 1u;     // benign race: all write 1
                 val[u] = slot_pack(lo, sgn << 16, li);
-                uint32_t cs[3];
-                cuckoo_slots(lo, nslots, cs);
-                sl[u] = cs[0];
-                cs1[u] = cs[1];
-                cs2[u] = cs[2];
+                cuckoo_slots(lo, nslots, csu[u]);
                 ins[u] = true;
             }
         }
         if (COMPARE) {
             // first try: claim an EMPTY candidate with a CAS (at load <= 1/2 one of the
             // three almost always is), so eviction chains stay rare
-            uint64_t c0[U1], c1[U1], c2[U1];
+            uint64_t cv[U1][NCAND];
 #pragma unroll
             for (int u = 0; u < U1; ++u)
-                if (ins[u]) { c0[u] = slots[sl[u]]; c1[u] = slots[cs1[u]]; c2[u] = slots[cs2[u]]; }
+                if (ins[u]) {
+#pragma unroll
+                    for (int j = 0; j < NCAND; ++j) cv[u][j] = slots[csu[u][j]];
+                }
 #pragma unroll
             for (int u = 0; u < U1; ++u) {
                 if (!ins[u]) continue;
-                const uint32_t t = c0[u] == 0ull ? sl[u] : (c1[u] == 0ull ? cs1[u]
-                                                          : (c2[u] == 0ull ? cs2[u] : 0xFFFFFFFFu));
+                uint32_t t = 0xFFFFFFFFu;
+#pragma unroll
+                for (int j = NCAND - 1; j >= 0; --j) t = cv[u][j] == 0ull ? csu[u][j] : t;
                 if (t == 0xFFFFFFFFu) continue;
                 const uint64_t o = atomicCAS(reinterpret_cast<unsigned long long *>(&slots[t]),
                                              0ull, (unsigned long long)val[u]);
@@ -741,6 +770,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         }
 #pragma unroll
         for (int u = 0; u < U1; ++u) { idv[u] = idn[u]; xv[u] = xn[u]; vv[u] = vn[u]; }
+        if (DYN && kp + 2 < NTRIP) tp[(kp + 2) % NTRIP] = __builtin_amdgcn_readfirstlane(f);
     }
 #undef OA_LOAD1
     WSTAMP(0);
@@ -804,21 +834,34 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         const uint32_t np = min(H.npend, pend_cap);
         for (uint32_t e = tid; e < np; e += WG) {
             uint64_t v = pend[e];
-            uint32_t cs[3];
+            uint32_t cs[NCAND];
             cuckoo_slots((uint32_t)v, nslots, cs);
             uint32_t t = cs[0];
             for (int it_ = 0;; ++it_) {
                 const uint64_t old = atomicExch(reinterpret_cast<unsigned long long *>(&slots[t]),
                                                 (unsigned long long)v);
-                if (old == 0ull) break;
+                if (old == 0ull) {
+                    if (OA_STAMPS) atomicMax(&H.pad1, (uint32_t)it_ + 1u);
+                    break;
+                }
                 if (it_ == MAX_EVICT) {
+                    if (OA_STAMPS) atomicMax(&H.pad1, 1000u);
                     const uint32_t k = atomicAdd(&H.nstash, 1u);
                     if (k < (uint32_t)STASH) H.stash[k] = old;
                     else H.overflow = 2u;
                     break;
                 }
                 cuckoo_slots((uint32_t)old, nslots, cs);
-                t = cs[cs[0] == t ? 1 : (cs[1] == t ? 2 : 0)];
+                // the displaced key moves to its candidate after the one it held
+                uint32_t nx = cs[0];
+#pragma unroll
+                for (int j = NCAND - 2; j >= 0; --j) nx = cs[j] == t ? cs[j + 1] : nx;
+                if (OA_RWALK && NCAND == 3) {
+                    // or, pseudo-randomly, to the other one (breaks walk cycles)
+                    const uint32_t alt = cs[0] ^ cs[1] ^ cs[2] ^ t ^ nx;
+                    if (((uint32_t)old ^ (uint32_t)it_) & 1u) nx = alt;
+                }
+                t = nx;
                 v = old;
             }
         }
@@ -827,6 +870,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     STAMP(3);
+    DIAG((uint64_t)H.npend | ((uint64_t)H.pad1 << 20) | ((uint64_t)H.nstash << 40));
     if (H.overflow || nrow > (uint32_t)(KROWS * NWAVE)) {
         if (tid == 0) atomicOr(a.status, H.overflow ? OA_STATUS_TABLE_OVERFLOW : OA_STATUS_PLAN);
         return;
@@ -855,20 +899,22 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             lmin = uni(H.lstart[hs]);
             lmax = uni(H.lstart[hs + 1]) - lmin;
         }
-        uint32_t cs[3];
+        uint32_t cs[NCAND];
         cuckoo_slots(lo, nslots, cs);
-        const uint64_t c0 = slots[cs[0]], c1 = slots[cs[1]], c2 = slots[cs[2]];
+        uint64_t cv[NCAND];
+#pragma unroll
+        for (int j = 0; j < NCAND; ++j) cv[j] = slots[cs[j]];
         auto m = [&](uint64_t v) { return ((uint32_t)v == lo) & (slot_pos(v) - lmin < lmax); };
-        const bool m0 = can & m(c0), m1 = can & m(c1), m2 = can & m(c2);
-        uint64_t hit;
+        uint64_t hit = 0ull;
         if (IDB == 8 && nonuniform) {
             // rare: candidates whose low word matches are confirmed on the full ID
-            hit = 0ull;
-            if (m0 && ids[base + slot_pos(c0)] == pid[k]) hit = c0;
-            else if (m1 && ids[base + slot_pos(c1)] == pid[k]) hit = c1;
-            else if (m2 && ids[base + slot_pos(c2)] == pid[k]) hit = c2;
+#pragma unroll
+            for (int j = 0; j < NCAND; ++j)
+                if (!hit && can && m(cv[j]) && ids[base + slot_pos(cv[j])] == pid[k]) hit = cv[j];
         } else {
-            hit = m0 ? c0 : (m1 ? c1 : (m2 ? c2 : 0ull));
+            // (halo, low word) is unique in an item whose IDs share their high word
+#pragma unroll
+            for (int j = NCAND - 1; j >= 0; --j) hit = (can && m(cv[j])) ? cv[j] : hit;
         }
         if (nstash && can && !hit) {
             for (uint32_t e = 0; e < nstash; ++e) {
@@ -912,7 +958,9 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // the item's current r̂, from the registers phase 1 left it in
 #pragma unroll
     for (int k = 0; k < SU; ++k) {
-        const uint32_t li = (wave + NWAVE * k) * 64 + lane;
+        if (DYN && (uint32_t)(k / U1) >= ntrips) break;
+        const uint32_t li = DYN ? (tp[k / U1] * U1 + k % U1) * 64 + lane
+                                : (uint32_t)(wave + NWAVE * k) * 64 + lane;
         if (li < n_span) { rcx[li] = rr[k].x; rcy[li] = rr[k].y; rcz[li] = rr[k].z; }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -968,6 +1016,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             const uint32_t q = (uint32_t)__popcll(mk & lanemask_lt);
             __builtin_nontemporal_store(pid[k], &scr_ids[sb + q]);
             __builtin_nontemporal_store(a16, &a.scratch_ang[sb + q]);
+            if (a.scratch_pos) a.scratch_pos[sb + q] = (int32_t)(kb + lane);
         }
         if (lane == 0) {
             a.seg_count[sb >> 6] = (uint8_t)cnt;
@@ -1067,6 +1116,7 @@ __global__ __launch_bounds__(256) void k_gather_items(const oa_compact_args a) {
             const int64_t from = it.scratch_off + ((c0 + r) << 6) + (j - roff[r]);
             out[carry + j] = src[from];
             oang[carry + j] = a.scratch_ang[from];
+            if (a.out_pos) a.out_pos[dst + carry + j] = a.scratch_pos[from];
         }
         carry += tot;
         __syncthreads();
@@ -1453,6 +1503,7 @@ __global__ __launch_bounds__(BIG_WG) void k_big_join(const oa_step_args a) {
                 const int64_t pos = it.scratch_off + segpos + __popcll(m & lanemask_lt);
                 scr_ids[pos] = pid;
                 a.scratch_ang[pos] = a16;
+                if (a.scratch_pos) a.scratch_pos[pos] = (int32_t)(pbase + p);
             }
             if (lane == 0) {
                 const uint32_t c = (uint32_t)__popcll(m);
@@ -1614,6 +1665,8 @@ int oa_step(const oa_step_args *args, void *stream) {
                       (a.n_items > 0 && (!a.scratch_ids || !a.scratch_ang || !a.item_count ||
                                          !a.seg_count))))
         return fail(OA_E_ARG, "null previous-state / scratch pointer");
+    if (a.compare && a.scratch_pos && a.n_prev >= (int64_t)INT32_MAX)
+        return fail(OA_E_ARG, "scratch_pos: previous state of 2^31 rows or more");
     if (a.onthefly && a.compare && (!a.angle_out || !a.matched_prev || !a.matched_cur))
         return fail(OA_E_ARG, "null on-the-fly output pointer");
     if (a.n_gchunk1 > 0 && (!a.gchunk1 || !a.gtab || (a.compare && !a.gkeys)))
@@ -1642,6 +1695,7 @@ int oa_compact(const oa_compact_args *args, void *stream) {
     if (a.id_bytes != 4 && a.id_bytes != 8) return fail(OA_E_ARG, "id_bytes must be 4 or 8");
     if (!a.offsets_out || !a.total_out || (a.n_slots > 0 && !a.halo_count))
         return fail(OA_E_ARG, "null output pointer");
+    if (!a.out_pos != !a.scratch_pos) return fail(OA_E_ARG, "out_pos needs scratch_pos");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(k_scan_slots, dim3(1), dim3(1024), 0, st, a.halo_count, a.n_slots,
                        a.offsets_out, a.total_out);

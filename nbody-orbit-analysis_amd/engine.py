@@ -26,11 +26,12 @@ from . import _native as N
 F32, F64 = np.dtype(np.float32), np.dtype(np.float64)
 # LDS table sizes per work-group item, by r̂ dtype.  One item's LDS is
 # the header + max(8-byte cuckoo slots + 2 B/entry insert list, 3 r̂ components per
-# entry) + 1 B/entry of signs, within the CU's 160 KB:
+# entry) + 1 B/entry of signs, within the CU's 160 KB (the table and the r̂ arrays
+# overlay each other):
 #   float32 r̂: 11776 entries, 15456 slots (load <= 0.76)   -> 163,072 B
-#   float64 r̂:  6144 entries, 12288 slots (load <= 0.5)    -> 157,696 B
+#   float64 r̂:  6144 entries, 16896 slots (load <= 0.36)   -> 157,696 B
 DEFAULT_ENTRIES = {False: 11776, True: 6144}
-DEFAULT_SLOTS = {False: 15456, True: 12288}
+DEFAULT_SLOTS = {False: 15456, True: 16896}
 
 _TORCH_FROM_NP = {
     np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
@@ -265,6 +266,7 @@ class StepResult:
     apsis_ang: Optional[torch.Tensor] = None   # device int16 (f16 bits)
     total: Optional[torch.Tensor] = None       # device int64 scalar
     halos: Optional[torch.Tensor] = None       # device halo table (bulk written on device)
+    apsis_pos: Optional[torch.Tensor] = None   # device int32 previous-state rows (optional)
     extra: dict = field(default_factory=dict)
 
 
@@ -305,10 +307,11 @@ class Workspace:
 
     FIELDS = ('scratch', 'n_prev', 'n_slots', 'n_items')
 
-    def __init__(self, device, id_torch_dtype, scratch, n_prev, n_slots, n_items):
+    def __init__(self, device, id_torch_dtype, scratch, n_prev, n_slots, n_items,
+                 positions=False):
         def e(n, dt):
             return torch.empty(max(int(n), 1), dtype=dt, device=device)
-        self.device, self.id_dtype = device, id_torch_dtype
+        self.device, self.id_dtype, self.positions = device, id_torch_dtype, bool(positions)
         self.cap = dict(scratch=int(scratch), n_prev=int(n_prev), n_slots=int(n_slots),
                         n_items=int(n_items))
         self.scratch_ids = e(scratch, id_torch_dtype)
@@ -321,6 +324,9 @@ class Workspace:
         self.out_ids = e(n_prev, id_torch_dtype)
         self.out_ang = e(n_prev, torch.int16)
         self.total = e(1, torch.int64)
+        # apsis records' previous-state indices (the sharded driver's merge key)
+        self.scratch_pos = e(scratch, torch.int32) if positions else None
+        self.out_pos = e(n_prev, torch.int32) if positions else None
         self.status.zero_()
 
     @staticmethod
@@ -333,9 +339,10 @@ class Workspace:
         dt = torch.int64 if pr.plan.ids.itemsize == 8 else torch.int32
         return cls(device, dt, **cls.need(pr))
 
-    def fits(self, pr):
+    def fits(self, pr, positions=False):
         dt = torch.int64 if pr.plan.ids.itemsize == 8 else torch.int32
-        return dt == self.id_dtype and all(self.cap[k] >= v for k, v in self.need(pr).items())
+        return dt == self.id_dtype and self.positions >= bool(positions) and \
+            all(self.cap[k] >= v for k, v in self.need(pr).items())
 
     def reset(self, n_slots):
         """Per-launch zeroing (the status word accumulates: callers clear it)."""
@@ -365,6 +372,8 @@ class OrbitEngine:
             self.table_sizes(f64)                   # validates the LDS budget
         self.prev: Optional[SnapshotState] = None
         self._ws: Optional[Workspace] = None
+        # apsis records also carry their previous-state row (ShardedEngine's merge)
+        self.emit_positions = False
 
     def table_sizes(self, dx_f64, entries=None):
         """(entries, slots) of one k_step item for a float32 / float64 r̂."""
@@ -383,12 +392,12 @@ class OrbitEngine:
 
     def workspace(self, pr):
         """The engine's compare-step workspace, grown to fit ``pr``."""
-        if self._ws is None or not self._ws.fits(pr):
+        if self._ws is None or not self._ws.fits(pr, self.emit_positions):
             old = self._ws.cap if self._ws is not None else {}
             need = Workspace.need(pr)
             cap = {k: max(need[k], old.get(k, 0)) for k in need}
             dt = torch.int64 if pr.plan.ids.itemsize == 8 else torch.int32
-            self._ws = Workspace(self.device, dt, **cap)
+            self._ws = Workspace(self.device, dt, positions=self.emit_positions, **cap)
         return self._ws
 
     def reset(self):
@@ -573,6 +582,7 @@ class OrbitEngine:
             a.seg_count = ws.seg_count.data_ptr()
             a.halo_count, a.item_count, a.status = (ws.halo_count.data_ptr(),
                                                    ws.item_count.data_ptr(), ws.status.data_ptr())
+            a.scratch_pos = _ptr(ws.scratch_pos)
         if step_events is not None:
             step_events[0].record()
         N.check(lib.oa_step(a, st), 'oa_step')
@@ -590,9 +600,11 @@ class OrbitEngine:
         c.offsets_out, c.out_ids, c.out_ang = (ws.offsets.data_ptr(), ws.out_ids.data_ptr(),
                                                ws.out_ang.data_ptr())
         c.total_out = ws.total.data_ptr()
+        c.scratch_pos, c.out_pos = _ptr(ws.scratch_pos), _ptr(ws.out_pos)
         N.check(lib.oa_compact(c, st), 'oa_compact')
         res.offsets = ws.offsets[:res.n_slots + 1]
         res.apsis_ids, res.apsis_ang, res.total = ws.out_ids, ws.out_ang, ws.total
+        res.apsis_pos = ws.out_pos
         return res
 
     # ------------------------------------------------------------------ host views

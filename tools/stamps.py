@@ -34,14 +34,14 @@ torch.cuda.synchronize()
 ni = len(p1.items)
 nw = eng.lib.oa_build_info(0) // 64
 NP = 9                                            # STAMP_NP in orbit_hip.hip
-sn = NP + 3 * nw
+sn = NP + 3 * nw + 1
 buf = np.zeros(ni * sn, dtype=np.uint64)
 got = eng.lib.oa_debug_stamps(buf.ctypes.data, buf.size)
 assert got > 0, 'not a stamps build'
 tw = buf.reshape(ni, sn).astype(np.float64) * 10.0 / 1000.0   # 100 MHz -> us
 tw -= tw[:, 0].min()
 t = tw[:, [0, 1, 8, 2, 3, 4, 5, 6, 7]]           # stamps in phase order
-w1, w2, w3 = tw[:, NP::3], tw[:, NP + 1::3], tw[:, NP + 2::3]   # per-wave loop ends
+w1, w2, w3 = (tw[:, NP + j:NP + 3 * nw:3] for j in range(3))  # per-wave loop ends
 for name, w in (('wave skew phase1 end', w1), ('wave skew phase2a end', w2),
                 ('wave skew phase2b end', w3)):
     d = w.max(1) - w.min(1)
@@ -56,5 +56,10 @@ for name, a, b in (('phase0', 0, 1), ('phase1(t0)', 1, 2), ('2a-issue+bar', 2, 3
     d = t[:, b] - t[:, a]
     print('%-12s mean %7.2f  p10 %7.2f  p50 %7.2f  p90 %7.2f  max %7.2f us'
           % (name, d.mean(), *np.percentile(d, [10, 50, 90]), d.max()))
+dg = buf.reshape(ni, sn)[:, -1]
+npend, chain, nst = dg & 0xFFFFF, (dg >> 20) & 0xFFFFF, dg >> 40
+for name, v in (('deferred inserts', npend), ('longest walk', chain), ('stashed', nst)):
+    print('%-17s mean %8.1f  p50 %6d  p90 %6d  max %6d' % (name, v.mean(), np.percentile(v, 50),
+                                                          np.percentile(v, 90), v.max()))
 ts = np.linspace(0, end.max(), 12)
 print('alive:', [int(((start <= x) & (end > x)).sum()) for x in ts])
