@@ -6,8 +6,11 @@ particles per GPU in 1e4 halo region blocks, float32 coordinates/velocities with
 float32 catalogue centres and bulk velocities, int64 IDs, periodic box, Hubble term
 on.  A step = one snapshot of track_orbits' per-snapshot body on device-resident
 inputs: fused frame + ID join + sign flip + angles (oa_step) and the apsis output
-assembly (oa_compact).  Multi-GPU: particles sharded by ID range, weak scaling (1e8
-per GPU), one RCCL all-gather of the halo catalogue rows per snapshot.
+assembly (oa_compact); the host plan of each snapshot is built before the timing.
+Multi-GPU: the product's ShardedEngine, particles sharded by ID range (every rank
+generates its own range: presharded), one RCCL all-gather of the halo catalogue rows
+per snapshot inside the timed step; --scaling weak (1e8 per GPU, default) or strong
+(1e8 in total, configs[3]).
 
 Prints ONE JSON line on rank 0 (contract in the task statement): value =
 particle-snapshots/s over all ranks; roofline = algorithmic bytes of the oa_step
@@ -104,6 +107,9 @@ def main():
                     help='processes of the P-core CPU baseline (0: min(16, cpu_count): the '
                          'GPU box gives one GPU 16 host cores)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--scaling', default='weak', choices=['weak', 'strong'],
+                    help='weak: --particles per GPU (configs[2] per rank); strong: --particles '
+                         'in total over the ranks (configs[3])')
     ap.add_argument('--backend', default='nccl',
                     help="collective backend for N > 1 ('gloo': rehearsal with several "
                          "ranks on one GPU; collectives go through host memory)")
@@ -141,7 +147,10 @@ def main():
     from orbitanalysis_amd.utils import hubble_parameter
 
     t_setup = time.perf_counter()
-    gen = DevicePlummer(n_halos=args.halos, n_particles=int(args.particles), seed=0,
+    # weak: args.particles per GPU (configs[2] on every rank); strong: args.particles
+    # in total, each rank holding one ID range (configs[3])
+    per_rank = int(args.particles) if args.scaling == 'weak' else int(args.particles) // world
+    gen = DevicePlummer(n_halos=args.halos, n_particles=per_rank, seed=0,
                         rank=rank, world=world, device=dev, dtype=args.dtype)
     # one snapshot per step, none reused: every timed pair is (s - 1, s) of one orbit
     S = args.steps + args.warmup + 1
@@ -159,31 +168,34 @@ def main():
     exists = np.arange(args.halos)
     eng = OrbitEngine(mode=args.mode, device=dev)
 
-    # snapshot 0: frame only (the reference's i == istart), outside the timing
-    prep0 = eng.prepare(snaps[0], cats[0][0], cats[0][2], H, z, exists, False)
-    eng.launch(prep0, None)
-    chain = [(prep0, 0)]
-    layout = (prep0.starts, prep0.counts, exists, prep0.plan, prep0.n)
-    for t in range(1, args.warmup + args.steps + 1):
-        s = t
-        pr = eng.prepare(snaps[s], cats[s][0], cats[s][2], H, z, exists, True, prev_layout=layout)
-        chain.append((pr, s))
-        layout = (pr.starts, pr.counts, exists, pr.plan, pr.n)
-    preps = [c[0] for c in chain[1:]]
+    if world == 1:
+        # snapshot 0: frame only (the reference's i == istart), outside the timing
+        prep0 = eng.prepare(snaps[0], cats[0][0], cats[0][2], H, z, exists, False)
+        eng.launch(prep0, None)
+        chain = [(prep0, 0)]
+        layout = (prep0.starts, prep0.counts, exists, prep0.plan, prep0.n)
+        for t in range(1, args.warmup + args.steps + 1):
+            pr = eng.prepare(snaps[t], cats[t][0], cats[t][2], H, z, exists, True,
+                             prev_layout=layout)
+            chain.append((pr, t))
+            layout = (pr.starts, pr.counts, exists, pr.plan, pr.n)
+        preps = [c[0] for c in chain[1:]]
+    else:
+        # the product's multi-GPU path: ShardedEngine over this rank's ID range (the
+        # generator hands every rank its own rows: presharded), one all-gather of the
+        # halo catalogue rows per snapshot inside the timed launch
+        from orbitanalysis_amd.sharding import ShardedEngine, EngineLocal
+        seng = ShardedEngine(EngineLocal(eng), presharded=True)
+        sp0 = seng.prepare(snaps[0], cats[0][0], cats[0][2], H, z, exists, False)
+        seng.launch(sp0)
+        chain = [(sp0, 0)]
+        for t in range(1, args.warmup + args.steps + 1):
+            chain.append((seng.prepare(snaps[t], cats[t][0], cats[t][2], H, z, exists, True,
+                                       prev=chain[-1][0]), t))
+        preps = [c[0].lp for c in chain[1:]]
     for p in preps:
         ws = eng.workspace(p)                 # grown to the largest step
-    # catalogue exchange (N > 1): rank r holds catalogue rows [r*nl, (r+1)*nl)
-    nl = -(-args.halos // world)
-    cat_local, cat_all = [], None
-    if world > 1:
-        cat_all = torch.empty(nl * world, 6, dtype=torch.float64, device=cdev)
-        for pr in preps:
-            hv = pr.halos.view(torch.float64).view(args.halos, 12)
-            rows = torch.zeros(nl, 6, dtype=torch.float64, device=dev)
-            lo, hi = rank * nl, min((rank + 1) * nl, args.halos)
-            if hi > lo:
-                rows[:hi - lo] = hv[lo:hi, 4:10]
-            cat_local.append(rows.to(cdev))
+    ws.status.zero_()
     log('setup %.1f s; items/step %d (large halos %d)'
         % (time.perf_counter() - t_setup, preps[0].n_small, preps[0].n_global))
 
@@ -194,10 +206,10 @@ def main():
         pr, s = chain[k + 1]
         prev_pr, ps = chain[k]
         if world > 1:
-            dist.all_gather_into_tensor(cat_all, cat_local[k])
-            pr.halos.view(torch.float64).view(args.halos, 12)[:, 4:10] = \
-                cat_all[:args.halos].to(dev, non_blocking=True)
-        eng.launch(pr, ws, State(snaps[ps]['ids'], prev_pr.rhat, prev_pr.meta), step_events=events)
+            seng.launch(pr, prev=prev_pr, step_events=events, check=False)
+        else:
+            eng.launch(pr, ws, State(snaps[ps]['ids'], prev_pr.rhat, prev_pr.meta),
+                       step_events=events)
 
     for k in range(args.warmup):
         run(k)
@@ -213,7 +225,7 @@ def main():
         barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    units = sum(chain[args.warmup + i + 1][0].n for i in range(args.steps))
+    units = sum(preps[args.warmup + i].n for i in range(args.steps))
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -225,11 +237,10 @@ def main():
     if status:
         raise RuntimeError('oa_step reported status %#x (table overflow) during the bench' % status)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    last = chain[-1][0]
+    last = preps[-1]
     n_apsis = int(ws.total.item())
-    bytes_launch = float(np.mean([step_bytes(chain[args.warmup + i + 1][0],
-                                             chain[args.warmup + i + 1][0].n_prev, n_apsis)
-                                  for i in range(args.steps)]))
+    bytes_launch = float(np.mean([step_bytes(preps[args.warmup + i], preps[args.warmup + i].n_prev,
+                                             n_apsis) for i in range(args.steps)]))
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     log('elapsed %.4f s for %d steps; k_step %.3f ms; %.1f GB/s; apsis %d'
         % (elapsed, args.steps, kern_ms, achieved, n_apsis))
@@ -241,7 +252,7 @@ def main():
             pj = json.load(f)
         # only for the workload the counters were collected on
         if (pj.get('particles'), pj.get('halos'), pj.get('n_gpus', 1)) == \
-                (int(args.particles), args.halos, world):
+                (per_rank, args.halos, 1):
             traffic = pj.get('hbm_bytes_per_launch')
 
     cpu = None
@@ -278,21 +289,25 @@ def main():
             'metric': METRIC, 'value': units / elapsed, 'unit': 'particle-snapshots/s',
             'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': elapsed / args.steps * 1e3, 'higher_is_better': True,
-            'scaling': 'weak', 'vs_baseline': None,
+            'scaling': args.scaling, 'vs_baseline': None,
             'dtype': last.plan.coord.name.replace('float', 'f'),
             'data': 'synthetic: %d Plummer spheres (device-generated, AHW sampling, leapfrog '
                     'orbits), region cut r<4a, per-snapshot shuffled blocks, int64 randperm IDs'
                     % args.halos,
-            'config': {'workload': 'BASELINE configs[%d]: %.0e particles/GPU, %d halos, %s '
+            'config': {'workload': 'BASELINE configs[%d]: %.0e particles%s, %d halos, %s '
                                    'coords/vels/centres, catalogue bulk velocities, periodic '
                                    'box, Hubble term, %s'
-                                   % (2 if args.dtype == 'float32' else 1, args.particles,
+                                   % ((3 if args.scaling == 'strong' else 2)
+                                      if args.dtype == 'float32' else 1, args.particles,
+                                      '/GPU' if args.scaling == 'weak' else ' in total',
                                       args.halos, last.plan.coord.name.replace('float', 'f'),
                                       args.mode),
                        'particles_per_step_per_gpu': int(last.n),
                        'halos': args.halos, 'work_items': int(last.n_small),
                        'large_halos': int(last.n_global),
-                       'parallelism': 'id-range shards x%d' % world},
+                       'parallelism': 'id-range shards x%d (ShardedEngine, presharded; one '
+                                      'catalogue all-gather per snapshot)' % world
+                                      if world > 1 else 'single GPU'},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
                          'traffic': traffic, 'kernel': 'k_step', 'kernel_ms': kern_ms,

@@ -1,37 +1,51 @@
-"""Multi-GPU orbit tagging: particles sharded by ID across ranks.
+"""Multi-GPU orbit tagging: particles sharded by ID range across ranks.
 
 One process per GPU, ``torch.distributed`` (RCCL on MI355X, gloo on CPU).  Every
-rank runs the same ``track_orbits`` driver; the loader may return the whole
-snapshot on every rank (the reference's callback contract, track_orbits.py:118-122)
-and each rank keeps the rows whose ID it owns.  Because ownership is a function of
-the ID, a particle's current and previous rows -- including its copies in
-overlapping regions -- sit on the same rank, so the join needs no exchange: the
-data path is collective-free and scales weakly.
+rank runs the same ``track_orbits`` driver.  The reference's only parallel axis is
+the halo pool of track_orbits.py:189-194; here the axis is the particle ID instead:
+rank r owns the IDs of one contiguous range (``IdRangeOwner``, the default), so a
+particle's current and previous rows -- including its copies in overlapping regions
+-- sit on the same rank, and the join needs no exchange.  The data path is
+collective-free and everything in it stays on the rank's device:
 
-Collectives per snapshot (small, all-gather only):
+* **shard**: with a loader that returns the whole snapshot on every rank (the
+  reference's callback contract, track_orbits.py:118-122), each rank moves it to its
+  GPU once and keeps its rows with a device mask + compaction (the block order is
+  preserved, and every kept row remembers its position in its global block, gpos).
+  A *presharded* loader (``presharded=True``, e.g. a distributed reader) hands each
+  rank its own rows directly; the global block is then the rank-ordered
+  concatenation of the ranks' blocks.
+* **step**: the rank's ``OrbitEngine`` on its shard; the kernel also emits each apsis
+  record's previous-state row, which maps to its global previous-block position
+  through the previous snapshot's gpos (a device gather).
+* **records** stay on the device as (halo slot << 32 | gpos, ID, f16 angle).
 
+Collectives per snapshot (all small):
+
+* one all-gather of the halo catalogue rows (centre, bulk velocity): every rank then
+  uses rank 0..N-1's identical rows (the north star's "all-gather of halo centres");
 * bulk velocities computed from the particles (no catalogue value,
   track_orbits.py:269-280) are sequential sums over a WHOLE block, which no
-  partial-sum exchange reproduces bit-for-bit; halo j's owner rank (j % world)
-  computes them on the full block and the rows are all-gathered;
-* apsis records (halo slot, position in the global previous block, ID, f16 angle)
-  are all-gathered and merged by (slot, position): exactly the reference's output
-  order (prev-block order within each halo, halos in ``halo_exists`` order,
-  track_orbits.py:199-227, 315-316);
-* checkpoint angles are all-gathered with their global row index.
+  partial-sum exchange reproduces bit for bit: halo j's owner rank (j % world)
+  computes them on the full block and the rows are all-gathered (not available with
+  presharded snapshots);
+* output: ``fetch`` (the savefile path, outside the per-snapshot tagging) all-gathers
+  the records and sorts them by key -- exactly the reference's order (previous-block
+  order within each halo, halos in ``halo_exists`` order, track_orbits.py:199-227,
+  315-316).  Checkpoint angles are gathered with their global row index.
 
 ``ShardedEngine`` exposes the ``OrbitEngine`` interface the driver uses, so
-``track_orbits(..., engine=ShardedEngine(...))`` is the multi-GPU drop-in.  The
-per-rank compute is a *local* object with ``step`` / ``angles`` / ``bulk``;
-``EngineLocal`` wraps the HIP engine (the product path).
+``track_orbits(..., engine=ShardedEngine(EngineLocal(OrbitEngine())))`` is the
+multi-GPU drop-in.
 """
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Optional
 
 import numpy as np
 import torch
 
 U64 = np.uint64
+_HASH_C = np.int64(-7046029254386353131)        # 0x9E3779B97F4A7C15 as int64
 
 
 # ------------------------------------------------------------------ ownership
@@ -39,21 +53,46 @@ class HashOwner:
     """rank = hash(ID) mod world (balanced for any ID distribution)."""
 
     def __call__(self, ids, world):
-        h = np.asarray(ids).astype(np.int64, copy=False).view(U64) * U64(0x9E3779B97F4A7C15)
-        return ((h >> U64(33)) % U64(world)).astype(np.int64)
+        h = np.asarray(ids).astype(np.int64, copy=False) * _HASH_C     # wrapping int64
+        return ((h >> 33) & 0x7FFFFFFF) % world
+
+    def fit(self, ids):
+        pass
+
+    def mask(self, ids_t, world, rank):
+        h = ids_t.to(torch.int64) * int(_HASH_C)
+        return ((h >> 33) & 0x7FFFFFFF) % world == rank
 
 
 class IdRangeOwner:
-    """rank = floor((ID - lo) * world / (hi - lo)): contiguous ID ranges."""
+    """rank = floor((ID - lo) * world / (hi - lo)), clipped: contiguous ID ranges.
+    Without bounds, [lo, hi) is taken from the first snapshot the engine sees (every
+    rank sees the same one); later IDs outside it go to the first / last rank."""
 
-    def __init__(self, lo, hi):
-        self.lo, self.hi = int(lo), int(hi)
+    def __init__(self, lo=None, hi=None):
+        self.lo = None if lo is None else int(lo)
+        self.hi = None if hi is None else int(hi)
+
+    def fit(self, ids):
+        if self.lo is not None:
+            return
+        if isinstance(ids, torch.Tensor):
+            lo, hi = (int(ids.min()), int(ids.max()) + 1) if ids.numel() else (0, 1)
+        else:
+            ids = np.asarray(ids)
+            lo, hi = (int(ids.min()), int(ids.max()) + 1) if ids.size else (0, 1)
+        self.lo, self.hi = lo, hi
 
     def __call__(self, ids, world):
         ids = np.asarray(ids).astype(np.int64)
         span = max(self.hi - self.lo, 1)
         r = ((ids - self.lo).astype(np.float64) * world / span).astype(np.int64)
         return np.clip(r, 0, world - 1)
+
+    def mask(self, ids_t, world, rank):
+        span = max(self.hi - self.lo, 1)
+        r = ((ids_t.to(torch.int64) - self.lo).to(torch.float64) * world / span).to(torch.int64)
+        return r.clamp_(0, world - 1) == rank
 
 
 def block_layout(region_offsets, n):
@@ -63,10 +102,9 @@ def block_layout(region_offsets, n):
 
 
 def shard_snapshot(snapshot, keep):
-    """Rows of ``snapshot`` selected by boolean ``keep`` (block order preserved).
-
-    Returns (shard dict, global row index of every kept row, shard block starts,
-    shard block counts)."""
+    """Host reference of the device shard (tests): rows of ``snapshot`` selected by
+    boolean ``keep`` (block order preserved).  Returns (shard dict, global row index of
+    every kept row, shard block starts, shard block counts)."""
     ids = np.asarray(snapshot['ids'])
     n = len(ids)
     starts, counts = block_layout(snapshot['region_offsets'], n)
@@ -92,29 +130,38 @@ def _comm_device():
 
 
 def allgather_rows(a, group=None):
-    """Variable-length all-gather of a 2-D int64 array; rank-ordered concatenation."""
+    """Variable-length all-gather of a 2-D int64 array (host); rank-ordered concatenation."""
+    t = allgather_v(torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64)), group)
+    return t.cpu().numpy()
+
+
+def allgather_v(t, group=None):
+    """Variable-length all-gather of a tensor along dim 0 (device tensors over RCCL
+    with the nccl backend, host tensors with gloo); rank-ordered concatenation, on
+    the communication device."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
     dev = _comm_device()
-    a = np.ascontiguousarray(a, dtype=np.int64)
-    if a.ndim != 2:
-        raise ValueError('allgather_rows expects a 2-D array')
-    width = a.shape[1]
-    n = torch.tensor([a.shape[0]], dtype=torch.int64, device=dev)
+    t = t.to(dev)
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=dev)
     ns = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(ns, n, group=group)
     ns = [int(x.item()) for x in ns]
     m = max(max(ns), 1)
-    buf = torch.zeros((m, width), dtype=torch.int64, device=dev)
-    if a.shape[0]:
-        buf[:a.shape[0]] = torch.from_numpy(a).to(dev)
+    buf = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+    buf[:t.shape[0]] = t
     outs = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(outs, buf, group=group)
-    return np.concatenate([o[:k].cpu().numpy() for o, k in zip(outs, ns)], axis=0)
+    return torch.cat([o[:k] for o, k in zip(outs, ns)], dim=0)
 
 
 def _f64_bits(x):
     return np.ascontiguousarray(x, dtype=np.float64).view(np.int64)
+
+
+def _as_i64(t):
+    """IDs of any 32/64-bit integer dtype as int64 values (bit pattern kept for 64-bit)."""
+    return t if t.dtype == torch.int64 else t.to(torch.int64)
 
 
 # ------------------------------------------------------------------ engine facade
@@ -122,22 +169,24 @@ def _f64_bits(x):
 class ShardedResult:
     n_slots: int
     has_prog: np.ndarray
-    offsets: Optional[np.ndarray] = None
-    ids: Optional[np.ndarray] = None
-    angles: Optional[np.ndarray] = None
+    records: Optional[tuple] = None          # device (offsets, ids, f16 bits, prev-state row)
+    gpos_prev: Optional[torch.Tensor] = None # previous shard row -> global block position
     bulk: Optional[np.ndarray] = None
 
 
 @dataclass
-class _Prev:
-    ids: np.ndarray            # shard IDs (loader dtype), shard order
-    gpos: np.ndarray           # position of each shard row inside its global block
-    starts: np.ndarray         # shard block starts / counts per halo
-    counts: np.ndarray
+class ShardedPrep:
+    """One snapshot's host half (ShardedEngine.prepare): the shard, its rows' global
+    block positions and the local engine's prepared step."""
+    n: int
     exists: np.ndarray
-    plan: object = None
-    sel: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int64))
-    n_global: int = 0
+    compare: bool
+    gpos: torch.Tensor
+    sel: Optional[torch.Tensor]
+    rows: Optional[np.ndarray]              # catalogue rows (centre, bulk) to exchange
+    bulk_out: Optional[np.ndarray]
+    plan: object
+    lp: object = None
 
 
 class _Plan:
@@ -147,21 +196,44 @@ class _Plan:
 
 
 class ShardedEngine:
-    """``OrbitEngine`` interface over ID-sharded ranks (see module docstring)."""
+    """``OrbitEngine`` interface over ID-sharded ranks (see module docstring).
 
-    def __init__(self, local, group=None, owner=None, mode=None):
+    ``step`` = ``prepare`` (host: shard, plan, uploads) + ``launch`` (the catalogue
+    all-gather and the device step).  The two halves are public so a benchmark can
+    prepare a chain of snapshots and time ``launch`` alone, as bench.py does."""
+
+    def __init__(self, local, group=None, owner=None, mode=None, presharded=False,
+                 share_catalogue=True):
         import torch.distributed as dist
         self.local = local
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
-        self.owner = owner or HashOwner()
+        self.owner = owner or IdRangeOwner()
         self.mode = mode or local.mode
-        self.prev: Optional[_Prev] = None
+        self.presharded = bool(presharded)
+        self.share_catalogue = bool(share_catalogue)
+        self.device = getattr(local, 'device', torch.device('cpu'))
+        self.prev: Optional[ShardedPrep] = None
 
     def reset(self):
         self.prev = None
         self.local.reset()
+
+    # ---------------------------------------------------------------- collectives
+    def _exchange(self, rows, nh):
+        """The one per-snapshot all-gather of catalogue rows: rank r contributes halos
+        [r * nl, (r + 1) * nl) of its (nh, 6) float64 rows; every rank gets all nh."""
+        import torch.distributed as dist
+        nl = -(-nh // self.world)
+        mine = np.zeros((nl, 6), dtype=np.float64)
+        lo, hi = self.rank * nl, min((self.rank + 1) * nl, nh)
+        if hi > lo:
+            mine[:hi - lo] = rows[lo:hi]
+        dev = _comm_device()
+        out = torch.empty((nl * self.world, 6), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(out, torch.from_numpy(mine).to(dev), group=self.group)
+        return out[:nh]
 
     def _bulk(self, snapshot, nh):
         own = np.flatnonzero(np.arange(nh) % self.world == self.rank)
@@ -177,60 +249,131 @@ class ShardedEngine:
         out[allr[:, 0]] = allr[:, 1:].copy().view(np.float64)
         return out.astype(np.float32 if size == 4 else np.float64)
 
-    def step(self, snapshot, centres, bulk_cat, H, z, exists, compare, angles_in=None):
+    # ---------------------------------------------------------------- shard
+    def _tensor(self, x):
+        if isinstance(x, torch.Tensor):
+            return x.to(self.device)
+        a = np.ascontiguousarray(x)
+        if a.dtype.kind == 'u':
+            a = a.view(a.dtype.str.replace('u', 'i'))
+        return torch.from_numpy(a).to(self.device)
+
+    def _shard(self, snapshot, starts, counts):
+        """Device shard of a whole snapshot: this rank's rows, block order kept."""
+        nh = len(starts)
+        ids_t = self._tensor(snapshot['ids'])
+        self.owner.fit(ids_t)
+        keep = self.owner.mask(ids_t, self.world, self.rank)
+        sel = torch.nonzero(keep).squeeze(1)
+        st_t = torch.from_numpy(starts).to(self.device)
+        block = torch.searchsorted(st_t, sel, right=True) - 1 if nh else sel
+        cnt = torch.bincount(block, minlength=nh) if nh else torch.zeros(0, dtype=torch.int64)
+        gpos = sel - st_t[block] if nh else sel
+        shard = dict(snapshot)
+        shard['ids'] = ids_t[sel]
+        for k in ('coordinates', 'velocities'):
+            shard[k] = self._tensor(snapshot[k]).reshape(-1, 3)[sel]
+        if isinstance(snapshot['masses'], (np.ndarray, torch.Tensor)):
+            shard['masses'] = self._tensor(snapshot['masses'])[sel]
+        cnt_h = cnt.cpu().numpy().astype(np.int64)
+        shard['region_offsets'] = np.concatenate([[0], np.cumsum(cnt_h)[:-1]]).astype(np.int64) \
+            if nh else cnt_h
+        return shard, sel, gpos
+
+    def _presharded_gpos(self, starts, counts):
+        """Global block = the ranks' blocks concatenated in rank order: a shard row's
+        position is the rows of lower ranks in its block + its own index."""
+        cnt_all = allgather_v(torch.from_numpy(counts.astype(np.int64))[None, :], self.group)
+        before = cnt_all[:self.rank].sum(0).to(self.device) if self.rank else \
+            torch.zeros(len(counts), dtype=torch.int64, device=self.device)
+        c = torch.from_numpy(counts).to(self.device)
+        block = torch.repeat_interleave(torch.arange(len(counts), device=self.device), c)
+        local = torch.arange(int(c.sum()), device=self.device) - \
+            torch.from_numpy(starts).to(self.device)[block]
+        return before[block] + local
+
+    # ---------------------------------------------------------------- step
+    def prepare(self, snapshot, centres, bulk_cat, H, z, exists, compare, angles_in=None,
+                prev=None):
+        """Host half of a step; ``prev`` (a ShardedPrep) defaults to the last step."""
         exists = np.asarray(exists)
-        ids = np.asarray(snapshot['ids'])
-        n = len(ids)
+        ids = snapshot['ids']
+        n = int(ids.numel()) if isinstance(ids, torch.Tensor) else len(ids)
         starts, counts = block_layout(snapshot['region_offsets'], n)
         nh = len(starts)
         bulk = bulk_cat
         if bulk_cat is None and nh:
+            if self.presharded:
+                raise NotImplementedError('computed bulk velocities need whole blocks: give '
+                                          'catalogue bulk velocities with presharded snapshots')
             bulk = self._bulk(snapshot, nh)
-        keep = self.owner(ids, self.world) == self.rank
-        shard, sel, st, cnt = shard_snapshot(snapshot, keep)
-        gpos = sel - np.repeat(starts, counts)[sel] if n else sel
-        a_in = None if angles_in is None else np.asarray(angles_in)[sel]
-        out = self.local.step(shard, centres, bulk, H, z, exists, compare, a_in)
-        res = ShardedResult(n_slots=0, has_prog=np.zeros(nh, dtype=bool), bulk=(
-            None if bulk_cat is not None else bulk))
-        if compare:
-            p = self.prev
-            has_prog = np.isin(exists, p.exists)
-            hinds = np.flatnonzero(has_prog)
-            res.has_prog, res.n_slots = has_prog, len(hinds)
-            offs, a_ids, a_ang = out
-            recs = []
-            for k, j in enumerate(hinds):
-                lo, hi = int(offs[k]), int(offs[k + 1])
-                if hi == lo:
-                    continue
-                q = int(np.searchsorted(p.exists, exists[j]))
-                a, b = int(p.starts[q]), int(p.starts[q] + p.counts[q])
-                blk = p.ids[a:b]
-                sorter = np.argsort(blk, kind='stable')
-                idx = sorter[np.searchsorted(blk, a_ids[lo:hi], sorter=sorter)]
-                r = np.empty((hi - lo, 4), dtype=np.int64)
-                r[:, 0] = k
-                r[:, 1] = p.gpos[a:b][idx]
-                r[:, 2] = np.asarray(a_ids[lo:hi]).astype(np.int64, copy=False)
-                r[:, 3] = np.asarray(a_ang[lo:hi]).view(np.uint16)
-                recs.append(r)
-            mine = np.concatenate(recs) if recs else np.zeros((0, 4), dtype=np.int64)
-            allr = allgather_rows(mine, self.group)
-            order = np.lexsort((allr[:, 1], allr[:, 0]))
-            allr = allr[order]
-            res.offsets = np.concatenate([[0], np.cumsum(
-                np.bincount(allr[:, 0], minlength=len(hinds)))]).astype(np.int64)
-            res.ids = allr[:, 2].astype(ids.dtype)
-            res.angles = allr[:, 3].astype(np.uint16).view(np.float16)
-        self.prev = _Prev(ids=shard['ids'], gpos=gpos, starts=st, counts=cnt, exists=exists,
-                          plan=_Plan(ids.dtype, None if bulk is None else
-                                     np.asarray(bulk).dtype),
-                          sel=sel, n_global=n)
+        if self.presharded:
+            shard, sel = dict(snapshot), None
+            gpos = self._presharded_gpos(starts, counts)
+            a_in = angles_in
+        else:
+            shard, sel, gpos = self._shard(snapshot, starts, counts)
+            a_in = None if angles_in is None else np.asarray(angles_in)[sel.cpu().numpy()]
+        rows = None
+        if self.share_catalogue and nh:
+            rows = np.zeros((nh, 6), dtype=np.float64)
+            rows[:, :3] = np.asarray(centres, dtype=np.float64).reshape(nh, 3)
+            if bulk_cat is not None:
+                rows[:, 3:] = np.asarray(bulk_cat, dtype=np.float64).reshape(nh, 3)
+        p = prev if prev is not None else self.prev
+        ids_dt = np.asarray(ids[:0].cpu() if isinstance(ids, torch.Tensor) else ids[:0]).dtype
+        sp = ShardedPrep(n=n, exists=exists, compare=bool(compare), gpos=gpos, sel=sel,
+                         rows=rows, bulk_out=None if bulk_cat is not None else bulk,
+                         plan=_Plan(ids_dt, None if bulk is None else np.asarray(bulk).dtype))
+        sp.lp = self.local.prepare(shard, centres, bulk, H, z, exists, compare, a_in,
+                                   None if (prev is None or p is None) else p.lp,
+                                   share=bulk_cat is not None)
+        return sp
+
+    def launch(self, sp, prev=None, step_events=None, check=True):
+        """Device half: the catalogue all-gather (written into the device halo table),
+        then the local step.  Records stay on the device (``fetch`` gathers them)."""
+        p = prev if prev is not None else self.prev
+        nh = len(sp.exists)
+        if sp.rows is not None:
+            self.local.set_catalogue(sp.lp, self._exchange(sp.rows, nh))
+        out = self.local.launch(sp.lp, None if prev is None else prev.lp, step_events, check)
+        res = ShardedResult(n_slots=0, has_prog=np.zeros(nh, dtype=bool), bulk=sp.bulk_out)
+        if sp.compare:
+            has_prog = np.isin(sp.exists, p.exists)
+            res.has_prog, res.n_slots = has_prog, int(has_prog.sum())
+            res.records, res.gpos_prev = out, p.gpos
         return res
 
+    def step(self, snapshot, centres, bulk_cat, H, z, exists, compare, angles_in=None):
+        if compare and self.prev is None:
+            raise RuntimeError('compare step without a previous snapshot')
+        sp = self.prepare(snapshot, centres, bulk_cat, H, z, exists, compare, angles_in)
+        res = self.launch(sp)
+        self.prev = sp
+        return res
+
+    # ---------------------------------------------------------------- outputs
     def fetch(self, res, ids_dtype):
-        return res.offsets, res.ids.astype(ids_dtype, copy=False), res.angles
+        """Gather every rank's records and put them in the reference's order: key =
+        halo slot << 32 | position in the global previous block."""
+        offs, a_ids, a_ang, a_pos = res.records
+        total = int(offs[-1])
+        slot = torch.repeat_interleave(torch.arange(res.n_slots, device=offs.device),
+                                       (offs[1:] - offs[:-1]).long())
+        g = res.gpos_prev[a_pos[:total].to(res.gpos_prev.device).long()]
+        key = allgather_v((slot.to(g.device) << 32) | g, self.group)
+        ids = allgather_v(_as_i64(a_ids[:total]), self.group)
+        ang = allgather_v(a_ang[:total].to(torch.int32), self.group)   # (gloo has no int16)
+        order = torch.argsort(key)
+        key, ids, ang = key[order], ids[order], ang[order]
+        cnt = torch.bincount((key >> 32).long(), minlength=res.n_slots)[:res.n_slots] \
+            if key.numel() else torch.zeros(res.n_slots, dtype=torch.int64)
+        offsets = np.concatenate([[0], np.cumsum(cnt.cpu().numpy())]).astype(np.int64)
+        dt = np.dtype(ids_dtype)
+        ids_h = ids.cpu().numpy()
+        ids_h = ids_h.view(np.uint64).astype(dt) if dt.kind == 'u' else ids_h.astype(dt)
+        return offsets, ids_h, ang.cpu().numpy().astype(np.uint16).view(np.float16)
 
     def bulk_velocities(self, res, plan):
         return res.bulk
@@ -238,11 +381,13 @@ class ShardedEngine:
     def angles(self):
         """Global float16 angle state in current-snapshot order (checkpoint payload)."""
         p = self.prev
-        loc = np.asarray(self.local.angles()).astype(np.float16).view(np.uint16)
-        rows = np.stack([p.sel.astype(np.int64), loc.astype(np.int64)], axis=1) \
-            if len(loc) else np.zeros((0, 2), dtype=np.int64)
-        allr = allgather_rows(rows, self.group)
-        out = np.zeros(p.n_global, dtype=np.uint16)
+        if p.sel is None:
+            raise NotImplementedError('checkpoint angles of presharded snapshots')
+        loc = self.local.angles_tensor().to(torch.int64)
+        rows = torch.stack([p.sel.to(loc.device), loc], dim=1) if loc.numel() else \
+            torch.zeros((0, 2), dtype=torch.int64)
+        allr = allgather_v(rows, self.group).cpu().numpy()
+        out = np.zeros(p.n_global if hasattr(p, 'n_global') else p.n, dtype=np.uint16)
         out[allr[:, 0]] = allr[:, 1].astype(np.uint16)
         return out.view(np.float16)
 
@@ -253,19 +398,72 @@ class EngineLocal:
     def __init__(self, engine):
         self.engine = engine
         self.mode = engine.mode
+        self.device = engine.device
+        engine.emit_positions = True
 
     def reset(self):
         self.engine.reset()
 
-    def step(self, snapshot, centres, bulk, H, z, exists, compare, angles_in):
-        res = self.engine.step(snapshot, centres, bulk, H, z, exists, compare,
-                               angles_in=angles_in)
-        if not compare:
-            return None
-        return self.engine.fetch(res, self.engine.prev.plan.ids)
+    def prepare(self, shard, centres, bulk, H, z, exists, compare, angles_in, prev_lp, share):
+        from .engine import SnapshotState  # noqa: F401
+        eng = self.engine
+        layout = None
+        if compare and prev_lp is not None:
+            layout = (prev_lp.starts, prev_lp.counts, prev_lp.exists, prev_lp.plan, prev_lp.n)
+        lp = eng.prepare(shard, centres, bulk, H, z, exists, compare, angles_in=angles_in,
+                         plan_src=shard, prev_layout=layout)
+        lp.exists = np.asarray(exists)
+        lp.src = (shard, centres, bulk, H, z, exists, compare, angles_in, layout)
+        lp.share_bulk = bool(share)
+        return lp
 
-    def angles(self):
-        return self.engine.angles()
+    def set_catalogue(self, lp, rows):
+        """The exchanged catalogue rows into the device halo table (centre, and the
+        bulk velocity when it comes from the catalogue)."""
+        hv = lp.halos.view(torch.float64).view(-1, 12)
+        hi = 10 if lp.share_bulk else 7
+        hv[:, 4:hi] = rows[:, :hi - 4].to(hv.device, non_blocking=True)
+
+    def launch(self, lp, prev_lp, step_events=None, check=True):
+        from .engine import SnapshotState
+        from . import _native as N
+        eng = self.engine
+        for _ in range(10):
+            ws = eng.workspace(lp) if lp.compare else None
+            prev = None
+            if lp.compare and prev_lp is not None:
+                prev = SnapshotState(ids=prev_lp.snap['ids'], rhat=prev_lp.rhat, meta=prev_lp.meta,
+                                     starts=prev_lp.starts, counts=prev_lp.counts,
+                                     exists=prev_lp.exists, plan=prev_lp.plan)
+            if check and ws is not None:
+                ws.status.zero_()
+            res = eng.launch(lp, ws, prev=prev, step_events=step_events)
+            st = int(ws.status.item()) if (check and ws is not None) else 0
+            if not st:
+                break
+            if st & N.STATUS_PLAN:
+                raise RuntimeError('oa_step: an item exceeds the kernel limits (planner bug)')
+            # re-plan with smaller items, finally all on the global-table path
+            shard, centres, bulk, H, z, exists, compare, angles_in, layout = lp.src
+            e = lp.entries
+            hv = lp.halos.view(torch.float64).view(-1, 12)[:, 4:10].clone()
+            lp2 = eng.prepare(shard, centres, bulk, H, z, exists, compare, angles_in=angles_in,
+                              plan_src=shard, prev_layout=layout,
+                              entries=0 if e <= 256 else max(256, e // 2))
+            lp2.halos.view(torch.float64).view(-1, 12)[:, 4:10] = hv
+            lp2.exists, lp2.src, lp2.share_bulk = lp.exists, lp.src, lp.share_bulk
+            lp.__dict__.update(lp2.__dict__)
+        else:
+            raise RuntimeError('LDS hash tables kept overflowing')
+        eng.prev = SnapshotState(ids=lp.snap['ids'], rhat=lp.rhat, meta=lp.meta, starts=lp.starts,
+                                 counts=lp.counts, exists=lp.exists, plan=lp.plan)
+        if not lp.compare:
+            return None
+        return res.offsets, res.apsis_ids, res.apsis_ang, res.apsis_pos
+
+    def angles_tensor(self):
+        """float16 bits of the current angle state (low half of the meta words)."""
+        return self.engine.prev.meta & 0xFFFF
 
     def bulk(self, snapshot, halo_idx):
         return self.engine.block_bulk(snapshot, halo_idx)

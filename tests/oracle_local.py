@@ -5,8 +5,13 @@ stand-in lets them exercise the product's sharding / collective / merge logic
 (nbody-orbit-analysis_amd/sharding.py) with the oracle as the per-rank step.  It is
 test infrastructure, like the oracle itself."""
 import numpy as np
+import torch
 
 from oracle import orbit_oracle as O
+
+
+def _np(x):
+    return x.numpy() if isinstance(x, torch.Tensor) else x
 
 
 class OracleLocal:
@@ -18,10 +23,11 @@ class OracleLocal:
         self.prev = None
 
     def step(self, snap, centres, bulk, H, z, exists, compare, angles_in):
+        snap = {k: _np(v) for k, v in snap.items()}
         n = len(snap['ids'])
         starts = np.asarray(snap['region_offsets'], dtype=np.int64)
         ends = np.append(starts[1:], n)
-        rh_l, vr_l, ang_l, a_ids, a_ang = [], [], [], [], []
+        rh_l, vr_l, ang_l, a_ids, a_ang, a_pos = [], [], [], [], [], []
         p = self.prev
         for j, hind in enumerate(exists):
             sl = (starts[j], ends[j])
@@ -36,6 +42,8 @@ class OracleLocal:
                 angs, aang = O.calc_angles(nj, p['angles'][a:b], d)
                 a_ids.append(d['apsis_ids'])
                 a_ang.append(aang)
+                kept = np.delete(np.arange(b - a), d['inds_departed'])
+                a_pos.append(a + kept[d['apsis_inds']])    # previous-state rows
             rh_l.append(rh.reshape(-1, 3))
             vr_l.append(vr)
             ang_l.append(angs)
@@ -51,12 +59,37 @@ class OracleLocal:
         offs = np.cumsum([0] + [len(x) for x in a_ids]).astype(np.int64)
         ids = np.concatenate(a_ids) if a_ids else np.zeros(0, snap['ids'].dtype)
         ang = np.concatenate(a_ang) if a_ang else np.zeros(0, np.float16)
-        return offs, ids, ang
+        pos = np.concatenate(a_pos) if a_pos else np.zeros(0, np.int64)
+        if ids.dtype.kind == 'u':
+            ids = ids.view(ids.dtype.str.replace('u', 'i'))
+        return (torch.from_numpy(offs), torch.from_numpy(ids.astype(ids.dtype)),
+                torch.from_numpy(ang.view(np.int16)), torch.from_numpy(pos.astype(np.int64)))
+
+    # two-phase interface of sharding.ShardedEngine (prepare / set_catalogue / launch)
+    def prepare(self, shard, centres, bulk, H, z, exists, compare, angles_in, prev_lp, share):
+        return {'args': [shard, np.asarray(centres), bulk, H, z, exists, compare, angles_in],
+                'share': share}
+
+    def set_catalogue(self, lp, rows):
+        r = rows.cpu().numpy()
+        c = lp['args'][1]
+        lp['args'][1] = r[:, :3].astype(c.dtype).reshape(c.shape)
+        if lp['share']:
+            b = np.asarray(lp['args'][2])
+            lp['args'][2] = r[:, 3:].astype(b.dtype).reshape(b.shape)
+
+    def launch(self, lp, prev_lp, step_events=None, check=True):
+        return self.step(*lp['args'])
 
     def angles(self):
         return self.prev['angles']
 
+    def angles_tensor(self):
+        return torch.from_numpy(np.asarray(self.prev['angles'], np.float16).view(np.int16)
+                                .astype(np.int64) & 0xFFFF)
+
     def bulk(self, snapshot, halo_idx):
+        snapshot = {k: _np(v) for k, v in snapshot.items()}
         n = len(snapshot['ids'])
         starts = np.asarray(snapshot['region_offsets'], dtype=np.int64)
         ends = np.append(starts[1:], n)

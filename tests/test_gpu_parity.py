@@ -151,6 +151,26 @@ def test_sharded_hip_engine_matches_reference(name, owner):
     assert rep.get('angle_mismatch', 0) <= ANGLE_MISMATCH_MAX * max(rep.get('angles', 1), 1)
 
 
+def test_sharded_hip_engine_matches_single_gpu():
+    """Two ranks (gloo, HIP engine each, one GPU) with the default ID-range owner on a
+    40-halo, 1e6-particle universe: rank 0's savefile equals the single-process run's
+    bit for bit (apsis IDs, offsets, angles, checkpoint)."""
+    from test_sharding import run_sharded, _groups
+    from orbitanalysis_amd.synthetic import PlummerSnapshots
+    from orbitanalysis_amd.savefile import MemorySavefile
+    gen = dict(n_halos=40, n_per_halo=25000, n_snapshots=4, seed=51, box_size=300.0,
+               dtype=np.float32, centre_dtype=np.float32, bulk='catalogue')
+    run = dict(mode='apocentric', checkpoint=True)
+    want = run_driver(PlummerSnapshots(**gen), run, savefile=MemorySavefile())
+    got = run_sharded({'gen': gen, 'run': run}, 2, 'default', local='hip')
+    g = _groups(got)
+    assert sorted(g) == sorted(want.groups)
+    for k in want.groups:
+        for d, w in want.groups[k].items():
+            assert np.array_equal(np.asarray(g[k][d]).view(np.uint8), np.asarray(w).view(np.uint8)), (k, d)
+    assert np.array_equal(got['checkpoint/angles'].view(np.uint16), want.checkpoint.view(np.uint16))
+
+
 @pytest.mark.parametrize('dtype,centre_dtype', [(np.float32, np.float32), (np.float32, np.float64),
                                                 (np.float64, np.float64)])
 def test_frame_state_bits_match_oracle(dtype, centre_dtype):
