@@ -13,7 +13,13 @@ distinct snapshots, cycled), so its own cost is ~0.
 value = particles of the timed snapshots / wall time of those snapshots (the first
 snapshot, which only frames, and one warm-up comparison are excluded).
 
-  python tools/bench_e2e.py [--particles 1e8] [--halos 10000] [--snapshots 6]
+--device-loader: the loader returns torch device tensors (snapshots resident in HBM,
+as a GPU-side reader or simulation would hand them over), so no H2D; what remains is
+the driver's own per-snapshot cost: the host plan (OrbitEngine.prepare), the kernels,
+the status read, the D2H of the apsis CSR and the savefile write.  The per-phase
+host times are reported beside the wall time.
+
+  python tools/bench_e2e.py [--particles 1e8] [--halos 10000] [--snapshots 6] [--device-loader]
 """
 import argparse
 import json
@@ -38,6 +44,8 @@ def main():
     ap.add_argument('--snapshots', type=int, default=6, help='snapshots in the run')
     ap.add_argument('--distinct', type=int, default=3, help='distinct host snapshots (cycled)')
     ap.add_argument('--mode', default='pericentric')
+    ap.add_argument('--device-loader', action='store_true',
+                    help='the loader returns device tensors (no H2D)')
     args = ap.parse_args()
     import torch
     import orbitanalysis_amd  # noqa: F401
@@ -53,12 +61,38 @@ def main():
     t0 = time.perf_counter()
     for s in range(S):
         sn = gen.snapshot(s)
-        h = {k: (v.cpu().numpy() if isinstance(v, torch.Tensor) else v) for k, v in sn.items()}
+        if args.device_loader:
+            h = {k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in sn.items()}
+        else:
+            h = {k: (v.cpu().numpy() if isinstance(v, torch.Tensor) else v) for k, v in sn.items()}
         host.append(h)
         cats.append(gen.catalogue(s))
         del sn
     del gen
     torch.cuda.empty_cache()
+    # per-phase host time of the driver's engine calls (tool-side instrumentation)
+    from orbitanalysis_amd.engine import OrbitEngine
+    phase = {'prepare': [], 'launch+status': [], 'fetch': []}
+
+    def timed(name, fn):
+        def w(*a, **k):
+            t = time.perf_counter()
+            r = fn(*a, **k)
+            phase[name].append(time.perf_counter() - t)
+            return r
+        return w
+    OrbitEngine.prepare = timed('prepare', OrbitEngine.prepare)
+    OrbitEngine.fetch = timed('fetch', OrbitEngine.fetch)
+    _launch = OrbitEngine.launch
+
+    def launch(self, pr, ws, *a, **k):
+        t = time.perf_counter()
+        r = _launch(self, pr, ws, *a, **k)
+        if ws is not None:
+            ws.status.item()                # the driver's status read follows the launch
+        phase['launch+status'].append(time.perf_counter() - t)
+        return r
+    OrbitEngine.launch = launch
     log('setup %.1f s: %d host snapshots of %s particles' % (
         time.perf_counter() - t0, S, [len(h['ids']) for h in host]))
 
@@ -89,15 +123,19 @@ def main():
     per = [stamps[s + 1] - stamps[s] for s in range(2, n - 1)] + [t_end - stamps[n - 1]]
     b = 32.0 * units / len(timed)
     res = {
-        'metric': 'particle-snapshots/s (track_orbits end to end, host NumPy loader)',
+        'metric': 'particle-snapshots/s (track_orbits end to end, %s loader)'
+                  % ('device-tensor' if args.device_loader else 'host NumPy'),
         'value': units / wall, 'unit': 'particle-snapshots/s', 'n_gpus': 1,
         'steps': len(timed), 'warmup': 2, 'ms_per_step': wall / len(timed) * 1e3,
-        'higher_is_better': True, 'dtype': 'f32', 'data': 'synthetic Plummer spheres, host NumPy',
+        'higher_is_better': True, 'dtype': 'f32', 'data': 'synthetic Plummer spheres, %s' % (
+                    'device tensors' if args.device_loader else 'host NumPy'),
         'config': {'workload': 'BASELINE configs[2] shape: %d particles/snapshot, %d halos, f32, '
                                'public track_orbits, in-memory savefile' % (units // len(timed),
                                                                           args.halos)},
         'ms_per_snapshot': [round(p * 1e3, 2) for p in per],
-        'h2d_bytes_per_snapshot': b,
+        'h2d_bytes_per_snapshot': 0.0 if args.device_loader else b,
+        'host_ms_per_snapshot': {k: round(float(np.mean(v[2:])) * 1e3, 3) if len(v) > 2 else None
+                                 for k, v in phase.items()},
         'apsis_records': n_apsis,
         'total_wall_s': t_end - t_start,
     }
