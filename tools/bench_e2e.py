@@ -1,8 +1,8 @@
 """End to end through the public batch API (SURVEY.md §8(d) "end-to-end"): BASELINE
 configs[2] shape (1e8 f32 particles in 1e4 halos per snapshot) fed by a host NumPy
 loader to ``orbitanalysis_amd.track_orbits.track_orbits``, the reference's call
-(track_orbits.py:9-244), with an in-memory savefile (the HDF5 write is excluded, as
-§8(d) says).
+(track_orbits.py:9-244), with a savefile that counts and drops each group's arrays (the HDF5
+write is excluded, as §8(d) says).
 
 Each snapshot pays what a drop-in user pays: the loader's host arrays go to the
 device (ids, coordinates, velocities: 32 B/particle, pageable NumPy memory), the
@@ -106,8 +106,16 @@ def main():
         stamps[snapshot_number] = time.perf_counter()
         return dict(host[snapshot_number % S])
 
+    class CountingSink(MemorySavefile):
+        """The savefile interface with the write left out (SURVEY §8(d) excludes the
+        HDF5 write): each group's arrays are counted and dropped, as an HDF5 writer
+        drops them once written (nothing accumulates in host memory)."""
+
+        def write_group(self, name, datasets):
+            self.groups[name] = {k: int(np.asarray(v).size) for k, v in datasets.items()}
+
     n = args.snapshots
-    sink = MemorySavefile()
+    sink = CountingSink()
     branches = np.tile(np.arange(args.halos), (n, 1))
     t_start = time.perf_counter()
     track_orbits(np.arange(n), branches, regions, load_snapshot_data, sink, mode=args.mode,
@@ -118,8 +126,8 @@ def main():
     timed = list(range(2, n))
     wall = t_end - stamps[2]
     units = sum(len(host[s % S]['ids']) for s in timed)
-    n_apsis = sum(len(g['pericenter_IDs' if args.mode == 'pericentric' else 'apocenter_IDs'])
-                  for g in sink.groups.values()) if hasattr(sink, 'groups') else None
+    n_apsis = sum(g['pericenter_IDs' if args.mode == 'pericentric' else 'apocenter_IDs']
+                  for g in sink.groups.values())
     per = [stamps[s + 1] - stamps[s] for s in range(2, n - 1)] + [t_end - stamps[n - 1]]
     b = 32.0 * units / len(timed)
     res = {
