@@ -180,6 +180,10 @@ typedef struct oa_compact_args {
     const int32_t *scratch_pos; /* optional: oa_step_args.scratch_pos of the step        */
     int32_t *out_pos;           /* optional: the records' previous-state indices, in
                                    output order (with scratch_pos)                     */
+    int32_t n_packed;           /* items[0, n_packed) are k_step items (records
+                                   contiguous from scratch_off), the rest global items
+                                   (records in 64-position segments)                  */
+    int32_t reserved_c;
 } oa_compact_args;
 
 /* ABI version (OA_ABI_VERSION) — lets the host reject a stale library. */

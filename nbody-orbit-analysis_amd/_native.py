@@ -54,7 +54,8 @@ class CompactArgs(ctypes.Structure):
                 ('scratch_ids', c_vp), ('scratch_ang', c_vp), ('seg_count', c_vp),
                 ('halo_count', c_vp), ('item_count', c_vp), ('n_slots', c_i32),
                 ('offsets_out', c_vp), ('out_ids', c_vp), ('out_ang', c_vp),
-                ('total_out', c_vp), ('scratch_pos', c_vp), ('out_pos', c_vp)]
+                ('total_out', c_vp), ('scratch_pos', c_vp), ('out_pos', c_vp),
+                ('n_packed', c_i32), ('reserved_c', c_i32)]
 
 
 class CollateArgs(ctypes.Structure):

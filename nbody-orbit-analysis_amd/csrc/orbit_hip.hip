@@ -222,6 +222,8 @@ struct ItemHdr {
     uint32_t vstart[HMAX + 1];      // virtual start of each progenitor segment
     int32_t seg_halo[HMAX];         // segment -> item-local halo
     int32_t halo_cnt[HMAX];         // apsis records per item halo
+    uint16_t rowoff[OA_KROWS * (OA_WG / 64)];   // item-local offset of each progenitor
+    uint8_t rowcnt[OA_KROWS * (OA_WG / 64)];    //   row's apsis records, and their count
     int32_t has_prev[HMAX];
     uint32_t seg_cnt[HMAX];         // progenitor particles of each segment
     int64_t seg_prev_off[HMAX];
@@ -872,7 +874,12 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     STAMP(3);
     DIAG((uint64_t)H.npend | ((uint64_t)H.pad1 << 20) | ((uint64_t)H.nstash << 40));
     if (H.overflow || nrow > (uint32_t)(KROWS * NWAVE)) {
-        if (tid == 0) atomicOr(a.status, H.overflow ? OA_STATUS_TABLE_OVERFLOW : OA_STATUS_PLAN);
+        // the host re-plans this snapshot; the compaction that follows must see no
+        // records from this item
+        if (tid == 0) {
+            atomicOr(a.status, H.overflow ? OA_STATUS_TABLE_OVERFLOW : OA_STATUS_PLAN);
+            a.item_count[blockIdx.x] = 0;
+        }
         return;
     }
     const bool nonuniform = IDB == 8 && uni(H.nonuniform) != 0;
@@ -934,6 +941,10 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             sgn8[c] = (uint8_t)(sc | 4u);
         }
         pk[k] = p;
+        // records per row: the apsis flags are known here, so phase 2b writes each
+        // item's records contiguously (item-local offsets scanned below)
+        const uint32_t fc = (uint32_t)__popcll(__ballot((p & PK_FLAG) != 0u));
+        if (lane == 0 && r < nrow) H.rowcnt[r] = (uint8_t)fc;
         if (OTF && r < nrow && (uint32_t)lane < nv) a.matched_prev[kb + lane] = hit ? 1 : 0;
     }
     WSTAMP(1);
@@ -955,6 +966,23 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();          // every lookup done: the table is dead
     __builtin_amdgcn_sched_barrier(0);
+    if (wave == 0) {
+        // item-local record offsets of the rows (exclusive scan, <= KROWS * NWAVE rows)
+        uint32_t carry = 0;
+        for (uint32_t c0 = 0; c0 < nrow; c0 += 64) {
+            const uint32_t r = c0 + lane;
+            const uint32_t v = r < nrow ? (uint32_t)H.rowcnt[r] : 0u;
+            uint32_t incl = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (lane >= o) incl += y;
+            }
+            if (r < nrow) H.rowoff[r] = (uint16_t)(carry + incl - v);
+            carry += (uint32_t)__shfl(incl, 63);
+        }
+        if (lane == 0) H.chunk_total = carry;
+    }
     // the item's current r̂, from the registers phase 1 left it in
 #pragma unroll
     for (int k = 0; k < SU; ++k) {
@@ -969,7 +997,6 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     STAMP(5);
 
     const uint64_t lanemask_lt = (1ull << lane) - 1ull;
-    uint32_t running = 0;
     ID *scr_ids = reinterpret_cast<ID *>(a.scratch_ids);
     uint32_t *rcw = reinterpret_cast<uint32_t *>(rcx);        // new angles over rc_x
     constexpr uint32_t RCW = sizeof(TD) / 4;
@@ -1007,25 +1034,20 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
         }
         // apsis records in previous-block order (:315-316): wave ballot + prefix
-        // popcount packs each 64-position row's records at its own scratch base;
-        // k_gather_items orders the rows (no work-group barrier here)
+        // popcount place each row's records at the row's item-local offset, so an
+        // item's records are contiguous and in order (k_gather_items copies them)
         const uint64_t mk = __ballot(flag);
         const uint32_t cnt = (uint32_t)__popcll(mk);
-        const int64_t sb = it.scratch_off + (int64_t)r * 64;
+        const int64_t sb = it.scratch_off + uni(H.rowoff[r]);
         if (flag) {
             const uint32_t q = (uint32_t)__popcll(mk & lanemask_lt);
             __builtin_nontemporal_store(pid[k], &scr_ids[sb + q]);
             __builtin_nontemporal_store(a16, &a.scratch_ang[sb + q]);
             if (a.scratch_pos) a.scratch_pos[sb + q] = (int32_t)(kb + lane);
         }
-        if (lane == 0) {
-            a.seg_count[sb >> 6] = (uint8_t)cnt;
-            if (cnt) atomicAdd(&H.halo_cnt[hs], (int)cnt);
-        }
-        running += cnt;
+        if (lane == 0 && cnt) atomicAdd(&H.halo_cnt[hs], (int)cnt);
     }
     WSTAMP(2);
-    if (lane == 0) atomicAdd(&H.chunk_total, running);
     STAMP(6);
     __syncthreads();
 
@@ -1073,8 +1095,9 @@ __global__ __launch_bounds__(1024) void k_scan_slots(const int32_t *cnt, int32_t
     if (tid == 0) { off[n] = carry; *total = carry; }
 }
 
-// Item records live in 64-position rows (k_step phase 2), packed at each row's base.
-// One work-group per item, rows in chunks of 256: a block-wide exclusive scan of the
+// Packed (k_step) items hold their records contiguously: a coalesced copy.  Global
+// items (k_big_join) keep theirs in 64-position segments, packed at each segment's
+// base.  One work-group per item, segments in chunks of 256: a block-wide exclusive scan of the
 // chunk's row counts (LDS), then the chunk's records are copied flat -- thread t moves
 // records t, t + 256, ... (consecutive records of consecutive rows: coalesced), each
 // finding its row by a binary search over the scanned offsets.
@@ -1084,7 +1107,8 @@ __global__ __launch_bounds__(256) void k_gather_items(const oa_compact_args a) {
     __shared__ uint32_t wsum[4];
     __shared__ uint32_t roff[257];
     const oa_item it = a.items[blockIdx.x];
-    const int32_t n = a.item_count[blockIdx.x];
+    // an item holds at most one record per (padded) progenitor position
+    const int32_t n = min((int64_t)a.item_count[blockIdx.x], it.n_pv);
     const int64_t slot = it.slot0;               // planned on the host: no halo walk
     if (n <= 0 || slot < 0) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1092,6 +1116,16 @@ __global__ __launch_bounds__(256) void k_gather_items(const oa_compact_args a) {
     const ID *src = reinterpret_cast<const ID *>(a.scratch_ids);
     ID *out = reinterpret_cast<ID *>(a.out_ids) + dst;
     uint16_t *oang = a.out_ang + dst;
+    if ((int32_t)blockIdx.x < a.n_packed) {
+        // k_step items: the records are already contiguous and in order
+        const int64_t s0 = it.scratch_off;
+        for (int32_t j = tid; j < n; j += 256) {
+            out[j] = src[s0 + j];
+            oang[j] = a.scratch_ang[s0 + j];
+            if (a.out_pos) a.out_pos[dst + j] = a.scratch_pos[s0 + j];
+        }
+        return;
+    }
     const int64_t nseg = (it.n_pv + 63) >> 6;
     const uint8_t *sc = a.seg_count + (it.scratch_off >> 6);
     int64_t carry = 0;

@@ -28,10 +28,10 @@ F32, F64 = np.dtype(np.float32), np.dtype(np.float64)
 # the header + max(8-byte cuckoo slots + 2 B/entry insert list, 3 r̂ components per
 # entry) + 1 B/entry of signs, within the CU's 160 KB (the table and the r̂ arrays
 # overlay each other):
-#   float32 r̂: 11776 entries, 15456 slots (load <= 0.76)   -> 163,072 B
-#   float64 r̂:  6144 entries, 16896 slots (load <= 0.36)   -> 157,696 B
+#   float32 r̂: 11776 entries, 15360 slots (load <= 0.77)
+#   float64 r̂:  6144 entries, 16896 slots (load <= 0.36)
 DEFAULT_ENTRIES = {False: 11776, True: 6144}
-DEFAULT_SLOTS = {False: 15456, True: 16896}
+DEFAULT_SLOTS = {False: 15360, True: 16896}
 
 _TORCH_FROM_NP = {
     np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
@@ -602,6 +602,7 @@ class OrbitEngine:
         c = pr.cargs
         c.halos, c.n_halos = a.halos, a.n_halos
         c.items, c.n_items = a.items, a.n_items + a.n_global_items
+        c.n_packed = a.n_items
         c.ids_prev, c.id_bytes = a.ids_prev, a.id_bytes
         c.scratch_ids, c.scratch_ang = a.scratch_ids, a.scratch_ang
         c.seg_count = a.seg_count
