@@ -66,6 +66,12 @@ constexpr int STASH = 64;           // cuckoo stash entries per item
 #ifndef OA_MAXEV
 #define OA_MAXEV 48
 #endif
+#ifndef OA_ROWGUARD
+#define OA_ROWGUARD 0       // 1: no loads for rows past the item (A/B r02 gp: +30 us, off)
+#endif
+#ifndef OA_P3V
+#define OA_P3V 1            // phase 3: four state words per 16-byte store
+#endif
 #ifndef OA_RWALK
 #define OA_RWALK 0
 #endif
@@ -507,6 +513,7 @@ __device__ f32x3 rbl_v3f32(i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.
 __device__ f64x2 rbl_v2f64(i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.load.v2f64");
 __device__ double rbl_f64(i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.load.f64");
 __device__ void rbs_i32(int32_t, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.i32");
+__device__ void rbs_v4i32(i32x4, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.v4i32");
 __device__ void rbs_v3f32(f32x3, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.v3f32");
 __device__ void rbs_v2f64(f64x2, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.v2f64");
 __device__ void rbs_f64(double, i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.store.f64");
@@ -820,6 +827,9 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < KROWS; ++k) {
+        pid[k] = 0;
+        pk[k] = 0u;
+        if (OA_ROWGUARD && (uint32_t)(wave + NWAVE * k) >= nrow) continue;      // uniform
         uint32_t nv, hs;
         int64_t kb;
         row_of(wave + NWAVE * k, nv, hs, kb);
@@ -957,6 +967,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < PF2 && k < KROWS; ++k) {
+        if (OA_ROWGUARD && (uint32_t)(wave + NWAVE * k) >= nrow) continue;      // uniform
         uint32_t nv, hs;
         int64_t kb;
         row_of(wave + NWAVE * k, nv, hs, kb);
@@ -1002,7 +1013,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     constexpr uint32_t RCW = sizeof(TD) / 4;
 #pragma unroll
     for (int k = 0; k < KROWS; ++k) {
-        if (k + PF2 < KROWS) {
+        if (k + PF2 < KROWS && (!OA_ROWGUARD || (uint32_t)(wave + NWAVE * (k + PF2)) < nrow)) {
             uint32_t nv, hs;
             int64_t kb;
             row_of(wave + NWAVE * (k + PF2), nv, hs, kb);
@@ -1055,7 +1066,20 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // matched: the new angle phase 2b left in rc_x; entered or in a halo without a
     // progenitor block: angle 0 (calc_angles :348-349).  Nothing in this launch reads
     // them again, so the stores are non-temporal.
-    for (uint32_t li = tid; li < n_span; li += WG) {
+    // (four consecutive positions per thread: one 16-byte store)
+    const uint32_t n4 = OA_P3V ? n_span & ~3u : 0u;
+    for (uint32_t l4 = (uint32_t)tid * 4u; l4 < n4; l4 += WG * 4u) {
+        const uint32_t s4 = *reinterpret_cast<const uint32_t *>(sgn8 + l4);
+        i32x4 w;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t sq = (s4 >> (8 * q)) & 0xFFu;
+            const uint32_t ang = (sq & 4u) ? (rcw[RCW * (l4 + q)] & 0xFFFFu) : 0u;
+            w[q] = (int32_t)(ang | ((sq & 3u) << 16));
+        }
+        rbs_v4i32(w, r_mt, (int32_t)(l4 * 4u), 0, AUX_NT);
+    }
+    for (uint32_t li = n4 + tid; li < n_span; li += WG) {
         const uint32_t s = sgn8[li];
         const uint32_t ang = (s & 4u) ? (rcw[RCW * li] & 0xFFFFu) : 0u;
         bst32<AUX_NT>(r_mt, li * 4u, ang | ((s & 3u) << 16));

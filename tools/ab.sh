@@ -5,7 +5,7 @@
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; O=$R/gpurun_out; mkdir -p "$O"; T=${TAG:-ab}
 D=$R/nbody-orbit-analysis_amd/variants
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
   for v in ${VARS:-base}; do
     lib=""; [ "$v" != base ] && lib="$D/lib_$v.so"
     ORBIT_HIP_LIB=$lib timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline \
