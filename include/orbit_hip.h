@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OA_ABI_VERSION 8
+#define OA_ABI_VERSION 9
 
 #define OA_OK 0
 #define OA_E_ARG (-1)       /* invalid argument / unsupported dtype plan */
@@ -43,6 +43,9 @@ extern "C" {
                                          oa_build_info(3) * work-group progenitor
                                          positions): the plan did not come from
                                          oa_plan_items                               */
+#define OA_STATUS_PART_OVERFLOW 8u    /* a large-halo hash partition outgrew its bucket
+                                         or LDS table: re-run the snapshot on the
+                                         global-table path (n_parts = 0)             */
 
 #define OA_MODE_PERICENTRIC 0
 #define OA_MODE_APOCENTRIC 1
@@ -156,6 +159,40 @@ typedef struct oa_step_args {
      * scratch_ids; the sharded driver maps it to the particle's position in the global
      * previous block, which orders the merged records (sharding.py) */
     int32_t *scratch_pos;
+    /* Partitioned large halos (compare steps, not on-the-fly; n_parts = 0: the
+     * global-table path above).  Each global item's IDs are cut into K hash partitions
+     * (partition = mulhi64(mix64(ID), K)) so one partition's current particles fit an
+     * LDS table of oa_build_info(4) entries:
+     *   k_part_scatter  frame of the current chunks (gchunk1) plus bucket appends of
+     *                   {ID, position | sign << 30}; bucket appends {ID, position, state
+     *                   word, r̂} of the previous chunks (gchunk2), whose apsis marks it
+     *                   clears
+     *   k_part_join     one work-group per plist row (LDS: oa_part_lds_bytes): LDS table of the current bucket,
+     *                   lookups of the previous bucket, state words and apsis marks
+     *   k_part_emit     previous chunks: marks -> records packed per 64-position
+     *                   segment (the layout k_big_join writes)                        */
+    int32_t n_parts;            /* rows of plist (padding rows included)              */
+    int32_t part_kmax;          /* largest K of any global item                       */
+    int32_t part_e;             /* current bucket capacity = LDS table entries of one
+                                   partition (multiple of 64, <= oa_build_info(4))    */
+    int32_t part_slots;         /* its cuckoo slots (part_e < slots <= 1.5 build max) */
+    const int32_t *plist;       /* [n_parts] (global item g = item - n_items, partition)
+                                   pairs; g = -1: an idle padding row                */
+    const int64_t *gpart;       /* per global item, 8 int64: current bucket base,
+                                   previous bucket base, K, previous bucket capacity,
+                                   first counter index, 0, 0, 0 (current buckets hold
+                                   oa_build_info(4) entries each)                    */
+    uint64_t *pkey_cur;         /* current buckets: IDs (zero-extended 4-byte IDs)    */
+    uint32_t *ppos_cur;         /*   position in the halo's block | sign(v_r) << 30   */
+    uint64_t *pkey_prev;        /* previous buckets: IDs                              */
+    uint32_t *ppos_prev;        /*   position in the halo's previous block            */
+    uint32_t *pmeta_prev;       /*   its previous state word                          */
+    void *prh_prev;             /*   its previous r̂ (3 values of the r̂ dtype)         */
+    uint32_t *pcnt;             /* [2 * sum K] bucket fill counters, zeroed by oa_step
+                                   (current K of an item, then its previous K)        */
+    uint32_t *gmark;            /* apsis marks, one per padded previous position of
+                                   the global items: 0 or 1 << 16 | float16 angle     */
+    int64_t gmark_base;         /* scratch_off of the first global item (gmark[0])    */
 } oa_step_args;
 
 /* Arguments of oa_compact: gather the per-item apsis records into the reference's
@@ -194,8 +231,14 @@ int oa_abi_version(void);
 int64_t oa_struct_size(int32_t which);
 
 /* Compile-time configuration: 0 work-group size, 1 max halos per item,
- * 2 phase-1 unroll, 3 progenitor rows (64 positions) per wave of an item; -1 otherwise. */
+ * 2 phase-1 unroll, 3 progenitor rows (64 positions) per wave of an item, 4 current
+ * entries per large-halo partition (k_part_join's LDS table), 5 largest K per halo
+ * (k_part_scatter's LDS counters); -1 otherwise. */
 int32_t oa_build_info(int32_t which);
+
+/* LDS bytes of one k_part_join work-group for a partition of `entries` current
+ * entries in a table of `slots` slots (oa_step_args.part_e / part_slots). */
+int64_t oa_part_lds_bytes(int32_t entries, int32_t slots);
 
 /* Message of the last failing call on this thread ("" if none). */
 const char *oa_last_error(void);

@@ -13,7 +13,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.abspath(__file__))
 # ORBIT_HIP_LIB selects an alternative build (kernel variants for tuning sweeps)
 LIB_PATH = os.environ.get('ORBIT_HIP_LIB') or os.path.join(PKG, 'liborbit_hip.so')
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -28,6 +28,7 @@ ITEM_DTYPE = np.dtype([('h0', '<i4'), ('h1', '<i4'), ('slot0', '<i4'), ('n_span'
 MODE = {'pericentric': 0, 'apocentric': 1}
 STATUS_TABLE_OVERFLOW = 2
 STATUS_PLAN = 4
+STATUS_PART_OVERFLOW = 8
 
 
 class StepArgs(ctypes.Structure):
@@ -45,7 +46,11 @@ class StepArgs(ctypes.Structure):
                 ('matched_prev', c_vp), ('matched_cur', c_vp), ('vr_out', c_vp),
                 ('n_global_items', c_i32), ('n_gchunk1', c_i32), ('n_gchunk2', c_i32),
                 ('gchunk1', c_vp), ('gchunk2', c_vp), ('gtab', c_vp), ('gkeys', c_vp),
-                ('gvals', c_vp), ('gtab_total', c_i64), ('scratch_pos', c_vp)]
+                ('gvals', c_vp), ('gtab_total', c_i64), ('scratch_pos', c_vp),
+                ('n_parts', c_i32), ('part_kmax', c_i32), ('part_e', c_i32), ('part_slots', c_i32), ('plist', c_vp), ('gpart', c_vp),
+                ('pkey_cur', c_vp), ('ppos_cur', c_vp), ('pkey_prev', c_vp), ('ppos_prev', c_vp),
+                ('pmeta_prev', c_vp), ('prh_prev', c_vp),
+                ('pcnt', c_vp), ('gmark', c_vp), ('gmark_base', c_i64)]
 
 
 class CompactArgs(ctypes.Structure):
@@ -99,6 +104,7 @@ SYMBOLS = {
     'oa_bulk_velocity': (ctypes.c_int, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp]),
     'oa_step': (ctypes.c_int, [ctypes.POINTER(StepArgs), c_vp]),
     'oa_step_lds_bytes': (c_i64, [c_i32, c_i32, c_i32]),
+    'oa_part_lds_bytes': (c_i64, [c_i32, c_i32]),
     'oa_plan_items': (c_i64, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp,
                               c_i64, c_vp, c_vp]),
     'oa_max_lds_bytes': (c_i64, []),

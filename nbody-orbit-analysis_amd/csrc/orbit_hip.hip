@@ -72,6 +72,9 @@ constexpr int STASH = 64;           // cuckoo stash entries per item
 #ifndef OA_P3V
 #define OA_P3V 1            // phase 3: four state words per 16-byte store
 #endif
+#ifndef OA_PU
+#define OA_PU 4             // k_part_join: previous entries per thread loaded up front
+#endif
 #ifndef OA_RWALK
 #define OA_RWALK 0
 #endif
@@ -1575,8 +1578,440 @@ __global__ __launch_bounds__(BIG_WG) void k_big_join(const oa_step_args a) {
     }
 }
 
+// ------------------------------------------------------------------ partitioned large halos
+// The default large-halo path of compare steps.  A halo too large for one work-group's
+// LDS table is cut into K partitions by a hash of the full ID, each small enough for an
+// LDS cuckoo table, so the join is LDS-local like k_step's and every HBM stream is
+// coalesced (the global-table path above pays a random HBM access per insert and probe):
+//   k_part_scatter  chunks of the current blocks: the frame (r̂ and the state word with
+//                   angle 0 in position order, as k_big_frame) plus each particle's
+//                   {ID, position | sign << 30} appended to its partition's bucket;
+//                   chunks of the previous blocks: {ID, position} appended, and the
+//                   apsis marks of those positions cleared.  A chunk counts its
+//                   partitions in LDS and reserves each bucket range with one atomic.
+//   k_part_join     one work-group per partition: LDS cuckoo table of the current
+//                   bucket, then every previous entry looked up; a match gathers the
+//                   two r̂ rows and the previous state word (the halo's blocks are
+//                   shared by its partitions, which plist keeps on one XCD), writes the
+//                   current particle's state word and, for an apsis, the mark at the
+//                   previous position
+//   k_part_emit     64-position segments of the previous blocks: marks -> records in
+//                   previous-block order (:315-316), packed per segment as k_big_join
+constexpr int PART_E = 4096;            // current entries of one partition, at most
+constexpr int PART_S = 6144;            // LDS table slots, at most
+// 512 threads, <= 128 VGPRs and ~74 KB of LDS: two join work-groups per CU, so one's
+// table build overlaps the other's streaming
+constexpr int PART_KMAX = 16384;        // partitions of one halo (scatter's LDS counters)
+constexpr int PART_WG = 512;
+constexpr int SCAT_WG = 256, SCAT_PER = 8;
+static_assert(PART_E - 1 <= (int)MAX_POS, "partition entries must fit the slot position field");
+
+// partition of an ID: the high bits of a 64-bit mix (the LDS table hashes the low
+// word with unrelated multipliers, so a partition's keys still spread over its table)
+__device__ __forceinline__ uint32_t part_of(uint64_t id, uint32_t K) {
+    return (uint32_t)__umul64hi(id_hash64(id ^ 0x2545F4914F6CDD1Dull), (uint64_t)K);
+}
+
+// CUR: current chunks (gchunk1), else previous chunks (gchunk2).  A previous bucket
+// entry carries the particle's whole previous state (ID, position, state word, r̂), so
+// the join streams it instead of gathering it.
+template <typename TX, typename TV, typename TD, int IDB, bool CUR>
+__device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK &fk, uint32_t *lcnt,
+                                             int64_t chunk) {
+    typedef typename IdT<IDB>::T ID;
+    const int64_t *ch = (CUR ? a.gchunk1 : a.gchunk2) + 3 * chunk;
+    const int64_t gi = ch[0], start = ch[1], cnt = ch[2];
+    const oa_item it = a.items[gi];
+    const oa_halo &h = a.halos[it.h0];
+    const int64_t gk = gi - a.n_items;
+    const int64_t *gp = a.gpart + 8 * gk;
+    const uint32_t K = (uint32_t)gp[2];
+    const bool part = h.prev_cnt > 0 && K > 0;
+    const int tid = threadIdx.x;
+    double cb[6];
+    float cf[6];
+    if (CUR) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) { cb[d] = h.centre[d]; cb[3 + d] = h.bulk[d]; }
+#pragma unroll
+        for (int d = 0; d < 6; ++d) cf[d] = (float)cb[d];
+    }
+    const ID *ids = static_cast<const ID *>(CUR ? a.ids : a.ids_prev);
+    const TX *xs = static_cast<const TX *>(a.coords);
+    const TV *vs = static_cast<const TV *>(a.vels);
+    TD *rhat_out = static_cast<TD *>(a.rhat_out);
+    const TD *rhat_prev = static_cast<const TD *>(a.rhat_prev);
+    const int64_t base = CUR ? h.cur_off : h.prev_off;
+    uint32_t *ctr = a.pcnt + gp[4] + (CUR ? 0 : K);
+    const uint32_t bcap = CUR ? (uint32_t)a.part_e : (uint32_t)gp[3];
+    const int64_t bb = CUR ? gp[0] : gp[1];
+    uint64_t *bkey = (CUR ? a.pkey_cur : a.pkey_prev) + bb;
+    uint32_t *bpos = (CUR ? a.ppos_cur : a.ppos_prev) + bb;
+    uint32_t *bmeta = a.pmeta_prev + bb;
+    TD *brh = static_cast<TD *>(a.prh_prev) + 3 * bb;
+    uint32_t *mark = a.gmark + (it.scratch_off - a.gmark_base);
+    for (int64_t s0 = start; s0 < start + cnt; s0 += SCAT_WG * SCAT_PER) {
+        const int64_t n0 = min(start + cnt - s0, (int64_t)SCAT_WG * SCAT_PER);
+        if (part) {
+            for (uint32_t k = tid; k < K; k += SCAT_WG) lcnt[k] = 0u;
+            __syncthreads();
+        }
+        uint64_t key[SCAT_PER];
+        uint32_t pw[SCAT_PER], pr[SCAT_PER], pm[SCAT_PER];
+        V3<TD> rh[SCAT_PER];
+        // every load of the sub-chunk first (independent), then the arithmetic
+#pragma unroll
+        for (int q = 0; q < SCAT_PER; ++q) {
+            const int64_t j = (int64_t)q * SCAT_WG + tid;
+            key[q] = 0ull;
+            pm[q] = 0u;
+            if (j >= n0) continue;
+            const int64_t i = base + s0 + j;
+            key[q] = (uint64_t)lds_nt(&ids[i]);
+            if (!CUR) {
+                pm[q] = lds_nt(&a.meta_prev[i]);
+                rh[q] = ld3_nt(rhat_prev, i);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < SCAT_PER; ++q) {
+            pr[q] = 0xFFFFFFFFu;
+            pw[q] = 0u;
+            const int64_t j = (int64_t)q * SCAT_WG + tid;
+            if (j >= n0) continue;
+            const int64_t p = s0 + j;                   // position in the halo's block
+            const int64_t i = base + p;
+            if (CUR) {
+                const V3<TX> x = ld3_nt(xs, i);
+                const V3<TV> v = ld3_nt(vs, i);
+                TD r[3];
+                const uint32_t sgn = frame<TX, TV, TD>(x, v, cb, cf, a, fk, r);
+                TD *ro = rhat_out + 3 * i;
+                ro[0] = r[0]; ro[1] = r[1]; ro[2] = r[2];
+                // angle 0: entered particles keep it (calc_angles :348-349), matched
+                // ones get theirs from k_part_join
+                a.meta_out[i] = sgn << 16;
+                pw[q] = (uint32_t)p | (sgn << 30);
+            } else {
+                mark[p] = 0u;
+                pw[q] = (uint32_t)p;
+            }
+            if (part) {
+                const uint32_t pp = part_of(key[q], K);
+                pr[q] = (pp << 16) | atomicAdd(&lcnt[pp], 1u);
+            }
+        }
+        if (!part) continue;                            // uniform
+        __syncthreads();
+        for (uint32_t k = tid; k < K; k += SCAT_WG) {
+            const uint32_t c = lcnt[k];
+            if (c) lcnt[k] = atomicAdd(&ctr[k], c);     // this chunk's range of bucket k
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < SCAT_PER; ++q) {
+            if (pr[q] == 0xFFFFFFFFu) continue;
+            const uint32_t pp = pr[q] >> 16, e = lcnt[pp] + (pr[q] & 0xFFFFu);
+            if (e < bcap) {                             // an overflow is reported by the join
+                const int64_t o = (int64_t)pp * bcap + e;
+                bkey[o] = key[q];
+                bpos[o] = pw[q];
+                if (!CUR) {
+                    bmeta[o] = pm[q];
+                    TD *d = brh + 3 * o;
+                    d[0] = rh[q].x; d[1] = rh[q].y; d[2] = rh[q].z;
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// Current and previous chunks interleaved in one grid (their latencies overlap):
+// even work-groups take current chunks, odd ones previous chunks, then the longer
+// list's remainder.
+template <typename TX, typename TV, typename TD, int IDB>
+__global__ __launch_bounds__(SCAT_WG) void k_part_scatter(const oa_step_args a, const FrameK fk) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lcnt[];   // [K]
+    const int64_t b = blockIdx.x, n1 = a.n_gchunk1, n2 = a.n_gchunk2;
+    const int64_t m = n1 < n2 ? n1 : n2;
+    bool cur;
+    int64_t c;
+    if (b < 2 * m) { cur = (b & 1) == 0; c = b >> 1; }
+    else { cur = n1 > n2; c = b - m; }
+    if (cur) part_scatter<TX, TV, TD, IDB, true>(a, fk, lcnt, c);
+    else part_scatter<TX, TV, TD, IDB, false>(a, fk, lcnt, c);
+}
+
+// LDS of one k_part_join work-group for a partition capacity of e entries, s slots
+__host__ __device__ inline int64_t part_lds_bytes(int e, int sl) {
+    return (int64_t)sl * 8 + (int64_t)(e / 4) * 8 + (int64_t)STASH * 8 + (int64_t)e * 4 + 16;
+}
+
+template <typename TD, int IDB>
+__global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
+    extern __shared__ __attribute__((aligned(16))) char psm[];
+    const uint32_t PE = (uint32_t)a.part_e, PS = (uint32_t)a.part_slots;
+    uint64_t *slots = reinterpret_cast<uint64_t *>(psm);               // [PS]
+    uint64_t *pend = slots + PS;                                        // [PE / 4]
+    uint64_t *stash = pend + PE / 4;                                    // [STASH]
+    uint32_t *posl = reinterpret_cast<uint32_t *>(stash + STASH);       // [PE]
+    uint32_t *flags = posl + PE;       // npend, nstash, overflow, nonuniform
+    const int tid = threadIdx.x;
+    const int32_t g = a.plist[2 * blockIdx.x], pp = a.plist[2 * blockIdx.x + 1];
+    if (g < 0) return;                                  // padding row
+    const oa_item it = a.items[a.n_items + g];
+    const oa_halo &h = a.halos[it.h0];
+    const int64_t *gp = a.gpart + 8 * (int64_t)g;
+    const uint32_t K = (uint32_t)gp[2], pcap = (uint32_t)gp[3];
+    const uint32_t nc = a.pcnt[gp[4] + pp], np = a.pcnt[gp[4] + K + pp];
+    if (nc > PE || np > pcap) {
+        if (tid == 0) atomicOr(a.status, OA_STATUS_PART_OVERFLOW);
+        return;
+    }
+    const uint64_t *ck = a.pkey_cur + gp[0] + (int64_t)pp * PE;
+    const uint32_t *cp = a.ppos_cur + gp[0] + (int64_t)pp * PE;
+    const int64_t qb = gp[1] + (int64_t)pp * pcap;
+    const uint64_t *qk = a.pkey_prev + qb;
+    const uint32_t *qp = a.ppos_prev + qb;
+    const uint32_t *qm = a.pmeta_prev + qb;
+    const TD *qr = static_cast<const TD *>(a.prh_prev) + 3 * qb;
+    // Every load of the partition goes out first (both buckets are streamed once):
+    // their HBM latency hides behind the table clear, the inserts and the walks.
+    constexpr int CU = PART_E / PART_WG, PU = OA_PU;
+    uint64_t ckey[CU];
+    uint32_t cpw[CU];
+#pragma unroll
+    for (int u = 0; u < CU; ++u) {
+        const uint32_t i = (uint32_t)u * PART_WG + tid;
+        ckey[u] = i < nc ? ck[i] : 0ull;
+        cpw[u] = i < nc ? cp[i] : 0u;
+    }
+    uint64_t qkey[PU];
+    uint32_t qpos[PU], qmeta[PU];
+    V3<TD> qrh[PU];
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+        const uint32_t j = (uint32_t)u * PART_WG + tid;
+        qkey[u] = j < np ? qk[j] : 0ull;
+        qpos[u] = j < np ? qp[j] : 0u;
+        qmeta[u] = j < np ? qm[j] : 0u;
+        if (j < np) qrh[u] = ld3(qr, j);
+    }
+    uint32_t nsl = nc + nc / 2u + 64u;
+    nsl = nsl < PS ? nsl : PS;
+    for (uint32_t w = tid; w < nsl; w += PART_WG) slots[w] = 0ull;
+    if (tid < 4) flags[tid] = 0u;
+    const uint32_t hi0 = nc ? (uint32_t)(ck[0] >> 32) : 0u;
+    __syncthreads();
+    // current bucket -> LDS table: lo32(ID) | (sign << 16 | (entry + 1) << 18) << 32
+    const uint32_t pend_cap = PE / 4;
+#pragma unroll
+    for (int u = 0; u < CU; ++u) {
+        const uint32_t i = (uint32_t)u * PART_WG + tid;
+        if (i >= nc) continue;
+        const uint64_t key = ckey[u];
+        posl[i] = cpw[u] & 0x3FFFFFFFu;
+        if ((uint32_t)(key >> 32) != hi0) flags[3] = 1u;        // benign race: all write 1
+        const uint64_t val = slot_pack((uint32_t)key, (cpw[u] >> 30) << 16, i);
+        uint32_t cs[NCAND];
+        cuckoo_slots((uint32_t)key, nsl, cs);
+        uint64_t cv[NCAND];
+#pragma unroll
+        for (int j = 0; j < NCAND; ++j) cv[j] = slots[cs[j]];
+        uint32_t t = 0xFFFFFFFFu;
+#pragma unroll
+        for (int j = NCAND - 1; j >= 0; --j) t = cv[j] == 0ull ? cs[j] : t;
+        if (t != 0xFFFFFFFFu &&
+            atomicCAS(reinterpret_cast<unsigned long long *>(&slots[t]), 0ull,
+                      (unsigned long long)val) == 0ull)
+            continue;
+        const uint32_t e = atomicAdd(&flags[0], 1u);
+        if (e < pend_cap) pend[e] = val; else flags[2] = 1u;
+    }
+    __syncthreads();
+    {   // deferred eviction walks (as k_step's)
+        const uint32_t npd = min(flags[0], pend_cap);
+        for (uint32_t e = tid; e < npd; e += PART_WG) {
+            uint64_t v = pend[e];
+            uint32_t cs[NCAND];
+            cuckoo_slots((uint32_t)v, nsl, cs);
+            uint32_t t = cs[0];
+            for (int s = 0;; ++s) {
+                const uint64_t old = atomicExch(reinterpret_cast<unsigned long long *>(&slots[t]),
+                                                (unsigned long long)v);
+                if (old == 0ull) break;
+                if (s == MAX_EVICT) {
+                    const uint32_t k = atomicAdd(&flags[1], 1u);
+                    if (k < (uint32_t)STASH) stash[k] = old; else flags[2] = 1u;
+                    break;
+                }
+                cuckoo_slots((uint32_t)old, nsl, cs);
+                uint32_t nx = cs[0];
+#pragma unroll
+                for (int j = NCAND - 2; j >= 0; --j) nx = cs[j] == t ? cs[j + 1] : nx;
+                t = nx;
+                v = old;
+            }
+        }
+    }
+    __syncthreads();
+    if (flags[2]) {
+        if (tid == 0) atomicOr(a.status, OA_STATUS_PART_OVERFLOW);
+        return;
+    }
+    const bool nonuniform = IDB == 8 && flags[3] != 0u;
+    const uint32_t nstash = min(flags[1], (uint32_t)STASH);
+    const TD *rhat_cur = static_cast<const TD *>(a.rhat_out);
+    uint32_t *mark = a.gmark + (it.scratch_off - a.gmark_base);
+    // previous entries, PU per thread: lookups, then the gathers of the matched
+    // current r̂ (the halo's block, L2-resident: plist keeps a halo's partitions on one
+    // XCD), then the angle and state-word arithmetic
+    for (uint32_t j0 = 0; j0 < np; j0 += (uint32_t)PART_WG * PU) {
+        if (j0) {
+#pragma unroll
+            for (int u = 0; u < PU; ++u) {
+                const uint32_t j = j0 + (uint32_t)u * PART_WG + tid;
+                qkey[u] = j < np ? qk[j] : 0ull;
+                qpos[u] = j < np ? qp[j] : 0u;
+                qmeta[u] = j < np ? qm[j] : 0u;
+                if (j < np) qrh[u] = ld3(qr, j);
+            }
+        }
+        uint32_t hit[PU];
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+            hit[u] = 0xFFFFFFFFu;
+            const uint32_t j = j0 + (uint32_t)u * PART_WG + tid;
+            const uint32_t lo = (uint32_t)qkey[u];
+            if (j >= np || (IDB == 8 && !nonuniform && (uint32_t)(qkey[u] >> 32) != hi0)) continue;
+            uint32_t cs[NCAND];
+            cuckoo_slots(lo, nsl, cs);
+            uint64_t m = 0ull;
+#pragma unroll
+            for (int q = 0; q < NCAND; ++q) {
+                const uint64_t v = slots[cs[q]];
+                if (!m && v && (uint32_t)v == lo && slot_pos(v) < nc &&
+                    (!nonuniform || ck[slot_pos(v)] == qkey[u]))
+                    m = v;
+            }
+            for (uint32_t e = 0; !m && e < nstash; ++e) {
+                const uint64_t v = stash[e];
+                if ((uint32_t)v == lo && (!nonuniform || ck[slot_pos(v)] == qkey[u])) m = v;
+            }
+            if (m) hit[u] = posl[slot_pos(m)] | ((slot_meta(m) >> 16) << 30);
+        }
+        V3<TD> crh[PU];
+#pragma unroll
+        for (int u = 0; u < PU; ++u)
+            if (hit[u] != 0xFFFFFFFFu) crh[u] = ld3(rhat_cur, h.cur_off + (hit[u] & 0x3FFFFFFFu));
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+            if (hit[u] == 0xFFFFFFFFu) continue;
+            const uint32_t sc = hit[u] >> 30, sp = qmeta[u] >> 16;
+            // strict sign test (:311-314), arccos of the r̂ dot product (:324-325),
+            // f16 + change rounded once, reset at an apsis (:342-349)
+            const bool flag = a.mode == OA_MODE_PERICENTRIC ? (sp == 2u && sc == 1u)
+                                                            : (sp == 1u && sc == 2u);
+            const TD dt = dot3(qrh[u].x, qrh[u].y, qrh[u].z, crh[u].x, crh[u].y, crh[u].z);
+            const uint16_t acc = angle_add((uint16_t)(qmeta[u] & 0xFFFFu), acos_td(dt));
+            a.meta_out[h.cur_off + (hit[u] & 0x3FFFFFFFu)] = (uint32_t)(flag ? 0u : acc) | (sc << 16);
+            if (flag) mark[qpos[u]] = 0x10000u | acc;
+        }
+    }
+}
+
+template <int IDB>
+__global__ __launch_bounds__(BIG_WG) void k_part_emit(const oa_step_args a) {
+    typedef typename IdT<IDB>::T ID;
+    const int64_t *ch = a.gchunk2 + 3 * blockIdx.x;
+    const int64_t gi = ch[0], start = ch[1], cnt = ch[2];
+    const oa_item it = a.items[gi];
+    const oa_halo &h = a.halos[it.h0];
+    const ID *ids_prev = static_cast<const ID *>(a.ids_prev);
+    const uint32_t *mark = a.gmark + (it.scratch_off - a.gmark_base);
+    ID *scr_ids = static_cast<ID *>(a.scratch_ids);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lanemask_lt = (1ull << lane) - 1ull;
+    int32_t tot = 0;
+    constexpr int EU = 8;                       // marks of EU rows loaded before any is used
+    uint32_t mk[EU];
+    for (int64_t w0 = start; w0 < start + cnt; w0 += BIG_WG * EU) {
+#pragma unroll
+    for (int e = 0; e < EU; ++e) {
+        const int64_t p = w0 + e * BIG_WG + threadIdx.x;
+        mk[e] = p < start + cnt ? mark[p] : 0u;
+    }
+#pragma unroll
+    for (int e = 0; e < EU; ++e) {
+        const int64_t v0 = w0 + e * BIG_WG;
+        const int64_t p = v0 + threadIdx.x;
+        const uint32_t m = mk[e];
+        const bool flag = m != 0u;
+        const uint64_t b = __ballot(flag);
+        const int64_t segpos = v0 + wave * 64;
+        if (segpos < start + cnt) {
+            if (flag) {
+                const int64_t pos = it.scratch_off + segpos + __popcll(b & lanemask_lt);
+                scr_ids[pos] = ids_prev[h.prev_off + p];
+                a.scratch_ang[pos] = (uint16_t)(m & 0xFFFFu);
+                if (a.scratch_pos) a.scratch_pos[pos] = (int32_t)(h.prev_off + p);
+            }
+            if (lane == 0) {
+                const uint32_t c = (uint32_t)__popcll(b);
+                a.seg_count[(it.scratch_off + segpos) >> 6] = (uint8_t)c;
+                tot += (int32_t)c;
+            }
+        }
+    }
+    }
+    // one pair of device atomics per work-group (per-wave atomics on the halo's two
+    // counters serialise across the chunks of a large halo)
+    __shared__ int32_t wtot[BIG_WG / 64];
+    if (lane == 0) wtot[wave] = tot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < BIG_WG / 64; ++w) t += wtot[w];
+        if (t) {
+            atomicAdd(&a.halo_count[h.out_slot], t);
+            atomicAdd(&a.item_count[gi], t);
+        }
+    }
+}
+
+template <typename TX, typename TV, typename TD, int IDB>
+int launch_part(const oa_step_args &a, hipStream_t st) {
+    if (hipMemsetAsync(a.pcnt, 0, (size_t)a.n_parts * 8, st) != hipSuccess)
+        return fail(OA_E_LAUNCH, "oa_step: partition counters reset");
+    const int64_t lds = ((int64_t)a.part_kmax * 4 + 15) & ~int64_t(15);
+    if (a.n_gchunk1 + a.n_gchunk2 > 0) {
+        auto k = k_part_scatter<TX, TV, TD, IDB>;
+        if (int rc = set_lds(k, lds)) return rc;
+        hipLaunchKernelGGL(k, dim3((unsigned)(a.n_gchunk1 + a.n_gchunk2)), dim3(SCAT_WG), (size_t)lds,
+                           st, a, make_frame_k(a));
+        if (int rc = check_launch("k_part_scatter")) return rc;
+    }
+    if (a.n_parts > 0) {
+        auto k = k_part_join<TD, IDB>;
+        const int64_t lds = part_lds_bytes(a.part_e, a.part_slots);
+        if (int rc = set_lds(k, lds)) return rc;
+        hipLaunchKernelGGL(k, dim3((unsigned)a.n_parts), dim3(PART_WG), (size_t)lds, st, a);
+        if (int rc = check_launch("k_part_join")) return rc;
+    }
+    if (a.n_gchunk2 > 0) {
+        hipLaunchKernelGGL((k_part_emit<IDB>), dim3((unsigned)a.n_gchunk2), dim3(BIG_WG), 0, st, a);
+        if (int rc = check_launch("k_part_emit")) return rc;
+    }
+    return OA_OK;
+}
+
 template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
 int launch_big(const oa_step_args &a, hipStream_t st) {
+    if constexpr (COMPARE && !OTF) {
+        if (a.n_parts > 0) return launch_part<TX, TV, TD, IDB>(a, st);
+    }
     if (a.n_gchunk1 > 0) {
         hipLaunchKernelGGL((k_big_frame<TX, TV, TD, IDB, COMPARE, OTF>), dim3((unsigned)a.n_gchunk1),
                            dim3(BIG_WG), 0, st, a, make_frame_k(a));
@@ -1608,6 +2043,8 @@ int32_t oa_build_info(int32_t which) {
         case 1: return HMAX;
         case 2: return UNR1;
         case 3: return KROWS;
+        case 4: return PART_E;
+        case 5: return PART_KMAX;
         default: return -1;
     }
 }
@@ -1623,6 +2060,10 @@ int64_t oa_struct_size(int32_t which) {
 }
 
 const char *oa_last_error(void) { return g_err; }
+
+int64_t oa_part_lds_bytes(int32_t entries, int32_t slots) {
+    return part_lds_bytes(entries, slots);
+}
 
 int64_t oa_step_lds_bytes(int32_t entries, int32_t slots, int32_t dx_f64) {
     return step_lds_bytes(entries, slots, dx_f64 ? 8 : 4);
@@ -1727,13 +2168,24 @@ int oa_step(const oa_step_args *args, void *stream) {
         return fail(OA_E_ARG, "scratch_pos: previous state of 2^31 rows or more");
     if (a.onthefly && a.compare && (!a.angle_out || !a.matched_prev || !a.matched_cur))
         return fail(OA_E_ARG, "null on-the-fly output pointer");
-    if (a.n_gchunk1 > 0 && (!a.gchunk1 || !a.gtab || (a.compare && !a.gkeys)))
+    if (a.n_gchunk1 > 0 && (!a.gchunk1 || !a.gtab ||
+                            (a.compare && !(a.n_parts > 0 && !a.onthefly) && !a.gkeys)))
         return fail(OA_E_ARG, "null large-halo table pointer");
     if (a.compare && a.n_gchunk2 > 0 && !a.gchunk2)
         return fail(OA_E_ARG, "null large-halo chunk pointer");
+    const bool part = a.compare && !a.onthefly && a.n_parts > 0;
+    if (part && (!a.plist || !a.gpart || !a.pkey_cur || !a.ppos_cur || !a.pcnt || !a.gmark ||
+                 (a.n_gchunk2 > 0 && (!a.pkey_prev || !a.ppos_prev || !a.pmeta_prev ||
+                                      !a.prh_prev)) || a.part_kmax < 1 ||
+                 a.part_e < 64 || a.part_e > PART_E || a.part_e % 64 ||
+                 a.part_slots <= a.part_e || a.part_slots > PART_S ||
+                 a.part_kmax > PART_KMAX))
+        return fail(OA_E_ARG, "bad large-halo partition arguments");
+    if (a.onthefly && a.n_parts > 0)
+        return fail(OA_E_ARG, "the partitioned large-halo path is not for on-the-fly steps");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (a.compare && a.n_global_items > 0) {
-        if (hipMemsetAsync(a.gkeys, 0, (size_t)a.gtab_total * 16, st) != hipSuccess ||
+        if ((!part && hipMemsetAsync(a.gkeys, 0, (size_t)a.gtab_total * 16, st) != hipSuccess) ||
             hipMemsetAsync(a.item_count + a.n_items, 0, (size_t)a.n_global_items * 4, st) != hipSuccess)
             return fail(OA_E_LAUNCH, "oa_step: large-halo table reset");
     }

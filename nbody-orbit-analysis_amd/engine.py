@@ -198,6 +198,69 @@ def plan_global(glob, cur_cnt, prev_cnt, first_index, compare):
     return chunks(n1).reshape(-1, 3), chunks(n2).reshape(-1, 3), tab, int(cap.sum())
 
 
+PART_FILL = 0.9      # mean fill of a large-halo partition's LDS table (k_part_join)
+PART_SPREAD = int(os.environ.get('ORBIT_PART_SPREAD', 32))   # partitions per large
+                     # halo at least: the join work-groups one XCD runs at once (32 CUs x 2)
+
+
+def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, n_xcd=8):
+    """Partition layout of the global items for the partitioned large-halo path
+    (k_part_scatter / k_part_join / k_part_emit), vectorised.
+
+    A halo with a progenitor block gets K = ceil(C / (0.9 part_e)) hash partitions
+    of its IDs: a partition's current count is binomial with mean <= 0.9 part_e, so
+    the LDS capacity is many standard deviations away (an overflow is reported by the
+    kernel and the snapshot re-runs on the global-table path).  Previous buckets hold
+    mean + 8 sqrt(mean) + 64 entries.  plist deals the partitions to the 8 XCDs in
+    contiguous runs (work-group b runs on XCD b % 8), so one halo's partitions share
+    an L2 for their gathers.  Returns None when no halo needs the join or one needs
+    more than ``kmax`` partitions."""
+    h = np.asarray(glob['h0'], dtype=np.int64)
+    c = np.asarray(cur_cnt, dtype=np.int64)[h]
+    p = np.maximum(np.asarray(prev_cnt, dtype=np.int64)[h], 0)
+    # at least PART_SPREAD partitions (of >= 1024 particles): as many as one XCD runs
+    # at once, so an XCD works on one halo at a time and that halo's gathered r̂ and
+    # state words stay in the XCD's 4 MB L2
+    K = np.maximum(-(-c // int(part_e * PART_FILL)), np.minimum(PART_SPREAD, c // 1024))
+    K = np.where(p > 0, np.maximum(K, 1), 0).astype(np.int64)
+    nk = int(K.sum())
+    if nk == 0 or K.max() > kmax:
+        return None
+    mean = p / np.maximum(K, 1)
+    cap2 = np.where(K > 0, np.ceil(mean + 8 * np.sqrt(mean) + 64), 0).astype(np.int64)
+    cur_sz, prev_sz = K * int(part_e), K * cap2
+    gpart = np.zeros((len(h), 8), dtype=np.int64)
+    gpart[:, 0] = np.cumsum(cur_sz) - cur_sz
+    gpart[:, 1] = np.cumsum(prev_sz) - prev_sz
+    gpart[:, 2], gpart[:, 3] = K, cap2
+    gpart[:, 4] = np.cumsum(2 * K) - 2 * K
+    g = np.repeat(np.arange(len(h)), K)
+    pp = np.arange(nk) - np.repeat(np.cumsum(K) - K, K)
+    per = -(-nk // n_xcd)
+    b = np.arange(per * n_xcd)
+    idx = (b % n_xcd) * per + b // n_xcd
+    ok = idx < nk
+    plist = np.zeros((len(b), 2), dtype=np.int32)
+    plist[:, 0] = -1
+    plist[ok, 0], plist[ok, 1] = g[idx[ok]], pp[idx[ok]]
+    return dict(gpart=gpart, plist=plist, n_cur=int(cur_sz.sum()), n_prev=int(prev_sz.sum()),
+                kmax=int(K.max()))
+
+
+def retry_plan(pr, st):
+    """(entries, part) of the re-run of a step whose kernels reported status ``st``:
+    a full LDS table halves the items (at the floor every halo takes the global-table
+    path, which keys on the full 64-bit ID); an overflowing large-halo partition
+    moves the large halos to the global-table path."""
+    from . import _native as N
+    if st & N.STATUS_PLAN:
+        raise RuntimeError('oa_step: an item exceeds the kernel limits (planner bug)')
+    e = pr.entries
+    if st & N.STATUS_TABLE_OVERFLOW:
+        e = 0 if e <= 256 else max(256, e // 2)
+    return e, pr.part and not (st & N.STATUS_PART_OVERFLOW)
+
+
 def set_item_slots(items, out_slot):
     """items['slot0'] = the first output slot among each item's halos [h0, h1), or -1
     (k_gather_items then needs no serial walk over the halo table)."""
@@ -293,6 +356,7 @@ class PreparedStep:
     compare: bool
     n_prev: int = 0
     entries: int = 0               # per-item particle budget the plan used
+    part: bool = False             # large halos on the partitioned path (k_part_*)
     halos: Optional[torch.Tensor] = None
     d_items: Optional[torch.Tensor] = None
     glob: dict = field(default_factory=dict)       # device chunk lists / tables
@@ -383,6 +447,14 @@ class OrbitEngine:
         self._ws: Optional[Workspace] = None
         # apsis records also carry their previous-state row (ShardedEngine's merge)
         self.emit_positions = False
+        # large halos of compare steps: hash partitions joined in LDS (k_part_*);
+        # ORBIT_PART=0 keeps them on the per-halo global tables (k_big_*)
+        self.part_large = env('ORBIT_PART', '1') != '0'
+        # partition capacity: 4096 entries in 6144 slots (~74 KB of LDS: two join
+        # work-groups per CU); at most oa_build_info(4)
+        self.part_e = min(int(env('ORBIT_PART_ENTRIES', 4096)), self.lib.oa_build_info(4))
+        self.part_slots = self.part_e + self.part_e // 2
+        self.part_kmax = self.lib.oa_build_info(5)
 
     def table_sizes(self, dx_f64, entries=None):
         """(entries, slots) of one k_step item for a float32 / float64 r̂."""
@@ -458,11 +530,11 @@ class OrbitEngine:
             snap[k] = to_device(snapshot[k], dev)
         if is_array(snapshot['masses']):
             snap['masses'] = to_device(snapshot['masses'], dev)
-        entries = None
+        entries, part = None, True
         for attempt in range(10):
             prep = self.prepare(snap, centres, bulk_cat, H, z, exists, compare,
                                 angles_in=angles_in, plan_src=snapshot,
-                                entries=entries)
+                                entries=entries, part=part)
             ws = self.workspace(prep) if compare else None
             if ws is not None:
                 ws.status.zero_()
@@ -471,12 +543,7 @@ class OrbitEngine:
             st = int(ws.status.item()) if compare else 0
             if not st:
                 break
-            if st & N.STATUS_PLAN:
-                raise RuntimeError('oa_step: an item exceeds the kernel limits (planner bug)')
-            # cuckoo stash full: smaller items; at the floor every halo takes the
-            # global-table path, which keys on the full 64-bit ID
-            e = prep.entries
-            entries = 0 if e <= 256 else max(256, e // 2)
+            entries, part = retry_plan(prep, st)
         else:
             raise RuntimeError('LDS hash tables kept overflowing')
         self.prev = SnapshotState(ids=snap['ids'], rhat=prep.rhat, meta=prep.meta,
@@ -485,13 +552,14 @@ class OrbitEngine:
         return res
 
     def prepare(self, snap, centres, bulk_cat, H, z, exists, compare, angles_in=None,
-                plan_src=None, prev_layout=None, entries=None):
+                plan_src=None, prev_layout=None, entries=None, part=True):
         """Host half of a step: dtype plan, halo/item tables, device uploads.
 
         ``snap`` holds device tensors for ids/coordinates/velocities(/masses);
         ``prev_layout`` (starts, counts, exists, plan) defaults to the engine state.
         ``entries`` overrides the per-item particle budget of the plan (0: every halo
-        on the global-table path)."""
+        on the large-halo path); ``part`` = False keeps large halos on the global-table
+        path (k_big_*) instead of the partitioned one (k_part_*)."""
         dev = self.device
         exists = np.asarray(exists)
         plan = plan_dtypes(plan_src if plan_src is not None else snap,
@@ -531,7 +599,26 @@ class OrbitEngine:
             g['ch2'] = torch.from_numpy(ch2).to(dev) if len(ch2) else None
             g['tab'] = torch.from_numpy(tab).to(dev)
             g['total'] = total
-            if compare:
+            pl = None
+            if compare and part and self.part_large:
+                pl = plan_part(glob, counts, halos['prev_cnt'], self.part_e, self.part_kmax)
+            if pl is not None:
+                pr.part = True
+                i32, i64 = torch.int32, torch.int64
+                g['plist'] = torch.from_numpy(pl['plist'].reshape(-1)).to(dev)
+                g['gpart'] = torch.from_numpy(pl['gpart'].reshape(-1)).to(dev)
+                g['pkey_cur'] = torch.empty(pl['n_cur'], dtype=i64, device=dev)
+                g['ppos_cur'] = torch.empty(pl['n_cur'], dtype=i32, device=dev)
+                g['pkey_prev'] = torch.empty(max(pl['n_prev'], 1), dtype=i64, device=dev)
+                g['ppos_prev'] = torch.empty(max(pl['n_prev'], 1), dtype=i32, device=dev)
+                g['pmeta_prev'] = torch.empty(max(pl['n_prev'], 1), dtype=i32, device=dev)
+                g['prh_prev'] = torch.empty(3 * max(pl['n_prev'], 1), dtype=plan.torch_dx,
+                                            device=dev)
+                g['pcnt'] = torch.empty(2 * len(pl['plist']), dtype=i32, device=dev)
+                g['gmark_base'] = int(glob['scratch_off'][0])
+                g['gmark'] = torch.empty(max(scratch - g['gmark_base'], 1), dtype=i32, device=dev)
+                g['n_parts'], g['kmax'] = len(pl['plist']), pl['kmax']
+            elif compare:
                 g['keys'] = torch.empty(2 * total, dtype=torch.int64, device=dev)
             g['n1'], g['n2'] = len(ch1), len(ch2)
         pr.rhat = torch.empty(n * 3, dtype=plan.torch_dx, device=dev)
@@ -556,6 +643,15 @@ class OrbitEngine:
             a.gchunk1, a.gchunk2 = g['ch1'].data_ptr(), _ptr(g['ch2'])
             a.gtab, a.gtab_total = g['tab'].data_ptr(), g['total']
             a.gkeys, a.gvals = _ptr(g.get('keys')), _ptr(g.get('vals'))
+            if pr.part:
+                a.n_parts, a.part_kmax = g['n_parts'], g['kmax']
+                a.part_e, a.part_slots = self.part_e, self.part_slots
+                a.plist, a.gpart = g['plist'].data_ptr(), g['gpart'].data_ptr()
+                a.pkey_cur, a.ppos_cur = g['pkey_cur'].data_ptr(), g['ppos_cur'].data_ptr()
+                a.pkey_prev, a.ppos_prev = g['pkey_prev'].data_ptr(), g['ppos_prev'].data_ptr()
+                a.pmeta_prev, a.prh_prev = g['pmeta_prev'].data_ptr(), g['prh_prev'].data_ptr()
+                a.pcnt, a.gmark, a.gmark_base = (g['pcnt'].data_ptr(), g['gmark'].data_ptr(),
+                                                 g['gmark_base'])
         a.H, a.one_plus_z = float(H), float(1 + z)
         a.n_box_dims = len(plan.box)
         for d, L in enumerate(plan.box):

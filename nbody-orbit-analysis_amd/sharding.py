@@ -425,8 +425,7 @@ class EngineLocal:
         hv[:, 4:hi] = rows[:, :hi - 4].to(hv.device, non_blocking=True)
 
     def launch(self, lp, prev_lp, step_events=None, check=True):
-        from .engine import SnapshotState
-        from . import _native as N
+        from .engine import SnapshotState, retry_plan
         eng = self.engine
         for _ in range(10):
             ws = eng.workspace(lp) if lp.compare else None
@@ -441,15 +440,12 @@ class EngineLocal:
             st = int(ws.status.item()) if (check and ws is not None) else 0
             if not st:
                 break
-            if st & N.STATUS_PLAN:
-                raise RuntimeError('oa_step: an item exceeds the kernel limits (planner bug)')
-            # re-plan with smaller items, finally all on the global-table path
+            # re-plan: smaller items / large halos on the global-table path
+            entries, part = retry_plan(lp, st)
             shard, centres, bulk, H, z, exists, compare, angles_in, layout = lp.src
-            e = lp.entries
             hv = lp.halos.view(torch.float64).view(-1, 12)[:, 4:10].clone()
             lp2 = eng.prepare(shard, centres, bulk, H, z, exists, compare, angles_in=angles_in,
-                              plan_src=shard, prev_layout=layout,
-                              entries=0 if e <= 256 else max(256, e // 2))
+                              plan_src=shard, prev_layout=layout, entries=entries, part=part)
             lp2.halos.view(torch.float64).view(-1, 12)[:, 4:10] = hv
             lp2.exists, lp2.src, lp2.share_bulk = lp.exists, lp.src, lp.share_bulk
             lp.__dict__.update(lp2.__dict__)

@@ -108,7 +108,7 @@ class OnTheFly:
         if compare:
             layout = (prev.starts, prev.counts, prev.exists, prev.plan, prev.ids.numel())
         pr = eng.prepare(dsnap, centres, None, np.float64(0.0), 0.0, np.arange(nh), compare,
-                         plan_src=s, prev_layout=layout, entries=entries)
+                         plan_src=s, prev_layout=layout, entries=entries, part=False)
         plan = pr.plan
         coord = np.dtype(plan.coord)
         # on-the-fly frame: r̂ stored in the coordinate dtype (:82-83, 112-113)

@@ -92,9 +92,55 @@ def test_global_and_packed_paths_match(name):
     # (entries, slots): the last config packs the cuckoo tables to ~90 % load so insert
     # chains hit the stash and the table-overflow re-plan path
     for entries, slots in ((256, None), (700, None), (700, 760)):
-        eng = OrbitEngine(mode=meta['run']['mode'], lds_entries=entries, hmax=7, lds_slots=slots)
-        out = run_driver(u, meta['run'], engine=eng)
-        compare_groups(out.groups, groups(fix), {})
+        for part in (True, False):              # partitioned / global-table large halos
+            eng = OrbitEngine(mode=meta['run']['mode'], lds_entries=entries, hmax=7,
+                              lds_slots=slots)
+            eng.part_large = part
+            out = run_driver(u, meta['run'], engine=eng)
+            compare_groups(out.groups, groups(fix), {})
+
+
+def _recording(eng):
+    """Wrap eng.prepare to record which large-halo path each compare step planned."""
+    seen = []
+    orig = eng.prepare
+
+    def prepare(*a, **k):
+        pr = orig(*a, **k)
+        if pr.compare and pr.n_global:
+            seen.append(pr.part)
+        return pr
+    eng.prepare = prepare
+    return seen
+
+
+@pytest.mark.parametrize('mode', ['pericentric', 'apocentric'])
+def test_partitioned_large_halos(mode, monkeypatch):
+    """Halos larger than a k_step item (30000 particles) through the partitioned path
+    (k_part_scatter / k_part_join / k_part_emit), through the global tables (k_big_*),
+    and with partitions forced past their LDS capacity (the kernel reports it and the
+    snapshot re-runs on the global tables): all three equal the oracle."""
+    from orbitanalysis_amd import engine as E
+    from orbitanalysis_amd.engine import OrbitEngine
+    from orbitanalysis_amd.synthetic import PlummerSnapshots
+    u = PlummerSnapshots(n_halos=6, n_per_halo=30000, n_snapshots=4, seed=41)
+    want = _oracle_run(u, mode)
+    eng = OrbitEngine(mode=mode)
+    seen = _recording(eng)
+    rep = {}
+    compare_groups(run_driver(u, dict(mode=mode), engine=eng).groups, want, rep)
+    assert seen and all(seen), seen                  # every compare step partitioned
+    assert rep['angles'] > 0
+    eng = OrbitEngine(mode=mode)
+    eng.part_large = False
+    compare_groups(run_driver(u, dict(mode=mode), engine=eng).groups, want, {})
+    # mean partition fill 2x the LDS table: every compare step overflows, then re-runs
+    monkeypatch.setattr(E, 'PART_FILL', 2.0)
+    monkeypatch.setattr(E, 'PART_SPREAD', 1)
+    eng = OrbitEngine(mode=mode)
+    seen = _recording(eng)
+    compare_groups(run_driver(u, dict(mode=mode), engine=eng).groups, want, {})
+    assert True in seen and False in seen, seen
 
 
 @pytest.mark.parametrize('mode', ['pericentric', 'apocentric'])
