@@ -756,6 +756,11 @@ class OrbitEngine:
             ms = snapshot['masses']
             m = ms[torch.from_numpy(rows).to(ms.device)].to(dev).contiguous() \
                 if isinstance(ms, torch.Tensor) else to_device(np.asarray(ms)[rows], dev)
+        # every listed block empty: the kernel still needs real (unread) arrays
+        if v.numel() == 0:
+            v = torch.zeros(3, dtype=v.dtype, device=dev)
+        if m is not None and m.numel() == 0:
+            m = torch.zeros(1, dtype=m.dtype, device=dev)
         halos = np.zeros(len(halo_idx), dtype=N.HALO_DTYPE)
         halos['cur_off'] = np.concatenate([[0], np.cumsum(c)[:-1]]) if len(c) else c
         halos['cur_cnt'] = c

@@ -67,31 +67,40 @@ class HashOwner:
 class IdRangeOwner:
     """rank = floor((ID - lo) * world / (hi - lo)), clipped: contiguous ID ranges.
     Without bounds, [lo, hi) is taken from the first snapshot the engine sees (every
-    rank sees the same one); later IDs outside it go to the first / last rank."""
+    rank sees the same one); later IDs outside it go to the first / last rank.
+    IDs are taken as their int64 bit patterns (uint64 IDs >= 2^63 sort below the
+    others, as device tensors hold them), and the ratio is evaluated in float64 (the
+    same operations on the host and the device)."""
 
     def __init__(self, lo=None, hi=None):
         self.lo = None if lo is None else int(lo)
         self.hi = None if hi is None else int(hi)
 
+    @staticmethod
+    def _i64(ids):
+        ids = np.asarray(ids)
+        return ids.view(np.int64) if ids.dtype.itemsize == 8 else ids.astype(np.int64)
+
     def fit(self, ids):
         if self.lo is not None:
             return
         if isinstance(ids, torch.Tensor):
-            lo, hi = (int(ids.min()), int(ids.max()) + 1) if ids.numel() else (0, 1)
+            t = ids.to(torch.int64)
+            lo, hi = (int(t.min()), int(t.max()) + 1) if t.numel() else (0, 1)
         else:
-            ids = np.asarray(ids)
-            lo, hi = (int(ids.min()), int(ids.max()) + 1) if ids.size else (0, 1)
+            v = self._i64(ids)
+            lo, hi = (int(v.min()), int(v.max()) + 1) if v.size else (0, 1)
         self.lo, self.hi = lo, hi
 
     def __call__(self, ids, world):
-        ids = np.asarray(ids).astype(np.int64)
-        span = max(self.hi - self.lo, 1)
-        r = ((ids - self.lo).astype(np.float64) * world / span).astype(np.int64)
-        return np.clip(r, 0, world - 1)
+        span = float(max(self.hi - self.lo, 1))
+        v = self._i64(ids).astype(np.float64)
+        r = np.floor((v - float(self.lo)) * world / span)
+        return np.clip(r, 0, world - 1).astype(np.int64)
 
     def mask(self, ids_t, world, rank):
-        span = max(self.hi - self.lo, 1)
-        r = ((ids_t.to(torch.int64) - self.lo).to(torch.float64) * world / span).to(torch.int64)
+        span = float(max(self.hi - self.lo, 1))
+        r = torch.floor((ids_t.to(torch.int64).to(torch.float64) - float(self.lo)) * world / span)
         return r.clamp_(0, world - 1) == rank
 
 

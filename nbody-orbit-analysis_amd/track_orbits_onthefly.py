@@ -93,7 +93,7 @@ class OnTheFly:
         self.eng = engine if engine is not None else OrbitEngine(mode=mode)
         self.mode = self.eng.mode
 
-    def _prepare(self, snap, slices, centres, compare, prev=None, entries=None):
+    def _prepare(self, snap, slices, centres, compare, prev=None, entries=None, bulk=None):
         eng = self.eng
         n = len(snap['ids'])
         s = dict(snap)
@@ -107,7 +107,9 @@ class OnTheFly:
         layout = None
         if compare:
             layout = (prev.starts, prev.counts, prev.exists, prev.plan, prev.ids.numel())
-        pr = eng.prepare(dsnap, centres, None, np.float64(0.0), 0.0, np.arange(nh), compare,
+        # bulk velocities computed from the blocks (:85-98), unless given (a shard's
+        # rows do not hold whole blocks: ShardedOnTheFly passes the full-block ones)
+        pr = eng.prepare(dsnap, centres, bulk, np.float64(0.0), 0.0, np.arange(nh), compare,
                          plan_src=s, prev_layout=layout, entries=entries, part=False)
         plan = pr.plan
         coord = np.dtype(plan.coord)
@@ -119,8 +121,14 @@ class OnTheFly:
         a.vr_f64 = int(np.result_type(plan.vel, coord) == F64)
         return pr
 
-    def run(self, snaps, slices, centres, carried=None):
+    def run(self, snaps, slices, centres, carried=None, bulks=None, merge_parts=False):
         """snaps / slices / centres: [current, previous].  Returns host outputs.
+
+        ``bulks``: [current, previous] bulk-velocity rows to use instead of computing
+        them from the blocks.  ``merge_parts``: also return, under ``'parts'``, what a
+        sharded run needs to merge ranks (the previous-state rows of the apsis records
+        and of the angle changes, the per-halo entered lists before interleaving and
+        the current rows of the loader-order ones).
 
         ``carried``: the (state, bulk velocities) a previous call left for its current
         snapshot (``self.carry``), when that snapshot is this call's previous one with
@@ -131,7 +139,8 @@ class OnTheFly:
             if np_dtype(cur['coordinates']) != np_dtype(prv['coordinates']):
                 raise NotImplementedError('coordinate dtype differs between the two snapshots')
             # previous snapshot: frame only
-            pp = self._prepare(prv, slices[1], centres[1], False)
+            pp = self._prepare(prv, slices[1], centres[1], False,
+                               bulk=None if bulks is None else bulks[1])
             eng.launch(pp, None)
             prev = SnapshotState(ids=pp.snap['ids'], rhat=pp.rhat, meta=pp.meta,
                                  starts=pp.starts, counts=pp.counts,
@@ -144,7 +153,8 @@ class OnTheFly:
         n_prev = prev.ids.numel()
         entries = None
         for _ in range(10):
-            pc = self._prepare(cur, slices[0], centres[0], True, prev=prev, entries=entries)
+            pc = self._prepare(cur, slices[0], centres[0], True, prev=prev, entries=entries,
+                               bulk=None if bulks is None else bulks[0])
             coord = _TORCH[np.dtype(pc.plan.coord)]
             angle_out = torch.empty(max(n_prev, 1), dtype=coord, device=eng.device)
             matched_prev = torch.zeros(max(n_prev, 1), dtype=torch.uint8, device=eng.device)
@@ -220,11 +230,136 @@ class OnTheFly:
         self.carry = (SnapshotState(ids=pc.snap['ids'], rhat=pc.rhat, meta=pc.meta,
                                     starts=pc.starts, counts=pc.counts, exists=np.arange(nh),
                                     plan=pc.plan), bulk_c)
-        return {'apsis_offsets': offsets, 'apsis_ids': apsis_ids,
+        extra = {}
+        if merge_parts:
+            total = int(offsets[-1]) if len(offsets) else 0
+            extra['parts'] = dict(
+                apsis_pos=res.apsis_pos[:total].cpu().numpy().astype(np.int64),
+                angle_pos=torch.nonzero(mp).squeeze(1).cpu().numpy(),
+                srt=srt, s_off=s_off, raw=raw, r_off=r_off,
+                raw_pos=esel[~sorted_h].cpu().numpy(), p_has=p_has)
+        return {**extra, 'apsis_offsets': offsets, 'apsis_ids': apsis_ids,
                 'angles': angles.astype(adt, copy=False),
                 'entered_offsets': e_off, 'entered_ids': entered,
                 'departed_offsets': d_off, 'departed_ids': departed,
                 'bulk_velocities': [bulk_c, bulk_p]}
+
+
+def merge_onthefly(parts, nh):
+    """Merge the ranks' on-the-fly outputs of one snapshot pair (ShardedOnTheFly).
+
+    ``parts``: per rank, a dict with the rank's per-halo CSR outputs and each element's
+    global row (``*_gpos``).  A halo's previous and current blocks tile their snapshots
+    in halo order, so a global previous row orders apsis records and angle changes
+    exactly as the reference emits them (previous-block order, halos in order,
+    :154-174); entered / departed IDs are per-halo sorted unique (setdiff1d, :145,
+    :168; the ranks' ID sets are disjoint), except the entered IDs of a halo without a
+    progenitor block, which keep loader order (:178), i.e. global current-row order."""
+    def cat(key, dt=None):
+        xs = [np.asarray(q[key]) for q in parts]
+        return np.concatenate(xs) if xs else np.zeros(0, dt)
+
+    def halo_of(key):
+        return np.concatenate([np.repeat(np.arange(nh), np.diff(q[key])) for q in parts]) \
+            if parts else np.zeros(0, np.int64)
+
+    def counts(key):
+        return np.sum([np.diff(q[key]) for q in parts], axis=0) if parts else np.zeros(nh, np.int64)
+
+    def offsets(c):
+        return np.concatenate([[0], np.cumsum(c)]).astype(np.int64)
+
+    out = {}
+    order = np.argsort(cat('apsis_gpos'), kind='stable')
+    out['apsis_ids'] = cat('apsis_ids')[order]
+    out['apsis_offsets'] = offsets(counts('apsis_offsets'))
+    out['angles'] = cat('angles')[np.argsort(cat('angle_gpos'), kind='stable')]
+    dep, dh = cat('departed_ids'), halo_of('departed_offsets')
+    out['departed_ids'] = dep[np.lexsort((dep, dh))]
+    out['departed_offsets'] = offsets(counts('departed_offsets'))
+    srt, sh = cat('srt'), halo_of('s_off')
+    srt = srt[np.lexsort((srt, sh))]
+    raw, rh = cat('raw'), halo_of('r_off')
+    raw = raw[np.lexsort((cat('raw_gpos'), rh))]
+    out['entered_ids'], out['entered_offsets'] = _interleave_halos(
+        parts[0]['p_has'], srt, offsets(counts('s_off')), raw, offsets(counts('r_off')))
+    return out
+
+
+class ShardedOnTheFly:
+    """The on-the-fly driver over ID-range shards (BASELINE configs[4]):
+    one process per GPU, ``torch.distributed`` (RCCL, or gloo in the tests).
+
+    Every rank receives both snapshots from the loader (the reference's contract),
+    keeps the particles of its ID range (``IdRangeOwner``, fitted on the first
+    snapshot it sees) and runs the on-the-fly pipeline on them; a particle's rows in
+    the two snapshots are on the same rank, so the join has no exchange.  Bulk
+    velocities are whole-block sums: halo j's is computed by rank j % world on the
+    full block and the rows are all-gathered.  The outputs -- small next to the
+    snapshots -- are all-gathered with their global rows and merged
+    (``merge_onthefly``) into exactly the single-process file; rank 0 writes it.
+
+    ``track_orbits(..., engine=ShardedOnTheFly(OrbitEngine(mode=...)))``."""
+
+    def __init__(self, engine, group=None, owner=None):
+        from .sharding import IdRangeOwner
+        self.eng = engine
+        self.mode = engine.mode
+        self.group = group
+        self.owner = owner if owner is not None else IdRangeOwner()
+        engine.emit_positions = True
+        self.otf = OnTheFly(engine)
+        self.carry = None
+
+    @property
+    def rank(self):
+        import torch.distributed as dist
+        return dist.get_rank(self.group)
+
+    def run(self, snaps, slices, centres, carried=None):
+        import torch.distributed as dist
+        from .sharding import shard_snapshot
+        world, rank = dist.get_world_size(self.group), dist.get_rank(self.group)
+        eng = self.eng
+        self.owner.fit(np.asarray(snaps[0]['ids']))
+        shards, lslices, sels, bulks = [], [], [], []
+        for snap, sl in zip(snaps, slices):
+            sl = np.asarray(sl, dtype=np.int64).reshape(-1, 2)
+            n = len(snap['ids'])
+            nh = len(sl)
+            full = dict(snap)
+            full['region_offsets'] = _block_starts(sl, n)
+            mine = np.arange(rank, nh, world)
+            rows = eng.block_bulk(full, mine) if len(mine) else None
+            got = [None] * world
+            dist.all_gather_object(got, (mine, rows), group=self.group)
+            bulk = None
+            for idx, r in got:
+                if r is not None:
+                    if bulk is None:
+                        bulk = np.zeros((nh, 3), dtype=r.dtype)
+                    bulk[idx] = r
+            keep = self.owner(np.asarray(snap['ids']), world) == rank
+            sh, sel, st, cnt = shard_snapshot(full, keep)
+            lsl = np.where(sl[:, :1] >= 0, np.stack([st, st + cnt], axis=1), -1)
+            shards.append(sh)
+            lslices.append(lsl)
+            sels.append(sel)
+            bulks.append(bulk if bulk is not None else np.zeros((0, 3)))
+        out = self.otf.run(shards, lslices, centres, bulks=bulks, merge_parts=True)
+        q = out.pop('parts')
+        mine = dict(apsis_offsets=out['apsis_offsets'], apsis_ids=out['apsis_ids'],
+                    apsis_gpos=sels[1][q['apsis_pos']],
+                    angles=out['angles'], angle_gpos=sels[1][q['angle_pos']],
+                    departed_offsets=out['departed_offsets'], departed_ids=out['departed_ids'],
+                    srt=q['srt'], s_off=q['s_off'], raw=q['raw'], r_off=q['r_off'],
+                    raw_gpos=sels[0][q['raw_pos']], p_has=q['p_has'])
+        allp = [None] * world
+        dist.all_gather_object(allp, mine, group=self.group)
+        merged = merge_onthefly(allp, len(slices[0]))
+        out.update(merged)
+        out['angles'] = out['angles'].astype(mine['angles'].dtype, copy=False)
+        return out
 
 
 # Frame state of the last call's current snapshot, keyed by the loader callable
@@ -251,7 +386,8 @@ def clear_carry():
 def track_orbits(snapshot_number, progenitor_links, regions, load_snapshot_data,
                  savefile, mode='pericentric', verbose=True, engine=None):
     """track_orbits_onthefly.py:8-58 (signature, callbacks and errors of the reference;
-    ``engine`` optionally supplies a configured ``OrbitEngine``)."""
+    ``engine`` optionally supplies a configured ``OrbitEngine``, or a
+    ``ShardedOnTheFly`` for one rank of a multi-GPU run)."""
     if (mode != 'pericentric') and (mode != 'apocentric'):
         raise ValueError(
             "Orbit detection mode not recognized. Please specify either "
@@ -265,7 +401,11 @@ def track_orbits(snapshot_number, progenitor_links, regions, load_snapshot_data,
     except TypeError:                     # an unhashable callable: no carry
         key, entry = None, None
     carried = None
-    otf = OnTheFly(engine, mode)
+    sharded = isinstance(engine, ShardedOnTheFly)
+    if sharded:
+        otf, entry, key = engine, None, None          # every call loads both snapshots
+    else:
+        otf = OnTheFly(engine, mode)
     if otf.mode != mode:
         raise ValueError('engine mode %r != mode %r' % (otf.mode, mode))
     # device tensors of a carry belong to the engine (device, LDS configuration) that
@@ -319,7 +459,8 @@ def track_orbits(snapshot_number, progenitor_links, regions, load_snapshot_data,
             'region_positions': np.array(positions),
             'bulk_velocities': np.array(out['bulk_velocities'])}
     attrs = {} if box_size is None else {'box_size': box_size}
-    save_to_file(savefile, snapshot_number, data, attrs, verbose)
+    if not sharded or otf.rank == 0:                  # one file per snapshot
+        save_to_file(savefile, snapshot_number, data, attrs, verbose)
     return data
 
 
