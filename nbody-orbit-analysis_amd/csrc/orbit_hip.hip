@@ -41,7 +41,7 @@ namespace {
 #define OA_WG 1024
 #endif
 #ifndef OA_UNR1
-#define OA_UNR1 2           // phase 1: rows per wave trip
+#define OA_UNR1 1           // phase 1: rows per wave trip (2: dynamic trips; A/B r02 wg: 1 is 0.7 % faster)
 #endif
 #ifndef OA_KROWS
 #define OA_KROWS 12         // phase 2: progenitor rows held per wave (n_pv <= KROWS * WG)

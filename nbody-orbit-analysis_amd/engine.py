@@ -151,6 +151,13 @@ def plan_items(cur_cnt, prev_cnt, entries, hmax=128, out_slot=None, max_pv=None,
     progenitor row, global items after the packed ones).  An item's ``n_pv`` counts
     its progenitor rows of 64 virtual positions: every progenitor block is padded to
     whole rows, so a row of k_step's phase 2 lies in one block."""
+    out, k, n, scratch = _plan(cur_cnt, prev_cnt, entries, hmax, out_slot, max_pv, slots, cur_off)
+    return out[:k], out[k:n], scratch
+
+
+def _plan(cur_cnt, prev_cnt, entries, hmax, out_slot, max_pv, slots, cur_off):
+    """oa_plan_items into one ITEM_DTYPE buffer: (items, n_small, n, scratch), the
+    packed items first (no copies: prepare uploads items[:n] as they are)."""
     lib = N.load()
     cur = np.ascontiguousarray(cur_cnt, dtype=np.int64)
     prev = np.ascontiguousarray(prev_cnt, dtype=np.int64)
@@ -162,7 +169,7 @@ def plan_items(cur_cnt, prev_cnt, entries, hmax=128, out_slot=None, max_pv=None,
     osl = None if out_slot is None else np.ascontiguousarray(out_slot, dtype=np.int64)
     if max_pv is None:
         max_pv = lib.oa_build_info(3) * lib.oa_build_info(0)
-    out = np.zeros(max(nh, 1), dtype=N.ITEM_DTYPE)
+    out = np.empty(max(nh, 1), dtype=N.ITEM_DTYPE)       # every planned row is written
     n_small, scratch = ctypes.c_int64(0), ctypes.c_int64(0)
     n = lib.oa_plan_items(off.ctypes.data, cur.ctypes.data, prev.ctypes.data,
                           None if osl is None else osl.ctypes.data, nh, int(entries),
@@ -170,8 +177,7 @@ def plan_items(cur_cnt, prev_cnt, entries, hmax=128, out_slot=None, max_pv=None,
                           ctypes.byref(n_small), ctypes.byref(scratch))
     if n < 0:
         raise ValueError(lib.oa_last_error().decode())
-    k = n_small.value
-    return out[:k].copy(), out[k:n].copy(), int(scratch.value)
+    return out, n_small.value, n, int(scratch.value)
 
 
 def plan_global(glob, cur_cnt, prev_cnt, first_index, compare):
@@ -513,10 +519,9 @@ class OrbitEngine:
             halos['prev_off'][has_prog] = p_starts[p[has_prog]]
             halos['prev_cnt'][has_prog] = p_counts[p[has_prog]]
             halos['out_slot'][has_prog] = np.arange(int(has_prog.sum()))
-        items, glob, scratch = plan_items(counts, halos['prev_cnt'], entries, self.hmax,
-                                          out_slot=halos['out_slot'], max_pv=self.max_pv,
-                                          slots=slots, cur_off=starts)
-        return halos, items, glob, scratch, starts, counts, has_prog
+        buf, k, n_it, scratch = _plan(counts, halos['prev_cnt'], entries, self.hmax,
+                                      halos['out_slot'], self.max_pv, slots, starts)
+        return halos, buf[:n_it], k, scratch, starts, counts, has_prog
 
     # ------------------------------------------------------------------ step
     def step(self, snapshot, centres, bulk_cat, H, z, exists, compare, angles_in=None):
@@ -582,11 +587,11 @@ class OrbitEngine:
             check_angles_in(angles_in, n)
         lds_e, lds_s = self.table_sizes(plan.dx == F64)
         plan_e = lds_e if entries is None else min(int(entries), lds_e)
-        halos, items, glob, scratch, starts, counts, has_prog = self.build_tables(
+        halos, all_items, n_small, scratch, starts, counts, has_prog = self.build_tables(
             snap, centres, bulk_cat, exists, compare, prev_layout, plan_e, lds_s)
-        all_items = np.concatenate([items, glob])
+        items, glob = all_items[:n_small], all_items[n_small:]
         pr = PreparedStep(plan=plan, n=n, starts=starts, counts=counts, has_prog=has_prog,
-                          items=all_items, n_small=len(items), scratch=scratch,
+                          items=all_items, n_small=n_small, scratch=scratch,
                           compare=bool(compare), n_prev=prev_layout[4] if compare else 0,
                           entries=plan_e)
         pr.halos = _upload(halos.view(np.uint8), dev)
