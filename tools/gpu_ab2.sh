@@ -7,7 +7,7 @@ D=$R/nbody-orbit-analysis_amd/variants
 for rep in ${REPS:-1 2 3}; do
   for spec in $SPECS; do
     v=${spec%%:*}; envs=${spec#*:}
-    lib=""; [ "$v" != base ] && lib="$D/lib_$v.so"
+    lib=""; [ -f "$D/lib_$v.so" ] && lib="$D/lib_$v.so"     # else the default build
     ( export ORBIT_HIP_LIB=$lib; for kv in ${envs//,/ }; do export "$kv"; done
       timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline \
         > "$O/ab_${T}_${v}_$rep.json" 2> "$O/ab_${T}_${v}_$rep.err" )
