@@ -180,8 +180,8 @@ typedef struct oa_step_args {
                                    pairs; g = -1: an idle padding row                */
     const int64_t *gpart;       /* per global item, 8 int64: current bucket base,
                                    previous bucket base, K, previous bucket capacity,
-                                   first counter index, 0, 0, 0 (current buckets hold
-                                   oa_build_info(4) entries each)                    */
+                                   first counter index, 0, 0, 0 (current buckets
+                                   hold part_e entries each)                         */
     uint64_t *pkey_cur;         /* current buckets: IDs (zero-extended 4-byte IDs)    */
     uint32_t *ppos_cur;         /*   position in the halo's block | sign(v_r) << 30   */
     uint64_t *pkey_prev;        /* previous buckets: IDs                              */
@@ -284,6 +284,11 @@ int64_t oa_plan_items(const int64_t *cur_off, const int64_t *cur_cnt, const int6
  * (s_memrealtime, 100 MHz; 6 per work-group) of the last oa_step to host memory.
  * Returns the number of values copied, -1 in normal builds. */
 int64_t oa_debug_stamps(uint64_t *host, int64_t n);
+
+/* Diagnostic builds only: stamps of the large-halo partition kernels of the last
+ * oa_step (which = 0: k_part_join, 8 per work-group; 1: k_part_scatter, 2 per
+ * work-group).  Returns the number of values copied, -1 in normal builds. */
+int64_t oa_debug_part_stamps(int32_t which, uint64_t *host, int64_t n);
 
 /* Largest dynamic LDS allocation a work-group may use on this device (bytes). */
 int64_t oa_max_lds_bytes(void);

@@ -109,6 +109,7 @@ SYMBOLS = {
                               c_i64, c_vp, c_vp]),
     'oa_max_lds_bytes': (c_i64, []),
     'oa_debug_stamps': (c_i64, [c_vp, c_i64]),
+    'oa_debug_part_stamps': (c_i64, [c_i32, c_vp, c_i64]),
     'oa_compact': (ctypes.c_int, [ctypes.POINTER(CompactArgs), c_vp]),
     'oa_match_workspace_bytes': (c_i64, [c_i64]),
     'oa_match_ids': (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp]),

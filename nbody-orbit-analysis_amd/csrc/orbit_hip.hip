@@ -121,10 +121,21 @@ __device__ uint64_t g_stamps[STAMP_MAX_WG * STAMP_N];
 // the last word: a diagnostic value of the work-group (table walks)
 #define DIAG(v) do { if (threadIdx.x == 0 && blockIdx.x < STAMP_MAX_WG) \
     g_stamps[blockIdx.x * STAMP_N + STAMP_N - 1] = (v); } while (0)
+// large-halo partition kernels: 8 stamps per work-group of k_part_join, then 2 per
+// work-group of k_part_scatter
+constexpr int PSTAMP_N = 8;
+__device__ uint64_t g_pstamps[STAMP_MAX_WG * PSTAMP_N];
+__device__ uint64_t g_sstamps[STAMP_MAX_WG * 2];
+#define PSTAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < STAMP_MAX_WG) \
+    g_pstamps[blockIdx.x * PSTAMP_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define SSTAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < STAMP_MAX_WG) \
+    g_sstamps[blockIdx.x * 2 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define WSTAMP(k) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < STAMP_MAX_WG) \
     g_stamps[blockIdx.x * STAMP_N + STAMP_NP + 3 * (threadIdx.x >> 6) + (k)] = \
         __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
+#define PSTAMP(k) do { } while (0)
+#define SSTAMP(k) do { } while (0)
 #define STAMP(k) do { } while (0)
 #define WSTAMP(k) do { } while (0)
 #define DIAG(v) do { } while (0)
@@ -1739,8 +1750,10 @@ __global__ __launch_bounds__(SCAT_WG) void k_part_scatter(const oa_step_args a, 
     int64_t c;
     if (b < 2 * m) { cur = (b & 1) == 0; c = b >> 1; }
     else { cur = n1 > n2; c = b - m; }
+    SSTAMP(0);
     if (cur) part_scatter<TX, TV, TD, IDB, true>(a, fk, lcnt, c);
     else part_scatter<TX, TV, TD, IDB, false>(a, fk, lcnt, c);
+    SSTAMP(1);
 }
 
 // LDS of one k_part_join work-group for a partition capacity of e entries, s slots
@@ -1758,6 +1771,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     uint32_t *posl = reinterpret_cast<uint32_t *>(stash + STASH);       // [PE]
     uint32_t *flags = posl + PE;       // npend, nstash, overflow, nonuniform
     const int tid = threadIdx.x;
+    PSTAMP(0);
     const int32_t g = a.plist[2 * blockIdx.x], pp = a.plist[2 * blockIdx.x + 1];
     if (g < 0) return;                                  // padding row
     const oa_item it = a.items[a.n_items + g];
@@ -1804,6 +1818,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     if (tid < 4) flags[tid] = 0u;
     const uint32_t hi0 = nc ? (uint32_t)(ck[0] >> 32) : 0u;
     __syncthreads();
+    PSTAMP(1);
     // current bucket -> LDS table: lo32(ID) | (sign << 16 | (entry + 1) << 18) << 32
     const uint32_t pend_cap = PE / 4;
 #pragma unroll
@@ -1830,6 +1845,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
         if (e < pend_cap) pend[e] = val; else flags[2] = 1u;
     }
     __syncthreads();
+    PSTAMP(2);
     {   // deferred eviction walks (as k_step's)
         const uint32_t npd = min(flags[0], pend_cap);
         for (uint32_t e = tid; e < npd; e += PART_WG) {
@@ -1856,6 +1872,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
         }
     }
     __syncthreads();
+    PSTAMP(3);
     if (flags[2]) {
         if (tid == 0) atomicOr(a.status, OA_STATUS_PART_OVERFLOW);
         return;
@@ -1918,7 +1935,9 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
             a.meta_out[h.cur_off + (hit[u] & 0x3FFFFFFFu)] = (uint32_t)(flag ? 0u : acc) | (sc << 16);
             if (flag) mark[qpos[u]] = 0x10000u | acc;
         }
+        if (j0 == 0) PSTAMP(4);
     }
+    PSTAMP(5);
 }
 
 template <int IDB>
@@ -2129,6 +2148,21 @@ int64_t oa_debug_stamps(uint64_t *host, int64_t n) {
     return m;
 #else
     (void)host; (void)n;
+    return -1;
+#endif
+}
+
+// Diagnostic builds: stamps of the large-halo partition kernels of the last oa_step
+// (which = 0: k_part_join, 8 per work-group; 1: k_part_scatter, 2 per work-group).
+int64_t oa_debug_part_stamps(int32_t which, uint64_t *host, int64_t n) {
+#if OA_STAMPS
+    const int64_t cap = (int64_t)STAMP_MAX_WG * (which ? 2 : PSTAMP_N);
+    const int64_t m = n < cap ? n : cap;
+    hipError_t e = which ? hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sstamps), m * sizeof(uint64_t))
+                         : hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pstamps), m * sizeof(uint64_t));
+    return e == hipSuccess ? m : -1;
+#else
+    (void)which; (void)host; (void)n;
     return -1;
 #endif
 }
