@@ -317,7 +317,13 @@ class ShardedEngine:
                                           'catalogue bulk velocities with presharded snapshots')
             bulk = self._bulk(snapshot, nh)
         if self.presharded:
+            # this rank's rows as they are; host arrays (a distributed reader) move to
+            # the rank's device once
             shard, sel = dict(snapshot), None
+            for k in ('ids', 'coordinates', 'velocities'):
+                shard[k] = self._tensor(snapshot[k])
+            if isinstance(snapshot['masses'], (np.ndarray, torch.Tensor)):
+                shard['masses'] = self._tensor(snapshot['masses'])
             gpos = self._presharded_gpos(starts, counts)
             a_in = angles_in
         else:

@@ -217,6 +217,33 @@ def test_sharded_hip_engine_matches_single_gpu():
     assert np.array_equal(got['checkpoint/angles'].view(np.uint16), want.checkpoint.view(np.uint16))
 
 
+def test_presharded_hip_engine_matches_single_gpu():
+    """bench.py's N>1 leg: two ranks (gloo, HIP engine each, one GPU) fed by a
+    presharded loader (each rank gets only its ID range's rows, rank-major global
+    blocks) reproduce the single-process savefile bit for bit, with ranks' blocks
+    re-ordered into the global layout by the sharded engine."""
+    from test_sharding import run_sharded, _groups
+    from orbitanalysis_amd.synthetic import PlummerSnapshots
+    from orbitanalysis_amd.savefile import MemorySavefile
+    gen = dict(n_halos=30, n_per_halo=20000, n_snapshots=4, seed=57, box_size=300.0,
+               dtype=np.float32, centre_dtype=np.float32, bulk='catalogue')
+    run = dict(mode='pericentric', checkpoint=True)
+    got = run_sharded({'gen': gen, 'run': run}, 2, 'presharded', local='hip')
+    # the single-process run on the rank-major snapshots the ranks' rows form
+    from test_sharding import _rank_major
+    from orbitanalysis_amd.sharding import IdRangeOwner
+    u = PlummerSnapshots(**gen)
+    own = IdRangeOwner(int(u.ids.min()), int(u.ids.max()) + 1)
+    orig = u.load_snapshot_data
+    u.load_snapshot_data = lambda s, pos, rad: _rank_major(orig(s, pos, rad), own, 2)
+    want = run_driver(u, run, savefile=MemorySavefile())
+    g = _groups(got)
+    assert sorted(g) == sorted(want.groups)
+    for k in want.groups:
+        for d, w in want.groups[k].items():
+            assert np.array_equal(np.asarray(g[k][d]).view(np.uint8), np.asarray(w).view(np.uint8)), (k, d)
+
+
 @pytest.mark.parametrize('dtype,centre_dtype', [(np.float32, np.float32), (np.float32, np.float64),
                                                 (np.float64, np.float64)])
 def test_frame_state_bits_match_oracle(dtype, centre_dtype):
