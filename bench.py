@@ -233,7 +233,7 @@ def main():
         u = torch.tensor([units], dtype=torch.float64, device=cdev)
         dist.all_reduce(u, op=dist.ReduceOp.SUM)
         units = float(u.item())
-    status = int(ws.status.item())
+    status = int(ws.status[0].item())
     if status:
         raise RuntimeError('oa_step reported status %#x (table overflow) during the bench' % status)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))

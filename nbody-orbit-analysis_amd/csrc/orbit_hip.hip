@@ -46,6 +46,12 @@ namespace {
 #ifndef OA_KROWS
 #define OA_KROWS 12         // phase 2: progenitor rows held per wave (n_pv <= KROWS * WG)
 #endif
+#ifndef OA_PF1
+#define OA_PF1 1            // phase 1: trips of loads in flight ahead (static trips; 2: A/B r02 neutral)
+#endif
+#ifndef OA_P3BAR
+#define OA_P3BAR 1          // 1: LDS-only barrier before phase 3 (the records' stores stay in flight)
+#endif
 #ifndef OA_PF2
 #define OA_PF2 3            // phase 2b: rows of previous r̂ loads in flight ahead
 #endif
@@ -60,7 +66,9 @@ constexpr int NWAVE = WG / 64;
 constexpr int HMAX = OA_HMAX;       // halos per item
 constexpr int UNR1 = OA_UNR1;       // phase-1 particles per thread per loop trip
 constexpr int KROWS = OA_KROWS;
+constexpr int PF1 = OA_PF1;
 constexpr int PF2 = OA_PF2;
+static_assert(PF1 == 1 || PF1 == 2, "phase-1 prefetch depth is 1 or 2 trips");
 constexpr int BULK_CHUNK = 8192;    // numpy pairwise-sum buffer chunk
 constexpr int STASH = 64;           // cuckoo stash entries per item
 #ifndef OA_MAXEV
@@ -252,8 +260,11 @@ struct ItemHdr {
 };
 constexpr int64_t HDR_BYTES = (sizeof(ItemHdr) + 255) & ~int64_t(255);
 
+#ifndef OA_PENDDIV
+#define OA_PENDDIV 8        // deferral list: lds_entries / OA_PENDDIV entries of 8 bytes
+#endif
 __host__ __device__ inline int64_t table_bytes(int entries, int slots) {
-    int64_t b = (int64_t)slots * 8 + (int64_t)entries * 2;
+    int64_t b = (int64_t)slots * 8 + (int64_t)entries * 8 / OA_PENDDIV;
     return (b + 15) & ~int64_t(15);
 }
 
@@ -590,7 +601,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     const uint32_t nslots_max = (uint32_t)a.lds_slots, E = (uint32_t)a.lds_entries;
     uint64_t *slots = reinterpret_cast<uint64_t *>(smem + HDR_BYTES);
     uint64_t *pend = slots + nslots_max;              // phase 1: deferred cuckoo inserts
-    const uint32_t pend_cap = E / 4u;
+    const uint32_t pend_cap = E / (uint32_t)OA_PENDDIV;
     TD *rcx = reinterpret_cast<TD *>(smem + HDR_BYTES);   // phases 2b-3 (over the table)
     TD *rcy = rcx + E, *rcz = rcy + E;
     uint8_t *sgn8 = reinterpret_cast<uint8_t *>(
@@ -654,11 +665,14 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         XA[u] = bld3<TX, AUX_NT>(r_x, li_ * SX);                                   \
         VA[u] = bld3<TV, AUX_NT>(r_v, li_ * SV);                                   \
     }
-    ID idv[U1], idn[U1];
-    V3<TX> xv[U1], xn[U1];
-    V3<TV> vv[U1], vn[U1];
+    // static trips keep PF1 trips of loads in flight ahead of the one computing
+    constexpr int PF = DYN ? 1 : PF1;
+    ID idv[U1], idn[U1], idm[U1];
+    V3<TX> xv[U1], xn[U1], xm[U1];
+    V3<TV> vv[U1], vn[U1], vm[U1];
     V3<TD> rr[SU];
     OA_LOAD1(idv, xv, vv, tp[0])
+    if (PF == 2) OA_LOAD1(idn, xn, vn, tp[1])
     __builtin_amdgcn_sched_barrier(0);
     if (COMPARE) {
         for (uint32_t w = tid; w < nslots; w += WG) slots[w] = 0ull;
@@ -712,7 +726,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         const uint32_t tcur = DYN ? tp[kp] : (uint32_t)(wave + NWAVE * kp);
         uint32_t f = 0;
         if (DYN && kp + 2 < NTRIP && lane == 0) f = atomicAdd(&H.ctr1, 1u);   // trip kp + 2
-        if (kp + 1 < NTRIP) OA_LOAD1(idn, xn, vn, (DYN ? tp[(kp + 1) % NTRIP] : (uint32_t)(wave + NWAVE * (kp + 1))))
+        if (PF == 1 && kp + 1 < NTRIP) OA_LOAD1(idn, xn, vn, (DYN ? tp[(kp + 1) % NTRIP] : (uint32_t)(wave + NWAVE * (kp + 1))))
+        if (PF == 2 && kp + 2 < NTRIP) OA_LOAD1(idm, xm, vm, (uint32_t)(wave + NWAVE * (kp + 2)))
         uint64_t val[U1];
         uint32_t csu[U1][NCAND];
         bool ins[U1];
@@ -792,7 +807,10 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
         }
 #pragma unroll
-        for (int u = 0; u < U1; ++u) { idv[u] = idn[u]; xv[u] = xn[u]; vv[u] = vn[u]; }
+        for (int u = 0; u < U1; ++u) {
+            idv[u] = idn[u]; xv[u] = xn[u]; vv[u] = vn[u];
+            if (PF == 2) { idn[u] = idm[u]; xn[u] = xm[u]; vn[u] = vm[u]; }
+        }
         if (DYN && kp + 2 < NTRIP) tp[(kp + 2) % NTRIP] = __builtin_amdgcn_readfirstlane(f);
     }
 #undef OA_LOAD1
@@ -1074,7 +1092,14 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     }
     WSTAMP(2);
     STAMP(6);
-    __syncthreads();
+    if (OA_P3BAR) {
+        // phase 3 reads LDS alone: the records' global stores stay in flight
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    } else {
+        __syncthreads();
+    }
 
     // ---- phase 3: every state word of the item, in position order ---------------
     // matched: the new angle phase 2b left in rc_x; entered or in a halo without a

@@ -28,10 +28,10 @@ F32, F64 = np.dtype(np.float32), np.dtype(np.float64)
 # the header + max(8-byte cuckoo slots + 2 B/entry insert list, 3 r̂ components per
 # entry) + 1 B/entry of signs, within the CU's 160 KB (the table and the r̂ arrays
 # overlay each other):
-#   float32 r̂: 11776 entries, 15360 slots (load <= 0.77)
+#   float32 r̂: 11776 entries, 16960 slots (load <= 0.69)
 #   float64 r̂:  6144 entries, 16896 slots (load <= 0.36)
 DEFAULT_ENTRIES = {False: 11776, True: 6144}
-DEFAULT_SLOTS = {False: 15360, True: 16896}
+DEFAULT_SLOTS = {False: 16960, True: 16896}
 
 _TORCH_FROM_NP = {
     np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
@@ -545,7 +545,7 @@ class OrbitEngine:
                 ws.status.zero_()
             res = self.launch(prep, ws)
             # one small read-back per snapshot (the driver fetches the results anyway)
-            st = int(ws.status.item()) if compare else 0
+            st = int(ws.status[0].item()) if compare else 0
             if not st:
                 break
             entries, part = retry_plan(prep, st)

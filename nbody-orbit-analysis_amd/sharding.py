@@ -191,7 +191,8 @@ class ShardedPrep:
     exists: np.ndarray
     compare: bool
     gpos: torch.Tensor
-    sel: Optional[torch.Tensor]
+    sel: torch.Tensor                       # this rank's rows in the global snapshot
+    n_global: int
     rows: Optional[np.ndarray]              # catalogue rows (centre, bulk) to exchange
     bulk_out: Optional[np.ndarray]
     plan: object
@@ -291,15 +292,19 @@ class ShardedEngine:
 
     def _presharded_gpos(self, starts, counts):
         """Global block = the ranks' blocks concatenated in rank order: a shard row's
-        position is the rows of lower ranks in its block + its own index."""
+        position is the rows of lower ranks in its block + its own index.  Returns the
+        block positions, the global snapshot rows and the global row count."""
         cnt_all = allgather_v(torch.from_numpy(counts.astype(np.int64))[None, :], self.group)
         before = cnt_all[:self.rank].sum(0).to(self.device) if self.rank else \
             torch.zeros(len(counts), dtype=torch.int64, device=self.device)
+        tot = cnt_all.sum(0).to(self.device)
+        gstart = torch.cumsum(tot, 0) - tot
         c = torch.from_numpy(counts).to(self.device)
         block = torch.repeat_interleave(torch.arange(len(counts), device=self.device), c)
         local = torch.arange(int(c.sum()), device=self.device) - \
             torch.from_numpy(starts).to(self.device)[block]
-        return before[block] + local
+        gpos = before[block] + local
+        return gpos, gstart[block] + gpos, int(tot.sum())
 
     # ---------------------------------------------------------------- step
     def prepare(self, snapshot, centres, bulk_cat, H, z, exists, compare, angles_in=None,
@@ -324,10 +329,12 @@ class ShardedEngine:
                 shard[k] = self._tensor(snapshot[k])
             if isinstance(snapshot['masses'], (np.ndarray, torch.Tensor)):
                 shard['masses'] = self._tensor(snapshot['masses'])
-            gpos = self._presharded_gpos(starts, counts)
-            a_in = angles_in
+            gpos, sel, n_global = self._presharded_gpos(starts, counts)
+            # a checkpoint holds the global snapshot's angles (rank-major blocks)
+            a_in = None if angles_in is None else np.asarray(angles_in)[sel.cpu().numpy()]
         else:
             shard, sel, gpos = self._shard(snapshot, starts, counts)
+            n_global = n
             a_in = None if angles_in is None else np.asarray(angles_in)[sel.cpu().numpy()]
         rows = None
         if self.share_catalogue and nh:
@@ -338,6 +345,7 @@ class ShardedEngine:
         p = prev if prev is not None else self.prev
         ids_dt = np.asarray(ids[:0].cpu() if isinstance(ids, torch.Tensor) else ids[:0]).dtype
         sp = ShardedPrep(n=n, exists=exists, compare=bool(compare), gpos=gpos, sel=sel,
+                         n_global=n_global,
                          rows=rows, bulk_out=None if bulk_cat is not None else bulk,
                          plan=_Plan(ids_dt, None if bulk is None else np.asarray(bulk).dtype))
         sp.lp = self.local.prepare(shard, centres, bulk, H, z, exists, compare, a_in,
@@ -396,13 +404,11 @@ class ShardedEngine:
     def angles(self):
         """Global float16 angle state in current-snapshot order (checkpoint payload)."""
         p = self.prev
-        if p.sel is None:
-            raise NotImplementedError('checkpoint angles of presharded snapshots')
         loc = self.local.angles_tensor().to(torch.int64)
         rows = torch.stack([p.sel.to(loc.device), loc], dim=1) if loc.numel() else \
             torch.zeros((0, 2), dtype=torch.int64)
         allr = allgather_v(rows, self.group).cpu().numpy()
-        out = np.zeros(p.n_global if hasattr(p, 'n_global') else p.n, dtype=np.uint16)
+        out = np.zeros(p.n_global, dtype=np.uint16)
         out[allr[:, 0]] = allr[:, 1].astype(np.uint16)
         return out.view(np.float16)
 
@@ -452,7 +458,7 @@ class EngineLocal:
             if check and ws is not None:
                 ws.status.zero_()
             res = eng.launch(lp, ws, prev=prev, step_events=step_events)
-            st = int(ws.status.item()) if (check and ws is not None) else 0
+            st = int(ws.status[0].item()) if (check and ws is not None) else 0
             if not st:
                 break
             # re-plan: smaller items / large halos on the global-table path

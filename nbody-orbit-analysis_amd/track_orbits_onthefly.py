@@ -166,7 +166,7 @@ class OnTheFly:
             ws = eng.workspace(pc)
             ws.status.zero_()
             res = eng.launch(pc, ws, prev=prev)
-            st = int(ws.status.item())
+            st = int(ws.status[0].item())
             if not st:
                 break
             if st & N.STATUS_PLAN:

@@ -180,3 +180,24 @@ def test_presharded_loader_matches_rank_major_oracle(name):
                           O.MemoryRecord(), **meta['run']).groups
     got = run_sharded(name, world, 'presharded')
     assert_groups_equal(_groups(got), want)
+
+
+def test_presharded_checkpoint_is_global_rank_major():
+    """With a presharded loader the checkpoint still holds the global snapshot's angles
+    (rows of the rank-major blocks), as the single-process run writes them."""
+    from oracle import orbit_oracle as O
+    from orbitanalysis_amd.sharding import IdRangeOwner
+    from orbitanalysis_amd.synthetic import PlummerSnapshots
+    gen = dict(n_halos=6, n_per_halo=400, n_snapshots=4, seed=11, box_size=80.0,
+               bulk='catalogue')
+    run = dict(mode='pericentric', checkpoint=True)
+    u = PlummerSnapshots(**gen)
+    own = IdRangeOwner(int(u.ids.min()), int(u.ids.max()) + 1)
+    rec = O.MemoryRecord()
+    want = O.track_orbits(u.snapshot_numbers, u.main_branches(), u.regions,
+                          lambda s, p, r: _rank_major(u.load_snapshot_data(s, p, r), own, 2),
+                          rec, **run)
+    got = run_sharded({'gen': gen, 'run': run}, 2, 'presharded')
+    assert_groups_equal(_groups(got), want.groups)
+    assert np.array_equal(got['checkpoint/angles'].view(np.uint16),
+                          np.asarray(rec.checkpoint).view(np.uint16))
