@@ -49,6 +49,12 @@ namespace {
 #ifndef OA_PF1
 #define OA_PF1 1            // phase 1: trips of loads in flight ahead (static trips; 2: A/B r02 neutral)
 #endif
+#ifndef OA_RDEFER
+#define OA_RDEFER 1         // compare steps: r̂ stored in phase 2b from registers, not in phase 1
+#endif
+#ifndef OA_EWALK
+#define OA_EWALK 1          // waves done with phase 1 walk the deferred inserts appended so far
+#endif
 #ifndef OA_P3BAR
 #define OA_P3BAR 1          // 1: LDS-only barrier before phase 3 (the records' stores stay in flight)
 #endif
@@ -67,6 +73,8 @@ constexpr int HMAX = OA_HMAX;       // halos per item
 constexpr int UNR1 = OA_UNR1;       // phase-1 particles per thread per loop trip
 constexpr int KROWS = OA_KROWS;
 constexpr int PF1 = OA_PF1;
+constexpr bool RDEFER = OA_RDEFER != 0;
+constexpr bool EWALK = OA_EWALK != 0;
 constexpr int PF2 = OA_PF2;
 static_assert(PF1 == 1 || PF1 == 2, "phase-1 prefetch depth is 1 or 2 trips");
 constexpr int BULK_CHUNK = 8192;    // numpy pairwise-sum buffer chunk
@@ -244,7 +252,7 @@ struct ItemHdr {
     uint32_t nonuniform, hi0, pad0, overflow;
     uint32_t nh, nseg, n_span, n_pv;
     uint32_t chunk_total, nsl, nstash, npend;
-    uint32_t ctr1, pad1, pad2, pad3;    // phase-1 trip counter, walk diagnostics
+    uint32_t ctr1, pad1, pad2, pad3;    // phase-1 trip counter, walk diagnostics, walk cursor
     uint64_t stash[STASH];          // cuckoo entries whose eviction chain ran out
     uint32_t lstart[HMAX + 1];      // local start of each item halo's current block
     uint32_t vstart[HMAX + 1];      // virtual start of each progenitor segment
@@ -644,6 +652,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // (<= SU rows) and keeps each row's r̂ in registers (rr) until phase 2b writes it
     // into the LDS the table held -- no read-back of the rows it stored.
     constexpr int SU = sizeof(TD) == 4 ? STAGE_F32 : STAGE_F64;
+    // float64 r̂ keeps its phase-1 stores (register budget)
+    constexpr bool RD = RDEFER && COMPARE && sizeof(TD) == 4;
     // float64 inputs: one row per trip (register budget of 1024-thread work-groups)
     constexpr int U1 = (sizeof(TX) == 8 || sizeof(TV) == 8) ? 1 : UNR1;
     constexpr int NTRIP = SU / U1;
@@ -676,6 +686,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     __builtin_amdgcn_sched_barrier(0);
     if (COMPARE) {
         for (uint32_t w = tid; w < nslots; w += WG) slots[w] = 0ull;
+        // early walks read appended entries: an unwritten one is still 0
+        if (EWALK) for (uint32_t w = tid; w < pend_cap; w += WG) pend[w] = 0ull;
     }
     if (wave == 0) {
         // progenitor segments: every halo with a non-empty progenitor block, in halo
@@ -709,7 +721,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             H.lstart[nh] = n_span;
             H.vstart[nseg] = n_pv; H.nseg = nseg; H.n_pv = n_pv;
             H.nonuniform = 0; H.overflow = 0; H.chunk_total = 0; H.nstash = 0; H.npend = 0;
-            H.pad1 = 0;
+            H.pad1 = 0; H.pad2 = 0;
             H.ctr1 = 2 * NWAVE;             // phase 1: the first two trips of every wave are static
         }
     }
@@ -756,7 +768,9 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                 sgn = OTF ? frame_otf<TX, TV, TD>(xv[u], vv[u], H.cb[hl], a, fk, r)
                           : frame<TX, TV, TD>(xv[u], vv[u], H.cb[hl], H.cf[hl], a, fk, r);
             }
-            bst3<TD>(r_rh, li * SD, r);
+            // compare steps store r̂ from registers in phase 2b (RDEFER): phase 1 then
+            // issues loads only and ends without waiting on stores
+            if (!RD) bst3<TD>(r_rh, li * SD, r);
             rr[kp * U1 + u] = V3<TD>{r[0], r[1], r[2]};
             if constexpr (!COMPARE) {
                 uint32_t ang = 0;
@@ -827,7 +841,20 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // phase 2a to phase 2b.
     const uint32_t n_pv = uni(H.n_pv), nseg = uni(H.nseg);
     const uint32_t nrow = (n_pv + 63) / 64;
+    // r̂ of every row this wave computed, from registers (RDEFER); rows past the
+    // item fall outside r_rh and are dropped
+    auto store_rhat = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < SU; ++k) {
+            if (DYN && (uint32_t)(k / U1) >= ntrips) break;
+            const uint32_t li = DYN ? (tp[k / U1] * U1 + k % U1) * 64 + lane
+                                    : (uint32_t)(wave + NWAVE * k) * 64 + lane;
+            const TD w[3] = {rr[k].x, rr[k].y, rr[k].z};
+            bst3<TD>(r_rh, li * SD, w);
+        }
+    };
     if (n_pv == 0) {                                 // nothing to join: state words only
+        if (RD) store_rhat();
         __syncthreads();
         for (uint32_t li = tid; li < n_span; li += WG)
             bst32<AUX_NT>(r_mt, li * 4u, (uint32_t)(sgn8[li] & 3u) << 16);
@@ -869,6 +896,69 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         pk[k] = bld<uint32_t, AUX_NT>(make_rsrc(a.meta_prev + kb, nv * 4u), lane * 4u);
     }
     __builtin_amdgcn_sched_barrier(0);
+    // one deferred insert's eviction walk (atomic exchanges: safe beside the first-try
+    // CAS inserts of waves still in phase 1, and beside other walks)
+    auto walk = [&](uint64_t v) __attribute__((always_inline)) {
+        uint32_t cs[NCAND];
+        cuckoo_slots((uint32_t)v, nslots, cs);
+        uint32_t t = cs[0];
+        for (int it_ = 0;; ++it_) {
+            const uint64_t old = atomicExch(reinterpret_cast<unsigned long long *>(&slots[t]),
+                                            (unsigned long long)v);
+            if (old == 0ull) {
+                if (OA_STAMPS) atomicMax(&H.pad1, (uint32_t)it_ + 1u);
+                break;
+            }
+            if (it_ == MAX_EVICT) {
+                if (OA_STAMPS) atomicMax(&H.pad1, 1000u);
+                const uint32_t k = atomicAdd(&H.nstash, 1u);
+                if (k < (uint32_t)STASH) H.stash[k] = old;
+                else H.overflow = 2u;
+                break;
+            }
+            cuckoo_slots((uint32_t)old, nslots, cs);
+            // the displaced key moves to its candidate after the one it held
+            uint32_t nx = cs[0];
+#pragma unroll
+            for (int j = NCAND - 2; j >= 0; --j) nx = cs[j] == t ? cs[j + 1] : nx;
+            if (OA_RWALK && NCAND == 3) {
+                // or, pseudo-randomly, to the other one (breaks walk cycles)
+                const uint32_t alt = cs[0] ^ cs[1] ^ cs[2] ^ t ^ nx;
+                if (((uint32_t)old ^ (uint32_t)it_) & 1u) nx = alt;
+            }
+            t = nx;
+            v = old;
+        }
+    };
+    if (EWALK) {
+        // a wave done with phase 1 walks the deferred inserts appended so far, claimed
+        // in runs of 64 from a cursor, while later waves still stream; the barrier
+        // below leaves the rest to the whole work-group
+        volatile uint32_t *vnp = &H.npend, *vcur = &H.pad2;
+        volatile uint64_t *vpend = pend;
+        for (;;) {
+            uint32_t c = 0, c2 = 0;
+            if (lane == 0) {
+                const uint32_t n = min(*vnp, pend_cap);
+                c = *vcur;
+                while (c < n) {
+                    const uint32_t want = min(c + 64u, n);
+                    const uint32_t old = atomicCAS(&H.pad2, c, want);
+                    if (old == c) { c2 = want; break; }
+                    c = old;
+                }
+            }
+            c = __builtin_amdgcn_readlane(c, 0);
+            c2 = __builtin_amdgcn_readlane(c2, 0);
+            if (c2 <= c) break;
+            const uint32_t e = c + (uint32_t)lane;
+            if (e < c2) {
+                uint64_t v;
+                do { v = vpend[e]; } while (v == 0ull);     // reserved, not yet written
+                walk(v);
+            }
+        }
+    }
     // barrier on LDS traffic only: the loads above and phase 1's r̂ stores stay in flight
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -876,39 +966,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     STAMP(2);
     {
         const uint32_t np = min(H.npend, pend_cap);
-        for (uint32_t e = tid; e < np; e += WG) {
-            uint64_t v = pend[e];
-            uint32_t cs[NCAND];
-            cuckoo_slots((uint32_t)v, nslots, cs);
-            uint32_t t = cs[0];
-            for (int it_ = 0;; ++it_) {
-                const uint64_t old = atomicExch(reinterpret_cast<unsigned long long *>(&slots[t]),
-                                                (unsigned long long)v);
-                if (old == 0ull) {
-                    if (OA_STAMPS) atomicMax(&H.pad1, (uint32_t)it_ + 1u);
-                    break;
-                }
-                if (it_ == MAX_EVICT) {
-                    if (OA_STAMPS) atomicMax(&H.pad1, 1000u);
-                    const uint32_t k = atomicAdd(&H.nstash, 1u);
-                    if (k < (uint32_t)STASH) H.stash[k] = old;
-                    else H.overflow = 2u;
-                    break;
-                }
-                cuckoo_slots((uint32_t)old, nslots, cs);
-                // the displaced key moves to its candidate after the one it held
-                uint32_t nx = cs[0];
-#pragma unroll
-                for (int j = NCAND - 2; j >= 0; --j) nx = cs[j] == t ? cs[j + 1] : nx;
-                if (OA_RWALK && NCAND == 3) {
-                    // or, pseudo-randomly, to the other one (breaks walk cycles)
-                    const uint32_t alt = cs[0] ^ cs[1] ^ cs[2] ^ t ^ nx;
-                    if (((uint32_t)old ^ (uint32_t)it_) & 1u) nx = alt;
-                }
-                t = nx;
-                v = old;
-            }
-        }
+        for (uint32_t e = (EWALK ? H.pad2 : 0u) + tid; e < np; e += WG) walk(pend[e]);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -1034,6 +1092,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                                 : (uint32_t)(wave + NWAVE * k) * 64 + lane;
         if (li < n_span) { rcx[li] = rr[k].x; rcy[li] = rr[k].y; rcz[li] = rr[k].z; }
     }
+    if (RD) store_rhat();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
