@@ -59,7 +59,7 @@ namespace {
 #define OA_P3BAR 1          // 1: LDS-only barrier before phase 3 (the records' stores stay in flight)
 #endif
 #ifndef OA_PF2
-#define OA_PF2 3            // phase 2b: rows of previous r̂ loads in flight ahead
+#define OA_PF2 5            // phase 2b: rows of previous r̂ loads in flight ahead (A/B r02: 2 +3.5 %, 4 = 3, 5 -0.4 %)
 #endif
 #ifndef OA_HMAX
 #define OA_HMAX 32
