@@ -316,14 +316,34 @@ class ShardedOnTheFly:
         import torch.distributed as dist
         return dist.get_rank(self.group)
 
+    def agree(self, flag):
+        """True on every rank iff ``flag`` is true on every rank (a carry is used only
+        when all ranks hold one, so their collectives stay in step)."""
+        import torch.distributed as dist
+        got = [None] * dist.get_world_size(self.group)
+        dist.all_gather_object(got, bool(flag), group=self.group)
+        return all(got)
+
     def run(self, snaps, slices, centres, carried=None):
+        """``carried``: this object's ``carry`` from the previous call, whose current
+        snapshot is this call's previous one (``snaps[1]`` is then None): the rank's
+        shard of it, its device frame state and its bulk velocities are reused."""
         import torch.distributed as dist
         from .sharding import shard_snapshot
         world, rank = dist.get_world_size(self.group), dist.get_rank(self.group)
         eng = self.eng
         self.owner.fit(np.asarray(snaps[0]['ids']))
         shards, lslices, sels, bulks = [], [], [], []
+        otf_carry = None
+        if carried is not None:
+            otf_carry, sel_prev = carried
         for snap, sl in zip(snaps, slices):
+            if snap is None:                  # the carried previous snapshot
+                shards.append(None)
+                lslices.append(None)
+                sels.append(sel_prev)
+                bulks.append(None)
+                continue
             sl = np.asarray(sl, dtype=np.int64).reshape(-1, 2)
             n = len(snap['ids'])
             nh = len(sl)
@@ -346,7 +366,9 @@ class ShardedOnTheFly:
             lslices.append(lsl)
             sels.append(sel)
             bulks.append(bulk if bulk is not None else np.zeros((0, 3)))
-        out = self.otf.run(shards, lslices, centres, bulks=bulks, merge_parts=True)
+        out = self.otf.run(shards, lslices, centres, carried=otf_carry, bulks=bulks,
+                           merge_parts=True)
+        self.carry = (self.otf.carry, sels[0])
         q = out.pop('parts')
         mine = dict(apsis_offsets=out['apsis_offsets'], apsis_ids=out['apsis_ids'],
                     apsis_gpos=sels[1][q['apsis_pos']],
@@ -403,7 +425,7 @@ def track_orbits(snapshot_number, progenitor_links, regions, load_snapshot_data,
     carried = None
     sharded = isinstance(engine, ShardedOnTheFly)
     if sharded:
-        otf, entry, key = engine, None, None          # every call loads both snapshots
+        otf = engine                      # a carry is used only when every rank has one
     else:
         otf = OnTheFly(engine, mode)
     if otf.mode != mode:
@@ -418,9 +440,12 @@ def track_orbits(snapshot_number, progenitor_links, regions, load_snapshot_data,
         region_pos, region_rad = regions(s, halo_ids)
         positions.append(repack(region_pos, len(halo_ids_), halo_exists))
         radii.append(repack(region_rad, len(halo_ids_), halo_exists))
-        if s == snapshot_number - 1 and entry is not None and entry['s'] == s and \
-                np.array_equal(entry['row'], halo_ids_) and \
-                _same(entry['pos'], region_pos) and _same(entry['rad'], region_rad):
+        use = s == snapshot_number - 1 and entry is not None and entry['s'] == s and \
+            np.array_equal(entry['row'], halo_ids_) and \
+            _same(entry['pos'], region_pos) and _same(entry['rad'], region_rad)
+        if sharded and s == snapshot_number - 1:
+            use = otf.agree(use)
+        if use:
             # the previous call's current snapshot, same regions: its device frame state
             # is reused and the snapshot is not loaded again
             snaps.append(None)

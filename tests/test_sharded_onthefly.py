@@ -130,3 +130,70 @@ def test_sharded_onthefly_matches_reference_golden(name, mode):
             assert np.array_equal(v, w, equal_nan=True), k
         else:
             assert np.array_equal(v, w), k
+
+
+def _stream_worker(rank, world, port, outdir):
+    import json
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from orbitanalysis_amd import track_orbits_onthefly as T
+        from orbitanalysis_amd.engine import OrbitEngine
+        from orbitanalysis_amd.savefile import MemorySavefile
+        from orbitanalysis_amd.synthetic import PlummerSnapshots
+        u = PlummerSnapshots(n_halos=3, n_per_halo=[900, 700, 500], n_snapshots=5, seed=41,
+                             dt=0.5, box_size=40.0, region_returns=2)
+        links = np.array([[0, 1, 2], [0, 1, 2]])
+        loads = []
+
+        class Loader:
+            def __call__(self, s, pos, rad):
+                loads.append(s)
+                return u.load_snapshot_data(s, pos, rad)
+        flat, calls = {}, {}
+        for carry in ('1', '0'):
+            os.environ['ORBIT_OTF_CARRY'] = carry
+            T.clear_carry()
+            loads.clear()
+            out = MemorySavefile()
+            load = Loader()
+            eng = T.ShardedOnTheFly(OrbitEngine(mode='pericentric'))
+            for s in (2, 3, 4):
+                T.track_orbits(s, links, u.regions, load, out, mode='pericentric',
+                               verbose=False, engine=eng)
+            calls[carry] = list(loads)
+            if rank == 0:
+                for s, (d, _) in out.files.items():
+                    flat.update({'%s/%d/%s' % (carry, s, k): np.asarray(v) for k, v in d.items()})
+        T.clear_carry()
+        with open(os.path.join(outdir, 'loads%d.json' % rank), 'w') as f:
+            json.dump(calls, f)
+        if rank == 0:
+            np.savez(os.path.join(outdir, 'stream.npz'), **flat)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_onthefly_stream_carry_matches_fresh_calls():
+    """World 2: a stream of calls s = 2, 3, 4 reuses each rank's shard and device frame
+    state of the previous call's current snapshot (s-1 is loaded once per rank) and
+    writes exactly the files of calls that load and frame both snapshots."""
+    import json
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_stream_worker, args=(2, _free_port(), d), nprocs=2, join=True,
+                           start_method='spawn')
+        f = np.load(os.path.join(d, 'stream.npz'))
+        got = {k: f[k] for k in f.files}
+        calls = [json.load(open(os.path.join(d, 'loads%d.json' % r))) for r in range(2)]
+    for c in calls:
+        assert c['1'] == [2, 1, 3, 4], c['1']
+        assert c['0'] == [2, 1, 3, 2, 4, 3], c['0']
+    on = sorted(k[2:] for k in got if k.startswith('1/'))
+    off = sorted(k[2:] for k in got if k.startswith('0/'))
+    assert on == off and len(on) > 0
+    for k in on:
+        assert np.array_equal(got['1/' + k], got['0/' + k], equal_nan=True), k

@@ -63,3 +63,24 @@ for name, v in (('deferred inserts', npend), ('longest walk', chain), ('stashed'
                                                           np.percentile(v, 90), v.max()))
 ts = np.linspace(0, end.max(), 12)
 print('alive:', [int(((start <= x) & (end > x)).sum()) for x in ts])
+# tail: busy fraction of the 256 CUs over the span, and the stretch at the end where
+# fewer than 240 items are alive (the last dispatch round's quantisation + skew)
+busy = (end - start).sum() / (256 * end.max())
+grid = np.linspace(0, end.max(), 2000)
+alive = np.array([int(((start <= x) & (end > x)).sum()) for x in grid])
+low = np.nonzero(alive[len(grid) // 2:] < 240)[0]
+t_low = grid[len(grid) // 2 + low[0]] if len(low) else end.max()
+print('busy %.4f of 256 CUs over the span; tail (<240 alive) %.1f us, its idle %.1f CU-us '
+      '(%.2f %% of span), last start %.1f us' % (
+          busy, end.max() - t_low,
+          ((256 - alive[grid >= t_low]) * (grid[1] - grid[0])).sum(),
+          100 * ((256 - alive[grid >= t_low]) * (grid[1] - grid[0])).sum() / (256 * end.max()),
+          start.max()))
+# dispatch gap: the k-th work-group to start after the first 256 takes the CU the k-th
+# one to end released (in order), so start[256 + k] - end_sorted[k] estimates the time a
+# CU sits between two items
+ss, es = np.sort(start), np.sort(end)
+if ni > 256:
+    g = ss[256:] - es[:ni - 256]
+    print('dispatch gap mean %.2f p10 %.2f p50 %.2f p90 %.2f us; first-round start spread %.2f us'
+          % (g.mean(), *np.percentile(g, [10, 50, 90]), ss[255] - ss[0]))
