@@ -260,7 +260,8 @@ struct ItemHdr {
     int32_t halo_cnt[HMAX];         // apsis records per item halo
     uint16_t rowoff[OA_KROWS * (OA_WG / 64)];   // item-local offset of each progenitor
     uint8_t rowcnt[OA_KROWS * (OA_WG / 64)];    //   row's apsis records, and their count
-    int32_t has_prev[HMAX];
+    uint32_t hslot[HMAX];           // bit 0: joined (non-empty progenitor block);
+                                    // bits 1-31: the halo's out_slot + 1 (0: none)
     uint32_t seg_cnt[HMAX];         // progenitor particles of each segment
     int64_t seg_prev_off[HMAX];
     double cb[HMAX][6];             // centre[3], bulk[3]
@@ -706,7 +707,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             H.lstart[lane] = (uint32_t)(hrow.cur_off - base);
             // joined halos: those with a non-empty progenitor block (an empty one
             // matches nothing: its particles keep angle 0)
-            H.has_prev[lane] = hp;
+            // with the output slot, so the item's end needs no reload of the halo row
+            H.hslot[lane] = ((uint32_t)(hrow.out_slot + 1) << 1) | (hp ? 1u : 0u);
             H.halo_cnt[lane] = 0;
             for (int d = 0; d < 3; ++d) { H.cb[lane][d] = hrow.centre[d]; H.cb[lane][3 + d] = hrow.bulk[d]; }
             for (int d = 0; d < 3; ++d) { H.cf[lane][d] = (float)hrow.centre[d]; H.cf[lane][3 + d] = (float)hrow.bulk[d]; }
@@ -780,7 +782,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             } else {
                 // every state word is written by phase 3, from this sign
                 if (ok) sgn8[li] = (uint8_t)sgn;
-                if (!ok || !H.has_prev[hl]) continue;
+                if (!ok || !(H.hslot[hl] & 1u)) continue;
                 uint32_t lo, hi;
                 id_split<IDB>(idv[u], lo, hi);
                 if (IDB == 8 && hi != hi0) H.nonuniform = 1u;     // benign race: all write 1
@@ -1183,8 +1185,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         bst32<AUX_NT>(r_mt, li * 4u, ang | ((s & 3u) << 16));
     }
     if (tid < nh) {
-        const oa_halo &h = a.halos[it.h0 + tid];
-        if (h.out_slot >= 0) a.halo_count[h.out_slot] = H.halo_cnt[tid];
+        const uint32_t os = H.hslot[tid] >> 1;
+        if (os) a.halo_count[os - 1u] = H.halo_cnt[tid];
     }
     if (tid == 0) a.item_count[blockIdx.x] = (int32_t)H.chunk_total;
     STAMP(7);
