@@ -1700,7 +1700,10 @@ constexpr int PART_S = 6144;            // LDS table slots, at most
 // table build overlaps the other's streaming
 constexpr int PART_KMAX = 16384;        // partitions of one halo (scatter's LDS counters)
 constexpr int PART_WG = 512;
-constexpr int SCAT_WG = 256, SCAT_PER = 8;
+#ifndef OA_SCAT_PER
+#define OA_SCAT_PER 8
+#endif
+constexpr int SCAT_WG = 256, SCAT_PER = OA_SCAT_PER;
 static_assert(PART_E - 1 <= (int)MAX_POS, "partition entries must fit the slot position field");
 
 // partition of an ID: the high bits of a 64-bit mix (the LDS table hashes the low
@@ -1828,7 +1831,15 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
 // even work-groups take current chunks, odd ones previous chunks, then the longer
 // list's remainder.
 template <typename TX, typename TV, typename TD, int IDB>
-__global__ __launch_bounds__(SCAT_WG) void k_part_scatter(const oa_step_args a, const FrameK fk) {
+#ifndef OA_SCAT_WPE
+#define OA_SCAT_WPE 0       // k_part_scatter: minimum waves per SIMD asked of the compiler (0: none)
+#endif
+#if OA_SCAT_WPE
+#define SCAT_ATTR __attribute__((amdgpu_waves_per_eu(OA_SCAT_WPE)))
+#else
+#define SCAT_ATTR
+#endif
+__global__ __launch_bounds__(SCAT_WG) SCAT_ATTR void k_part_scatter(const oa_step_args a, const FrameK fk) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lcnt[];   // [K]
     const int64_t b = blockIdx.x, n1 = a.n_gchunk1, n2 = a.n_gchunk2;
     const int64_t m = n1 < n2 ? n1 : n2;

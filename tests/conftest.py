@@ -12,3 +12,23 @@ GOLDEN = os.path.join(ROOT, 'tests', 'golden')
 def pytest_configure(config):
     config.addinivalue_line('markers', 'gpu: needs a real MI355X (HIP device)')
     config.addinivalue_line('markers', 'slow: long-running CPU test')
+
+
+def pytest_terminal_summary(terminalreporter):
+    """Session total of f16 apsis angles that differ from the reference's by one ulp
+    (test_gpu_parity.compare_groups; the per-test bound is ANGLE_MISMATCH_MAX)."""
+    gu = sys.modules.get('golden_util')
+    t = getattr(gu, 'ANGLE_TALLY', None)
+    if not t or not t['angles']:
+        return
+    rate = t['mismatch'] / t['angles']
+    terminalreporter.write_line('f16 apsis angles vs reference fixtures: %d of %d differ by 1 ulp '
+                                '(%.4f %%)' % (t['mismatch'], t['angles'], 100 * rate))
+    out = os.path.join(ROOT, 'gpurun_out')
+    try:
+        import json
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, 'angle_mismatch.json'), 'w') as f:
+            json.dump(dict(t, rate=rate), f)
+    except OSError:
+        pass

@@ -16,6 +16,7 @@ BATCH = ['g1_config1', 'g2_overlap_birth_massarray', 'g3_apo_periodic',
          'g5_fp32_catalogue32', 'g8_many_small_halos', 'g11_edges']
 
 ANGLE_MISMATCH_MAX = 0.01      # fraction of apsis angles allowed to differ by 1 f16 ulp
+from golden_util import ANGLE_TALLY   # noqa: E402  (session total, printed by conftest)
 
 
 def compare_groups(got, want, report):
@@ -33,6 +34,8 @@ def compare_groups(got, want, report):
                 assert np.all(same | near), (g, 'angle off by more than 1 f16 ulp')
                 report['angles'] = report.get('angles', 0) + a.size
                 report['angle_mismatch'] = report.get('angle_mismatch', 0) + int((~same).sum())
+                ANGLE_TALLY['angles'] += int(a.size)
+                ANGLE_TALLY['mismatch'] += int((~same).sum())
             elif w.dtype.kind == 'f':
                 assert np.array_equal(v, w, equal_nan=True), (g, k)
             else:
