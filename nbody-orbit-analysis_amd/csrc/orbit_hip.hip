@@ -1701,7 +1701,7 @@ constexpr int PART_S = 6144;            // LDS table slots, at most
 constexpr int PART_KMAX = 16384;        // partitions of one halo (scatter's LDS counters)
 constexpr int PART_WG = 512;
 #ifndef OA_SCAT_PER
-#define OA_SCAT_PER 8
+#define OA_SCAT_PER 8       // k_part_scatter: particles per thread per sub-chunk (4: A/B r02 neutral)
 #endif
 constexpr int SCAT_WG = 256, SCAT_PER = OA_SCAT_PER;
 static_assert(PART_E - 1 <= (int)MAX_POS, "partition entries must fit the slot position field");
@@ -1832,7 +1832,7 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
 // list's remainder.
 template <typename TX, typename TV, typename TD, int IDB>
 #ifndef OA_SCAT_WPE
-#define OA_SCAT_WPE 0       // k_part_scatter: minimum waves per SIMD asked of the compiler (0: none)
+#define OA_SCAT_WPE 0       // k_part_scatter: minimum waves per SIMD (0: none; 4 spills, A/B r02 +3-6 %)
 #endif
 #if OA_SCAT_WPE
 #define SCAT_ATTR __attribute__((amdgpu_waves_per_eu(OA_SCAT_WPE)))
