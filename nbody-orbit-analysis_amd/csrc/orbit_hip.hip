@@ -1195,28 +1195,30 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
 // ------------------------------------------------------------------ compaction
 __global__ __launch_bounds__(1024) void k_scan_slots(const int32_t *cnt, int32_t n,
                                                      int64_t *off, int64_t *total) {
+    // exclusive scan of the per-halo record counts (one work-group).  Thread t owns the
+    // contiguous run [t*c, t*c + c): its loads are independent and go out together (a
+    // blocked scan has no serial chain of global loads), the run totals are scanned
+    // across the work-group, and the second read of the run hits the cache.
     __shared__ int64_t wsum[16];
-    __shared__ int64_t carry;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) carry = 0;
-    __syncthreads();
-    for (int b = 0; b < n; b += 1024) {
-        int i = b + tid;
-        int64_t x = i < n ? cnt[i] : 0, incl = x;
-        for (int o = 1; o < 64; o <<= 1) {
-            int64_t y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
-        }
-        if (lane == 63) wsum[wave] = incl;
-        __syncthreads();
-        int64_t wpre = 0;
-        for (int w = 0; w < wave; ++w) wpre += wsum[w];
-        if (i < n) off[i] = carry + wpre + incl - x;
-        __syncthreads();
-        if (tid == 0) { int64_t s = 0; for (int w = 0; w < 16; ++w) s += wsum[w]; carry += s; }
-        __syncthreads();
+    const int c = (n + 1023) / 1024;
+    const int s0 = min(n, tid * c), s1 = min(n, s0 + c);
+    int64_t tot = 0;
+#pragma unroll 8
+    for (int i = s0; i < s1; ++i) tot += cnt[i];
+    int64_t incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
     }
-    if (tid == 0) { off[n] = carry; *total = carry; }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int64_t run = incl - tot;
+    for (int w = 0; w < wave; ++w) run += wsum[w];
+#pragma unroll 8
+    for (int i = s0; i < s1; ++i) { off[i] = run; run += cnt[i]; }
+    if (tid == 1023) { off[n] = run; *total = run; }
 }
 
 // Packed (k_step) items hold their records contiguously: a coalesced copy.  Global
