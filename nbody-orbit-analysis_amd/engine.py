@@ -524,9 +524,15 @@ class OrbitEngine:
         return halos, buf[:n_it], k, scratch, starts, counts, has_prog
 
     # ------------------------------------------------------------------ step
-    def step(self, snapshot, centres, bulk_cat, H, z, exists, compare, angles_in=None):
-        """Process one snapshot.  ``compare`` is the reference's ``i > istart``."""
+    def step(self, snapshot, centres, bulk_cat, H, z, exists, compare, angles_in=None,
+             angles_layout=None):
+        """Process one snapshot.  ``compare`` is the reference's ``i > istart``.
+        ``angles_layout``: the row layout a resumed checkpoint was written in (None:
+        the snapshot's own rows, the only layout a single GPU reads)."""
         exists = np.asarray(exists)
+        if angles_in is not None and angles_layout is not None:
+            from .sharding import check_layout
+            check_layout(angles_layout, None)
         if compare and self.prev is None:
             raise RuntimeError('compare step without a previous snapshot')
         dev = self.device
@@ -744,31 +750,28 @@ class OrbitEngine:
         Returns an (len(halo_idx), 3) array in the reference's result dtype."""
         halo_idx = np.asarray(halo_idx, dtype=np.int64)
         vel = snapshot['velocities']
-        n = len(snapshot['ids'])
+        ids = snapshot['ids']
+        n = int(ids.numel()) if isinstance(ids, torch.Tensor) else len(ids)
         starts = np.asarray(snapshot['region_offsets'], dtype=np.int64).reshape(-1)
         counts = np.append(starts[1:], n) - starts
         plan = plan_dtypes(snapshot, np.zeros(3), None, 0.0, 0.0)
-        c = counts[halo_idx]
-        rows = np.concatenate([np.arange(s, s + k) for s, k in zip(starts[halo_idx], c)]) \
-            if len(halo_idx) else np.zeros(0, dtype=np.int64)
         dev = self.device
-        if isinstance(vel, torch.Tensor):
-            v = vel.reshape(-1, 3)[torch.from_numpy(rows).to(vel.device)].to(dev).contiguous()
-        else:
-            v = to_device(np.asarray(vel).reshape(-1, 3)[rows], dev)
+        # the kernel reads each listed block in place (no row gather): the arrays move
+        # to the device whole (a sharded run passes its stripe only)
+        v = vel.reshape(-1, 3).to(dev).contiguous() if isinstance(vel, torch.Tensor) \
+            else to_device(np.asarray(vel).reshape(-1, 3), dev)
         m = None
         if plan.mass is not None:
             ms = snapshot['masses']
-            m = ms[torch.from_numpy(rows).to(ms.device)].to(dev).contiguous() \
-                if isinstance(ms, torch.Tensor) else to_device(np.asarray(ms)[rows], dev)
-        # every listed block empty: the kernel still needs real (unread) arrays
+            m = ms.to(dev).contiguous() if isinstance(ms, torch.Tensor) else to_device(ms, dev)
+        # no rows at all: the kernel still needs real (unread) arrays
         if v.numel() == 0:
-            v = torch.zeros(3, dtype=v.dtype, device=dev)
+            v = torch.zeros((1, 3), dtype=v.dtype, device=dev)
         if m is not None and m.numel() == 0:
             m = torch.zeros(1, dtype=m.dtype, device=dev)
         halos = np.zeros(len(halo_idx), dtype=N.HALO_DTYPE)
-        halos['cur_off'] = np.concatenate([[0], np.cumsum(c)[:-1]]) if len(c) else c
-        halos['cur_cnt'] = c
+        halos['cur_off'] = starts[halo_idx]
+        halos['cur_cnt'] = counts[halo_idx]
         d_h = torch.from_numpy(halos.view(np.uint8)).to(dev)
         lst = torch.arange(len(halo_idx), dtype=torch.int32, device=dev)
         st = torch.cuda.current_stream(dev).cuda_stream
@@ -787,3 +790,7 @@ class OrbitEngine:
     def angles(self):
         """Current per-particle float16 angles (checkpoint payload, track_orbits.py:390-394)."""
         return meta_angles(self.prev.meta)
+
+    def checkpoint_layout(self):
+        """Row layout of ``angles()``: None, the snapshot's own row order."""
+        return None

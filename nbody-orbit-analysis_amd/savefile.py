@@ -20,6 +20,7 @@ class MemorySavefile:
         self.attrs = {}
         self.groups = {}
         self.checkpoint = None
+        self.checkpoint_layout = None
 
     def initialize(self, mode, box_size):
         self.attrs = {'mode': mode}
@@ -32,14 +33,18 @@ class MemorySavefile:
             raise ValueError('group %s exists' % name)
         self.groups[name] = {k: np.asarray(v) for k, v in datasets.items()}
 
-    def write_checkpoint(self, angles):
+    def write_checkpoint(self, angles, layout=None):
         self.checkpoint = np.asarray(angles)
+        self.checkpoint_layout = layout
 
     def last_snapshot_number(self):
         return int(sorted(self.groups)[-1].split('_')[1])
 
     def read_checkpoint(self):
         return self.checkpoint
+
+    def read_checkpoint_layout(self):
+        return self.checkpoint_layout
 
     def write_file(self, snapshot_number, datasets, attrs):
         """On-the-fly driver: one 'file' per snapshot (track_orbits_onthefly.py:229)."""
@@ -67,10 +72,12 @@ class HDF5Savefile:
             for k, v in datasets.items():
                 g.create_dataset(k, data=v)
 
-    def write_checkpoint(self, angles):
+    def write_checkpoint(self, angles, layout=None):
         import h5py
         with h5py.File(self.path + '.checkpoint', 'w') as hf:
             hf.create_dataset('angles', data=angles)
+            if layout is not None:            # only sharded runs with presharded loaders
+                hf.attrs['row_layout'] = layout
 
     def last_snapshot_number(self):
         import h5py
@@ -81,6 +88,12 @@ class HDF5Savefile:
         import h5py
         with h5py.File(self.path + '.checkpoint', 'r') as hf:
             return hf['angles'][:]
+
+    def read_checkpoint_layout(self):
+        import h5py
+        with h5py.File(self.path + '.checkpoint', 'r') as hf:
+            v = hf.attrs.get('row_layout')
+        return None if v is None else (v.decode() if isinstance(v, bytes) else str(v))
 
 
 class RankSink:
@@ -96,7 +109,7 @@ class RankSink:
     def write_group(self, name, datasets):
         pass
 
-    def write_checkpoint(self, angles):
+    def write_checkpoint(self, angles, layout=None):
         pass
 
     def last_snapshot_number(self):
@@ -104,6 +117,10 @@ class RankSink:
 
     def read_checkpoint(self):
         return self.source.read_checkpoint()
+
+    def read_checkpoint_layout(self):
+        f = getattr(self.source, 'read_checkpoint_layout', None)
+        return f() if f is not None else None
 
 
 def open_savefile(savefile):

@@ -5,39 +5,38 @@ rank runs the same ``track_orbits`` driver.  The reference's only parallel axis 
 the halo pool of track_orbits.py:189-194; here the axis is the particle ID instead:
 rank r owns the IDs of one contiguous range (``IdRangeOwner``, the default), so a
 particle's current and previous rows -- including its copies in overlapping regions
--- sit on the same rank, and the join needs no exchange.  The data path is
-collective-free and everything in it stays on the rank's device:
+-- sit on the same rank, and the join needs no exchange.
 
-* **shard**: with a loader that returns the whole snapshot on every rank (the
-  reference's callback contract, track_orbits.py:118-122), each rank moves it to its
-  GPU once and keeps its rows with a device mask + compaction (the block order is
-  preserved, and every kept row remembers its position in its global block, gpos).
-  A *presharded* loader (``presharded=True``, e.g. a distributed reader) hands each
-  rank its own rows directly; the global block is then the rank-ordered
-  concatenation of the ranks' blocks.
+* **shard** (the reference's loader contract: every rank is handed the whole
+  snapshot, track_orbits.py:118-122): the snapshot is cut into W block-aligned
+  *stripes* of about N/W rows (``stripe_halos``).  Rank r moves only stripe r to its
+  GPU -- 1/W of the snapshot over its own PCIe link -- computes the bulk velocities of
+  the stripe's blocks there (whole blocks: the reference's sequential sums, bit for
+  bit), sorts the stripe's rows by owner rank and routes them with one all-to-all
+  over xGMI (``RowExchange``).  Received rows arrive in source-rank order, i.e. in
+  global row order, so block order is preserved, and every row carries its global
+  row (``sel``).  A *presharded* loader (``presharded=True``, e.g. a distributed
+  reader) hands each rank its own rows directly; the global block is then the
+  rank-ordered concatenation of the ranks' blocks.
 * **step**: the rank's ``OrbitEngine`` on its shard; the kernel also emits each apsis
   record's previous-state row, which maps to its global previous-block position
   through the previous snapshot's gpos (a device gather).
-* **records** stay on the device as (halo slot << 32 | gpos, ID, f16 angle).
-
-Collectives per snapshot (all small):
-
-* one all-gather of the halo catalogue rows (centre, bulk velocity): every rank then
-  uses rank 0..N-1's identical rows (the north star's "all-gather of halo centres");
-* bulk velocities computed from the particles (no catalogue value,
-  track_orbits.py:269-280) are sequential sums over a WHOLE block, which no
-  partial-sum exchange reproduces bit for bit: halo j's owner rank (j % world)
-  computes them on the full block and the rows are all-gathered (not available with
-  presharded snapshots);
-* output: ``fetch`` (the savefile path, outside the per-snapshot tagging) all-gathers
-  the records and sorts them by key -- exactly the reference's order (previous-block
+* **records** stay on the device as (halo slot << 32 | gpos, ID, f16 angle) until the
+  savefile needs them: ``fetch`` gathers them to rank 0 -- the only writer -- and
+  sorts them there by key, which is exactly the reference's order (previous-block
   order within each halo, halos in ``halo_exists`` order, track_orbits.py:199-227,
-  315-316).  Checkpoint angles are gathered with their global row index.
+  315-316).
+
+Collectives per snapshot: the shard's all-to-all (not with presharded loaders), one
+all-gather of the halo catalogue rows (centre, bulk velocity), an all-gather of the
+computed bulk velocities when the catalogue gives none, and the records' gather to
+rank 0.  None of them exchanges per-particle data with every rank.
 
 ``ShardedEngine`` exposes the ``OrbitEngine`` interface the driver uses, so
 ``track_orbits(..., engine=ShardedEngine(EngineLocal(OrbitEngine())))`` is the
 multi-GPU drop-in.
 """
+import hashlib
 from dataclasses import dataclass
 from typing import Optional
 
@@ -46,6 +45,7 @@ import torch
 
 U64 = np.uint64
 _HASH_C = np.int64(-7046029254386353131)        # 0x9E3779B97F4A7C15 as int64
+_I64_MAX, _I64_MIN = np.iinfo(np.int64).max, np.iinfo(np.int64).min
 
 
 # ------------------------------------------------------------------ ownership
@@ -59,15 +59,25 @@ class HashOwner:
     def fit(self, ids):
         pass
 
-    def mask(self, ids_t, world, rank):
+    def fit_group(self, ids_t, group):
+        pass
+
+    def reset(self):
+        pass
+
+    def ranks(self, ids_t, world):
         h = ids_t.to(torch.int64) * int(_HASH_C)
-        return ((h >> 33) & 0x7FFFFFFF) % world == rank
+        return ((h >> 33) & 0x7FFFFFFF) % world
+
+    def mask(self, ids_t, world, rank):
+        return self.ranks(ids_t, world) == rank
 
 
 class IdRangeOwner:
     """rank = floor((ID - lo) * world / (hi - lo)), clipped: contiguous ID ranges.
-    Without bounds, [lo, hi) is taken from the first snapshot the engine sees (every
-    rank sees the same one); later IDs outside it go to the first / last rank.
+    Without bounds, [lo, hi) is fitted on the first snapshot the engine sees (the
+    min / max over all ranks' rows); later IDs outside it go to the first / last rank.
+    A fitted range is dropped by ``reset`` (a new run); given bounds are kept.
     IDs are taken as their int64 bit patterns (uint64 IDs >= 2^63 sort below the
     others, as device tensors hold them), and the ratio is evaluated in float64 (the
     same operations on the host and the device)."""
@@ -75,6 +85,11 @@ class IdRangeOwner:
     def __init__(self, lo=None, hi=None):
         self.lo = None if lo is None else int(lo)
         self.hi = None if hi is None else int(hi)
+        self.fixed = lo is not None
+
+    def reset(self):
+        if not self.fixed:
+            self.lo = self.hi = None
 
     @staticmethod
     def _i64(ids):
@@ -92,16 +107,33 @@ class IdRangeOwner:
             lo, hi = (int(v.min()), int(v.max()) + 1) if v.size else (0, 1)
         self.lo, self.hi = lo, hi
 
+    def fit_group(self, ids_t, group):
+        """Fit on the union of the ranks' rows (one 2-element all-reduce)."""
+        import torch.distributed as dist
+        if self.lo is not None:
+            return
+        t = ids_t.to(torch.int64)
+        mn = int(t.min()) if t.numel() else _I64_MAX
+        mx = int(t.max()) if t.numel() else _I64_MIN + 1
+        if dist.get_world_size(group) > 1:
+            r = torch.tensor([mn, -mx], dtype=torch.int64, device=_comm_device())
+            dist.all_reduce(r, op=dist.ReduceOp.MIN, group=group)
+            mn, mx = int(r[0]), -int(r[1])
+        self.lo, self.hi = (mn, mx + 1) if mn <= mx else (0, 1)
+
     def __call__(self, ids, world):
         span = float(max(self.hi - self.lo, 1))
         v = self._i64(ids).astype(np.float64)
         r = np.floor((v - float(self.lo)) * world / span)
         return np.clip(r, 0, world - 1).astype(np.int64)
 
-    def mask(self, ids_t, world, rank):
+    def ranks(self, ids_t, world):
         span = float(max(self.hi - self.lo, 1))
         r = torch.floor((ids_t.to(torch.int64).to(torch.float64) - float(self.lo)) * world / span)
-        return r.clamp_(0, world - 1) == rank
+        return r.clamp_(0, world - 1).to(torch.int64)
+
+    def mask(self, ids_t, world, rank):
+        return self.ranks(ids_t, world) == rank
 
 
 def block_layout(region_offsets, n):
@@ -131,11 +163,89 @@ def shard_snapshot(snapshot, keep):
     return shard, sel, st, cnt
 
 
+def stripe_halos(starts, n, world):
+    """Block-aligned stripes of a snapshot: halo boundaries hb[0..world] such that rank
+    r's stripe is the blocks [hb[r], hb[r+1]), i.e. rows [row(hb[r]), row(hb[r+1]))
+    with row(j) = starts[j] (n past the last block), each about (n - starts[0]) / world
+    rows.  Rows before the first block belong to no halo and to no stripe."""
+    starts = np.asarray(starts, dtype=np.int64)
+    nh = len(starts)
+    hb = np.zeros(world + 1, dtype=np.int64)
+    hb[world] = nh
+    if nh and world > 1:
+        lo = int(starts[0])
+        targets = lo + (n - lo) * np.arange(1, world, dtype=np.float64) / world
+        hb[1:world] = np.searchsorted(starts, targets, side='left')
+    return hb
+
+
+def stripe_rows(starts, n, hb, r):
+    """Row range [lo, hi) of stripe r (``stripe_halos``)."""
+    nh = len(starts)
+
+    def row(j):
+        return int(starts[j]) if j < nh else int(n)
+    return row(int(hb[r])), row(int(hb[r + 1]))
+
+
 # ------------------------------------------------------------------ collectives
 def _comm_device():
     import torch.distributed as dist
     return torch.device('cuda', torch.cuda.current_device()) \
         if dist.get_backend() == 'nccl' else torch.device('cpu')
+
+
+# gloo moves neither 16-bit integers nor bool: they travel widened
+_WIDEN = {torch.int16: torch.int32, torch.bool: torch.uint8, torch.float16: torch.float32}
+
+
+class RowExchange:
+    """Point-to-point row routing with known per-destination counts: one
+    ``all_to_all_single`` per tensor, uneven splits, rows already sorted by destination
+    rank.  The received rows are the senders' rows in rank order.  The counts are
+    exchanged once (a W-element all-to-all), so several tensors with the same rows
+    cost one small exchange plus one collective each.  World 1 moves nothing."""
+
+    def __init__(self, send_counts, group=None):
+        import torch.distributed as dist
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.send = [int(c) for c in send_counts]
+        if self.world == 1:
+            self.recv = list(self.send)
+            return
+        self.dev = _comm_device()
+        s = torch.tensor(self.send, dtype=torch.int64, device=self.dev)
+        r = torch.empty_like(s)
+        dist.all_to_all_single(r, s, group=group)
+        self.recv = [int(x) for x in r.cpu()]
+
+    @property
+    def n_recv(self):
+        return sum(self.recv)
+
+    def move(self, t):
+        import torch.distributed as dist
+        if self.world == 1:
+            return t
+        home = t.device
+        x = t.contiguous()
+        dt = x.dtype
+        wire = _WIDEN.get(dt, dt) if self.dev.type == 'cpu' else dt
+        x = x.to(self.dev).to(wire)
+        out = torch.empty((self.n_recv,) + tuple(x.shape[1:]), dtype=wire, device=self.dev)
+        dist.all_to_all_single(out, x, self.recv, self.send, group=self.group)
+        return out.to(dt).to(home)
+
+
+def gather_rows(group, root, *tensors):
+    """Gather the rows of each tensor (same row count) to ``root``, rank-ordered; the
+    other ranks get empty tensors.  One count exchange + one collective per tensor."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    n = int(tensors[0].shape[0])
+    rx = RowExchange([n if q == root else 0 for q in range(world)], group)
+    return [rx.move(t) for t in tensors]
 
 
 def allgather_rows(a, group=None):
@@ -164,6 +274,16 @@ def allgather_v(t, group=None):
     return torch.cat([o[:k] for o, k in zip(outs, ns)], dim=0)
 
 
+def all_true(flag, group=None):
+    """True on every rank iff ``flag`` is true on every rank (one 1-element all-reduce)."""
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return bool(flag)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=_comm_device())
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
+
+
 def _f64_bits(x):
     return np.ascontiguousarray(x, dtype=np.float64).view(np.int64)
 
@@ -171,6 +291,100 @@ def _f64_bits(x):
 def _as_i64(t):
     """IDs of any 32/64-bit integer dtype as int64 values (bit pattern kept for 64-bit)."""
     return t if t.dtype == torch.int64 else t.to(torch.int64)
+
+
+def _to_tensor(x, device):
+    """A row range of a loader array -> tensor on ``device`` (uint dtypes bit-cast)."""
+    if isinstance(x, torch.Tensor):
+        return x.to(device)
+    a = np.ascontiguousarray(x)
+    if a.dtype.kind == 'u':
+        a = a.view(a.dtype.str.replace('u', 'i'))
+    return torch.from_numpy(a).to(device)
+
+
+def gather_bulk(rows_local, h0, nh, group=None):
+    """All-gather the bulk-velocity rows each rank computed for its halos [h0, h0+k):
+    returns the (nh, 3) array in the computed dtype (float64 bits on the wire)."""
+    b = np.asarray(rows_local).reshape(-1, 3) if rows_local is not None else np.zeros((0, 3))
+    dt = b.dtype if len(b) else None
+    rows = np.concatenate([(h0 + np.arange(len(b)))[:, None].astype(np.int64),
+                           _f64_bits(b).reshape(-1, 3)], axis=1)
+    allr = allgather_rows(rows, group)
+    dts = allgather_rows(np.array([[0 if dt is None else np.dtype(dt).itemsize]]), group)[:, 0]
+    size = int(dts.max()) if len(dts) else 8
+    out = np.full((nh, 3), np.nan, dtype=np.float64)
+    out[allr[:, 0]] = allr[:, 1:].copy().view(np.float64)
+    return out.astype(np.float32 if size == 4 else np.float64)
+
+
+# ------------------------------------------------------------------ stripes -> shards
+@dataclass
+class Shard:
+    """This rank's rows of one snapshot (device tensors in block order)."""
+    snap: dict                         # ids / coordinates / velocities (/ masses) + region_offsets
+    sel: torch.Tensor                  # global snapshot row of every shard row (int64)
+    gpos: torch.Tensor                 # position of every shard row in its global block
+    counts: np.ndarray                 # shard rows per halo
+    bulk: Optional[np.ndarray] = None  # (nh, 3) bulk velocities of the whole blocks
+    h2d_bytes: int = 0                 # loader bytes this rank moved to its device
+
+
+def stripe_shard(snapshot, starts, owner, group, device, bulk_fn=None):
+    """The whole-snapshot loader contract on one rank (module docstring): upload stripe
+    r only, compute its blocks' bulk velocities (``bulk_fn(stripe_snapshot, halos)``,
+    when given), route its rows to their owners with one all-to-all per array, and lay
+    the received rows out in block order.  Returns a ``Shard``."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    ids = snapshot['ids']
+    n = int(ids.numel()) if isinstance(ids, torch.Tensor) else len(ids)
+    starts = np.asarray(starts, dtype=np.int64)
+    nh = len(starts)
+    hb = stripe_halos(starts, n, world)
+    lo, hi = stripe_rows(starts, n, hb, rank)
+    h0, h1 = int(hb[rank]), int(hb[rank + 1])
+    masses = snapshot['masses']
+    has_m = isinstance(masses, (np.ndarray, torch.Tensor))
+    keys = ('ids', 'coordinates', 'velocities') + (('masses',) if has_m else ())
+    st = {k: _to_tensor(snapshot[k][lo:hi], device) for k in keys}
+    h2d = sum(int(v.numel()) * v.element_size() for k, v in st.items()
+              if not (isinstance(snapshot[k], torch.Tensor) and snapshot[k].device.type ==
+                      torch.device(device).type))
+    for k in ('coordinates', 'velocities'):
+        st[k] = st[k].reshape(-1, 3)
+    bulk = None
+    if bulk_fn is not None:
+        stripe = dict(snapshot)
+        stripe.update(st)
+        stripe['region_offsets'] = starts[h0:h1] - lo
+        rows = bulk_fn(stripe, np.arange(h1 - h0)) if h1 > h0 else None
+        bulk = gather_bulk(rows, h0, nh, group) if world > 1 else \
+            (np.asarray(rows) if rows is not None else np.zeros((0, 3)))
+    owner.fit_group(st['ids'], group)
+    if world > 1:
+        dest = owner.ranks(st['ids'], world)
+        dest, perm = torch.sort(dest, stable=True)
+        cnt = torch.bincount(dest, minlength=world).cpu().tolist()
+        rx = RowExchange(cnt, group)
+        sel = rx.move(perm + lo)
+        sh = {k: rx.move(v[perm]) for k, v in st.items()}
+    else:
+        sel = torch.arange(lo, hi, dtype=torch.int64, device=device)
+        sh = st
+    st_t = torch.from_numpy(starts).to(device)
+    if nh:
+        block = torch.searchsorted(st_t, sel, right=True) - 1
+        counts = torch.bincount(block, minlength=nh).cpu().numpy().astype(np.int64)
+        gpos = sel - st_t[block]
+    else:
+        counts, gpos = np.zeros(0, np.int64), sel
+    shard = dict(snapshot)
+    shard.update(sh)
+    shard['region_offsets'] = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64) \
+        if nh else counts
+    return Shard(snap=shard, sel=sel, gpos=gpos, counts=counts, bulk=bulk, h2d_bytes=h2d)
 
 
 # ------------------------------------------------------------------ engine facade
@@ -197,6 +411,8 @@ class ShardedPrep:
     bulk_out: Optional[np.ndarray]
     plan: object
     lp: object = None
+    layout: Optional[str] = None            # checkpoint row layout (presharded runs)
+    h2d_bytes: int = 0
 
 
 class _Plan:
@@ -205,12 +421,23 @@ class _Plan:
         self.bulk = bulk_dtype
 
 
+def check_layout(want, have):
+    """A checkpoint written in one row layout resumes only in the same one (ADVICE r02:
+    a presharded checkpoint's rows depend on the world size and the reader's split)."""
+    if (want or None) != (have or None):
+        raise ValueError('checkpoint angles were written in row layout %r, this run reads '
+                         'the snapshot in layout %r: resume with the same sharding'
+                         % (want or 'global', have or 'global'))
+
+
 class ShardedEngine:
     """``OrbitEngine`` interface over ID-sharded ranks (see module docstring).
 
     ``step`` = ``prepare`` (host: shard, plan, uploads) + ``launch`` (the catalogue
     all-gather and the device step).  The two halves are public so a benchmark can
     prepare a chain of snapshots and time ``launch`` alone, as bench.py does."""
+
+    ROOT = 0                              # the rank that writes the savefile
 
     def __init__(self, local, group=None, owner=None, mode=None, presharded=False,
                  share_catalogue=True):
@@ -228,6 +455,7 @@ class ShardedEngine:
 
     def reset(self):
         self.prev = None
+        self.owner.reset()
         self.local.reset()
 
     # ---------------------------------------------------------------- collectives
@@ -245,55 +473,12 @@ class ShardedEngine:
         dist.all_gather_into_tensor(out, torch.from_numpy(mine).to(dev), group=self.group)
         return out[:nh]
 
-    def _bulk(self, snapshot, nh):
-        own = np.flatnonzero(np.arange(nh) % self.world == self.rank)
-        b = np.asarray(self.local.bulk(snapshot, own)) if len(own) else np.zeros((0, 3))
-        dt = b.dtype if len(own) else None
-        rows = np.concatenate([own[:, None].astype(np.int64),
-                               _f64_bits(b.reshape(-1, 3)).reshape(-1, 3)], axis=1)
-        allr = allgather_rows(rows, self.group)
-        dts = allgather_rows(np.array([[0 if dt is None else np.dtype(dt).itemsize]]),
-                             self.group)[:, 0]
-        size = int(dts.max())
-        out = np.empty((nh, 3), dtype=np.float64)
-        out[allr[:, 0]] = allr[:, 1:].copy().view(np.float64)
-        return out.astype(np.float32 if size == 4 else np.float64)
-
     # ---------------------------------------------------------------- shard
-    def _tensor(self, x):
-        if isinstance(x, torch.Tensor):
-            return x.to(self.device)
-        a = np.ascontiguousarray(x)
-        if a.dtype.kind == 'u':
-            a = a.view(a.dtype.str.replace('u', 'i'))
-        return torch.from_numpy(a).to(self.device)
-
-    def _shard(self, snapshot, starts, counts):
-        """Device shard of a whole snapshot: this rank's rows, block order kept."""
-        nh = len(starts)
-        ids_t = self._tensor(snapshot['ids'])
-        self.owner.fit(ids_t)
-        keep = self.owner.mask(ids_t, self.world, self.rank)
-        sel = torch.nonzero(keep).squeeze(1)
-        st_t = torch.from_numpy(starts).to(self.device)
-        block = torch.searchsorted(st_t, sel, right=True) - 1 if nh else sel
-        cnt = torch.bincount(block, minlength=nh) if nh else torch.zeros(0, dtype=torch.int64)
-        gpos = sel - st_t[block] if nh else sel
-        shard = dict(snapshot)
-        shard['ids'] = ids_t[sel]
-        for k in ('coordinates', 'velocities'):
-            shard[k] = self._tensor(snapshot[k]).reshape(-1, 3)[sel]
-        if isinstance(snapshot['masses'], (np.ndarray, torch.Tensor)):
-            shard['masses'] = self._tensor(snapshot['masses'])[sel]
-        cnt_h = cnt.cpu().numpy().astype(np.int64)
-        shard['region_offsets'] = np.concatenate([[0], np.cumsum(cnt_h)[:-1]]).astype(np.int64) \
-            if nh else cnt_h
-        return shard, sel, gpos
-
     def _presharded_gpos(self, starts, counts):
         """Global block = the ranks' blocks concatenated in rank order: a shard row's
         position is the rows of lower ranks in its block + its own index.  Returns the
-        block positions, the global snapshot rows and the global row count."""
+        block positions, the global snapshot rows, the global row count and the row
+        layout tag of a checkpoint written in this layout."""
         cnt_all = allgather_v(torch.from_numpy(counts.astype(np.int64))[None, :], self.group)
         before = cnt_all[:self.rank].sum(0).to(self.device) if self.rank else \
             torch.zeros(len(counts), dtype=torch.int64, device=self.device)
@@ -304,38 +489,51 @@ class ShardedEngine:
         local = torch.arange(int(c.sum()), device=self.device) - \
             torch.from_numpy(starts).to(self.device)[block]
         gpos = before[block] + local
-        return gpos, gstart[block] + gpos, int(tot.sum())
+        digest = hashlib.sha256(np.ascontiguousarray(cnt_all.cpu().numpy(), dtype='<i8')
+                                .tobytes()).hexdigest()[:16]
+        layout = 'rank-major/world=%d/blocks=%s' % (self.world, digest)
+        return gpos, gstart[block] + gpos, int(tot.sum()), layout
 
     # ---------------------------------------------------------------- step
     def prepare(self, snapshot, centres, bulk_cat, H, z, exists, compare, angles_in=None,
-                prev=None):
-        """Host half of a step; ``prev`` (a ShardedPrep) defaults to the last step."""
+                prev=None, angles_layout=None):
+        """Host half of a step; ``prev`` (a ShardedPrep) defaults to the last step.
+        ``angles_layout``: the row layout the resumed checkpoint was written in."""
+        from .engine import check_angles_in
         exists = np.asarray(exists)
         ids = snapshot['ids']
         n = int(ids.numel()) if isinstance(ids, torch.Tensor) else len(ids)
         starts, counts = block_layout(snapshot['region_offsets'], n)
         nh = len(starts)
         bulk = bulk_cat
-        if bulk_cat is None and nh:
-            if self.presharded:
+        layout, h2d = None, 0
+        if self.presharded:
+            if bulk_cat is None and nh:
                 raise NotImplementedError('computed bulk velocities need whole blocks: give '
                                           'catalogue bulk velocities with presharded snapshots')
-            bulk = self._bulk(snapshot, nh)
-        if self.presharded:
             # this rank's rows as they are; host arrays (a distributed reader) move to
             # the rank's device once
-            shard, sel = dict(snapshot), None
+            shard = dict(snapshot)
             for k in ('ids', 'coordinates', 'velocities'):
-                shard[k] = self._tensor(snapshot[k])
+                shard[k] = _to_tensor(snapshot[k], self.device)
             if isinstance(snapshot['masses'], (np.ndarray, torch.Tensor)):
-                shard['masses'] = self._tensor(snapshot['masses'])
-            gpos, sel, n_global = self._presharded_gpos(starts, counts)
-            # a checkpoint holds the global snapshot's angles (rank-major blocks)
-            a_in = None if angles_in is None else np.asarray(angles_in)[sel.cpu().numpy()]
+                shard['masses'] = _to_tensor(snapshot['masses'], self.device)
+            h2d = sum(int(np.asarray(snapshot[k]).nbytes) for k in ('ids', 'coordinates',
+                                                                    'velocities')
+                      if not isinstance(snapshot[k], torch.Tensor))
+            gpos, sel, n_global, layout = self._presharded_gpos(starts, counts)
         else:
-            shard, sel, gpos = self._shard(snapshot, starts, counts)
-            n_global = n
-            a_in = None if angles_in is None else np.asarray(angles_in)[sel.cpu().numpy()]
+            sh = stripe_shard(snapshot, starts, self.owner, self.group, self.device,
+                              bulk_fn=self.local.bulk if (bulk_cat is None and nh) else None)
+            shard, sel, gpos, n_global, h2d = sh.snap, sh.sel, sh.gpos, n, sh.h2d_bytes
+            if bulk_cat is None and nh:
+                bulk = sh.bulk
+        a_in = None
+        if angles_in is not None and not compare:
+            # a checkpoint holds the global snapshot's angles in this run's row layout
+            check_layout(angles_layout, layout)
+            check_angles_in(angles_in, n_global)
+            a_in = np.asarray(angles_in)[sel.cpu().numpy()]
         rows = None
         if self.share_catalogue and nh:
             rows = np.zeros((nh, 6), dtype=np.float64)
@@ -347,7 +545,8 @@ class ShardedEngine:
         sp = ShardedPrep(n=n, exists=exists, compare=bool(compare), gpos=gpos, sel=sel,
                          n_global=n_global,
                          rows=rows, bulk_out=None if bulk_cat is not None else bulk,
-                         plan=_Plan(ids_dt, None if bulk is None else np.asarray(bulk).dtype))
+                         plan=_Plan(ids_dt, None if bulk is None else np.asarray(bulk).dtype),
+                         layout=layout, h2d_bytes=h2d)
         sp.lp = self.local.prepare(shard, centres, bulk, H, z, exists, compare, a_in,
                                    None if (prev is None or p is None) else p.lp,
                                    share=bulk_cat is not None)
@@ -368,49 +567,63 @@ class ShardedEngine:
             res.records, res.gpos_prev = out, p.gpos
         return res
 
-    def step(self, snapshot, centres, bulk_cat, H, z, exists, compare, angles_in=None):
+    def step(self, snapshot, centres, bulk_cat, H, z, exists, compare, angles_in=None,
+             angles_layout=None):
         if compare and self.prev is None:
             raise RuntimeError('compare step without a previous snapshot')
-        sp = self.prepare(snapshot, centres, bulk_cat, H, z, exists, compare, angles_in)
+        sp = self.prepare(snapshot, centres, bulk_cat, H, z, exists, compare, angles_in,
+                          angles_layout=angles_layout)
         res = self.launch(sp)
         self.prev = sp
         return res
 
     # ---------------------------------------------------------------- outputs
     def fetch(self, res, ids_dtype):
-        """Gather every rank's records and put them in the reference's order: key =
-        halo slot << 32 | position in the global previous block."""
+        """Gather every rank's records to rank 0 and put them in the reference's order:
+        key = halo slot << 32 | position in the global previous block.  Ranks other
+        than 0 (which write nothing) get zero offsets and no records."""
         offs, a_ids, a_ang, a_pos = res.records
         total = int(offs[-1])
         slot = torch.repeat_interleave(torch.arange(res.n_slots, device=offs.device),
                                        (offs[1:] - offs[:-1]).long())
         g = res.gpos_prev[a_pos[:total].to(res.gpos_prev.device).long()]
-        key = allgather_v((slot.to(g.device) << 32) | g, self.group)
-        ids = allgather_v(_as_i64(a_ids[:total]), self.group)
-        ang = allgather_v(a_ang[:total].to(torch.int32), self.group)   # (gloo has no int16)
-        order = torch.argsort(key)
-        key, ids, ang = key[order], ids[order], ang[order]
-        cnt = torch.bincount((key >> 32).long(), minlength=res.n_slots)[:res.n_slots] \
-            if key.numel() else torch.zeros(res.n_slots, dtype=torch.int64)
-        offsets = np.concatenate([[0], np.cumsum(cnt.cpu().numpy())]).astype(np.int64)
+        rec = torch.stack([(slot.to(g.device) << 32) | g, _as_i64(a_ids[:total]).to(g.device),
+                           a_ang[:total].to(torch.int64).to(g.device)], dim=1)
+        rec, = gather_rows(self.group, self.ROOT, rec)
         dt = np.dtype(ids_dtype)
-        ids_h = ids.cpu().numpy()
-        ids_h = ids_h.view(np.uint64).astype(dt) if dt.kind == 'u' else ids_h.astype(dt)
-        return offsets, ids_h, ang.cpu().numpy().astype(np.uint16).view(np.float16)
+        if self.rank != self.ROOT:
+            return (np.zeros(res.n_slots + 1, np.int64), np.zeros(0, dt),
+                    np.zeros(0, np.float16))
+        order = torch.argsort(rec[:, 0])
+        rec = rec[order]
+        cnt = torch.bincount((rec[:, 0] >> 32).long(), minlength=res.n_slots)[:res.n_slots] \
+            if rec.shape[0] else torch.zeros(res.n_slots, dtype=torch.int64)
+        offsets = np.concatenate([[0], np.cumsum(cnt.cpu().numpy())]).astype(np.int64)
+        h = rec[:, 1:].cpu().numpy()
+        ids_h = h[:, 0].view(np.uint64).astype(dt) if dt.kind == 'u' else h[:, 0].astype(dt)
+        return offsets, ids_h, h[:, 1].astype(np.uint16).view(np.float16)
 
     def bulk_velocities(self, res, plan):
         return res.bulk
 
     def angles(self):
-        """Global float16 angle state in current-snapshot order (checkpoint payload)."""
+        """Global float16 angle state in current-snapshot order (checkpoint payload),
+        gathered to rank 0; None on the other ranks."""
         p = self.prev
         loc = self.local.angles_tensor().to(torch.int64)
         rows = torch.stack([p.sel.to(loc.device), loc], dim=1) if loc.numel() else \
-            torch.zeros((0, 2), dtype=torch.int64)
-        allr = allgather_v(rows, self.group).cpu().numpy()
+            torch.zeros((0, 2), dtype=torch.int64, device=loc.device)
+        allr, = gather_rows(self.group, self.ROOT, rows)
+        if self.rank != self.ROOT:
+            return None
+        allr = allr.cpu().numpy()
         out = np.zeros(p.n_global, dtype=np.uint16)
         out[allr[:, 0]] = allr[:, 1].astype(np.uint16)
         return out.view(np.float16)
+
+    def checkpoint_layout(self):
+        """Row layout of ``angles()`` (None: the global snapshot's own row order)."""
+        return self.prev.layout if self.prev is not None else None
 
 
 class EngineLocal:
@@ -426,7 +639,6 @@ class EngineLocal:
         self.engine.reset()
 
     def prepare(self, shard, centres, bulk, H, z, exists, compare, angles_in, prev_lp, share):
-        from .engine import SnapshotState  # noqa: F401
         eng = self.engine
         layout = None
         if compare and prev_lp is not None:

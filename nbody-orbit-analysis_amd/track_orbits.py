@@ -100,13 +100,16 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
                 print('Savefile initialized\n')
 
         compare = i > istart
-        angles_in = None
+        angles_in, step_kw = None, {}
         if resume and not compare:
             # the reference opens savefile + '.checkpoint' here (track_orbits.py:229-232)
             angles_in = out.read_checkpoint()
             if angles_in is None:
                 raise FileNotFoundError('resume: no checkpoint angles in the savefile '
                                         '(run with checkpoint=True first)')
+            layout = read_checkpoint_layout(out)
+            if layout is not None:
+                step_kw['angles_layout'] = layout
         # apsis IDs are the previous snapshot's IDs (ids_prev_[apsis_inds], :315-316):
         # they keep that snapshot's dtype
         ids_dtype_prev = eng.prev.plan.ids if compare else None
@@ -114,7 +117,7 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
         if verbose:
             t0 = time.time()
         res = eng.step(snapshot, region_positions, region_bulk_vels, H, snapshot['redshift'],
-                       halo_exists, compare, angles_in=angles_in)
+                       halo_exists, compare, angles_in=angles_in, **step_kw)
         if compare:
             apsis_offsets, apsis_ids, apsis_angles = eng.fetch(res, ids_dtype_prev)
         if verbose:
@@ -135,7 +138,8 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
             save_to_file(out, apsis_ids, apsis_offsets, apsis_angles,
                          region_positions[hinds], region_radii[hinds], bulk[hinds],
                          halo_ids_[hinds], halo_ids_final, snapshot_number, mode,
-                         checkpoint, eng.angles() if checkpoint else None, verbose)
+                         checkpoint, eng.angles() if checkpoint else None, verbose,
+                         layout=checkpoint_layout(eng) if checkpoint else None)
 
         progen_exists = halo_exists
 
@@ -144,9 +148,20 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
             time.time() - tstart))
 
 
+def checkpoint_layout(eng):
+    """Row layout of the engine's checkpoint angles (None: the snapshot's own rows)."""
+    f = getattr(eng, 'checkpoint_layout', None)
+    return f() if f is not None else None
+
+
+def read_checkpoint_layout(out):
+    f = getattr(out, 'read_checkpoint_layout', None)
+    return f() if f is not None else None
+
+
 def save_to_file(savefile, apsis_ids, apsis_offsets, apsis_angles, region_positions,
                  region_radii, bulk_velocities, halo_ids, halo_ids_final, snapshot_number,
-                 mode, checkpoint, angles, verbose):
+                 mode, checkpoint, angles, verbose, layout=None):
     """Write one snapshot group (+ checkpoint) in the reference layout (:366-397)."""
     out = open_savefile(savefile)
     if verbose:
@@ -157,7 +172,12 @@ def save_to_file(savefile, apsis_ids, apsis_offsets, apsis_angles, region_positi
                                    region_positions, region_radii, bulk_velocities,
                                    halo_ids, halo_ids_final))
     if checkpoint:
-        out.write_checkpoint(angles)
+        # a checkpoint in a non-global row layout (presharded ranks) records it, so a
+        # resume in another layout is refused instead of mis-assigning angles
+        if layout is None:
+            out.write_checkpoint(angles)
+        else:
+            out.write_checkpoint(angles, layout=layout)
     if verbose:
         print('Saved to file ({} s)\n'.format(time.time() - t0))
 

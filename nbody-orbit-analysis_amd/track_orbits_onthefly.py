@@ -19,12 +19,13 @@ compacted and sorted on the device from the kernel's match flags.
 """
 import os
 import time
+from dataclasses import dataclass
 
 import numpy as np
 import torch
 
 from . import _native as N
-from .engine import OrbitEngine, SnapshotState, to_device, F64, np_dtype
+from .engine import OrbitEngine, SnapshotState, to_device, F64, np_dtype, is_array
 
 _TORCH = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64}
 
@@ -42,9 +43,13 @@ def repack(arr, length, inds):
 def _block_starts(slices, n):
     """Repacked (start, end) rows (-1, -1 = absent) -> non-decreasing block starts that
     tile [0, n) (an absent halo gets an empty block)."""
+    slices = np.asarray(slices, dtype=np.int64).reshape(-1, 2)
     starts = np.empty(len(slices), dtype=np.int64)
-    pos = 0
-    for j, (a, b) in enumerate(np.asarray(slices, dtype=np.int64)):
+    present = slices[:, 0] >= 0
+    # an absent halo before the first present one starts where that one starts (rows
+    # before the first block are in no block)
+    pos = int(slices[present, 0][0]) if present.any() else 0
+    for j, (a, b) in enumerate(slices):
         if a >= 0:
             if a < pos:
                 raise ValueError('region blocks must follow halo order')
@@ -101,7 +106,7 @@ class OnTheFly:
         dev = {k: to_device(snap[k], eng.device) for k in ('ids', 'coordinates', 'velocities')}
         dsnap = dict(s)
         dsnap.update(dev)
-        if isinstance(snap['masses'], np.ndarray):
+        if is_array(snap['masses']):
             dsnap['masses'] = to_device(snap['masses'], eng.device)
         nh = len(slices)
         layout = None
@@ -121,18 +126,17 @@ class OnTheFly:
         a.vr_f64 = int(np.result_type(plan.vel, coord) == F64)
         return pr
 
-    def run(self, snaps, slices, centres, carried=None, bulks=None, merge_parts=False):
-        """snaps / slices / centres: [current, previous].  Returns host outputs.
+    def compare(self, snaps, slices, centres, carried=None, bulks=None):
+        """Device half of a call: frame the previous snapshot (unless ``carried``),
+        frame + join the current one.  Returns the device outputs (``OTFDevice``) and
+        leaves this call's current frame state in ``self.carry``.
 
-        ``bulks``: [current, previous] bulk-velocity rows to use instead of computing
-        them from the blocks.  ``merge_parts``: also return, under ``'parts'``, what a
-        sharded run needs to merge ranks (the previous-state rows of the apsis records
-        and of the angle changes, the per-halo entered lists before interleaving and
-        the current rows of the loader-order ones).
-
-        ``carried``: the (state, bulk velocities) a previous call left for its current
-        snapshot (``self.carry``), when that snapshot is this call's previous one with
-        the same regions; its frame is then not recomputed (``snaps[1]`` unused)."""
+        snaps / slices / centres: [current, previous].  ``bulks``: [current, previous]
+        bulk-velocity rows to use instead of computing them from the blocks (a shard's
+        rows do not hold whole blocks).  ``carried``: the (state, bulk velocities) a
+        previous call left for its current snapshot (``self.carry``), when that
+        snapshot is this call's previous one with the same regions; its frame is then
+        not recomputed (``snaps[1]`` unused)."""
         eng = self.eng
         cur, prv = snaps
         if carried is None:
@@ -176,21 +180,36 @@ class OnTheFly:
         else:
             raise RuntimeError('LDS hash tables kept overflowing')
         nh = len(slices[0])
-        ids_dtype = np_dtype(cur['ids'])
-        unsigned = ids_dtype.kind == 'u'
+        bulk_c = pc.halos.cpu().numpy().view(N.HALO_DTYPE)['bulk'].astype(pc.plan.bulk)
+        if bulk_p is None:
+            bulk_p = pp.halos.cpu().numpy().view(N.HALO_DTYPE)['bulk'].astype(pp.plan.bulk)
+        # this snapshot's frame state (r̂ in the coordinate dtype, sign bits) is exactly
+        # what the next call needs for its previous snapshot
+        self.carry = (SnapshotState(ids=pc.snap['ids'], rhat=pc.rhat, meta=pc.meta,
+                                    starts=pc.starts, counts=pc.counts, exists=np.arange(nh),
+                                    plan=pc.plan), bulk_c)
+        return OTFDevice(pc=pc, prev=prev, res=res, angle_out=angle_out[:n_prev],
+                         matched_prev=matched_prev[:n_prev].bool(),
+                         matched_cur=matched_cur[:pc.n] != 0, bulk_c=bulk_c, bulk_p=bulk_p)
+
+    def run(self, snaps, slices, centres, carried=None, bulks=None):
+        """One call on this GPU (``compare``), outputs brought to the host in the
+        reference's layout (track_orbits_onthefly.py:123-205)."""
+        eng = self.eng
+        d = self.compare(snaps, slices, centres, carried=carried, bulks=bulks)
+        pc, prev, res = d.pc, d.prev, d.res
+        nh = len(slices[0])
+        ids_dtype = np_dtype(snaps[0]['ids'])
         # apsis records per halo, previous-block order (:154-166)
         offsets, apsis_ids, _ = eng.fetch(res, ids_dtype)
         # angle changes of every matched particle, previous-block order (:173-174):
         # N values, brought back through pinned memory
-        mp = matched_prev[:n_prev].bool()
-        sel = angle_out[:n_prev][mp]
+        mp = d.matched_prev
+        sel = d.angle_out[mp]
         angles_h = torch.empty(sel.shape, dtype=sel.dtype, pin_memory=True)
         angles_h.copy_(sel)
         angles = angles_h.numpy()
         p_has = pc.halos.cpu().numpy().view(N.HALO_DTYPE)['prev_cnt'] > 0
-
-        def host_ids(t):
-            return t.cpu().numpy().view(ids_dtype) if t.numel() else np.zeros(0, ids_dtype)
 
         def halo_of(pos, starts):
             # block of each selected position (blocks tile [0, n) in halo order)
@@ -205,84 +224,135 @@ class OnTheFly:
             torch.bincount(dh, minlength=nh).cpu().numpy(), ids_dtype)
         # entered: setdiff1d(current, previous) per halo (:168); all of a halo's
         # particles, in loader order, when its progenitor block is empty (:178)
-        esel = torch.nonzero(matched_cur[:pc.n] == 0).squeeze(1)
+        esel = torch.nonzero(d.matched_cur == 0).squeeze(1)
         e_ids = pc.snap['ids'][esel]
         eh = halo_of(esel, pc.starts)
         sorted_h = torch.from_numpy(p_has).to(eng.device)[eh]
         srt, s_off = _sorted_unique_per_halo(
             eng.lib, eng.device, e_ids[sorted_h],
             torch.bincount(eh[sorted_h], minlength=nh).cpu().numpy(), ids_dtype)
-        raw = host_ids(e_ids[~sorted_h])
+        raw_t = e_ids[~sorted_h]
+        raw = raw_t.cpu().numpy().view(ids_dtype) if raw_t.numel() else np.zeros(0, ids_dtype)
         r_off = np.concatenate([[0], np.cumsum(torch.bincount(eh[~sorted_h], minlength=nh)
                                                 .cpu().numpy())]).astype(np.int64)
         entered, e_off = _interleave_halos(p_has, srt, s_off, raw, r_off)
-        # concatenation dtype of the reference's per-halo lists (:183, :203): an empty
-        # halo contributes np.array([], dtype=ids.dtype)
-        parts = [np.zeros(0, np.dtype(pc.plan.coord))] * int(p_has.sum()) + \
-                [np.zeros(0, ids_dtype)] * int((~p_has).sum())
-        adt = np.concatenate(parts).dtype if parts else np.dtype(np.float64)
-
-        bulk_c = pc.halos.cpu().numpy().view(N.HALO_DTYPE)['bulk'].astype(pc.plan.bulk)
-        if bulk_p is None:
-            bulk_p = pp.halos.cpu().numpy().view(N.HALO_DTYPE)['bulk'].astype(pp.plan.bulk)
-        # this snapshot's frame state (r̂ in the coordinate dtype, sign bits) is exactly
-        # what the next call needs for its previous snapshot
-        self.carry = (SnapshotState(ids=pc.snap['ids'], rhat=pc.rhat, meta=pc.meta,
-                                    starts=pc.starts, counts=pc.counts, exists=np.arange(nh),
-                                    plan=pc.plan), bulk_c)
-        extra = {}
-        if merge_parts:
-            total = int(offsets[-1]) if len(offsets) else 0
-            extra['parts'] = dict(
-                apsis_pos=res.apsis_pos[:total].cpu().numpy().astype(np.int64),
-                angle_pos=torch.nonzero(mp).squeeze(1).cpu().numpy(),
-                srt=srt, s_off=s_off, raw=raw, r_off=r_off,
-                raw_pos=esel[~sorted_h].cpu().numpy(), p_has=p_has)
-        return {**extra, 'apsis_offsets': offsets, 'apsis_ids': apsis_ids,
+        adt = _angles_dtype(pc.plan.coord, ids_dtype, p_has)
+        return {'apsis_offsets': offsets, 'apsis_ids': apsis_ids,
                 'angles': angles.astype(adt, copy=False),
                 'entered_offsets': e_off, 'entered_ids': entered,
                 'departed_offsets': d_off, 'departed_ids': departed,
-                'bulk_velocities': [bulk_c, bulk_p]}
+                'bulk_velocities': [d.bulk_c, d.bulk_p]}
 
 
-def merge_onthefly(parts, nh):
-    """Merge the ranks' on-the-fly outputs of one snapshot pair (ShardedOnTheFly).
+@dataclass
+class OTFDevice:
+    """Device outputs of one on-the-fly compare (OnTheFly.compare)."""
+    pc: object                      # the current snapshot's PreparedStep
+    prev: SnapshotState             # the previous snapshot's frame state
+    res: object                     # StepResult: apsis CSR (+ previous-state rows)
+    angle_out: torch.Tensor         # arccos(r̂_prev . r̂) per previous row (matched rows)
+    matched_prev: torch.Tensor      # bool per previous row
+    matched_cur: torch.Tensor       # bool per current row
+    bulk_c: np.ndarray
+    bulk_p: np.ndarray
 
-    ``parts``: per rank, a dict with the rank's per-halo CSR outputs and each element's
-    global row (``*_gpos``).  A halo's previous and current blocks tile their snapshots
-    in halo order, so a global previous row orders apsis records and angle changes
-    exactly as the reference emits them (previous-block order, halos in order,
-    :154-174); entered / departed IDs are per-halo sorted unique (setdiff1d, :145,
-    :168; the ranks' ID sets are disjoint), except the entered IDs of a halo without a
-    progenitor block, which keep loader order (:178), i.e. global current-row order."""
-    def cat(key, dt=None):
-        xs = [np.asarray(q[key]) for q in parts]
-        return np.concatenate(xs) if xs else np.zeros(0, dt)
 
-    def halo_of(key):
-        return np.concatenate([np.repeat(np.arange(nh), np.diff(q[key])) for q in parts]) \
-            if parts else np.zeros(0, np.int64)
+def _angles_dtype(coord, ids_dtype, p_has):
+    """Concatenation dtype of the reference's per-halo angle lists (:173-174, :183): a
+    halo with a progenitor block contributes arccos in the coordinate dtype, one
+    without an empty array of the IDs' dtype."""
+    parts = [np.zeros(0, np.dtype(coord))] * int(np.sum(p_has)) + \
+            [np.zeros(0, ids_dtype)] * int(np.sum(~np.asarray(p_has, bool)))
+    return np.concatenate(parts).dtype if parts else np.dtype(np.float64)
 
-    def counts(key):
-        return np.sum([np.diff(q[key]) for q in parts], axis=0) if parts else np.zeros(nh, np.int64)
 
-    def offsets(c):
-        return np.concatenate([[0], np.cumsum(c)]).astype(np.int64)
+# ------------------------------------------------------------------ multi-GPU
+def id_order_key(ids64, ids_dtype):
+    """int64 keys whose signed order is the IDs' numeric order (``ids64``: the IDs as
+    int64 -- sign-extended 32-bit values, 64-bit bit patterns)."""
+    dt = np.dtype(ids_dtype)
+    if dt.kind == 'u' and dt.itemsize == 8:
+        return ids64 ^ torch.tensor(np.iinfo(np.int64).min, dtype=torch.int64,
+                                    device=ids64.device)
+    if dt.kind == 'u':
+        return ids64 & 0xFFFFFFFF
+    return ids64
 
+
+def ids_to_host(ids64, ids_dtype):
+    """Device int64 IDs -> host array of the loader's dtype."""
+    dt = np.dtype(ids_dtype)
+    h = ids64.cpu().numpy()
+    if dt.itemsize == 8:
+        return h.view(dt)
+    return h.astype(dt)
+
+
+def _pinned_host(t):
+    """Device tensor -> host numpy through a page-locked block (one DMA)."""
+    if t.device.type == 'cpu':
+        return t.numpy()
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t)
+    return h.numpy()
+
+
+def _sort_pairs(h, key):
+    """Order of the rows by (h, key): a stable sort by key, then a stable one by h."""
+    o = torch.sort(key, stable=True)[1]
+    o2 = torch.sort(h[o], stable=True)[1]
+    return o[o2]
+
+
+def merge_onthefly(parts, nh, prev_starts, p_has, ids_dtype):
+    """Merge the ranks' on-the-fly records of one snapshot pair on the root rank
+    (ShardedOnTheFly), on whatever device the tensors are on.
+
+    ``parts``: the rank-ordered concatenation of every rank's rows:
+      * ``apsis`` (n, 2) int64: global previous row, ID;
+      * ``angle_g`` (n,) int64 global previous row, ``angle_v`` (n,) the angle change;
+      * ``departed`` (n, 2) int64: halo, ID;
+      * ``entered`` (n, 3) int64: halo, ID, global current row.
+    A halo's previous and current blocks tile their snapshots in halo order, so the
+    global previous row orders apsis records and angle changes exactly as the reference
+    emits them (previous-block order, halos in order, :154-174).  Departed and entered
+    IDs are per-halo sorted unique (setdiff1d, :145, :168), except the entered IDs of a
+    halo without a progenitor block, which keep loader order (:178), i.e. global
+    current-row order.  Returns host arrays (IDs in ``ids_dtype``)."""
+    ap = parts['apsis']
+    dev = ap.device
     out = {}
-    order = np.argsort(cat('apsis_gpos'), kind='stable')
-    out['apsis_ids'] = cat('apsis_ids')[order]
-    out['apsis_offsets'] = offsets(counts('apsis_offsets'))
-    out['angles'] = cat('angles')[np.argsort(cat('angle_gpos'), kind='stable')]
-    dep, dh = cat('departed_ids'), halo_of('departed_offsets')
-    out['departed_ids'] = dep[np.lexsort((dep, dh))]
-    out['departed_offsets'] = offsets(counts('departed_offsets'))
-    srt, sh = cat('srt'), halo_of('s_off')
-    srt = srt[np.lexsort((srt, sh))]
-    raw, rh = cat('raw'), halo_of('r_off')
-    raw = raw[np.lexsort((cat('raw_gpos'), rh))]
-    out['entered_ids'], out['entered_offsets'] = _interleave_halos(
-        parts[0]['p_has'], srt, offsets(counts('s_off')), raw, offsets(counts('r_off')))
+    order = torch.argsort(ap[:, 0])
+    ap = ap[order]
+    st = torch.from_numpy(np.asarray(prev_starts, dtype=np.int64)).to(dev)
+    halo = torch.searchsorted(st, ap[:, 0].contiguous(), right=True) - 1 if len(st) else ap[:, 0]
+    cnt = torch.bincount(halo, minlength=nh)[:nh] if ap.shape[0] else \
+        torch.zeros(nh, dtype=torch.int64, device=dev)
+    out['apsis_offsets'] = np.concatenate([[0], np.cumsum(cnt.cpu().numpy())]).astype(np.int64)
+    out['apsis_ids'] = ids_to_host(ap[:, 1], ids_dtype)
+    out['angles'] = _pinned_host(parts['angle_v'][torch.argsort(parts['angle_g'])])
+
+    def grouped(h, ids, second, uniq):
+        o = _sort_pairs(h, second)
+        h, ids, uniq = h[o], ids[o], uniq[o]
+        if h.numel() > 1:                     # setdiff1d is unique: drop repeats in a halo
+            dup = torch.zeros_like(h, dtype=torch.bool)
+            dup[1:] = (h[1:] == h[:-1]) & (ids[1:] == ids[:-1]) & uniq[1:]
+            h, ids = h[~dup], ids[~dup]
+        c = torch.bincount(h, minlength=nh)[:nh] if h.numel() else \
+            torch.zeros(nh, dtype=torch.int64, device=dev)
+        return ids_to_host(ids, ids_dtype), \
+            np.concatenate([[0], np.cumsum(c.cpu().numpy())]).astype(np.int64)
+
+    dp = parts['departed']
+    out['departed_ids'], out['departed_offsets'] = grouped(
+        dp[:, 0], dp[:, 1], id_order_key(dp[:, 1], ids_dtype),
+        torch.ones(dp.shape[0], dtype=torch.bool, device=dev))
+    en = parts['entered']
+    ph = torch.from_numpy(np.asarray(p_has, dtype=bool)).to(dev)
+    srt = ph[en[:, 0]] if en.shape[0] else torch.zeros(0, dtype=torch.bool, device=dev)
+    second = torch.where(srt, id_order_key(en[:, 1], ids_dtype), en[:, 2])
+    out['entered_ids'], out['entered_offsets'] = grouped(en[:, 0], en[:, 1], second, srt)
     return out
 
 
@@ -290,16 +360,26 @@ class ShardedOnTheFly:
     """The on-the-fly driver over ID-range shards (BASELINE configs[4]):
     one process per GPU, ``torch.distributed`` (RCCL, or gloo in the tests).
 
-    Every rank receives both snapshots from the loader (the reference's contract),
-    keeps the particles of its ID range (``IdRangeOwner``, fitted on the first
-    snapshot it sees) and runs the on-the-fly pipeline on them; a particle's rows in
-    the two snapshots are on the same rank, so the join has no exchange.  Bulk
-    velocities are whole-block sums: halo j's is computed by rank j % world on the
-    full block and the rows are all-gathered.  The outputs -- small next to the
-    snapshots -- are all-gathered with their global rows and merged
-    (``merge_onthefly``) into exactly the single-process file; rank 0 writes it.
+    Each snapshot reaches the ranks as the reference's loader returns it (the whole
+    snapshot, host or device arrays) and is sharded as ``ShardedEngine`` shards it
+    (``sharding.stripe_shard``): rank r moves only its block-aligned stripe to its GPU,
+    computes the bulk velocities of the stripe's blocks there (whole blocks, the
+    reference's sums; the rows are all-gathered), and routes the stripe's rows to their
+    owners with one all-to-all.  A particle's rows in the two snapshots are then on
+    the same rank, so the join has no exchange.  A caller that already holds each
+    rank's stripe on the device (``stripes``: a double-buffered reader, as
+    ``tools/bench_onthefly.py --sharded``) skips the upload.
+
+    The outputs stay on the devices: every rank's records -- apsis (global previous
+    row, ID), angle changes (global previous row, value), departed (halo, ID), entered
+    (halo, ID, global current row) -- are gathered to rank 0, the only writer, and
+    merged there with device sorts (``merge_onthefly``) into exactly the
+    single-process file.  Ranks other than 0 return the per-halo tables with empty
+    record arrays.
 
     ``track_orbits(..., engine=ShardedOnTheFly(OrbitEngine(mode=...)))``."""
+
+    ROOT = 0
 
     def __init__(self, engine, group=None, owner=None):
         from .sharding import IdRangeOwner
@@ -310,29 +390,47 @@ class ShardedOnTheFly:
         engine.emit_positions = True
         self.otf = OnTheFly(engine)
         self.carry = None
+        self.h2d_bytes = 0
 
     @property
     def rank(self):
         import torch.distributed as dist
         return dist.get_rank(self.group)
 
+    @property
+    def world(self):
+        import torch.distributed as dist
+        return dist.get_world_size(self.group)
+
     def agree(self, flag):
         """True on every rank iff ``flag`` is true on every rank (a carry is used only
         when all ranks hold one, so their collectives stay in step)."""
-        import torch.distributed as dist
-        got = [None] * dist.get_world_size(self.group)
-        dist.all_gather_object(got, bool(flag), group=self.group)
-        return all(got)
+        from .sharding import all_true
+        return all_true(flag, self.group)
+
+    def shard(self, snap, sl):
+        """This rank's shard of one snapshot (``sharding.stripe_shard``) and its local
+        slices (absent halos (-1, -1))."""
+        from .sharding import stripe_shard
+        sl = np.asarray(sl, dtype=np.int64).reshape(-1, 2)
+        ids = snap['ids']
+        n = int(ids.numel()) if isinstance(ids, torch.Tensor) else len(ids)
+        eng = self.eng
+        sh = stripe_shard(snap, _block_starts(sl, n), self.owner, self.group, eng.device,
+                          bulk_fn=eng.block_bulk)
+        st = np.concatenate([[0], np.cumsum(sh.counts)[:-1]]).astype(np.int64)
+        lsl = np.where(sl[:, :1] >= 0, np.stack([st, st + sh.counts], axis=1), -1)
+        self.h2d_bytes += sh.h2d_bytes
+        return sh, lsl
 
     def run(self, snaps, slices, centres, carried=None):
         """``carried``: this object's ``carry`` from the previous call, whose current
         snapshot is this call's previous one (``snaps[1]`` is then None): the rank's
         shard of it, its device frame state and its bulk velocities are reused."""
-        import torch.distributed as dist
-        from .sharding import shard_snapshot
-        world, rank = dist.get_world_size(self.group), dist.get_rank(self.group)
+        from .sharding import gather_rows
         eng = self.eng
-        self.owner.fit(np.asarray(snaps[0]['ids']))
+        if carried is None:
+            self.owner.reset()                # a fresh pair: fit the ID ranges on it
         shards, lslices, sels, bulks = [], [], [], []
         otf_carry = None
         if carried is not None:
@@ -344,44 +442,62 @@ class ShardedOnTheFly:
                 sels.append(sel_prev)
                 bulks.append(None)
                 continue
-            sl = np.asarray(sl, dtype=np.int64).reshape(-1, 2)
-            n = len(snap['ids'])
-            nh = len(sl)
-            full = dict(snap)
-            full['region_offsets'] = _block_starts(sl, n)
-            mine = np.arange(rank, nh, world)
-            rows = eng.block_bulk(full, mine) if len(mine) else None
-            got = [None] * world
-            dist.all_gather_object(got, (mine, rows), group=self.group)
-            bulk = None
-            for idx, r in got:
-                if r is not None:
-                    if bulk is None:
-                        bulk = np.zeros((nh, 3), dtype=r.dtype)
-                    bulk[idx] = r
-            keep = self.owner(np.asarray(snap['ids']), world) == rank
-            sh, sel, st, cnt = shard_snapshot(full, keep)
-            lsl = np.where(sl[:, :1] >= 0, np.stack([st, st + cnt], axis=1), -1)
-            shards.append(sh)
+            sh, lsl = self.shard(snap, sl)
+            shards.append(sh.snap)
             lslices.append(lsl)
-            sels.append(sel)
-            bulks.append(bulk if bulk is not None else np.zeros((0, 3)))
-        out = self.otf.run(shards, lslices, centres, carried=otf_carry, bulks=bulks,
-                           merge_parts=True)
+            sels.append(sh.sel)
+            bulks.append(sh.bulk)
+        d = self.otf.compare(shards, lslices, centres, carried=otf_carry, bulks=bulks)
         self.carry = (self.otf.carry, sels[0])
-        q = out.pop('parts')
-        mine = dict(apsis_offsets=out['apsis_offsets'], apsis_ids=out['apsis_ids'],
-                    apsis_gpos=sels[1][q['apsis_pos']],
-                    angles=out['angles'], angle_gpos=sels[1][q['angle_pos']],
-                    departed_offsets=out['departed_offsets'], departed_ids=out['departed_ids'],
-                    srt=q['srt'], s_off=q['s_off'], raw=q['raw'], r_off=q['r_off'],
-                    raw_gpos=sels[0][q['raw_pos']], p_has=q['p_has'])
-        allp = [None] * world
-        dist.all_gather_object(allp, mine, group=self.group)
-        merged = merge_onthefly(allp, len(slices[0]))
-        out.update(merged)
-        out['angles'] = out['angles'].astype(mine['angles'].dtype, copy=False)
-        return out
+        pc, prev, res = d.pc, d.prev, d.res
+        nh = len(slices[0])
+        ids_dtype = np.dtype(pc.plan.ids) if snaps[0] is None else np_dtype(snaps[0]['ids'])
+        sel_c, sel_p = sels[0].to(eng.device), sels[1].to(eng.device)
+        # this rank's records, each with its global row (device)
+        total = int(res.offsets[-1]) if res.offsets is not None and res.offsets.numel() else 0
+        a_ids = _i64(res.apsis_ids[:total])
+        apsis = torch.stack([sel_p[res.apsis_pos[:total].long()], a_ids], dim=1)
+        mrow = torch.nonzero(d.matched_prev).squeeze(1)
+        angle_g, angle_v = sel_p[mrow], d.angle_out[mrow]
+        drow = torch.nonzero(~d.matched_prev).squeeze(1)
+        departed = torch.stack([_halo_of(drow, prev.starts, eng.device),
+                                _i64(prev.ids[drow])], dim=1)
+        erow = torch.nonzero(~d.matched_cur).squeeze(1)
+        entered = torch.stack([_halo_of(erow, pc.starts, eng.device),
+                               _i64(pc.snap['ids'][erow]), sel_c[erow]], dim=1)
+        apsis, = gather_rows(self.group, self.ROOT, apsis)
+        angle_g, angle_v = gather_rows(self.group, self.ROOT, angle_g, angle_v)
+        departed, = gather_rows(self.group, self.ROOT, departed)
+        entered, = gather_rows(self.group, self.ROOT, entered)
+        sl1 = np.asarray(slices[1], dtype=np.int64).reshape(-1, 2)
+        p_has = (sl1[:, 1] - sl1[:, 0]) > 0            # the reference's np.diff(sl_prev) > 0
+        adt = _angles_dtype(pc.plan.coord, ids_dtype, p_has)
+        if self.rank == self.ROOT:
+            n_prev = int(np.max(sl1[:, 1])) if len(sl1) else 0
+            merged = merge_onthefly(dict(apsis=apsis, angle_g=angle_g, angle_v=angle_v,
+                                         departed=departed, entered=entered), nh,
+                                    _block_starts(sl1, max(n_prev, 0)), p_has, ids_dtype)
+            merged['angles'] = merged['angles'].astype(adt, copy=False)
+        else:
+            z = np.zeros(nh + 1, np.int64)
+            merged = {'apsis_offsets': z, 'apsis_ids': np.zeros(0, ids_dtype),
+                      'angles': np.zeros(0, adt), 'entered_offsets': z,
+                      'entered_ids': np.zeros(0, ids_dtype), 'departed_offsets': z,
+                      'departed_ids': np.zeros(0, ids_dtype)}
+        merged['bulk_velocities'] = [d.bulk_c, d.bulk_p]
+        return merged
+
+
+def _i64(t):
+    return t if t.dtype == torch.int64 else t.to(torch.int64)
+
+
+def _halo_of(rows, starts, device):
+    """Block of each row (blocks tile their snapshot in halo order)."""
+    st = torch.from_numpy(np.asarray(starts, dtype=np.int64)).to(device)
+    if not len(st):
+        return rows
+    return torch.searchsorted(st, rows, right=True) - 1
 
 
 # Frame state of the last call's current snapshot, keyed by the loader callable

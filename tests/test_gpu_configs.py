@@ -2,19 +2,27 @@
 
 configs[2]: 1e8 particles in 1e4 halos, float32, every halo on the packed k_step path.
 configs[1]: 1e7 particles in 1e2 halos, float64, every halo (1e5 particles) on the
-large-halo path (k_big_frame / k_big_join).  Three snapshots each, device-generated
-(synthetic_device.DevicePlummer), run through OrbitEngine (the path track_orbits uses).
+partitioned large-halo path (k_part_scatter / k_part_join / k_part_emit).  Three
+snapshots each, device-generated (synthetic_device.DevicePlummer), run through
+OrbitEngine (the path track_orbits uses).
 
 At full size the checks are size-independent properties (reference semantics,
 track_orbits.py:199-227, 300-351):
   * offsets non-decreasing from 0 to the record count;
   * every apsis ID is in its halo's previous block, once, in previous-block order;
   * an apsis particle's new angle is 0 (calc_angles resets it, :346);
-  * the packed plan and a forced all-global plan give identical outputs;
-plus oracle parity on a halo sample (the oracle's per-halo path on the same arrays).
+  * a second run on another kernel path gives identical outputs: configs[2] with
+    every halo forced onto the large-halo path (tiny LDS items), configs[1] with the
+    large halos on the per-halo global tables (k_big_frame / k_big_join,
+    ``part_large = False``) instead of the partitions;
+plus oracle parity on a halo sample (the oracle's per-halo path on the same arrays):
+apsis IDs and per-halo offsets bit-exact, f16 apsis angles within one ulp with at most
+ANGLE_MISMATCH_MAX of them off.
 """
 import numpy as np
 import pytest
+
+from test_gpu_parity import mismatch_ok
 
 pytestmark = pytest.mark.gpu
 
@@ -71,18 +79,29 @@ def _oracle_sample(gen, s, H, n_halos, got, mode='pericentric'):
     from oracle import orbit_oracle as O
     prv, cur = gen_host(gen, s - 1, n_halos), gen_host(gen, s, n_halos)
     cp, cc = gen.catalogue(s - 1), gen.catalogue(s)
-    ang = np.zeros(prv['n'], np.float16)          # snapshot s-1 = 1 is the first compare
-    want = []
+    ang = np.zeros(prv['n'], np.float16)          # snapshot s-1 = 0: angles start at 0
+    want, want_ang, lens = [], [], []
     for j in range(n_halos):
         pb, cb = prv['off'], cur['off']
         rp, vp, _ = O.region_frame(prv, (pb[j], pb[j + 1]), cp[0][j], cp[2][j], H)
         rc, vc, _ = O.region_frame(cur, (cb[j], cb[j + 1]), cc[0][j], cc[2][j], H)
         d = O.compare_radial_velocities(cur['ids'][cb[j]:cb[j + 1]], prv['ids'][pb[j]:pb[j + 1]],
                                         vc, vp, rc, rp, mode)
-        O.calc_angles(cb[j + 1] - cb[j], ang[pb[j]:pb[j + 1]], d)
+        _, aang = O.calc_angles(cb[j + 1] - cb[j], ang[pb[j]:pb[j + 1]], d)
         want.append(d['apsis_ids'])
+        want_ang.append(aang)
+        lens.append(len(d['apsis_ids']))
     want = np.concatenate(want)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    assert np.array_equal(got['offs'][:n_halos + 1], offs), 'per-halo offsets'
     assert np.array_equal(got['ids'][:got['offs'][n_halos]], want)
+    a = got['ang'][:got['offs'][n_halos]].astype(np.float64)
+    b = np.concatenate(want_ang).astype(np.float64)
+    same = (a == b) | (np.isnan(a) & np.isnan(b))
+    ulp = np.spacing(np.maximum(np.abs(a), np.abs(b)).astype(np.float16)).astype(np.float64)
+    assert np.all(same | (np.abs(a - b) <= ulp)), 'apsis angle off by more than 1 f16 ulp'
+    assert mismatch_ok(int((~same).sum()), a.size), (int((~same).sum()), a.size)
+    return a.size
 
 
 _HOST = {}
@@ -121,16 +140,44 @@ def test_baseline_config_full_size(cfg):
         return snap
     gen.snapshot = keep
     eng = OrbitEngine()
+    first = []
+    orig1 = eng.prepare
+
+    def prepare1(*a, **k):
+        pr = orig1(*a, **k)
+        if pr.compare:
+            first.append((pr.n_small, pr.n_global, pr.part))
+        return pr
+    eng.prepare = prepare1
     packed, last, H = _run(gen, steps, eng)
-    if cfg == 'configs2':
-        assert eng._ws is not None
+    if cfg == 'configs2':                         # every halo packed into k_step items
+        assert first and all(ng == 0 for _, ng, _ in first), first
+    else:                                         # every halo partitioned
+        assert first and all(ns == 0 and ng > 0 and part for ns, ng, part in first), first
     for s in range(1, steps):
         _check_properties(gen, _HOST[(id(gen), s - 1)], _HOST[(id(gen), s)], packed[s - 1])
-    _oracle_sample(gen, 1, H, sample, packed[0])
-    # the same snapshots with every halo on the global-table path
+    assert _oracle_sample(gen, 1, H, sample, packed[0]) > 0
+    # the same snapshots through another kernel path
     gen2 = DevicePlummer(seed=3, **kw)
-    eng2 = OrbitEngine(lds_entries=64)
+    if cfg == 'configs2':
+        eng2 = OrbitEngine(lds_entries=64)        # every halo a large halo
+    else:
+        eng2 = OrbitEngine()                      # large halos on the global tables
+        eng2.part_large = False
+    seen = []
+    orig2 = eng2.prepare
+
+    def prepare2(*a, **k):
+        pr = orig2(*a, **k)
+        if pr.compare:
+            seen.append((pr.n_small, pr.n_global, pr.part))
+        return pr
+    eng2.prepare = prepare2
     glob, _, _ = _run(gen2, steps, eng2)
+    # the second run really took the other path (and the first one the partitions)
+    assert seen and all(ns == 0 and ng > 0 for ns, ng, _ in seen), seen
+    if cfg == 'configs1':
+        assert not any(part for _, _, part in seen), seen
     for a, b in zip(packed, glob):
         for k in ('offs', 'ids', 'ang'):
             assert np.array_equal(a[k].view(np.uint8), b[k].view(np.uint8)), k

@@ -1,0 +1,219 @@
+"""BASELINE.json's multi-GPU configurations at their workload on the product paths
+(needs a GPU; the ranks share it and talk over gloo).
+
+* configs[4] -- the track_orbits_onthefly stream, 1e9 particles over 8 GPUs: one rank's
+  share (1.25e8 f32 particles, 12,500 halos) through ``ShardedOnTheFly`` at world 1,
+  three chained calls with the frame state carried, checked by size-independent
+  properties, against the oracle on a halo sample, and bit for bit against the
+  single-GPU on-the-fly path.
+* configs[3] -- 1e8 particles in total sharded by ID range: two ranks run
+  ``ShardedEngine`` over 1e4 halos, three snapshots, with the reference's whole-snapshot
+  loader (stripes + all-to-all) and with a presharded loader; rank 0's savefile
+  (groups and checkpoint) equals a single-process ``OrbitEngine`` run's bit for bit
+  (track_orbits.py:189-194 is the reference's parallel axis).
+"""
+import json
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from device_universe import DeviceUniverse, rank_major, digest
+from test_sharding import _free_port
+
+pytestmark = pytest.mark.gpu
+
+
+def _keys(snap, nh):
+    """(halo << 40 | ID) of every row of a device snapshot, and each row's halo."""
+    import torch
+    dev = snap['ids'].device
+    off = np.append(snap['region_offsets'], snap['ids'].numel())
+    h = torch.repeat_interleave(torch.arange(nh, device=dev), torch.from_numpy(np.diff(off)).to(dev))
+    return (h << 40) | snap['ids'], h
+
+
+def _member(sorted_keys, q):
+    import torch
+    if not sorted_keys.numel():
+        return torch.zeros_like(q, dtype=torch.bool)
+    k = torch.searchsorted(sorted_keys, q).clamp_(max=sorted_keys.numel() - 1)
+    return sorted_keys[k] == q
+
+
+def check_apsis_in_prev_blocks(prev_snap, nh, offs, ids):
+    """Apsis IDs: offsets from 0 to the record count, every ID in its halo's previous
+    block once, in that block's order (track_orbits.py:300-316)."""
+    import torch
+    assert offs[0] == 0 and np.all(np.diff(offs) >= 0) and offs[-1] == len(ids)
+    pkey, _ = _keys(prev_snap, nh)
+    srt, perm = torch.sort(pkey)
+    dev = pkey.device
+    ah = torch.repeat_interleave(torch.arange(nh, device=dev), torch.from_numpy(np.diff(offs)).to(dev))
+    akey = (ah << 40) | torch.from_numpy(np.asarray(ids, np.int64)).to(dev)
+    assert bool(_member(srt, akey).all()), 'apsis ID not in its previous block'
+    pos = perm[torch.searchsorted(srt, akey)]
+    same = ah[1:] == ah[:-1]
+    assert bool((pos[1:] > pos[:-1])[same].all()), 'apsis IDs out of previous-block order'
+    return akey
+
+
+def check_onthefly_properties(prev_snap, cur_snap, nh, data, tag='pericenter'):
+    """Size-independent properties of one on-the-fly file (track_orbits_onthefly.py:
+    123-205): apsis IDs in previous-block order and matched; one angle change per
+    matched particle; per halo, departed = previous minus current and entered =
+    current minus previous, each sorted and unique."""
+    import torch
+    pkey, ph = _keys(prev_snap, nh)
+    ckey, ch = _keys(cur_snap, nh)
+    psrt, csrt = torch.sort(pkey)[0], torch.sort(ckey)[0]
+    matched_p = _member(csrt, pkey)
+    n_match = torch.bincount(ph[matched_p], minlength=nh).cpu().numpy()
+    akey = check_apsis_in_prev_blocks(prev_snap, nh, data[tag + '_offsets'], data[tag + '_IDs'])
+    assert bool(_member(csrt, akey).all()), 'apsis particle not in the current block'
+    assert len(data['angles']) == int(n_match.sum())
+    p_cnt = np.diff(np.append(prev_snap['region_offsets'], prev_snap['ids'].numel()))
+    c_cnt = np.diff(np.append(cur_snap['region_offsets'], cur_snap['ids'].numel()))
+    dev = pkey.device
+    for name, own, other, cnt in (('departed', psrt, csrt, p_cnt), ('entered', csrt, psrt, c_cnt)):
+        off, ids = data[name + '_offsets'], np.asarray(data[name + '_IDs'], np.int64)
+        assert np.array_equal(np.diff(off), cnt - n_match), name
+        h = torch.repeat_interleave(torch.arange(nh, device=dev), torch.from_numpy(np.diff(off)).to(dev))
+        key = (h << 40) | torch.from_numpy(ids).to(dev)
+        assert bool(_member(own, key).all()) and not bool(_member(other, key).any()), name
+        assert bool((key[1:] > key[:-1]).all()), name + ' not sorted unique per halo'
+
+
+def test_configs4_onthefly_rank_share_world1():
+    """configs[4] at one GPU's share through the sharded on-the-fly driver (world 1):
+    1.25e8 f32 particles in 12,500 halos, calls s = 1, 2, 3 with the carry on (each
+    snapshot loaded once)."""
+    import torch
+    import torch.distributed as dist
+    from oracle import orbit_oracle as O
+    from orbitanalysis_amd import track_orbits_onthefly as T
+    from orbitanalysis_amd.engine import OrbitEngine
+    from orbitanalysis_amd.savefile import MemorySavefile
+    dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d' % _free_port(),
+                            rank=0, world_size=1)
+    try:
+        T.clear_carry()
+        nh = 12500
+        u = DeviceUniverse(4, n_halos=nh, n_particles=125_000_000, seed=9, dtype='float32')
+        links = np.tile(np.arange(nh), (2, 1))
+        eng = T.ShardedOnTheFly(OrbitEngine(mode='pericentric'))
+        out = MemorySavefile()
+        for s in (1, 2, 3):
+            T.track_orbits(s, links, u.regions_otf, u.load_snapshot_data, out, verbose=False,
+                           engine=eng)
+            data = out.files[s][0]
+            assert data['angles'].dtype == np.float32
+            check_onthefly_properties(u.snaps[s - 1], u.snaps[s], nh, data)
+        assert u.loads == [1, 0, 2, 3], u.loads            # s - 1 carried, not reloaded
+        got = out.files[3][0]
+        # the oracle on the first 40 halos of the pair (2, 3)
+        k = 40
+        hs = {s: u.host_blocks(s, k) for s in (2, 3)}
+        want = O.onthefly_track_orbits(3, np.tile(np.arange(k), (2, 1)),
+                                       lambda s, ids: (u.cats[s][0][ids], u.cats[s][1][ids]),
+                                       lambda s, p, r: hs[s], mode='pericentric')
+        for name in ('pericenter', 'entered', 'departed'):
+            o = want[name + '_offsets']
+            assert np.array_equal(got[name + '_offsets'][:k + 1], o), name
+            assert np.array_equal(got[name + '_IDs'][:o[-1]], want[name + '_IDs']), name
+        w = want['angles']
+        v = got['angles'][:len(w)]
+        nan = np.isnan(w)
+        assert np.array_equal(np.isnan(v), nan)
+        ulp = np.spacing(np.abs(w[~nan]).astype(np.float32)).astype(np.float64)
+        assert np.all(np.abs(v[~nan].astype(np.float64) - w[~nan]) <= 2 * ulp)
+        for a, b in zip(got['bulk_velocities'], want['bulk_velocities']):
+            assert np.array_equal(a[:k], b), 'bulk velocities'
+        # the single-GPU on-the-fly path on the same pair: the same file bit for bit
+        T.clear_carry()
+        single = MemorySavefile()
+        T.track_orbits(3, links, u.regions_otf, u.load_snapshot_data, single, verbose=False)
+        ref = single.files[3][0]
+        assert sorted(ref) == sorted(got)
+        for key in ref:
+            a, b = np.asarray(got[key]), np.asarray(ref[key])
+            assert a.dtype == b.dtype and a.shape == b.shape, key
+            assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), key
+    finally:
+        T.clear_carry()
+        dist.destroy_process_group()
+
+
+def _universe(contract, rank, world):
+    if contract == 'whole':          # every rank generates (is handed) the whole snapshot
+        return DeviceUniverse(3, n_halos=10000, n_particles=100_000_000, seed=13,
+                              dtype='float32')
+    return DeviceUniverse(3, n_halos=10000, n_particles=100_000_000 // world, seed=13,
+                          rank=rank, world=world, dtype='float32')
+
+
+def _cfg3_worker(rank, world, port, contract, outdir):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from orbitanalysis_amd.engine import OrbitEngine
+        from orbitanalysis_amd.savefile import MemorySavefile
+        from orbitanalysis_amd.sharding import ShardedEngine, EngineLocal
+        from orbitanalysis_amd.track_orbits import track_orbits
+        u = _universe(contract, rank, world)
+        eng = ShardedEngine(EngineLocal(OrbitEngine(mode='pericentric')),
+                            presharded=contract == 'presharded')
+        out = MemorySavefile()
+        track_orbits(u.snapshot_numbers, u.main_branches(), u.regions, u.load_snapshot_data,
+                     out, verbose=False, engine=eng, checkpoint=True)
+        if rank == 0:
+            d = digest(out.groups)
+            d['checkpoint'] = digest({'c': {'a': out.checkpoint}})['c/a']
+            with open(os.path.join(outdir, 'digest.json'), 'w') as f:
+                json.dump(d, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize('contract', ['whole', 'presharded'])
+def test_configs3_sharded_engine_world2(contract):
+    """configs[3]: 1e8 particles in total over two ranks (ID ranges), 1e4 halos, f32,
+    three snapshots; rank 0's savefile equals the single-process run's."""
+    import torch
+    from orbitanalysis_amd.engine import OrbitEngine
+    from orbitanalysis_amd.savefile import MemorySavefile
+    from orbitanalysis_amd.track_orbits import track_orbits
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_cfg3_worker, args=(world, _free_port(), contract, d), nprocs=world,
+                           join=True, start_method='spawn')
+        with open(os.path.join(d, 'digest.json')) as f:
+            got = json.load(f)
+    # the single-process reference on the global snapshots
+    if contract == 'whole':
+        u = _universe('whole', 0, 1)
+    else:
+        us = [_universe('presharded', r, world) for r in range(world)]
+        u = us[0]
+        u.snaps = [rank_major([x.snaps[s] for x in us]) for s in range(3)]
+        del us
+    want = MemorySavefile()
+    track_orbits(u.snapshot_numbers, u.main_branches(), u.regions, u.load_snapshot_data,
+                 want, verbose=False, engine=OrbitEngine(mode='pericentric'), checkpoint=True)
+    wd = digest(want.groups)
+    wd['checkpoint'] = digest({'c': {'a': want.checkpoint}})['c/a']
+    assert sorted(got) == sorted(wd)
+    bad = [k for k in wd if got[k] != wd[k]]
+    assert not bad, bad
+    for s in (1, 2):
+        g = want.groups['snapshot_%03d' % s]
+        assert len(g['pericenter_IDs']) > 1e6
+        check_apsis_in_prev_blocks(u.snaps[s - 1], u.n_halos, g['region_offsets'],
+                                   g['pericenter_IDs'])
+    torch.cuda.empty_cache()

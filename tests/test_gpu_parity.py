@@ -15,8 +15,16 @@ BATCH = ['g1_config1', 'g2_overlap_birth_massarray', 'g3_apo_periodic',
          'g4_hubble_catalogue', 'g5_fp32_centre32', 'g5_fp32_centre64',
          'g5_fp32_catalogue32', 'g8_many_small_halos', 'g11_edges']
 
-ANGLE_MISMATCH_MAX = 0.01      # fraction of apsis angles allowed to differ by 1 f16 ulp
+# fraction of f16 angles allowed to differ by 1 f16 ulp, rounded up to whole angles
+# (observed over the whole suite: 5 of 509,958, ~1e-5; profiles/r02/angle_mismatch_r02t.json)
+ANGLE_MISMATCH_MAX = 1e-4
 from golden_util import ANGLE_TALLY   # noqa: E402  (session total, printed by conftest)
+
+
+def mismatch_ok(mismatch, total):
+    """At most ANGLE_MISMATCH_MAX of ``total`` angles off by one ulp (ceil: a test with
+    fewer than 1e4 angles may have one)."""
+    return mismatch <= int(np.ceil(ANGLE_MISMATCH_MAX * max(total, 1)))
 
 
 def compare_groups(got, want, report):
@@ -62,10 +70,10 @@ def test_driver_matches_reference_golden(name):
     if 'checkpoint/angles' in fix.files:
         c, w = out.checkpoint, fix['checkpoint/angles']
         assert c.dtype == w.dtype and c.shape == w.shape
-        frac = float(np.mean((c != w) & ~(np.isnan(c) & np.isnan(w))))
-        assert frac < ANGLE_MISMATCH_MAX, frac
+        bad = int(np.sum((c != w) & ~(np.isnan(c) & np.isnan(w))))
+        assert mismatch_ok(bad, c.size), (bad, c.size)
     if rep.get('angles'):
-        assert rep['angle_mismatch'] / rep['angles'] < ANGLE_MISMATCH_MAX, rep
+        assert mismatch_ok(rep['angle_mismatch'], rep['angles']), rep
     print(name, rep)
 
 
@@ -184,7 +192,7 @@ def test_random_cases_match_oracle(kw, mode):
     rep = {}
     compare_groups(run_driver(u, dict(mode=mode)).groups, _oracle_run(u, mode), rep)
     assert rep['angles'] > 0
-    assert rep['angle_mismatch'] / rep['angles'] < ANGLE_MISMATCH_MAX, rep
+    assert mismatch_ok(rep['angle_mismatch'], rep['angles']), rep
 
 
 @pytest.mark.parametrize('name,owner', [('g2_overlap_birth_massarray', 'hash'),
@@ -197,7 +205,7 @@ def test_sharded_hip_engine_matches_reference(name, owner):
     got = run_sharded(name, 2, owner, local='hip')
     rep = {}
     compare_groups(_groups(got), groups(fix), rep)
-    assert rep.get('angle_mismatch', 0) <= ANGLE_MISMATCH_MAX * max(rep.get('angles', 1), 1)
+    assert mismatch_ok(rep.get('angle_mismatch', 0), rep.get('angles', 0)), rep
 
 
 def test_sharded_hip_engine_matches_single_gpu():

@@ -210,10 +210,10 @@ def test_onthefly_carry_key_and_switch(monkeypatch):
     assert T._CARRY == {}
 
 
-def test_plan_items_slots_and_speed():
-    """The host planner (C++) fills slot0 like set_item_slots and plans 1e4 halos in
-    well under a millisecond (the Python loop it replaced took ~43 ms)."""
-    import time
+def test_plan_items_slots():
+    """The host planner (C++) fills slot0 like set_item_slots (its speed, ~0.5 ms per
+    1e4 halos against ~43 ms for the Python loop it replaced, is measured by
+    tools/bench_e2e.py, not asserted here: a wall-clock bound flakes on loaded hosts)."""
     from orbitanalysis_amd.engine import plan_items, set_item_slots
     rng = np.random.default_rng(1)
     nh = 10000
@@ -225,10 +225,6 @@ def test_plan_items_slots_and_speed():
     want = items.copy()
     set_item_slots(want, out_slot)
     assert np.array_equal(items['slot0'], want['slot0'])
-    t0 = time.perf_counter()
-    for _ in range(20):
-        plan_items(cur, prev, 11776, 32, out_slot=out_slot)
-    assert (time.perf_counter() - t0) / 20 < 2e-3
 
 
 def test_checkpoint_angles_length_checked():

@@ -14,57 +14,70 @@ from golden_util import load, universe
 from test_sharding import _free_port
 
 
-def test_merge_onthefly_restores_single_rank_order():
-    from orbitanalysis_amd.track_orbits_onthefly import merge_onthefly, _interleave_halos
+@pytest.mark.parametrize('ids_dtype', [np.int64, np.uint64, np.uint32])
+def test_merge_onthefly_restores_single_rank_order(ids_dtype):
+    """The root's merge of every rank's records (rank-major concatenation of each
+    rank's rows, each rank's rows in its own order) restores the single-process
+    order: apsis records and angle changes by global previous row; departed and
+    entered IDs sorted unique per halo (unsigned IDs in unsigned order, repeats
+    dropped), except a halo without a progenitor block, whose entered IDs keep
+    global current-row order."""
+    import torch
+    from orbitanalysis_amd.track_orbits_onthefly import merge_onthefly, id_order_key
     rng = np.random.default_rng(3)
     nh, world = 7, 3
-    cnt = rng.integers(0, 40, nh)
-    cnt[2] = 0
-    off = np.concatenate([[0], np.cumsum(cnt)])
-    n = int(off[-1])
-    # apsis records / angle changes: global previous rows, increasing
-    gpos = np.sort(rng.choice(10 * n + 1, n, replace=False))
-    ids = rng.permutation(10 ** 6)[:n].astype(np.int64)
-    ang = rng.random(n).astype(np.float32)
-    # departed: per-halo sorted unique IDs
-    dep = np.concatenate([np.sort(ids[off[j]:off[j + 1]]) for j in range(nh)])
-    # entered: halos with a progenitor sorted, the others in loader (row) order
-    p_has = rng.random(nh) < 0.6
-    srt = np.concatenate([np.sort(ids[off[j]:off[j + 1]]) if p_has[j] else [] for j in range(nh)]).astype(np.int64)
-    s_cnt = np.where(p_has, cnt, 0)
-    raw = np.concatenate([ids[off[j]:off[j + 1]] if not p_has[j] else [] for j in range(nh)]).astype(np.int64)
-    r_cnt = np.where(p_has, 0, cnt)
-    raw_g = np.concatenate([gpos[off[j]:off[j + 1]] if not p_has[j] else [] for j in range(nh)]).astype(np.int64)
-    owner = rng.integers(0, world, n)                  # the rank of each particle
-    o = lambda c: np.concatenate([[0], np.cumsum(c)])  # noqa: E731
-    s_own = np.concatenate([owner[off[j]:off[j + 1]] for j in range(nh) if p_has[j]] or [np.zeros(0, int)])
-    r_own = np.concatenate([owner[off[j]:off[j + 1]] for j in range(nh) if not p_has[j]] or [np.zeros(0, int)])
-    parts = []
-    for r in range(world):
-        m = owner == r
-        h = np.repeat(np.arange(nh), cnt)
-        c = np.bincount(h[m], minlength=nh)
-        # departed of rank r: its own IDs of each halo, sorted
-        dsel = np.concatenate([np.sort(ids[off[j]:off[j + 1]][m[off[j]:off[j + 1]]]) for j in range(nh)]).astype(np.int64)
-        ss = s_own == r
-        rs = r_own == r
-        sh = np.repeat(np.arange(nh), s_cnt)
-        rh = np.repeat(np.arange(nh), r_cnt)
-        sv = np.concatenate([np.sort(srt[sh == j][ss[sh == j]]) for j in range(nh)]).astype(np.int64)
-        parts.append(dict(apsis_offsets=o(c), apsis_ids=ids[m], apsis_gpos=gpos[m],
-                          angles=ang[m], angle_gpos=gpos[m],
-                          departed_offsets=o(c), departed_ids=dsel,
-                          srt=sv, s_off=o(np.bincount(sh[ss], minlength=nh)),
-                          raw=raw[rs], r_off=o(np.bincount(rh[rs], minlength=nh)),
-                          raw_gpos=raw_g[rs], p_has=p_has))
-    got = merge_onthefly(parts, nh)
-    assert np.array_equal(got['apsis_offsets'], off)
-    assert np.array_equal(got['apsis_ids'], ids)
-    assert np.array_equal(got['angles'], ang)
-    assert np.array_equal(got['departed_ids'], dep) and np.array_equal(got['departed_offsets'], off)
-    want_e, want_off = _interleave_halos(p_has, srt, o(s_cnt), raw, o(r_cnt))
-    assert np.array_equal(got['entered_ids'], want_e)
-    assert np.array_equal(got['entered_offsets'], want_off)
+    dt = np.dtype(ids_dtype)
+    pcnt = rng.integers(0, 60, nh)
+    pcnt[2] = 0
+    p_has = pcnt > 0
+    pstart = np.concatenate([[0], np.cumsum(pcnt)[:-1]])
+    n_prev = int(pcnt.sum())
+    big = (1 << 63) + 5 if dt == np.uint64 else (1 << 31) + 5 if dt == np.uint32 else 1 << 40
+    pool = rng.permutation(10 ** 5)[:n_prev + 400].astype(dt) + dt.type(big)
+    i64 = lambda a: torch.from_numpy(np.asarray(a).astype(dt).view(np.int64) if dt.itemsize == 8  # noqa: E731
+                                     else np.asarray(a).astype(np.int64))
+    # apsis / angles: a subset of previous rows
+    arow = np.sort(rng.choice(n_prev, n_prev // 3, replace=False))
+    mrow = np.sort(rng.choice(n_prev, n_prev // 2, replace=False))
+    aval = rng.random(len(mrow)).astype(np.float32)
+    # departed: per-halo IDs in any order (one duplicate row to drop)
+    dh = np.repeat(np.arange(nh), rng.integers(0, 5, nh))
+    did = pool[n_prev:n_prev + len(dh)]
+    dh, did = np.append(dh, dh[:1]), np.append(did, did[:1])
+    # entered: halos with a progenitor sorted, the others in current-row order
+    eh = np.repeat(np.arange(nh), rng.integers(0, 6, nh))
+    eid = pool[n_prev + 100:n_prev + 100 + len(eh)]
+    eg = rng.permutation(10 ** 4)[:len(eh)].astype(np.int64)
+    owner = {k: rng.integers(0, world, len(v)) for k, v in
+             dict(a=arow, m=mrow, d=dh, e=eh).items()}
+
+    def rank_major(key, *cols):
+        o = np.argsort(owner[key], kind='stable')       # each rank keeps its own order
+        return [np.asarray(c)[o] for c in cols]
+    a_r, = rank_major('a', arow)
+    m_r, v_r = rank_major('m', mrow, aval)
+    d_h, d_i = rank_major('d', dh, did)
+    e_h, e_i, e_g = rank_major('e', eh, eid, eg)
+    parts = dict(apsis=torch.stack([torch.from_numpy(a_r), i64(pool[a_r])], 1),
+                 angle_g=torch.from_numpy(m_r), angle_v=torch.from_numpy(v_r),
+                 departed=torch.stack([torch.from_numpy(d_h), i64(d_i)], 1),
+                 entered=torch.stack([torch.from_numpy(e_h), i64(e_i), torch.from_numpy(e_g)], 1))
+    got = merge_onthefly(parts, nh, pstart, p_has, dt)
+    halo_of = np.repeat(np.arange(nh), pcnt)
+    assert np.array_equal(got['apsis_ids'], pool[arow]) and got['apsis_ids'].dtype == dt
+    assert np.array_equal(got['apsis_offsets'],
+                          np.concatenate([[0], np.cumsum(np.bincount(halo_of[arow], minlength=nh))]))
+    assert np.array_equal(got['angles'], aval)
+    want_d = [np.unique(did[dh == j]) for j in range(nh)]
+    assert np.array_equal(got['departed_ids'], np.concatenate(want_d))
+    assert np.array_equal(got['departed_offsets'], np.cumsum([0] + [len(x) for x in want_d]))
+    want_e = [np.unique(eid[eh == j]) if p_has[j] else eid[eh == j][np.argsort(eg[eh == j])]
+              for j in range(nh)]
+    assert np.array_equal(got['entered_ids'], np.concatenate(want_e).astype(dt))
+    assert np.array_equal(got['entered_offsets'], np.cumsum([0] + [len(x) for x in want_e]))
+    # the order key really is the unsigned order
+    k = id_order_key(i64(pool[:50]), dt)
+    assert np.array_equal(np.argsort(k.numpy(), kind='stable'), np.argsort(pool[:50], kind='stable'))
 
 
 def _worker(rank, world, port, name, mode, outdir):

@@ -85,8 +85,35 @@ def _worker(rank, world, port, name, owner, outdir, local='oracle'):
                 return _rank_major(u.load_snapshot_data(s, pos, rad), own, world, rank)
         track_orbits(u.snapshot_numbers, u.main_branches(), u.regions, loader,
                      out, verbose=False, engine=eng, **run)
+        layout = eng.checkpoint_layout()
+        if presharded and run.get('checkpoint'):
+            # a checkpoint in this rank-major layout resumes only in the same layout
+            # (ADVICE r02): another layout's tag is refused before any angle is read
+            s = u.snapshot_numbers[-1]
+            h = u.main_branches()[-1]
+            pos, rad, bulk = u.regions(s, h)
+            snap = loader(s, pos, rad)
+            n_global = len(u.load_snapshot_data(s, pos, rad)['ids'])
+            ang = np.zeros(n_global, np.float16)
+            ok = eng.prepare(snap, pos, bulk, 0.0, 0.0, np.arange(len(h)), False,
+                             angles_in=ang, angles_layout=layout)
+            assert ok.layout == layout
+            try:
+                eng.prepare(snap, pos, bulk, 0.0, 0.0, np.arange(len(h)), False, angles_in=ang,
+                            angles_layout=layout.replace('world=%d' % world, 'world=9'))
+                raise AssertionError('a checkpoint of another layout was accepted')
+            except ValueError:
+                pass
+            try:
+                eng.prepare(snap, pos, bulk, 0.0, 0.0, np.arange(len(h)), False,
+                            angles_in=ang[:-1], angles_layout=layout)
+                raise AssertionError('a short checkpoint was accepted')
+            except ValueError:
+                pass
         if rank == 0:
             flat = {'attr/mode': np.array(out.attrs['mode'])}
+            if out.checkpoint_layout is not None:
+                flat['checkpoint/layout'] = np.array(out.checkpoint_layout)
             for g, ds in out.groups.items():
                 for k, v in ds.items():
                     flat[g + '/' + k] = v
@@ -201,3 +228,35 @@ def test_presharded_checkpoint_is_global_rank_major():
     assert_groups_equal(_groups(got), want.groups)
     assert np.array_equal(got['checkpoint/angles'].view(np.uint16),
                           np.asarray(rec.checkpoint).view(np.uint16))
+    # the checkpoint records its row layout (world size + the ranks' block counts)
+    assert str(got['checkpoint/layout']).startswith('rank-major/world=2/blocks=')
+
+
+def test_checkpoint_layout_guard():
+    """Resuming a checkpoint in another row layout raises instead of silently
+    assigning each particle another particle's angle."""
+    from orbitanalysis_amd.sharding import check_layout
+    check_layout(None, None)
+    check_layout('rank-major/world=2/blocks=ab', 'rank-major/world=2/blocks=ab')
+    for want, have in (('rank-major/world=2/blocks=ab', None),
+                       (None, 'rank-major/world=2/blocks=ab'),
+                       ('rank-major/world=2/blocks=ab', 'rank-major/world=3/blocks=ab')):
+        with pytest.raises(ValueError):
+            check_layout(want, have)
+
+
+@pytest.mark.parametrize('world', [1, 2, 3, 8])
+def test_stripes_partition_rows_at_block_bounds(world):
+    from orbitanalysis_amd.sharding import stripe_halos, stripe_rows
+    rng = np.random.default_rng(world)
+    cnt = rng.integers(0, 500, 40)
+    cnt[5:9] = 0
+    starts = 7 + np.concatenate([[0], np.cumsum(cnt)[:-1]])
+    n = int(starts[-1] + cnt[-1])
+    hb = stripe_halos(starts, n, world)
+    assert hb[0] == 0 and hb[-1] == len(starts) and np.all(np.diff(hb) >= 0)
+    rows = [stripe_rows(starts, n, hb, r) for r in range(world)]
+    assert rows[0][0] == 7 and rows[-1][1] == n
+    assert all(rows[r][1] == rows[r + 1][0] for r in range(world - 1))
+    for lo, hi in rows:                              # balanced to within one block
+        assert abs((hi - lo) - (n - 7) / world) <= cnt.max()
