@@ -5,7 +5,8 @@ import glob
 import os
 import sys
 
-KEYS = ('k_step', 'k_big', 'k_part', 'k_gather', 'k_scan', 'k_bulk', 'fillBuffer')
+KEYS = ('k_step', 'k_big', 'k_part', 'k_gather', 'k_scan', 'k_bulk', 'k_central', 'k_mp', 'k_collate',
+        'k_retro', 'fillBuffer')
 for arg in sys.argv[1:]:
     files = [arg] if arg.endswith('.csv') else glob.glob(os.path.join(arg, '**', '*kernel_stats.csv'),
                                                           recursive=True)
