@@ -314,6 +314,35 @@ def _upload(a, device):
     return h.to(device, non_blocking=True)
 
 
+_PIN_GRAIN = 1 << 22
+
+
+def _pinned(n, dtype):
+    """A page-locked host tensor of n elements from torch's caching host allocator, the
+    block rounded up to 4 MiB: snapshots' record counts differ a little, and a block
+    that fits the next request is reused instead of page-locking a new one (that, not
+    the DMA, is what held the D2H of the records to ~20 GB/s)."""
+    itemsize = torch.empty(0, dtype=dtype).element_size()
+    nb = max(-(-int(n) * itemsize // _PIN_GRAIN) * _PIN_GRAIN, _PIN_GRAIN)
+    return torch.empty(nb // itemsize, dtype=dtype, pin_memory=True)[:n]
+
+
+class PendingFetch:
+    """Records on their way to the host (OrbitEngine.fetch_async)."""
+
+    def __init__(self, done, h_off, h_ids, h_ang, ids_dtype):
+        self.done, self.h_off, self.h_ids, self.h_ang = done, h_off, h_ids, h_ang
+        self.ids_dtype = ids_dtype
+
+    def wait(self):
+        self.done.synchronize()
+        offsets = self.h_off.numpy()
+        if self.h_ids is None:
+            return offsets, np.zeros(0, dtype=self.ids_dtype), np.zeros(0, dtype=np.float16)
+        return offsets, self.h_ids.numpy().view(self.ids_dtype), \
+            self.h_ang.numpy().view(np.float16)
+
+
 def meta_angles(meta):
     """float16 angles held in the low half of device meta words -> host array."""
     return (meta & 0xFFFF).cpu().numpy().astype(np.uint16).view(np.float16)
@@ -450,7 +479,11 @@ class OrbitEngine:
         for f64 in (False, True):
             self.table_sizes(f64)                   # validates the LDS budget
         self.prev: Optional[SnapshotState] = None
-        self._ws: Optional[Workspace] = None
+        # two compare-step workspaces, alternating between snapshots (step): a snapshot's
+        # records can still be on their way to the host (fetch_async) while the next
+        # snapshot's kernels write the other one
+        self._wss = [None, None]
+        self._wsi = 0
         # apsis records also carry their previous-state row (ShardedEngine's merge)
         self.emit_positions = False
         # large halos of compare steps: hash partitions joined in LDS (k_part_*);
@@ -477,15 +510,21 @@ class OrbitEngine:
     def entries(self):
         return self.table_sizes(False)[0]
 
+    @property
+    def _ws(self):
+        return self._wss[self._wsi]
+
     def workspace(self, pr):
-        """The engine's compare-step workspace, grown to fit ``pr``."""
-        if self._ws is None or not self._ws.fits(pr, self.emit_positions):
-            old = self._ws.cap if self._ws is not None else {}
+        """The engine's current compare-step workspace, grown to fit ``pr``."""
+        ws = self._wss[self._wsi]
+        if ws is None or not ws.fits(pr, self.emit_positions):
+            old = ws.cap if ws is not None else {}
             need = Workspace.need(pr)
             cap = {k: max(need[k], old.get(k, 0)) for k in need}
             dt = torch.int64 if pr.plan.ids.itemsize == 8 else torch.int32
-            self._ws = Workspace(self.device, dt, positions=self.emit_positions, **cap)
-        return self._ws
+            ws = self._wss[self._wsi] = Workspace(self.device, dt, positions=self.emit_positions,
+                                                  **cap)
+        return ws
 
     def reset(self):
         self.prev = None
@@ -560,6 +599,8 @@ class OrbitEngine:
         self.prev = SnapshotState(ids=snap['ids'], rhat=prep.rhat, meta=prep.meta,
                                   starts=prep.starts,
                                   counts=prep.counts, exists=exists, plan=prep.plan)
+        if compare:
+            self._wsi ^= 1                  # the next snapshot writes the other workspace
         return res
 
     def prepare(self, snap, centres, bulk_cat, H, z, exists, compare, angles_in=None,
@@ -725,6 +766,36 @@ class OrbitEngine:
         return res
 
     # ------------------------------------------------------------------ host views
+    def fetch_async(self, res, ids_dtype):
+        """Start the D2H of a compare step's records on the engine's copy stream and
+        return a ``PendingFetch`` whose ``wait()`` gives (offsets, ids, angles) as
+        ``fetch`` does.  The copies overlap whatever the compute stream runs next (the
+        next snapshot's kernels write the other workspace), so the records' transfer is
+        off the per-snapshot critical path.  The result's workspace must not be reused
+        before ``wait()``: ``step`` alternates two."""
+        dev = self.device
+        if getattr(self, '_copy_stream', None) is None:
+            self._copy_stream = torch.cuda.Stream(device=dev)
+        cs = self._copy_stream
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        n = res.n_slots + 1
+        # the record count (a 16-byte read; the status read already synchronised)
+        total = int(res.total.item()) if res.n_slots else 0
+        with torch.cuda.stream(cs):
+            cs.wait_event(ev)
+            h_off = _pinned(n, torch.int64)
+            h_off.copy_(res.offsets[:n], non_blocking=True)
+            h_ids = h_ang = None
+            if total:
+                h_ids = _pinned(total, res.apsis_ids.dtype)
+                h_ang = _pinned(total, torch.int16)
+                h_ids.copy_(res.apsis_ids[:total], non_blocking=True)
+                h_ang.copy_(res.apsis_ang[:total], non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(cs)
+        return PendingFetch(done, h_off, h_ids, h_ang, np.dtype(ids_dtype))
+
     def fetch(self, res, ids_dtype):
         """Device results -> host arrays in the reference's dtypes.
 
@@ -737,8 +808,8 @@ class OrbitEngine:
         if not total:
             return offsets, np.zeros(0, dtype=ids_dtype), np.zeros(0, dtype=np.float16)
         ids_t = res.apsis_ids[:total]
-        h_ids = torch.empty(total, dtype=ids_t.dtype, pin_memory=True)
-        h_ang = torch.empty(total, dtype=torch.int16, pin_memory=True)
+        h_ids = _pinned(total, ids_t.dtype)
+        h_ang = _pinned(total, torch.int16)
         h_ids.copy_(ids_t, non_blocking=True)
         h_ang.copy_(res.apsis_ang[:total], non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()

@@ -67,85 +67,120 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
 
     istart, started = 0, False
     progen_exists = None
-    for i, (halo_ids, snapshot_number) in enumerate(zip(main_branches, snapshot_numbers)):
+    # a compare step's records come back while the next snapshot is loaded, planned
+    # and run (engine.fetch_async): its group is written at the next iteration, or
+    # after the loop.  Engines without it (sharded: a collective gather) fetch inline.
+    pipelined = hasattr(eng, 'fetch_async')
+    pending = None
 
-        if verbose:
-            print('-' * 30, '\n')
-            print('Snapshot {}\n'.format('%03d' % snapshot_number))
+    def flush():
+        nonlocal pending
+        if pending is not None:
+            fetched, args, kw = pending
+            pending = None
+            offsets, ids, angles = fetched.wait()
+            save_to_file(out, ids, offsets, angles, *args, **kw)
 
-        halo_exists = np.argwhere(halo_ids != -1).flatten()
-        if len(halo_exists) == 0:
-            if started is False:
-                istart = i + 1
-            continue
-        halo_ids_ = halo_ids[halo_exists]
+    try:
+        for i, (halo_ids, snapshot_number) in enumerate(zip(main_branches, snapshot_numbers)):
 
-        region_positions, region_radii, region_bulk_vels = regions(snapshot_number, halo_ids_)
-        snapshot = load_snapshot_data(snapshot_number, region_positions, region_radii)
-        if len(snapshot['coordinates']) == 0:
-            if started is False:
-                istart = i + 1
-            continue
-        started = True
-
-        if 'Omega_k' not in snapshot:
-            snapshot['Omega_k'] = 0
-        H = hubble_parameter(snapshot['redshift'], snapshot['H0'], snapshot['Omega_m'],
-                             snapshot['Omega_L'], snapshot['Omega_k'])
-
-        if i == 0 and not resume:
-            box_size = snapshot['box_size'] if 'box_size' in snapshot else None
-            out.initialize(mode, box_size)
             if verbose:
-                print('Savefile initialized\n')
+                print('-' * 30, '\n')
+                print('Snapshot {}\n'.format('%03d' % snapshot_number))
 
-        compare = i > istart
-        angles_in, step_kw = None, {}
-        if resume and not compare:
-            # the reference opens savefile + '.checkpoint' here (track_orbits.py:229-232)
-            angles_in = out.read_checkpoint()
-            if angles_in is None:
-                raise FileNotFoundError('resume: no checkpoint angles in the savefile '
-                                        '(run with checkpoint=True first)')
-            layout = read_checkpoint_layout(out)
-            if layout is not None:
-                step_kw['angles_layout'] = layout
-        # apsis IDs are the previous snapshot's IDs (ids_prev_[apsis_inds], :315-316):
-        # they keep that snapshot's dtype
-        ids_dtype_prev = eng.prev.plan.ids if compare else None
+            halo_exists = np.argwhere(halo_ids != -1).flatten()
+            if len(halo_exists) == 0:
+                if started is False:
+                    istart = i + 1
+                continue
+            halo_ids_ = halo_ids[halo_exists]
 
-        if verbose:
-            t0 = time.time()
-        res = eng.step(snapshot, region_positions, region_bulk_vels, H, snapshot['redshift'],
-                       halo_exists, compare, angles_in=angles_in, **step_kw)
-        if compare:
-            apsis_offsets, apsis_ids, apsis_angles = eng.fetch(res, ids_dtype_prev)
-        if verbose:
-            print('Finished pericenter detection for snapshot {} in {} s\n'.format(
-                '%03d' % snapshot_number, time.time() - t0))
+            region_positions, region_radii, region_bulk_vels = regions(snapshot_number, halo_ids_)
+            snapshot = load_snapshot_data(snapshot_number, region_positions, region_radii)
+            if len(snapshot['coordinates']) == 0:
+                if started is False:
+                    istart = i + 1
+                continue
+            started = True
 
-        if compare:
-            if res.n_slots == 0:
+            if 'Omega_k' not in snapshot:
+                snapshot['Omega_k'] = 0
+            H = hubble_parameter(snapshot['redshift'], snapshot['H0'], snapshot['Omega_m'],
+                                 snapshot['Omega_L'], snapshot['Omega_k'])
+
+            if i == 0 and not resume:
+                box_size = snapshot['box_size'] if 'box_size' in snapshot else None
+                out.initialize(mode, box_size)
+                if verbose:
+                    print('Savefile initialized\n')
+
+            compare = i > istart
+            angles_in, step_kw = None, {}
+            if resume and not compare:
+                # the reference opens savefile + '.checkpoint' here (track_orbits.py:229-232)
+                angles_in = out.read_checkpoint()
+                if angles_in is None:
+                    raise FileNotFoundError('resume: no checkpoint angles in the savefile '
+                                            '(run with checkpoint=True first)')
+                layout = read_checkpoint_layout(out)
+                if layout is not None:
+                    step_kw['angles_layout'] = layout
+            # apsis IDs are the previous snapshot's IDs (ids_prev_[apsis_inds], :315-316):
+            # they keep that snapshot's dtype
+            ids_dtype_prev = eng.prev.plan.ids if compare else None
+
+            if verbose:
+                t0 = time.time()
+            res = eng.step(snapshot, region_positions, region_bulk_vels, H, snapshot['redshift'],
+                           halo_exists, compare, angles_in=angles_in, **step_kw)
+            # the previous snapshot's group: its records crossed PCIe during this step
+            flush()
+            if compare and res.n_slots == 0:
                 # the reference concatenates an empty list here (track_orbits.py:216)
                 raise ValueError('need at least one array to concatenate')
-            hinds = np.where(res.has_prog)[0]
-            if region_bulk_vels is None:
-                bulk = eng.bulk_velocities(res, eng.prev.plan)
-            else:
-                bulk = np.array([region_bulk_vels[j] for j in range(len(halo_exists))])
-            halo_ids_final = main_branches[-1][progen_exists] if \
-                snapshot_number != snapshot_numbers[-1] else None
-            save_to_file(out, apsis_ids, apsis_offsets, apsis_angles,
-                         region_positions[hinds], region_radii[hinds], bulk[hinds],
-                         halo_ids_[hinds], halo_ids_final, snapshot_number, mode,
-                         checkpoint, eng.angles() if checkpoint else None, verbose,
-                         layout=checkpoint_layout(eng) if checkpoint else None)
+            if compare:
+                fetched = eng.fetch_async(res, ids_dtype_prev) if pipelined else \
+                    _Fetched(eng.fetch(res, ids_dtype_prev))
+            if verbose:
+                if pipelined and compare:
+                    fetched.wait()
+                print('Finished pericenter detection for snapshot {} in {} s\n'.format(
+                    '%03d' % snapshot_number, time.time() - t0))
 
-        progen_exists = halo_exists
+            if compare:
+                hinds = np.where(res.has_prog)[0]
+                if region_bulk_vels is None:
+                    bulk = eng.bulk_velocities(res, eng.prev.plan)
+                else:
+                    bulk = np.array([region_bulk_vels[j] for j in range(len(halo_exists))])
+                halo_ids_final = main_branches[-1][progen_exists] if \
+                    snapshot_number != snapshot_numbers[-1] else None
+                # checkpoint angles now: the next step replaces the engine's state
+                pending = (fetched, (region_positions[hinds], region_radii[hinds], bulk[hinds],
+                                     halo_ids_[hinds], halo_ids_final, snapshot_number, mode,
+                                     checkpoint, eng.angles() if checkpoint else None, verbose),
+                           dict(layout=checkpoint_layout(eng) if checkpoint else None))
+                if not pipelined:
+                    flush()
+
+            progen_exists = halo_exists
+    finally:
+        # an error leaves no computed group unwritten (the reference wrote it already)
+        flush()
 
     if verbose:
         print('Finished pericenter detection for all snapshots in {} s\n'.format(
             time.time() - tstart))
+
+
+class _Fetched:
+    """An inline fetch's arrays behind the PendingFetch interface."""
+
+    def __init__(self, arrays):
+        self.arrays = arrays
+
+    def wait(self):
+        return self.arrays
 
 
 def checkpoint_layout(eng):
