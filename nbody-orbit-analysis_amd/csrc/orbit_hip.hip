@@ -187,6 +187,15 @@ __device__ __forceinline__ double acos_td(double x) { return acos(x); }
 // numpy's float32 arccos (SIMD) is not correctly rounded either: both differ from the
 // exact value by ~1 ulp; parity for float16 angles is checked to within 1 f16 ulp.
 __device__ __forceinline__ float acos_td(float x) { return acosf(x); }
+// The on-the-fly driver returns the angle changes themselves (track_orbits_onthefly.py:
+// 173-174): a float32 change is rounded from a float64 arccos, i.e. correctly rounded
+// (but for ~1e-8 of values), so it is within numpy's own float32 arccos error (<= 2 ulp,
+// measured) of the reference; acosf alone adds its error on top.  The batch path keeps
+// acosf: its changes only feed float16 sums.
+template <bool OTF, typename TD> __device__ __forceinline__ TD acos_change(TD x) {
+    if constexpr (OTF && sizeof(TD) == 4) return (float)acos((double)x);
+    else return acos_td(x);
+}
 
 __device__ __forceinline__ uint16_t f32_to_f16(float f) {
     _Float16 h = (_Float16)f;                     // v_cvt_f16_f32, round to nearest even
@@ -1124,7 +1133,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             const uint32_t c = p & (PK_HIT - 1u);
             // angle change = arccos(dot(r̂_prev, r̂_match)), no clamp (:324-325)
             const TD dt = dot3(prh[k].x, prh[k].y, prh[k].z, rcx[c], rcy[c], rcz[c]);
-            const TD change = acos_td(dt);
+            const TD change = acos_change<OTF>(dt);
             // calc_angles (:342-349): f16 + change, rounded once; reset at an apsis
             const uint16_t acc = angle_add((uint16_t)(p >> 16), change);
             flag = (p & PK_FLAG) != 0u;
@@ -1643,7 +1652,7 @@ __global__ __launch_bounds__(BIG_WG) void k_big_join(const oa_step_args a) {
                 flag = a.mode == OA_MODE_PERICENTRIC ? (sp == 2u && sc == 1u) : (sp == 1u && sc == 2u);
                 // arccos(dot(r̂_prev, r̂_match)) (:324-325), f16 + change (:342-351)
                 const TD dt = dot3(prh.x, prh.y, prh.z, cr[0], cr[1], cr[2]);
-                const TD change = acos_td(dt);
+                const TD change = acos_change<OTF>(dt);
                 const uint16_t acc = angle_add((uint16_t)(pmeta & 0xFFFFu), change);
                 a16 = acc;
                 a.meta_out[c] = (uint32_t)(flag ? 0u : acc) | (sc << 16);
