@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OA_ABI_VERSION 9
+#define OA_ABI_VERSION 10
 
 #define OA_OK 0
 #define OA_E_ARG (-1)       /* invalid argument / unsupported dtype plan */
@@ -161,16 +161,24 @@ typedef struct oa_step_args {
     int32_t *scratch_pos;
     /* Partitioned large halos (compare steps, not on-the-fly; n_parts = 0: the
      * global-table path above).  Each global item's IDs are cut into K hash partitions
-     * (partition = mulhi64(mix64(ID), K)) so one partition's current particles fit an
-     * LDS table of oa_build_info(4) entries:
-     *   k_part_scatter  frame of the current chunks (gchunk1) plus bucket appends of
-     *                   {ID, position | sign << 30}; bucket appends {ID, position, state
-     *                   word, r̂} of the previous chunks (gchunk2), whose apsis marks it
-     *                   clears
-     *   k_part_join     one work-group per plist row (LDS: oa_part_lds_bytes): LDS table of the current bucket,
-     *                   lookups of the previous bucket, state words and apsis marks
+     * (K a power of two, partition = mulhi64(mix64(ID), K)) so one partition's current
+     * particles fit an LDS table of oa_build_info(4) entries.  A *bucket set* holds one
+     * snapshot's state of those halos by partition: per entry the ID, the position in
+     * the halo's block (| sign(v_r) << 30 in a current set), the state word and r̂.
+     * The current set of one step is the previous set of the next (inherited), so the
+     * previous state is streamed from its buckets, never scattered again:
+     *   k_part_scatter  frame of the current chunks (gchunk1) into the current set
+     *                   (LDS-staged: each partition's entries leave as one run); the
+     *                   previous chunks (gchunk2) of halos without an inherited set
+     *                   into a fresh previous set, from the position-order state
+     *   k_part_join     one work-group per plist row (LDS: oa_part_lds_bytes): LDS table
+     *                   of a current bucket, lookups of the previous bucket(s) holding
+     *                   its IDs, the state word of every matched current entry, apsis
+     *                   marks at previous positions
      *   k_part_emit     previous chunks: marks -> records packed per 64-position
-     *                   segment (the layout k_big_join writes)                        */
+     *                   segment (the layout k_big_join writes)
+     * The position-order rhat_out / meta_out of these halos are NOT written
+     * (oa_part_unbucket restores them from the set when a caller needs them).      */
     int32_t n_parts;            /* rows of plist (padding rows included)              */
     int32_t part_kmax;          /* largest K of any global item                       */
     int32_t part_e;             /* current bucket capacity = LDS table entries of one
@@ -178,22 +186,55 @@ typedef struct oa_step_args {
     int32_t part_slots;         /* its cuckoo slots (part_e < slots <= 1.5 build max) */
     const int32_t *plist;       /* [n_parts] (global item g = item - n_items, partition)
                                    pairs; g = -1: an idle padding row                */
-    const int64_t *gpart;       /* per global item, 8 int64: current bucket base,
-                                   previous bucket base, K, previous bucket capacity,
-                                   first counter index, 0, 0, 0 (current buckets
-                                   hold part_e entries each)                         */
-    uint64_t *pkey_cur;         /* current buckets: IDs (zero-extended 4-byte IDs)    */
+    const int64_t *gpart;       /* per global item, oa_build_info(6) = 16 int64:
+                                   [0] current set base (entries; partition p at
+                                   base + p * part_e), [1] K, [2] index of its first
+                                   counter in pcnt, [3] previous set: 0 fresh (the
+                                   *_prev arrays, counters in pcnt), 1 inherited (the
+                                   i* arrays, counters in icnt), [4] previous set base,
+                                   [5] its K (a power of two), [6] its entries per
+                                   partition, [7] index of its first counter,
+                                   [8..15] 0                                          */
+    uint64_t *pkey_cur;         /* current set: IDs (zero-extended 4-byte IDs)        */
     uint32_t *ppos_cur;         /*   position in the halo's block | sign(v_r) << 30   */
-    uint64_t *pkey_prev;        /* previous buckets: IDs                              */
+    uint32_t *pmeta_cur;        /*   state word (f16 angle | sign << 16)              */
+    void *prh_cur;              /*   r̂ (3 values of the r̂ dtype)                      */
+    uint64_t *pkey_prev;        /* fresh previous set: IDs                            */
     uint32_t *ppos_prev;        /*   position in the halo's previous block            */
     uint32_t *pmeta_prev;       /*   its previous state word                          */
     void *prh_prev;             /*   its previous r̂ (3 values of the r̂ dtype)         */
-    uint32_t *pcnt;             /* [2 * sum K] bucket fill counters, zeroed by oa_step
-                                   (current K of an item, then its previous K)        */
+    const uint64_t *ikey;       /* inherited previous set (the previous step's current
+                                   set; any of these may be NULL when none is used)   */
+    const uint32_t *ipos;
+    const uint32_t *imeta;
+    const void *irh;
+    const uint32_t *icnt;       /*   its fill counters                                */
+    uint32_t *pcnt;             /* [n_pcnt] fill counters of the current set and of the
+                                   fresh previous set, zeroed by oa_step              */
+    int64_t n_pcnt;
     uint32_t *gmark;            /* apsis marks, one per padded previous position of
-                                   the global items: 0 or 1 << 16 | float16 angle     */
+                                   the global items: 0 or 1 << 16 | float16 angle;
+                                   zeroed by oa_step                                  */
     int64_t gmark_base;         /* scratch_off of the first global item (gmark[0])    */
+    int64_t gmark_n;            /* marks (padded previous positions of global items)  */
 } oa_step_args;
+
+/* Arguments of oa_part_unbucket: a bucket set's entries back to position order. */
+typedef struct oa_unbucket_args {
+    const uint32_t *bpos;       /* the set's position words (position | sign << 30)   */
+    const uint32_t *bmeta;      /* its state words                                    */
+    const void *brh;            /* its r̂ (3 values of the r̂ dtype per entry)          */
+    const uint32_t *bcnt;       /* its fill counters                                  */
+    const int64_t *rows;        /* per listed halo, 4 int64: set base, K, first counter
+                                   index, block offset of the halo in the state arrays */
+    const int32_t *plist;       /* [n_parts] (row, partition) pairs; row -1: padding   */
+    int32_t n_parts;
+    int32_t cap;                /* entries per partition of the set (part_e)          */
+    void *rhat_out;             /* the snapshot's position-order state arrays        */
+    uint32_t *meta_out;
+    int32_t td_f64;             /* r̂ dtype: 1 float64, 0 float32                      */
+    int32_t reserved;
+} oa_unbucket_args;
 
 /* Arguments of oa_compact: gather the per-item apsis records into the reference's
  * output layout (track_orbits.py:212-227 -> save_to_file :379-381). */
@@ -227,13 +268,14 @@ typedef struct oa_compact_args {
 int oa_abi_version(void);
 
 /* sizeof() of the ABI structs (0 oa_halo, 1 oa_item, 2 oa_step_args,
- * 3 oa_compact_args) so a binding can verify its layout; -1 otherwise. */
+ * 3 oa_compact_args, 4 oa_unbucket_args) so a binding can verify its layout; -1
+ * otherwise. */
 int64_t oa_struct_size(int32_t which);
 
 /* Compile-time configuration: 0 work-group size, 1 max halos per item,
  * 2 phase-1 unroll, 3 progenitor rows (64 positions) per wave of an item, 4 current
  * entries per large-halo partition (k_part_join's LDS table), 5 largest K per halo
- * (k_part_scatter's LDS counters); -1 otherwise. */
+ * (k_part_scatter's LDS counters), 6 int64 per gpart row; -1 otherwise. */
 int32_t oa_build_info(int32_t which);
 
 /* LDS bytes of one k_part_join work-group for a partition of `entries` current
@@ -292,6 +334,11 @@ int64_t oa_debug_part_stamps(int32_t which, uint64_t *host, int64_t n);
 
 /* Largest dynamic LDS allocation a work-group may use on this device (bytes). */
 int64_t oa_max_lds_bytes(void);
+
+/* Restore the position-order state (r̂, state word) of the listed halos from a bucket
+ * set (oa_step_args' partitioned large halos): for a checkpoint of the angles
+ * (track_orbits.py:390-394) or a next step that reads those halos in position order. */
+int oa_part_unbucket(const oa_unbucket_args *args, void *stream);
 
 /* Scan the per-halo / per-item apsis counts and gather the records in output order. */
 int oa_compact(const oa_compact_args *args, void *stream);

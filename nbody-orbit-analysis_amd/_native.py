@@ -13,7 +13,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.abspath(__file__))
 # ORBIT_HIP_LIB selects an alternative build (kernel variants for tuning sweeps)
 LIB_PATH = os.environ.get('ORBIT_HIP_LIB') or os.path.join(PKG, 'liborbit_hip.so')
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -47,10 +47,19 @@ class StepArgs(ctypes.Structure):
                 ('n_global_items', c_i32), ('n_gchunk1', c_i32), ('n_gchunk2', c_i32),
                 ('gchunk1', c_vp), ('gchunk2', c_vp), ('gtab', c_vp), ('gkeys', c_vp),
                 ('gvals', c_vp), ('gtab_total', c_i64), ('scratch_pos', c_vp),
-                ('n_parts', c_i32), ('part_kmax', c_i32), ('part_e', c_i32), ('part_slots', c_i32), ('plist', c_vp), ('gpart', c_vp),
-                ('pkey_cur', c_vp), ('ppos_cur', c_vp), ('pkey_prev', c_vp), ('ppos_prev', c_vp),
-                ('pmeta_prev', c_vp), ('prh_prev', c_vp),
-                ('pcnt', c_vp), ('gmark', c_vp), ('gmark_base', c_i64)]
+                ('n_parts', c_i32), ('part_kmax', c_i32), ('part_e', c_i32), ('part_slots', c_i32),
+                ('plist', c_vp), ('gpart', c_vp),
+                ('pkey_cur', c_vp), ('ppos_cur', c_vp), ('pmeta_cur', c_vp), ('prh_cur', c_vp),
+                ('pkey_prev', c_vp), ('ppos_prev', c_vp), ('pmeta_prev', c_vp), ('prh_prev', c_vp),
+                ('ikey', c_vp), ('ipos', c_vp), ('imeta', c_vp), ('irh', c_vp), ('icnt', c_vp),
+                ('pcnt', c_vp), ('n_pcnt', c_i64), ('gmark', c_vp), ('gmark_base', c_i64),
+                ('gmark_n', c_i64)]
+
+
+class UnbucketArgs(ctypes.Structure):
+    _fields_ = [('bpos', c_vp), ('bmeta', c_vp), ('brh', c_vp), ('bcnt', c_vp), ('rows', c_vp),
+                ('plist', c_vp), ('n_parts', c_i32), ('cap', c_i32), ('rhat_out', c_vp),
+                ('meta_out', c_vp), ('td_f64', c_i32), ('reserved', c_i32)]
 
 
 class CompactArgs(ctypes.Structure):
@@ -111,6 +120,7 @@ SYMBOLS = {
     'oa_debug_stamps': (c_i64, [c_vp, c_i64]),
     'oa_debug_part_stamps': (c_i64, [c_i32, c_vp, c_i64]),
     'oa_compact': (ctypes.c_int, [ctypes.POINTER(CompactArgs), c_vp]),
+    'oa_part_unbucket': (ctypes.c_int, [ctypes.POINTER(UnbucketArgs), c_vp]),
     'oa_match_workspace_bytes': (c_i64, [c_i64]),
     'oa_match_ids': (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp]),
     'oa_compare_pairs': (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,
@@ -156,7 +166,8 @@ def load(require_device=False):
             raise NativeUnavailable('liborbit_hip.so ABI %d != %d (stale build)'
                                     % (lib.oa_abi_version(), ABI_VERSION))
         sizes = {0: HALO_DTYPE.itemsize, 1: ITEM_DTYPE.itemsize,
-                 2: ctypes.sizeof(StepArgs), 3: ctypes.sizeof(CompactArgs)}
+                 2: ctypes.sizeof(StepArgs), 3: ctypes.sizeof(CompactArgs),
+                 4: ctypes.sizeof(UnbucketArgs)}
         for k, v in sizes.items():
             if lib.oa_struct_size(k) != v:
                 raise NativeUnavailable('ABI struct %d size mismatch: C %d, Python %d'

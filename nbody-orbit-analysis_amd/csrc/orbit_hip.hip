@@ -1707,27 +1707,63 @@ __global__ __launch_bounds__(BIG_WG) void k_big_join(const oa_step_args a) {
 //                   previous-block order (:315-316), packed per segment as k_big_join
 constexpr int PART_E = 4096;            // current entries of one partition, at most
 constexpr int PART_S = 6144;            // LDS table slots, at most
-// 512 threads, <= 128 VGPRs and ~74 KB of LDS: two join work-groups per CU, so one's
+// 512 threads, <= 128 VGPRs and ~58 KB of LDS: two join work-groups per CU, so one's
 // table build overlaps the other's streaming
-constexpr int PART_KMAX = 16384;        // partitions of one halo (scatter's LDS counters)
+constexpr int PART_KMAX = 4096;         // partitions of one halo (scatter's LDS counters)
 constexpr int PART_WG = 512;
+constexpr int GPART_W = 16;             // int64 per gpart row (orbit_hip.h)
 #ifndef OA_SCAT_PER
-#define OA_SCAT_PER 8       // k_part_scatter: particles per thread per sub-chunk (4: A/B r02 neutral)
+#define OA_SCAT_PER 4       // k_part_scatter: particles per thread per staged sub-chunk
 #endif
-constexpr int SCAT_WG = 256, SCAT_PER = OA_SCAT_PER;
+constexpr int SCAT_WG = 256, SCAT_PER = OA_SCAT_PER, SCAT_NS = SCAT_WG * SCAT_PER;
 static_assert(PART_E - 1 <= (int)MAX_POS, "partition entries must fit the slot position field");
+static_assert(PART_KMAX <= 65536, "staged partition numbers are 16-bit");
 
 // partition of an ID: the high bits of a 64-bit mix (the LDS table hashes the low
-// word with unrelated multipliers, so a partition's keys still spread over its table)
+// word with unrelated multipliers, so a partition's keys still spread over its table).
+// K is a power of two, so partition p of K is partitions [p*2^d, (p+1)*2^d) of K*2^d:
+// a bucket set built with one K serves a join with another.
 __device__ __forceinline__ uint32_t part_of(uint64_t id, uint32_t K) {
     return (uint32_t)__umul64hi(id_hash64(id ^ 0x2545F4914F6CDD1Dull), (uint64_t)K);
 }
 
-// CUR: current chunks (gchunk1), else previous chunks (gchunk2).  A previous bucket
-// entry carries the particle's whole previous state (ID, position, state word, r̂), so
-// the join streams it instead of gathering it.
+// LDS of one k_part_scatter work-group: per partition its sub-chunk count (scanned in
+// place into the run's first staged index) and reserved bucket index, then the staged
+// records {ID, r̂, position word, state word, partition} of one sub-chunk in partition
+// order, copied out as contiguous runs.
+__host__ __device__ inline int64_t scat_lds_bytes(int kmax, int td_bytes) {
+    const int64_t k = ((int64_t)kmax * 8 + 15) & ~int64_t(15);
+    return 64 + k + (int64_t)SCAT_NS * (8 + 3 * td_bytes + 4 + 4 + 2);
+}
+
+// exclusive scan of v[0, n) in place (n <= PART_KMAX), SCAT_WG threads, wtot[>= 4]
+__device__ __forceinline__ void block_scan_excl(uint32_t *v, uint32_t n, uint32_t *wtot) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t c = (n + SCAT_WG - 1) / SCAT_WG, b = tid * c;
+    uint32_t s = 0;
+    for (uint32_t i = 0; i < c; ++i) if (b + i < n) s += v[b + i];
+    uint32_t incl = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wtot[wave] = incl;
+    __syncthreads();
+    uint32_t run = incl - s;
+    for (int w = 0; w < wave; ++w) run += wtot[w];
+    for (uint32_t i = 0; i < c; ++i)
+        if (b + i < n) { const uint32_t x = v[b + i]; v[b + i] = run; run += x; }
+    __syncthreads();
+}
+
+// CUR: current chunks (gchunk1), else previous chunks (gchunk2).  A bucket entry holds
+// a particle's whole state -- ID, position in its block (| sign << 30 for current
+// entries), state word, r̂ -- so the join streams it and a current bucket set is the
+// next snapshot's previous one.  Previous chunks of halos whose previous state is
+// already such a set (gpart[3] = 1, inherited) are skipped.
 template <typename TX, typename TV, typename TD, int IDB, bool CUR>
-__device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK &fk, uint32_t *lcnt,
+__device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK &fk, char *lds,
                                              int64_t chunk) {
     typedef typename IdT<IDB>::T ID;
     const int64_t *ch = (CUR ? a.gchunk1 : a.gchunk2) + 3 * chunk;
@@ -1735,9 +1771,10 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
     const oa_item it = a.items[gi];
     const oa_halo &h = a.halos[it.h0];
     const int64_t gk = gi - a.n_items;
-    const int64_t *gp = a.gpart + 8 * gk;
-    const uint32_t K = (uint32_t)gp[2];
+    const int64_t *gp = a.gpart + GPART_W * gk;
+    const uint32_t K = (uint32_t)gp[1];
     const bool part = h.prev_cnt > 0 && K > 0;
+    if (!CUR && (!part || gp[3] != 0)) return;          // inherited previous set (uniform)
     const int tid = threadIdx.x;
     double cb[6];
     float cf[6];
@@ -1753,18 +1790,27 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
     TD *rhat_out = static_cast<TD *>(a.rhat_out);
     const TD *rhat_prev = static_cast<const TD *>(a.rhat_prev);
     const int64_t base = CUR ? h.cur_off : h.prev_off;
-    uint32_t *ctr = a.pcnt + gp[4] + (CUR ? 0 : K);
-    const uint32_t bcap = CUR ? (uint32_t)a.part_e : (uint32_t)gp[3];
-    const int64_t bb = CUR ? gp[0] : gp[1];
+    uint32_t *ctr = a.pcnt + (CUR ? gp[2] : gp[7]);
+    const uint32_t bcap = CUR ? (uint32_t)a.part_e : (uint32_t)gp[6];
+    const int64_t bb = CUR ? gp[0] : gp[4];
     uint64_t *bkey = (CUR ? a.pkey_cur : a.pkey_prev) + bb;
     uint32_t *bpos = (CUR ? a.ppos_cur : a.ppos_prev) + bb;
-    uint32_t *bmeta = a.pmeta_prev + bb;
-    TD *brh = static_cast<TD *>(a.prh_prev) + 3 * bb;
-    uint32_t *mark = a.gmark + (it.scratch_off - a.gmark_base);
-    for (int64_t s0 = start; s0 < start + cnt; s0 += SCAT_WG * SCAT_PER) {
-        const int64_t n0 = min(start + cnt - s0, (int64_t)SCAT_WG * SCAT_PER);
+    uint32_t *bmeta = (CUR ? a.pmeta_cur : a.pmeta_prev) + bb;
+    TD *brh = static_cast<TD *>(CUR ? a.prh_cur : a.prh_prev) + 3 * bb;
+    // LDS carve-up (scat_lds_bytes)
+    uint32_t *wtot = reinterpret_cast<uint32_t *>(lds);
+    uint32_t *lrun = wtot + 16;                         // [K] count -> first staged index
+    uint32_t *gres = lrun + K;                          // [K] reserved bucket index
+    char *stg = lds + 64 + (((int64_t)K * 8 + 15) & ~int64_t(15));
+    uint64_t *skey = reinterpret_cast<uint64_t *>(stg);
+    TD *srh = reinterpret_cast<TD *>(skey + SCAT_NS);
+    uint32_t *spw = reinterpret_cast<uint32_t *>(srh + 3 * SCAT_NS);
+    uint32_t *smeta = spw + SCAT_NS;
+    uint16_t *spart = reinterpret_cast<uint16_t *>(smeta + SCAT_NS);
+    for (int64_t s0 = start; s0 < start + cnt; s0 += SCAT_NS) {
+        const int64_t n0 = min(start + cnt - s0, (int64_t)SCAT_NS);
         if (part) {
-            for (uint32_t k = tid; k < K; k += SCAT_WG) lcnt[k] = 0u;
+            for (uint32_t k = tid; k < K; k += SCAT_WG) lrun[k] = 0u;
             __syncthreads();
         }
         uint64_t key[SCAT_PER];
@@ -1797,41 +1843,55 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
                 const V3<TV> v = ld3_nt(vs, i);
                 TD r[3];
                 const uint32_t sgn = frame<TX, TV, TD>(x, v, cb, cf, a, fk, r);
-                TD *ro = rhat_out + 3 * i;
-                ro[0] = r[0]; ro[1] = r[1]; ro[2] = r[2];
-                // angle 0: entered particles keep it (calc_angles :348-349), matched
-                // ones get theirs from k_part_join
-                a.meta_out[i] = sgn << 16;
+                if (!part) {
+                    // a halo without a progenitor: its state in position order (angle 0:
+                    // calc_angles :348-349), as k_big_frame writes it
+                    TD *ro = rhat_out + 3 * i;
+                    ro[0] = r[0]; ro[1] = r[1]; ro[2] = r[2];
+                    a.meta_out[i] = sgn << 16;
+                    continue;
+                }
+                rh[q] = V3<TD>{r[0], r[1], r[2]};
+                pm[q] = sgn << 16;                      // angle 0 until the join matches it
                 pw[q] = (uint32_t)p | (sgn << 30);
             } else {
-                mark[p] = 0u;
                 pw[q] = (uint32_t)p;
             }
-            if (part) {
-                const uint32_t pp = part_of(key[q], K);
-                pr[q] = (pp << 16) | atomicAdd(&lcnt[pp], 1u);
-            }
+            const uint32_t pp = part_of(key[q], K);
+            pr[q] = (pp << 16) | atomicAdd(&lrun[pp], 1u);
         }
         if (!part) continue;                            // uniform
         __syncthreads();
+        // this sub-chunk's range of every bucket (one device atomic per partition hit),
+        // then the runs' first staged indices
         for (uint32_t k = tid; k < K; k += SCAT_WG) {
-            const uint32_t c = lcnt[k];
-            if (c) lcnt[k] = atomicAdd(&ctr[k], c);     // this chunk's range of bucket k
+            const uint32_t c = lrun[k];
+            gres[k] = c ? atomicAdd(&ctr[k], c) : 0u;
         }
-        __syncthreads();
+        block_scan_excl(lrun, K, wtot);
 #pragma unroll
         for (int q = 0; q < SCAT_PER; ++q) {
             if (pr[q] == 0xFFFFFFFFu) continue;
-            const uint32_t pp = pr[q] >> 16, e = lcnt[pp] + (pr[q] & 0xFFFFu);
+            const uint32_t pp = pr[q] >> 16, e = lrun[pp] + (pr[q] & 0xFFFFu);
+            skey[e] = key[q];
+            srh[3 * e] = rh[q].x; srh[3 * e + 1] = rh[q].y; srh[3 * e + 2] = rh[q].z;
+            spw[e] = pw[q];
+            smeta[e] = pm[q];
+            spart[e] = (uint16_t)pp;
+        }
+        __syncthreads();
+        // copy-out: consecutive staged records of one partition go to consecutive bucket
+        // entries, so a wave's stores are a few contiguous runs, not 64 scattered words
+        for (int64_t s = tid; s < n0; s += SCAT_WG) {
+            const uint32_t k = spart[s];
+            const uint32_t e = gres[k] + (uint32_t)(s - lrun[k]);
             if (e < bcap) {                             // an overflow is reported by the join
-                const int64_t o = (int64_t)pp * bcap + e;
-                bkey[o] = key[q];
-                bpos[o] = pw[q];
-                if (!CUR) {
-                    bmeta[o] = pm[q];
-                    TD *d = brh + 3 * o;
-                    d[0] = rh[q].x; d[1] = rh[q].y; d[2] = rh[q].z;
-                }
+                const int64_t o = (int64_t)k * bcap + e;
+                __builtin_nontemporal_store(skey[s], &bkey[o]);
+                __builtin_nontemporal_store(spw[s], &bpos[o]);
+                __builtin_nontemporal_store(smeta[s], &bmeta[o]);
+                TD *d = brh + 3 * o;
+                d[0] = srh[3 * s]; d[1] = srh[3 * s + 1]; d[2] = srh[3 * s + 2];
             }
         }
         __syncthreads();
@@ -1842,16 +1902,8 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
 // even work-groups take current chunks, odd ones previous chunks, then the longer
 // list's remainder.
 template <typename TX, typename TV, typename TD, int IDB>
-#ifndef OA_SCAT_WPE
-#define OA_SCAT_WPE 0       // k_part_scatter: minimum waves per SIMD (0: none; 4 spills, A/B r02 +3-6 %)
-#endif
-#if OA_SCAT_WPE
-#define SCAT_ATTR __attribute__((amdgpu_waves_per_eu(OA_SCAT_WPE)))
-#else
-#define SCAT_ATTR
-#endif
-__global__ __launch_bounds__(SCAT_WG) SCAT_ATTR void k_part_scatter(const oa_step_args a, const FrameK fk) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lcnt[];   // [K]
+__global__ __launch_bounds__(SCAT_WG) void k_part_scatter(const oa_step_args a, const FrameK fk) {
+    extern __shared__ __attribute__((aligned(16))) char slds[];
     const int64_t b = blockIdx.x, n1 = a.n_gchunk1, n2 = a.n_gchunk2;
     const int64_t m = n1 < n2 ? n1 : n2;
     bool cur;
@@ -1859,16 +1911,21 @@ __global__ __launch_bounds__(SCAT_WG) SCAT_ATTR void k_part_scatter(const oa_ste
     if (b < 2 * m) { cur = (b & 1) == 0; c = b >> 1; }
     else { cur = n1 > n2; c = b - m; }
     SSTAMP(0);
-    if (cur) part_scatter<TX, TV, TD, IDB, true>(a, fk, lcnt, c);
-    else part_scatter<TX, TV, TD, IDB, false>(a, fk, lcnt, c);
+    if (cur) part_scatter<TX, TV, TD, IDB, true>(a, fk, slds, c);
+    else part_scatter<TX, TV, TD, IDB, false>(a, fk, slds, c);
     SSTAMP(1);
 }
 
 // LDS of one k_part_join work-group for a partition capacity of e entries, s slots
 __host__ __device__ inline int64_t part_lds_bytes(int e, int sl) {
-    return (int64_t)sl * 8 + (int64_t)(e / 4) * 8 + (int64_t)STASH * 8 + (int64_t)e * 4 + 16;
+    return (int64_t)sl * 8 + (int64_t)(e / 4) * 8 + (int64_t)STASH * 8 + 16;
 }
 
+// One work-group per current partition: LDS cuckoo table of its current bucket, then
+// every entry of the previous partitions that hold its IDs (one, several or a share of
+// one, as K and the previous set's K compare) looked up; a match gathers the current
+// r̂ from its bucket entry and writes that entry's state word; an apsis also marks the
+// previous position.
 template <typename TD, int IDB>
 __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     extern __shared__ __attribute__((aligned(16))) char psm[];
@@ -1876,28 +1933,35 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     uint64_t *slots = reinterpret_cast<uint64_t *>(psm);               // [PS]
     uint64_t *pend = slots + PS;                                        // [PE / 4]
     uint64_t *stash = pend + PE / 4;                                    // [STASH]
-    uint32_t *posl = reinterpret_cast<uint32_t *>(stash + STASH);       // [PE]
-    uint32_t *flags = posl + PE;       // npend, nstash, overflow, nonuniform
+    uint32_t *flags = reinterpret_cast<uint32_t *>(stash + STASH);      // npend, nstash, overflow, nonuniform
     const int tid = threadIdx.x;
     PSTAMP(0);
     const int32_t g = a.plist[2 * blockIdx.x], pp = a.plist[2 * blockIdx.x + 1];
     if (g < 0) return;                                  // padding row
     const oa_item it = a.items[a.n_items + g];
-    const oa_halo &h = a.halos[it.h0];
-    const int64_t *gp = a.gpart + 8 * (int64_t)g;
-    const uint32_t K = (uint32_t)gp[2], pcap = (uint32_t)gp[3];
-    const uint32_t nc = a.pcnt[gp[4] + pp], np = a.pcnt[gp[4] + K + pp];
-    if (nc > PE || np > pcap) {
+    const int64_t *gp = a.gpart + GPART_W * (int64_t)g;
+    const uint32_t K = (uint32_t)gp[1];
+    const int64_t cb = gp[0] + (int64_t)pp * PE;
+    const uint32_t nc = a.pcnt[gp[2] + pp];
+    const bool inh = gp[3] != 0;
+    const uint32_t Kp = (uint32_t)gp[5], pcap = (uint32_t)gp[6];
+    const uint32_t *qcnt = (inh ? a.icnt : a.pcnt) + gp[7];
+    const uint64_t *qk0 = (inh ? a.ikey : a.pkey_prev) + gp[4];
+    const uint32_t *qp0 = (inh ? a.ipos : a.ppos_prev) + gp[4];
+    const uint32_t *qm0 = (inh ? a.imeta : a.pmeta_prev) + gp[4];
+    const TD *qr0 = static_cast<const TD *>(inh ? a.irh : a.prh_prev) + 3 * gp[4];
+    // the previous partitions holding this partition's IDs: K and Kp are powers of two
+    const bool filt = Kp < K;
+    const uint32_t q0 = filt ? (uint32_t)pp / (K / Kp) : (uint32_t)pp * (Kp / K);
+    const uint32_t nq = filt ? 1u : Kp / K;
+    bool over = nc > PE;
+    for (uint32_t q = 0; q < nq; ++q) over |= qcnt[q0 + q] > pcap;
+    if (over) {
         if (tid == 0) atomicOr(a.status, OA_STATUS_PART_OVERFLOW);
         return;
     }
-    const uint64_t *ck = a.pkey_cur + gp[0] + (int64_t)pp * PE;
-    const uint32_t *cp = a.ppos_cur + gp[0] + (int64_t)pp * PE;
-    const int64_t qb = gp[1] + (int64_t)pp * pcap;
-    const uint64_t *qk = a.pkey_prev + qb;
-    const uint32_t *qp = a.ppos_prev + qb;
-    const uint32_t *qm = a.pmeta_prev + qb;
-    const TD *qr = static_cast<const TD *>(a.prh_prev) + 3 * qb;
+    const uint64_t *ck = a.pkey_cur + cb;
+    const uint32_t *cp = a.ppos_cur + cb;
     // Every load of the partition goes out first (both buckets are streamed once):
     // their HBM latency hides behind the table clear, the inserts and the walks.
     constexpr int CU = PART_E / PART_WG, PU = OA_PU;
@@ -1912,14 +1976,19 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     uint64_t qkey[PU];
     uint32_t qpos[PU], qmeta[PU];
     V3<TD> qrh[PU];
+    auto load_prev = [&](const uint64_t *qk, const uint32_t *qp, const uint32_t *qm, const TD *qr,
+                         uint32_t np, uint32_t j0) __attribute__((always_inline)) {
 #pragma unroll
-    for (int u = 0; u < PU; ++u) {
-        const uint32_t j = (uint32_t)u * PART_WG + tid;
-        qkey[u] = j < np ? qk[j] : 0ull;
-        qpos[u] = j < np ? qp[j] : 0u;
-        qmeta[u] = j < np ? qm[j] : 0u;
-        if (j < np) qrh[u] = ld3(qr, j);
-    }
+        for (int u = 0; u < PU; ++u) {
+            const uint32_t j = j0 + (uint32_t)u * PART_WG + tid;
+            qkey[u] = j < np ? qk[j] : 0ull;
+            qpos[u] = j < np ? qp[j] : 0u;
+            qmeta[u] = j < np ? qm[j] : 0u;
+            if (j < np) qrh[u] = ld3(qr, j);
+        }
+    };
+    load_prev(qk0 + (int64_t)q0 * pcap, qp0 + (int64_t)q0 * pcap, qm0 + (int64_t)q0 * pcap,
+              qr0 + 3 * (int64_t)q0 * pcap, qcnt[q0], 0u);
     uint32_t nsl = nc + nc / 2u + 64u;
     nsl = nsl < PS ? nsl : PS;
     for (uint32_t w = tid; w < nsl; w += PART_WG) slots[w] = 0ull;
@@ -1934,7 +2003,6 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
         const uint32_t i = (uint32_t)u * PART_WG + tid;
         if (i >= nc) continue;
         const uint64_t key = ckey[u];
-        posl[i] = cpw[u] & 0x3FFFFFFFu;
         if ((uint32_t)(key >> 32) != hi0) flags[3] = 1u;        // benign race: all write 1
         const uint64_t val = slot_pack((uint32_t)key, (cpw[u] >> 30) << 16, i);
         uint32_t cs[NCAND];
@@ -1987,65 +2055,86 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     }
     const bool nonuniform = IDB == 8 && flags[3] != 0u;
     const uint32_t nstash = min(flags[1], (uint32_t)STASH);
-    const TD *rhat_cur = static_cast<const TD *>(a.rhat_out);
+    const TD *crh0 = static_cast<const TD *>(a.prh_cur) + 3 * cb;
+    uint32_t *cmeta = a.pmeta_cur + cb;
     uint32_t *mark = a.gmark + (it.scratch_off - a.gmark_base);
-    // previous entries, PU per thread: lookups, then the gathers of the matched
-    // current r̂ (the halo's block, L2-resident: plist keeps a halo's partitions on one
-    // XCD), then the angle and state-word arithmetic
-    for (uint32_t j0 = 0; j0 < np; j0 += (uint32_t)PART_WG * PU) {
-        if (j0) {
+    // previous entries, PU per thread: lookups, then the gathers of the matched current
+    // r̂ (the partition's own bucket entries), then the angle and state-word arithmetic
+    for (uint32_t q = 0; q < nq; ++q) {
+        const int64_t qo = (int64_t)(q0 + q) * pcap;
+        const uint64_t *qk = qk0 + qo;
+        const uint32_t *qp = qp0 + qo, *qm = qm0 + qo;
+        const TD *qr = qr0 + 3 * qo;
+        const uint32_t np = qcnt[q0 + q];
+        for (uint32_t j0 = 0; j0 < np; j0 += (uint32_t)PART_WG * PU) {
+            if (j0 || q) load_prev(qk, qp, qm, qr, np, j0);
+            uint32_t hit[PU];
 #pragma unroll
             for (int u = 0; u < PU; ++u) {
+                hit[u] = 0xFFFFFFFFu;
                 const uint32_t j = j0 + (uint32_t)u * PART_WG + tid;
-                qkey[u] = j < np ? qk[j] : 0ull;
-                qpos[u] = j < np ? qp[j] : 0u;
-                qmeta[u] = j < np ? qm[j] : 0u;
-                if (j < np) qrh[u] = ld3(qr, j);
+                const uint32_t lo = (uint32_t)qkey[u];
+                if (j >= np || (IDB == 8 && !nonuniform && (uint32_t)(qkey[u] >> 32) != hi0)) continue;
+                if (filt && part_of(qkey[u], K) != (uint32_t)pp) continue;
+                uint32_t cs[NCAND];
+                cuckoo_slots(lo, nsl, cs);
+                uint64_t m = 0ull;
+#pragma unroll
+                for (int c = 0; c < NCAND; ++c) {
+                    const uint64_t v = slots[cs[c]];
+                    if (!m && v && (uint32_t)v == lo && slot_pos(v) < nc &&
+                        (!nonuniform || ck[slot_pos(v)] == qkey[u]))
+                        m = v;
+                }
+                for (uint32_t e = 0; !m && e < nstash; ++e) {
+                    const uint64_t v = stash[e];
+                    if ((uint32_t)v == lo && (!nonuniform || ck[slot_pos(v)] == qkey[u])) m = v;
+                }
+                if (m) hit[u] = slot_pos(m) | ((slot_meta(m) >> 16) << 30);
             }
-        }
-        uint32_t hit[PU];
+            V3<TD> crh[PU];
 #pragma unroll
-        for (int u = 0; u < PU; ++u) {
-            hit[u] = 0xFFFFFFFFu;
-            const uint32_t j = j0 + (uint32_t)u * PART_WG + tid;
-            const uint32_t lo = (uint32_t)qkey[u];
-            if (j >= np || (IDB == 8 && !nonuniform && (uint32_t)(qkey[u] >> 32) != hi0)) continue;
-            uint32_t cs[NCAND];
-            cuckoo_slots(lo, nsl, cs);
-            uint64_t m = 0ull;
+            for (int u = 0; u < PU; ++u)
+                if (hit[u] != 0xFFFFFFFFu) crh[u] = ld3(crh0, hit[u] & 0x3FFFFFFFu);
 #pragma unroll
-            for (int q = 0; q < NCAND; ++q) {
-                const uint64_t v = slots[cs[q]];
-                if (!m && v && (uint32_t)v == lo && slot_pos(v) < nc &&
-                    (!nonuniform || ck[slot_pos(v)] == qkey[u]))
-                    m = v;
+            for (int u = 0; u < PU; ++u) {
+                if (hit[u] == 0xFFFFFFFFu) continue;
+                const uint32_t sc = hit[u] >> 30, sp = qmeta[u] >> 16;
+                // strict sign test (:311-314), arccos of the r̂ dot product (:324-325),
+                // f16 + change rounded once, reset at an apsis (:342-349)
+                const bool flag = a.mode == OA_MODE_PERICENTRIC ? (sp == 2u && sc == 1u)
+                                                                : (sp == 1u && sc == 2u);
+                const TD dt = dot3(qrh[u].x, qrh[u].y, qrh[u].z, crh[u].x, crh[u].y, crh[u].z);
+                const uint16_t acc = angle_add((uint16_t)(qmeta[u] & 0xFFFFu), acos_td(dt));
+                cmeta[hit[u] & 0x3FFFFFFFu] = (uint32_t)(flag ? 0u : acc) | (sc << 16);
+                if (flag) mark[qpos[u]] = 0x10000u | acc;
             }
-            for (uint32_t e = 0; !m && e < nstash; ++e) {
-                const uint64_t v = stash[e];
-                if ((uint32_t)v == lo && (!nonuniform || ck[slot_pos(v)] == qkey[u])) m = v;
-            }
-            if (m) hit[u] = posl[slot_pos(m)] | ((slot_meta(m) >> 16) << 30);
+            if (j0 == 0 && q == 0) PSTAMP(4);
         }
-        V3<TD> crh[PU];
-#pragma unroll
-        for (int u = 0; u < PU; ++u)
-            if (hit[u] != 0xFFFFFFFFu) crh[u] = ld3(rhat_cur, h.cur_off + (hit[u] & 0x3FFFFFFFu));
-#pragma unroll
-        for (int u = 0; u < PU; ++u) {
-            if (hit[u] == 0xFFFFFFFFu) continue;
-            const uint32_t sc = hit[u] >> 30, sp = qmeta[u] >> 16;
-            // strict sign test (:311-314), arccos of the r̂ dot product (:324-325),
-            // f16 + change rounded once, reset at an apsis (:342-349)
-            const bool flag = a.mode == OA_MODE_PERICENTRIC ? (sp == 2u && sc == 1u)
-                                                            : (sp == 1u && sc == 2u);
-            const TD dt = dot3(qrh[u].x, qrh[u].y, qrh[u].z, crh[u].x, crh[u].y, crh[u].z);
-            const uint16_t acc = angle_add((uint16_t)(qmeta[u] & 0xFFFFu), acos_td(dt));
-            a.meta_out[h.cur_off + (hit[u] & 0x3FFFFFFFu)] = (uint32_t)(flag ? 0u : acc) | (sc << 16);
-            if (flag) mark[qpos[u]] = 0x10000u | acc;
-        }
-        if (j0 == 0) PSTAMP(4);
     }
     PSTAMP(5);
+}
+
+// A bucket set back to position order (the state arrays of the snapshot it holds):
+// one work-group per (halo row, partition) of plist; rows: base, K, counter index,
+// block offset per halo.
+template <typename TD>
+__global__ __launch_bounds__(256) void k_part_unbucket(const oa_unbucket_args a) {
+    const int32_t r = a.plist[2 * blockIdx.x], p = a.plist[2 * blockIdx.x + 1];
+    if (r < 0) return;
+    const int64_t *rw = a.rows + 4 * (int64_t)r;
+    const uint32_t cap = (uint32_t)a.cap;
+    uint32_t n = a.bcnt[rw[2] + p];
+    n = n < cap ? n : cap;
+    const int64_t o0 = rw[0] + (int64_t)p * cap, dst0 = rw[3];
+    const TD *brh = static_cast<const TD *>(a.brh);
+    TD *rh = static_cast<TD *>(a.rhat_out);
+    for (uint32_t e = threadIdx.x; e < n; e += 256) {
+        const int64_t o = o0 + e;
+        const int64_t d = dst0 + (a.bpos[o] & 0x3FFFFFFFu);
+        a.meta_out[d] = a.bmeta[o];
+        rh[3 * d] = brh[3 * o]; rh[3 * d + 1] = brh[3 * o + 1]; rh[3 * d + 2] = brh[3 * o + 2];
+    }
 }
 
 template <int IDB>
@@ -2110,11 +2199,12 @@ __global__ __launch_bounds__(BIG_WG) void k_part_emit(const oa_step_args a) {
 
 template <typename TX, typename TV, typename TD, int IDB>
 int launch_part(const oa_step_args &a, hipStream_t st) {
-    if (hipMemsetAsync(a.pcnt, 0, (size_t)a.n_parts * 8, st) != hipSuccess)
-        return fail(OA_E_LAUNCH, "oa_step: partition counters reset");
-    const int64_t lds = ((int64_t)a.part_kmax * 4 + 15) & ~int64_t(15);
+    if (hipMemsetAsync(a.pcnt, 0, (size_t)a.n_pcnt * 4, st) != hipSuccess ||
+        (a.gmark_n > 0 && hipMemsetAsync(a.gmark, 0, (size_t)a.gmark_n * 4, st) != hipSuccess))
+        return fail(OA_E_LAUNCH, "oa_step: partition counters / marks reset");
     if (a.n_gchunk1 + a.n_gchunk2 > 0) {
         auto k = k_part_scatter<TX, TV, TD, IDB>;
+        const int64_t lds = scat_lds_bytes(a.part_kmax, (int)sizeof(TD));
         if (int rc = set_lds(k, lds)) return rc;
         hipLaunchKernelGGL(k, dim3((unsigned)(a.n_gchunk1 + a.n_gchunk2)), dim3(SCAT_WG), (size_t)lds,
                            st, a, make_frame_k(a));
@@ -2172,6 +2262,7 @@ int32_t oa_build_info(int32_t which) {
         case 3: return KROWS;
         case 4: return PART_E;
         case 5: return PART_KMAX;
+        case 6: return GPART_W;
         default: return -1;
     }
 }
@@ -2182,6 +2273,7 @@ int64_t oa_struct_size(int32_t which) {
         case 1: return sizeof(oa_item);
         case 2: return sizeof(oa_step_args);
         case 3: return sizeof(oa_compact_args);
+        case 4: return sizeof(oa_unbucket_args);
         default: return -1;
     }
 }
@@ -2316,7 +2408,8 @@ int oa_step(const oa_step_args *args, void *stream) {
     if (a.compare && a.n_gchunk2 > 0 && !a.gchunk2)
         return fail(OA_E_ARG, "null large-halo chunk pointer");
     const bool part = a.compare && !a.onthefly && a.n_parts > 0;
-    if (part && (!a.plist || !a.gpart || !a.pkey_cur || !a.ppos_cur || !a.pcnt || !a.gmark ||
+    if (part && (!a.plist || !a.gpart || !a.pkey_cur || !a.ppos_cur || !a.pmeta_cur ||
+                 !a.prh_cur || !a.pcnt || !a.gmark || a.n_pcnt < 1 ||
                  (a.n_gchunk2 > 0 && (!a.pkey_prev || !a.ppos_prev || !a.pmeta_prev ||
                                       !a.prh_prev)) || a.part_kmax < 1 ||
                  a.part_e < 64 || a.part_e > PART_E || a.part_e % 64 ||
@@ -2338,6 +2431,20 @@ int oa_step(const oa_step_args *args, void *stream) {
                            : launch_step_v<float, double>(a, st);
     }
     return launch_step_v<float, float>(a, st);
+}
+
+int oa_part_unbucket(const oa_unbucket_args *args, void *stream) {
+    g_err[0] = 0;
+    if (!args) return fail(OA_E_ARG, "oa_part_unbucket: null args");
+    const oa_unbucket_args &a = *args;
+    if (a.n_parts <= 0) return OA_OK;
+    if (!a.bpos || !a.bmeta || !a.brh || !a.bcnt || !a.rows || !a.plist || !a.rhat_out ||
+        !a.meta_out || a.cap < 1)
+        return fail(OA_E_ARG, "oa_part_unbucket: null pointer / bad capacity");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (a.td_f64) hipLaunchKernelGGL(k_part_unbucket<double>, dim3((unsigned)a.n_parts), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_part_unbucket<float>, dim3((unsigned)a.n_parts), dim3(256), 0, st, a);
+    return check_launch("k_part_unbucket");
 }
 
 int oa_compact(const oa_compact_args *args, void *stream) {

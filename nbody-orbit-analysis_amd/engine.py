@@ -204,53 +204,80 @@ def plan_global(glob, cur_cnt, prev_cnt, first_index, compare):
     return chunks(n1).reshape(-1, 3), chunks(n2).reshape(-1, 3), tab, int(cap.sum())
 
 
-PART_FILL = 0.9      # mean fill of a large-halo partition's LDS table (k_part_join)
-PART_SPREAD = int(os.environ.get('ORBIT_PART_SPREAD', 32))   # partitions per large
-                     # halo at least: the join work-groups one XCD runs at once (32 CUs x 2)
+PART_FILL = 0.9      # mean fill of a large-halo partition's LDS table at most (k_part_join)
 
 
-def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, n_xcd=8):
+def _pow2_ceil(x):
+    x = np.maximum(np.asarray(x, dtype=np.int64), 1)
+    return np.left_shift(1, np.ceil(np.log2(x)).astype(np.int64))
+
+
+# partitions per large halo at least (a power of two): as many as one XCD's CUs run join
+# work-groups at once, so an XCD works on one halo at a time
+PART_SPREAD = int(_pow2_ceil(int(os.environ.get('ORBIT_PART_SPREAD', 32))))
+GPART_W = 16         # int64 per gpart row (orbit_hip.h)
+
+
+def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=None, n_xcd=8):
     """Partition layout of the global items for the partitioned large-halo path
     (k_part_scatter / k_part_join / k_part_emit), vectorised.
 
-    A halo with a progenitor block gets K = ceil(C / (0.9 part_e)) hash partitions
-    of its IDs: a partition's current count is binomial with mean <= 0.9 part_e, so
-    the LDS capacity is many standard deviations away (an overflow is reported by the
-    kernel and the snapshot re-runs on the global-table path).  Previous buckets hold
-    mean + 8 sqrt(mean) + 64 entries.  plist deals the partitions to the 8 XCDs in
-    contiguous runs (work-group b runs on XCD b % 8), so one halo's partitions share
-    an L2 for their gathers.  Returns None when no halo needs the join or one needs
-    more than ``kmax`` partitions."""
+    A halo with a progenitor block gets K = a power of two >= C / (0.9 part_e) (and
+    >= PART_SPREAD) hash partitions of its IDs: a partition's current count is binomial
+    with mean <= 0.9 part_e, so the LDS capacity is many standard deviations away (an
+    overflow is reported by the kernel and the snapshot re-runs on the global-table
+    path).  Its current state goes into the step's current bucket set (part_e entries
+    per partition).  Its previous state comes from the previous step's set when that
+    step bucketed the progenitor block (``prev_sets``, indexed by the previous
+    snapshot's halo number ``prev_idx``; any K: both are powers of two), else from a
+    fresh previous set scattered from the position-order state (mean + 8 sqrt(mean) + 64
+    entries per partition).  plist deals the partitions to the 8 XCDs in contiguous runs
+    (work-group b runs on XCD b % 8), so one halo's partitions share an L2.  Returns None
+    when no halo needs the join or one needs more than ``kmax`` partitions."""
     h = np.asarray(glob['h0'], dtype=np.int64)
     c = np.asarray(cur_cnt, dtype=np.int64)[h]
     p = np.maximum(np.asarray(prev_cnt, dtype=np.int64)[h], 0)
-    # at least PART_SPREAD partitions (of >= 1024 particles): as many as one XCD runs
-    # at once, so an XCD works on one halo at a time and that halo's gathered r̂ and
-    # state words stay in the XCD's 4 MB L2
-    K = np.maximum(-(-c // int(part_e * PART_FILL)), np.minimum(PART_SPREAD, c // 1024))
-    K = np.where(p > 0, np.maximum(K, 1), 0).astype(np.int64)
+    K = np.maximum(_pow2_ceil(-(-c // int(part_e * PART_FILL))), PART_SPREAD)
+    K = np.where(p > 0, K, 0).astype(np.int64)
     nk = int(K.sum())
     if nk == 0 or K.max() > kmax:
         return None
+    ng = len(h)
+    gpart = np.zeros((ng, GPART_W), dtype=np.int64)
+    gpart[:, 0] = (np.cumsum(K) - K) * int(part_e)
+    gpart[:, 1] = K
+    gpart[:, 2] = np.cumsum(K) - K
+    inh = np.zeros(ng, dtype=bool)
+    if prev_sets is not None and prev_idx is not None:
+        pc = np.asarray(prev_idx, dtype=np.int64)[h]
+        ok = (pc >= 0) & (K > 0)
+        pk = np.where(ok, prev_sets['K'][np.maximum(pc, 0)], 0)
+        inh = ok & (pk > 0)
+        gpart[inh, 3] = 1
+        gpart[inh, 4] = prev_sets['base'][pc[inh]]
+        gpart[inh, 5] = pk[inh]
+        gpart[inh, 6] = int(prev_sets['cap'])
+        gpart[inh, 7] = prev_sets['cbase'][pc[inh]]
+    fresh = (K > 0) & ~inh
     mean = p / np.maximum(K, 1)
-    cap2 = np.where(K > 0, np.ceil(mean + 8 * np.sqrt(mean) + 64), 0).astype(np.int64)
-    cur_sz, prev_sz = K * int(part_e), K * cap2
-    gpart = np.zeros((len(h), 8), dtype=np.int64)
-    gpart[:, 0] = np.cumsum(cur_sz) - cur_sz
-    gpart[:, 1] = np.cumsum(prev_sz) - prev_sz
-    gpart[:, 2], gpart[:, 3] = K, cap2
-    gpart[:, 4] = np.cumsum(2 * K) - 2 * K
-    g = np.repeat(np.arange(len(h)), K)
+    cap2 = np.where(fresh, np.ceil(mean + 8 * np.sqrt(mean) + 64), 0).astype(np.int64)
+    fsz = np.where(fresh, K * cap2, 0)
+    fk = np.where(fresh, K, 0)
+    gpart[fresh, 4] = (np.cumsum(fsz) - fsz)[fresh]
+    gpart[fresh, 5] = K[fresh]
+    gpart[fresh, 6] = cap2[fresh]
+    gpart[fresh, 7] = nk + (np.cumsum(fk) - fk)[fresh]
+    g = np.repeat(np.arange(ng), K)
     pp = np.arange(nk) - np.repeat(np.cumsum(K) - K, K)
     per = -(-nk // n_xcd)
     b = np.arange(per * n_xcd)
     idx = (b % n_xcd) * per + b // n_xcd
-    ok = idx < nk
+    okb = idx < nk
     plist = np.zeros((len(b), 2), dtype=np.int32)
     plist[:, 0] = -1
-    plist[ok, 0], plist[ok, 1] = g[idx[ok]], pp[idx[ok]]
-    return dict(gpart=gpart, plist=plist, n_cur=int(cur_sz.sum()), n_prev=int(prev_sz.sum()),
-                kmax=int(K.max()))
+    plist[okb, 0], plist[okb, 1] = g[idx[okb]], pp[idx[okb]]
+    return dict(gpart=gpart, plist=plist, n_cur=nk * int(part_e), n_prev=int(fsz.sum()),
+                n_pcnt=nk + int(fk.sum()), kmax=int(K.max()), K=K, inherited=inh, h=h)
 
 
 def retry_plan(pr, st):
@@ -353,6 +380,26 @@ def _ptr(t):
 
 
 @dataclass
+class BucketSet:
+    """One step's state of its partitioned large halos, by hash partition (k_part_*,
+    orbit_hip.h): per entry the ID, position | sign << 30, state word and r̂; part_e
+    entries per partition.  Per halo of that step: K (0: not bucketed), base entry and
+    first counter.  The position-order state arrays of those halos are not written
+    (OrbitEngine.unbucket restores them on demand); ``restored`` marks halos done."""
+    key: torch.Tensor
+    pos: torch.Tensor
+    meta: torch.Tensor
+    rh: torch.Tensor
+    cnt: torch.Tensor
+    K: np.ndarray
+    base: np.ndarray
+    cbase: np.ndarray
+    cap: int
+    td_f64: bool
+    restored: Optional[np.ndarray] = None
+
+
+@dataclass
 class SnapshotState:
     """Device state a snapshot leaves for the next one (track_orbits.py:234-240)."""
     ids: torch.Tensor
@@ -362,6 +409,7 @@ class SnapshotState:
     counts: np.ndarray
     exists: np.ndarray
     plan: DtypePlan
+    buckets: Optional[BucketSet] = None
 
 
 @dataclass
@@ -400,6 +448,8 @@ class PreparedStep:
     angles_in: Optional[torch.Tensor] = None
     halo_list: Optional[torch.Tensor] = None
     bulk_computed: bool = False
+    buckets: Optional['BucketSet'] = None          # this step's current bucket set
+    unbucket_prev: Optional[np.ndarray] = None     # previous halos to restore first
     snap: dict = field(default_factory=dict)
     args: N.StepArgs = field(default_factory=N.StepArgs)
     cargs: N.CompactArgs = field(default_factory=N.CompactArgs)
@@ -550,6 +600,7 @@ class OrbitEngine:
         halos['prev_cnt'] = -1
         halos['out_slot'] = -1
         has_prog = np.zeros(nh, dtype=bool)
+        prev_idx = np.full(nh, -1, dtype=np.int64)     # the progenitor's previous halo number
         if compare:
             p_starts, p_counts, pe = prev_layout[0], prev_layout[1], np.asarray(prev_layout[2])
             p = np.searchsorted(pe, exists)
@@ -558,8 +609,10 @@ class OrbitEngine:
             halos['prev_off'][has_prog] = p_starts[p[has_prog]]
             halos['prev_cnt'][has_prog] = p_counts[p[has_prog]]
             halos['out_slot'][has_prog] = np.arange(int(has_prog.sum()))
+            prev_idx[has_prog] = p[has_prog]
         buf, k, n_it, scratch = _plan(counts, halos['prev_cnt'], entries, self.hmax,
                                       halos['out_slot'], self.max_pv, slots, starts)
+        self._prev_idx = prev_idx
         return halos, buf[:n_it], k, scratch, starts, counts, has_prog
 
     # ------------------------------------------------------------------ step
@@ -598,7 +651,8 @@ class OrbitEngine:
             raise RuntimeError('LDS hash tables kept overflowing')
         self.prev = SnapshotState(ids=snap['ids'], rhat=prep.rhat, meta=prep.meta,
                                   starts=prep.starts,
-                                  counts=prep.counts, exists=exists, plan=prep.plan)
+                                  counts=prep.counts, exists=exists, plan=prep.plan,
+                                  buckets=prep.buckets)
         if compare:
             self._wsi ^= 1                  # the next snapshot writes the other workspace
         return res
@@ -619,7 +673,8 @@ class OrbitEngine:
                            None if bulk_cat is None else bulk_cat[0], H, z)
         if prev_layout is None and compare:
             p = self.prev
-            prev_layout = (p.starts, p.counts, p.exists, p.plan, p.ids.numel())
+            prev_layout = (p.starts, p.counts, p.exists, p.plan, p.ids.numel(), p.buckets)
+        prev_sets = prev_layout[5] if compare and len(prev_layout) > 5 else None
         if compare:
             pplan = prev_layout[3]
             if plan.dx != pplan.dx:
@@ -636,6 +691,7 @@ class OrbitEngine:
         plan_e = lds_e if entries is None else min(int(entries), lds_e)
         halos, all_items, n_small, scratch, starts, counts, has_prog = self.build_tables(
             snap, centres, bulk_cat, exists, compare, prev_layout, plan_e, lds_s)
+        prev_idx = self._prev_idx
         items, glob = all_items[:n_small], all_items[n_small:]
         pr = PreparedStep(plan=plan, n=n, starts=starts, counts=counts, has_prog=has_prog,
                           items=all_items, n_small=n_small, scratch=scratch,
@@ -653,26 +709,52 @@ class OrbitEngine:
             g['total'] = total
             pl = None
             if compare and part and self.part_large:
-                pl = plan_part(glob, counts, halos['prev_cnt'], self.part_e, self.part_kmax)
+                pl = plan_part(glob, counts, halos['prev_cnt'], self.part_e, self.part_kmax,
+                               prev_idx, prev_sets)
             if pl is not None:
                 pr.part = True
                 i32, i64 = torch.int32, torch.int64
                 g['plist'] = torch.from_numpy(pl['plist'].reshape(-1)).to(dev)
                 g['gpart'] = torch.from_numpy(pl['gpart'].reshape(-1)).to(dev)
+                # this step's current bucket set: the next step's previous state
                 g['pkey_cur'] = torch.empty(pl['n_cur'], dtype=i64, device=dev)
                 g['ppos_cur'] = torch.empty(pl['n_cur'], dtype=i32, device=dev)
+                g['pmeta_cur'] = torch.empty(pl['n_cur'], dtype=i32, device=dev)
+                g['prh_cur'] = torch.empty(3 * pl['n_cur'], dtype=plan.torch_dx, device=dev)
                 g['pkey_prev'] = torch.empty(max(pl['n_prev'], 1), dtype=i64, device=dev)
                 g['ppos_prev'] = torch.empty(max(pl['n_prev'], 1), dtype=i32, device=dev)
                 g['pmeta_prev'] = torch.empty(max(pl['n_prev'], 1), dtype=i32, device=dev)
                 g['prh_prev'] = torch.empty(3 * max(pl['n_prev'], 1), dtype=plan.torch_dx,
                                             device=dev)
-                g['pcnt'] = torch.empty(2 * len(pl['plist']), dtype=i32, device=dev)
+                g['pcnt'] = torch.empty(pl['n_pcnt'], dtype=i32, device=dev)
                 g['gmark_base'] = int(glob['scratch_off'][0])
-                g['gmark'] = torch.empty(max(scratch - g['gmark_base'], 1), dtype=i32, device=dev)
+                g['gmark_n'] = max(scratch - g['gmark_base'], 1)
+                g['gmark'] = torch.empty(g['gmark_n'], dtype=i32, device=dev)
                 g['n_parts'], g['kmax'] = len(pl['plist']), pl['kmax']
+                nh = len(halos)
+                K = np.zeros(nh, np.int64)
+                K[pl['h']] = pl['K']
+                base = np.full(nh, -1, np.int64)
+                base[pl['h']] = pl['gpart'][:, 0]
+                cbase = np.zeros(nh, np.int64)
+                cbase[pl['h']] = pl['gpart'][:, 2]
+                pr.buckets = BucketSet(key=g['pkey_cur'], pos=g['ppos_cur'], meta=g['pmeta_cur'],
+                                       rh=g['prh_cur'], cnt=g['pcnt'], K=K, base=base,
+                                       cbase=cbase, cap=self.part_e, td_f64=plan.dx == F64)
+                if prev_sets is not None and pl['inherited'].any():
+                    g['inherit'] = prev_sets           # keeps the previous set alive
             elif compare:
                 g['keys'] = torch.empty(2 * total, dtype=torch.int64, device=dev)
             g['n1'], g['n2'] = len(ch1), len(ch2)
+        if prev_sets is not None:
+            need = np.zeros(len(prev_sets.K), dtype=bool)
+            need[prev_idx[prev_idx >= 0]] = True
+            if pr.part:
+                done = np.zeros_like(need)
+                hh = pl['h'][pl['inherited']]
+                done[prev_idx[hh]] = True
+                need &= ~done
+            pr.unbucket_prev = np.flatnonzero(need & (prev_sets.K > 0))
         pr.rhat = torch.empty(n * 3, dtype=plan.torch_dx, device=dev)
         pr.meta = torch.empty(n, dtype=torch.int32, device=dev)
         pr.snap = snap
@@ -700,10 +782,16 @@ class OrbitEngine:
                 a.part_e, a.part_slots = self.part_e, self.part_slots
                 a.plist, a.gpart = g['plist'].data_ptr(), g['gpart'].data_ptr()
                 a.pkey_cur, a.ppos_cur = g['pkey_cur'].data_ptr(), g['ppos_cur'].data_ptr()
+                a.pmeta_cur, a.prh_cur = g['pmeta_cur'].data_ptr(), g['prh_cur'].data_ptr()
                 a.pkey_prev, a.ppos_prev = g['pkey_prev'].data_ptr(), g['ppos_prev'].data_ptr()
                 a.pmeta_prev, a.prh_prev = g['pmeta_prev'].data_ptr(), g['prh_prev'].data_ptr()
-                a.pcnt, a.gmark, a.gmark_base = (g['pcnt'].data_ptr(), g['gmark'].data_ptr(),
-                                                 g['gmark_base'])
+                inh = g.get('inherit')
+                a.ikey, a.ipos = _ptr(inh and inh.key), _ptr(inh and inh.pos)
+                a.imeta, a.irh, a.icnt = (_ptr(inh and inh.meta), _ptr(inh and inh.rh),
+                                          _ptr(inh and inh.cnt))
+                a.pcnt, a.n_pcnt = g['pcnt'].data_ptr(), int(g['pcnt'].numel())
+                a.gmark, a.gmark_base, a.gmark_n = (g['gmark'].data_ptr(), g['gmark_base'],
+                                                    g['gmark_n'])
         a.H, a.one_plus_z = float(H), float(1 + z)
         a.n_box_dims = len(plan.box)
         for d, L in enumerate(plan.box):
@@ -731,6 +819,10 @@ class OrbitEngine:
         res = StepResult(n_slots=int(pr.has_prog.sum()), has_prog=pr.has_prog, halos=pr.halos)
         if pr.compare:
             p = prev if prev is not None else self.prev
+            if pr.unbucket_prev is not None and len(pr.unbucket_prev):
+                # progenitor blocks this step reads in position order (packed items, the
+                # global tables) from the previous step's bucket set
+                self.unbucket(p.buckets, pr.unbucket_prev, p.starts, p.rhat, p.meta, st)
             a.ids_prev, a.rhat_prev, a.meta_prev = (p.ids.data_ptr(), p.rhat.data_ptr(),
                                                     p.meta.data_ptr())
             a.n_prev = pr.n_prev
@@ -858,9 +950,46 @@ class OrbitEngine:
         h = res.halos.cpu().numpy().view(N.HALO_DTYPE)
         return h['bulk'].astype(plan.bulk)
 
+    def unbucket(self, bs, halos, starts, rhat, meta, stream=None):
+        """Restore the position-order state (r̂, state word) of the listed halos of a
+        step from its bucket set ``bs`` into that step's ``rhat`` / ``meta`` arrays (block
+        starts ``starts``).  Idempotent; a halo is restored once."""
+        halos = np.asarray(halos, dtype=np.int64)
+        if bs.restored is None:
+            bs.restored = np.zeros(len(bs.K), dtype=bool)
+        halos = halos[(bs.K[halos] > 0) & ~bs.restored[halos]]
+        if not len(halos):
+            return
+        dev = self.device
+        st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        rows = np.stack([bs.base[halos], bs.K[halos], bs.cbase[halos],
+                         np.asarray(starts, np.int64)[halos]], axis=1).astype(np.int64)
+        K = bs.K[halos]
+        plist = np.stack([np.repeat(np.arange(len(halos)), K),
+                          np.arange(int(K.sum())) - np.repeat(np.cumsum(K) - K, K)],
+                         axis=1).astype(np.int32)
+        d_rows = _upload(rows.view(np.uint8), dev)
+        d_plist = _upload(plist.view(np.uint8), dev)
+        u = N.UnbucketArgs()
+        u.bpos, u.bmeta, u.brh, u.bcnt = (bs.pos.data_ptr(), bs.meta.data_ptr(),
+                                          bs.rh.data_ptr(), bs.cnt.data_ptr())
+        u.rows, u.plist, u.n_parts, u.cap = (d_rows.data_ptr(), d_plist.data_ptr(), len(plist),
+                                             int(bs.cap))
+        u.rhat_out, u.meta_out, u.td_f64 = rhat.data_ptr(), meta.data_ptr(), int(bs.td_f64)
+        N.check(self.lib.oa_part_unbucket(u, st), 'oa_part_unbucket')
+        bs.restored[halos] = True
+        self._keep = (d_rows, d_plist)      # until the next call (stream-ordered use)
+
+    def state_meta(self):
+        """The current state words in position order (bucketed large halos restored)."""
+        p = self.prev
+        if p.buckets is not None:
+            self.unbucket(p.buckets, np.arange(len(p.buckets.K)), p.starts, p.rhat, p.meta)
+        return p.meta
+
     def angles(self):
         """Current per-particle float16 angles (checkpoint payload, track_orbits.py:390-394)."""
-        return meta_angles(self.prev.meta)
+        return meta_angles(self.state_meta())
 
     def checkpoint_layout(self):
         """Row layout of ``angles()``: None, the snapshot's own row order."""

@@ -330,16 +330,34 @@ class Shard:
     h2d_bytes: int = 0                 # loader bytes this rank moved to its device
 
 
-def stripe_shard(snapshot, starts, owner, group, device, bulk_fn=None):
+def my_stripe(starts, n, group=None):
+    """(lo, hi) rows of this rank's stripe of a snapshot of n rows with these block
+    starts: what a reader that hands each rank its stripe (``STRIPE`` key) must load."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    return stripe_rows(np.asarray(starts, np.int64), n, stripe_halos(starts, n, world), rank)
+
+
+STRIPE = 'stripe_rows'     # snapshot key: the arrays hold only rows [lo, hi) (my_stripe)
+
+
+def stripe_shard(snapshot, starts, owner, group, device, bulk_fn=None, n=None):
     """The whole-snapshot loader contract on one rank (module docstring): upload stripe
     r only, compute its blocks' bulk velocities (``bulk_fn(stripe_snapshot, halos)``,
     when given), route its rows to their owners with one all-to-all per array, and lay
-    the received rows out in block order.  Returns a ``Shard``."""
+    the received rows out in block order.  A snapshot carrying ``STRIPE`` = (lo, hi)
+    holds this rank's stripe only (a striped reader, e.g. one that double-buffers its
+    stripe on a copy stream); ``n`` is then the global row count.  Returns a ``Shard``."""
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     ids = snapshot['ids']
-    n = int(ids.numel()) if isinstance(ids, torch.Tensor) else len(ids)
+    striped = snapshot.get(STRIPE)
+    if n is None:
+        if striped is not None:
+            raise ValueError('a striped snapshot needs the global row count n')
+        n = int(ids.numel()) if isinstance(ids, torch.Tensor) else len(ids)
     starts = np.asarray(starts, dtype=np.int64)
     nh = len(starts)
     hb = stripe_halos(starts, n, world)
@@ -348,7 +366,13 @@ def stripe_shard(snapshot, starts, owner, group, device, bulk_fn=None):
     masses = snapshot['masses']
     has_m = isinstance(masses, (np.ndarray, torch.Tensor))
     keys = ('ids', 'coordinates', 'velocities') + (('masses',) if has_m else ())
-    st = {k: _to_tensor(snapshot[k][lo:hi], device) for k in keys}
+    if striped is not None:
+        if tuple(int(x) for x in striped) != (lo, hi):
+            raise ValueError('striped snapshot holds rows %s, this rank\'s stripe is %s'
+                             % (tuple(striped), (lo, hi)))
+        st = {k: _to_tensor(snapshot[k], device) for k in keys}
+    else:
+        st = {k: _to_tensor(snapshot[k][lo:hi], device) for k in keys}
     h2d = sum(int(v.numel()) * v.element_size() for k, v in st.items()
               if not (isinstance(snapshot[k], torch.Tensor) and snapshot[k].device.type ==
                       torch.device(device).type))
@@ -642,7 +666,8 @@ class EngineLocal:
         eng = self.engine
         layout = None
         if compare and prev_lp is not None:
-            layout = (prev_lp.starts, prev_lp.counts, prev_lp.exists, prev_lp.plan, prev_lp.n)
+            layout = (prev_lp.starts, prev_lp.counts, prev_lp.exists, prev_lp.plan, prev_lp.n,
+                      prev_lp.buckets)
         lp = eng.prepare(shard, centres, bulk, H, z, exists, compare, angles_in=angles_in,
                          plan_src=shard, prev_layout=layout)
         lp.exists = np.asarray(exists)
@@ -666,7 +691,8 @@ class EngineLocal:
             if lp.compare and prev_lp is not None:
                 prev = SnapshotState(ids=prev_lp.snap['ids'], rhat=prev_lp.rhat, meta=prev_lp.meta,
                                      starts=prev_lp.starts, counts=prev_lp.counts,
-                                     exists=prev_lp.exists, plan=prev_lp.plan)
+                                     exists=prev_lp.exists, plan=prev_lp.plan,
+                                     buckets=prev_lp.buckets)
             if check and ws is not None:
                 ws.status.zero_()
             res = eng.launch(lp, ws, prev=prev, step_events=step_events)
@@ -685,14 +711,15 @@ class EngineLocal:
         else:
             raise RuntimeError('LDS hash tables kept overflowing')
         eng.prev = SnapshotState(ids=lp.snap['ids'], rhat=lp.rhat, meta=lp.meta, starts=lp.starts,
-                                 counts=lp.counts, exists=lp.exists, plan=lp.plan)
+                                 counts=lp.counts, exists=lp.exists, plan=lp.plan,
+                                 buckets=lp.buckets)
         if not lp.compare:
             return None
         return res.offsets, res.apsis_ids, res.apsis_ang, res.apsis_pos
 
     def angles_tensor(self):
         """float16 bits of the current angle state (low half of the meta words)."""
-        return self.engine.prev.meta & 0xFFFF
+        return self.engine.state_meta() & 0xFFFF
 
     def bulk(self, snapshot, halo_idx):
         return self.engine.block_bulk(snapshot, halo_idx)

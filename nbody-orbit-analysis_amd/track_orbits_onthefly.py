@@ -410,14 +410,16 @@ class ShardedOnTheFly:
 
     def shard(self, snap, sl):
         """This rank's shard of one snapshot (``sharding.stripe_shard``) and its local
-        slices (absent halos (-1, -1))."""
-        from .sharding import stripe_shard
+        slices (absent halos (-1, -1)).  A snapshot with ``sharding.STRIPE`` holds only
+        this rank's stripe, and then its ``n_rows`` the global row count."""
+        from .sharding import stripe_shard, STRIPE
         sl = np.asarray(sl, dtype=np.int64).reshape(-1, 2)
         ids = snap['ids']
-        n = int(ids.numel()) if isinstance(ids, torch.Tensor) else len(ids)
+        n = int(snap['n_rows']) if STRIPE in snap else \
+            (int(ids.numel()) if isinstance(ids, torch.Tensor) else len(ids))
         eng = self.eng
         sh = stripe_shard(snap, _block_starts(sl, n), self.owner, self.group, eng.device,
-                          bulk_fn=eng.block_bulk)
+                          bulk_fn=eng.block_bulk, n=n)
         st = np.concatenate([[0], np.cumsum(sh.counts)[:-1]]).astype(np.int64)
         lsl = np.where(sl[:, :1] >= 0, np.stack([st, st + sh.counts], axis=1), -1)
         self.h2d_bytes += sh.h2d_bytes

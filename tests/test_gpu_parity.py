@@ -138,9 +138,20 @@ def test_partitioned_large_halos(mode, monkeypatch):
     want = _oracle_run(u, mode)
     eng = OrbitEngine(mode=mode)
     seen = _recording(eng)
+    inh = []
+    orig = eng.prepare
+
+    def prepare(*a, **k):
+        pr = orig(*a, **k)
+        if pr.compare:
+            inh.append(pr.glob.get('inherit') is not None)
+        return pr
+    eng.prepare = prepare
     rep = {}
     compare_groups(run_driver(u, dict(mode=mode), engine=eng).groups, want, rep)
     assert seen and all(seen), seen                  # every compare step partitioned
+    # the first compare step scatters the frame-only step's state; later ones inherit
+    assert inh == [False] + [True] * (len(inh) - 1), inh
     assert rep['angles'] > 0
     eng = OrbitEngine(mode=mode)
     eng.part_large = False
@@ -152,6 +163,54 @@ def test_partitioned_large_halos(mode, monkeypatch):
     seen = _recording(eng)
     compare_groups(run_driver(u, dict(mode=mode), engine=eng).groups, want, {})
     assert True in seen and False in seen, seen
+
+
+@pytest.mark.parametrize('mode', ['pericentric', 'apocentric'])
+def test_bucket_sets_carried_between_steps(mode, monkeypatch):
+    """Large halos keep their state in bucket sets between snapshots (k_part_*): a
+    step's current set is the next step's previous one, for any ratio of the two K;
+    a halo that turns small reads its progenitor block restored to position order
+    (oa_part_unbucket), one that turns large scatters its position-order progenitor
+    block afresh; the checkpoint angles are restored from the sets.  Output, checkpoint
+    and every path against the oracle."""
+    from orbitanalysis_amd import engine as E
+    from orbitanalysis_amd.engine import OrbitEngine
+    from orbitanalysis_amd.synthetic import PlummerSnapshots
+    u = PlummerSnapshots(n_halos=5, n_per_halo=[30000, 9000, 30000, 5000, 14000], n_snapshots=7,
+                         seed=43, box_size=150.0, dtype=np.float32, centre_dtype=np.float32)
+    from oracle import orbit_oracle as O
+    rec = O.MemoryRecord()
+    want = O.track_orbits(u.snapshot_numbers, u.main_branches(), u.regions, u.load_snapshot_data,
+                          rec, mode=mode, checkpoint=True)
+    eng = OrbitEngine(mode=mode)
+    # per step: partition spread (K of the 30000 halos: 64, 16, 128, ...) and the item
+    # budget (halo 1, ~9000 particles, alternates between a packed and a large halo)
+    plan = iter([(64, 8000), (16, None), (128, 8000), (16, 8000), (64, None), (32, 8000),
+                 (64, None), (16, 8000)])
+    seen = []
+    orig = eng.prepare
+
+    def prepare(*a, **k):
+        spread, entries = next(plan, (32, None))
+        monkeypatch.setattr(E, 'PART_SPREAD', spread)
+        eng.entries_cfg = entries
+        pr = orig(*a, **k)
+        if pr.compare:
+            seen.append(dict(part=pr.part, inherit=pr.glob.get('inherit') is not None,
+                             unbucket=0 if pr.unbucket_prev is None else len(pr.unbucket_prev),
+                             glob=pr.n_global))
+        return pr
+    eng.prepare = prepare
+    rep = {}
+    out = run_driver(u, dict(mode=mode, checkpoint=True), engine=eng)
+    compare_groups(out.groups, want.groups, rep)
+    c, w = out.checkpoint, np.asarray(rec.checkpoint)
+    bad = int(np.sum((c != w) & ~(np.isnan(c) & np.isnan(w))))
+    assert c.shape == w.shape and mismatch_ok(bad, c.size), (bad, c.size)
+    assert all(x['part'] for x in seen), seen
+    assert sum(x['inherit'] for x in seen) >= 4, seen          # sets carried over
+    assert any(x['unbucket'] for x in seen), seen              # a halo turned small
+    assert len({x['glob'] for x in seen}) > 1, seen            # ... and large again
 
 
 @pytest.mark.parametrize('mode', ['pericentric', 'apocentric'])

@@ -95,17 +95,18 @@ def _worker(rank, world, port, name, owner, outdir, local='oracle'):
             snap = loader(s, pos, rad)
             n_global = len(u.load_snapshot_data(s, pos, rad)['ids'])
             ang = np.zeros(n_global, np.float16)
-            ok = eng.prepare(snap, pos, bulk, 0.0, 0.0, np.arange(len(h)), False,
+            H0 = np.float64(0.0)                # hubble_parameter returns float64
+            ok = eng.prepare(snap, pos, bulk, H0, 0.0, np.arange(len(h)), False,
                              angles_in=ang, angles_layout=layout)
             assert ok.layout == layout
             try:
-                eng.prepare(snap, pos, bulk, 0.0, 0.0, np.arange(len(h)), False, angles_in=ang,
+                eng.prepare(snap, pos, bulk, H0, 0.0, np.arange(len(h)), False, angles_in=ang,
                             angles_layout=layout.replace('world=%d' % world, 'world=9'))
                 raise AssertionError('a checkpoint of another layout was accepted')
             except ValueError:
                 pass
             try:
-                eng.prepare(snap, pos, bulk, 0.0, 0.0, np.arange(len(h)), False,
+                eng.prepare(snap, pos, bulk, H0, 0.0, np.arange(len(h)), False,
                             angles_in=ang[:-1], angles_layout=layout)
                 raise AssertionError('a short checkpoint was accepted')
             except ValueError:

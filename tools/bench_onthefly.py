@@ -19,6 +19,15 @@ CPU oracle (the reference's per-call algorithm: both frames + compare) on a boun
 sample of halos with its apsis IDs checked against the GPU's.
 
   python tools/bench_onthefly.py [--particles 1.25e8] [--steps 6]
+
+--sharded: the multi-GPU driver (``ShardedOnTheFly``) on every rank of a
+torch.distributed run (``python -m torch.distributed.run ... tools/bench_onthefly.py
+--sharded``; without a launcher, world 1).  Each rank holds only its block-aligned
+stripe of every snapshot in pinned host memory (a striped reader's view of the
+whole-snapshot contract), double-buffers that stripe's H2D on a copy stream, and runs
+the sharded pipeline on it: owner all-to-all, join, records gathered to rank 0 and
+merged there.  --particles is then the global snapshot size (configs[4]: 1e9 over 8
+GPUs; the default 1.25e8 is one GPU's share).
 """
 import argparse
 import json
@@ -45,25 +54,46 @@ def main():
     ap.add_argument('--snapshots', type=int, default=3, help='distinct host snapshots (cycled)')
     ap.add_argument('--cpu-halos', type=int, default=150)
     ap.add_argument('--mode', default='pericentric')
+    ap.add_argument('--sharded', action='store_true')
+    ap.add_argument('--backend', default='nccl')
     args = ap.parse_args()
     import torch
     import orbitanalysis_amd  # noqa: F401
     from orbitanalysis_amd.synthetic_device import DevicePlummer
-    from orbitanalysis_amd.track_orbits_onthefly import OnTheFly
-    dev = torch.device('cuda', 0)
+    from orbitanalysis_amd.track_orbits_onthefly import OnTheFly, ShardedOnTheFly
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0')) % max(torch.cuda.device_count(), 1)
+    dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
+    dist = None
+    if args.sharded:
+        import torch.distributed as dist
+        if world == 1 and 'MASTER_ADDR' not in os.environ:
+            os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT='29561')
+        if args.backend == 'gloo' or world == 1:
+            dist.init_process_group('gloo', rank=rank, world_size=world)
+        else:
+            dist.init_process_group('nccl', device_id=dev)
     nh = max(1, int(args.particles) // args.per_halo)
     gen = DevicePlummer(n_halos=nh, n_particles=int(args.particles), seed=5, device=dev)
     S = args.snapshots
-    host, cats, offs = [], [], []
+    host, cats, offs, stripes, n_rows = [], [], [], [], []
     t0 = time.perf_counter()
     for s in range(S):
         sn = gen.snapshot(s)
-        h = {k: torch.empty(sn[k].shape, dtype=sn[k].dtype, pin_memory=True)
-             for k in ('ids', 'coordinates', 'velocities')}
+        n = int(sn['ids'].numel())
+        lo, hi = 0, n
+        if args.sharded:
+            from orbitanalysis_amd.sharding import my_stripe
+            lo, hi = my_stripe(sn['region_offsets'], n)
+        h = {k: torch.empty((hi - lo,) + tuple(sn[k].shape[1:]), dtype=sn[k].dtype,
+                            pin_memory=True) for k in ('ids', 'coordinates', 'velocities')}
         for k in h:
-            h[k].copy_(sn[k])
+            h[k].copy_(sn[k][lo:hi])
         host.append(h)
+        stripes.append((lo, hi))
+        n_rows.append(n)
         offs.append(np.asarray(sn['region_offsets'], dtype=np.int64))
         cats.append(gen.catalogue(s)[0])
         del sn
@@ -91,14 +121,22 @@ def main():
         evs[k] = ev
 
     def snap_dict(k):
-        n = int(host[k % S]['ids'].numel())
-        d = {key: slots[k % 3][key][:n] for key in host[0]}
+        m = int(host[k % S]['ids'].numel())
+        n = n_rows[k % S]
+        d = {key: slots[k % 3][key][:m] for key in host[0]}
         d.update(masses=1.0, box_size=box)
+        if args.sharded:
+            from orbitanalysis_amd.sharding import STRIPE
+            d[STRIPE], d['n_rows'] = stripes[k % S], n
         o = offs[k % S]
         sl = np.stack([o, np.append(o[1:], n)], axis=1)
         return d, sl
 
-    otf = OnTheFly(mode=args.mode)
+    if args.sharded:
+        from orbitanalysis_amd.engine import OrbitEngine
+        otf = ShardedOnTheFly(OrbitEngine(mode=args.mode, device=dev))
+    else:
+        otf = OnTheFly(mode=args.mode)
     # H2D alone (copy-engine rate) on one snapshot, warm (the first copy into fresh
     # device memory is slower)
     for _ in range(2):
@@ -114,19 +152,25 @@ def main():
     h2d(1)
     torch.cuda.current_stream().wait_event(evs[0])
     d0, sl0 = snap_dict(0)
-    pp = otf._prepare(d0, sl0, cats[0], False)
-    otf.eng.launch(pp, None)
-    from orbitanalysis_amd.engine import SnapshotState
-    from orbitanalysis_amd import _native as N
-    bulk0 = pp.halos.cpu().numpy().view(N.HALO_DTYPE)['bulk'].astype(pp.plan.bulk)
-    carried = (SnapshotState(ids=pp.snap['ids'], rhat=pp.rhat, meta=pp.meta, starts=pp.starts,
-                             counts=pp.counts, exists=np.arange(nh), plan=pp.plan), bulk0)
+    if args.sharded:
+        carried = None                          # step 1 frames snapshot 0 itself
+    else:
+        pp = otf._prepare(d0, sl0, cats[0], False)
+        otf.eng.launch(pp, None)
+        from orbitanalysis_amd.engine import SnapshotState
+        from orbitanalysis_amd import _native as N
+        bulk0 = pp.halos.cpu().numpy().view(N.HALO_DTYPE)['bulk'].astype(pp.plan.bulk)
+        carried = (SnapshotState(ids=pp.snap['ids'], rhat=pp.rhat, meta=pp.meta,
+                                 starts=pp.starts, counts=pp.counts, exists=np.arange(nh),
+                                 plan=pp.plan), bulk0)
     total_steps = 1 + args.steps              # 1 warm-up step
     comp_ms, units, outs = [], 0, None
     t_start = None
     for k in range(1, total_steps + 1):
         if k == 2:
             torch.cuda.synchronize()
+            if dist is not None:
+                dist.barrier()
             t_start = time.perf_counter()
         if k + 1 <= total_steps:
             h2d(k + 1)                         # overlaps this step's compare
@@ -135,15 +179,27 @@ def main():
         dp, slp = snap_dict(k - 1)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        outs = otf.run([dk, None], [slk, slp], [cats[k % S], cats[(k - 1) % S]], carried=carried)
+        if carried is None:                    # sharded, first step: both snapshots
+            outs = otf.run([dk, dp], [slk, slp], [cats[k % S], cats[(k - 1) % S]])
+        else:
+            outs = otf.run([dk, None], [slk, slp], [cats[k % S], cats[(k - 1) % S]],
+                           carried=carried)
         e1.record()
         carried = otf.carry
         if k >= 2:
             e1.synchronize()
             comp_ms.append(e0.elapsed_time(e1))
-            units += int(dk['ids'].numel())
+            units += n_rows[k % S]
     torch.cuda.synchronize()
     wall = time.perf_counter() - t_start
+    if dist is not None:
+        nccl = dist.get_backend() == 'nccl'
+        t = torch.tensor([wall], dtype=torch.float64, device=dev if nccl else 'cpu')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+        if rank != 0:
+            dist.destroy_process_group()
+            return
     n_apsis = int(outs['apsis_offsets'][-1])
 
     # CPU oracle: the reference per-call algorithm (frames of both snapshots + compare)
@@ -173,7 +229,9 @@ def main():
 
     res = {
         'metric': 'particle-snapshots/s (track_orbits_onthefly stream, H2D inclusive)',
-        'value': units / wall, 'unit': 'particle-snapshots/s', 'n_gpus': 1,
+        'value': units / wall, 'unit': 'particle-snapshots/s', 'n_gpus': world,
+        'driver': 'ShardedOnTheFly (stripe H2D + owner all-to-all + gather to rank 0)'
+                  if args.sharded else 'OnTheFly (single GPU)',
         'steps': args.steps, 'warmup': 1, 'ms_per_step': wall / args.steps * 1e3,
         'higher_is_better': True, 'dtype': 'f32', 'data': 'synthetic Plummer spheres, pinned host',
         'config': {'workload': 'BASELINE configs[4] per-GPU share: %d particles/snapshot, %d '
@@ -191,6 +249,8 @@ def main():
                          % (ch, nh, cdt, ok)},
     }
     print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 if __name__ == '__main__':
