@@ -50,7 +50,6 @@ int check_launch(const char *what) {
 
 constexpr uint64_t SIGN = 0x8000000000000000ull;
 constexpr int CH = OA_COLLATE_CHUNK;
-constexpr int KC = 12288;                // k_central: radius keys cached in LDS
 constexpr int SC = OA_CENTRAL_MAX_N;     // k_central: survivors sorted in LDS
 
 // value of element i as 64-bit two's complement (signed kinds sign-extend)
@@ -351,152 +350,245 @@ __device__ __forceinline__ uint64_t radius_key(const TX (&x)[3], const double *c
     return (uint64_t)__double_as_longlong(r);   // r >= +0 or NaN: bit order = numeric order, NaN last
 }
 
+constexpr int KR = 12;                     // k_central: radius keys per thread in registers
+constexpr int HB = 12;                     // k_central: digit bits of the threshold pass
+
 template <typename TX, typename TD>
 __global__ __launch_bounds__(1024) void k_central(const oa_central_args a) {
-    __shared__ uint64_t kc[KC];
     __shared__ uint64_t sk[SC];
     __shared__ uint32_t si[SC];
-    __shared__ int hist[256];
+    __shared__ int hist[1 << HB];
     __shared__ int wsum[17];
     __shared__ uint64_t s_prefix;
     __shared__ unsigned long long s_min, s_max;
-    __shared__ int s_need, s_cnt, s_done;
-    const int h = blockIdx.x;
+    __shared__ int s_need, s_cnt, s_done, s_bin, s_cum;
+    const int h = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int64_t off = a.offsets[h];
     const int m = (int)(a.offsets[h + 1] - off);
     const int k = m < a.n ? m : a.n;
     if (k <= 0) return;
-    const bool cached = m <= KC;
     const TX *x = static_cast<const TX *>(a.coords);
     const double *c = a.positions + 3 * (int64_t)h;
-    if (threadIdx.x == 0) { s_min = ~0ull; s_max = 0; s_cnt = 0; s_done = 0; }
+    if (tid == 0) { s_min = ~0ull; s_max = 0; s_cnt = 0; s_done = 0; }
+    for (int d = tid; d < (1 << HB); d += 1024) hist[d] = 0;
     __syncthreads();
-    uint64_t lmin = ~0ull, lmax = 0;
-    // four particles per thread per trip: their coordinate loads are all in flight
-    // before the first radius is computed
-    constexpr int RU = 4;
-    for (int i0 = threadIdx.x; i0 < m; i0 += 1024 * RU) {
-        TX xs[RU][3];
+    bool fast = m <= KR * 1024;                // uniform
+    uint64_t key[KR];
+    if (fast) {
+        // Fast path (blocks of <= KR * 1024): every radius key stays in its thread's
+        // registers.  One histogram of the HB bits below the block's common key prefix
+        // gives a threshold digit B whose keys, with every smaller one, hold the k
+        // smallest; when those are <= SC they are sorted by (key, position) in LDS and
+        // the first k taken -- the same k keys, in the same order, as the exact select
+        // below, in one pass over the keys instead of up to eight.
+        TX xs[KR][3];
 #pragma unroll
-        for (int u = 0; u < RU; ++u) {
-            const int i = i0 + u * 1024;
+        for (int u = 0; u < KR; ++u) {
+            const int i = u * 1024 + tid;
             const int64_t p = off + (i < m ? i : 0);
 #pragma unroll
             for (int d = 0; d < 3; ++d) xs[u][d] = x[3 * p + d];
         }
+        uint64_t lmin = ~0ull, lmax = 0;
 #pragma unroll
-        for (int u = 0; u < RU; ++u) {
-            const int i = i0 + u * 1024;
-            if (i >= m) break;
-            const uint64_t key = radius_key<TX, TD>(xs[u], c, a);
-            lmin = key < lmin ? key : lmin;
-            lmax = key > lmax ? key : lmax;
-            if (cached) kc[i] = key; else a.scratch[off + i] = key;
+        for (int u = 0; u < KR; ++u) {
+            const int i = u * 1024 + tid;
+            key[u] = i < m ? radius_key<TX, TD>(xs[u], c, a) : ~0ull;
+            if (i < m) { lmin = key[u] < lmin ? key[u] : lmin; lmax = key[u] > lmax ? key[u] : lmax; }
         }
-    }
-    if (threadIdx.x < m) { atomicMin(&s_min, lmin); atomicMax(&s_max, lmax); }
-    __syncthreads();
-#define KEY(i) (cached ? kc[i] : a.scratch[off + (i)])
-    if (k == m) {
-        for (int i = threadIdx.x; i < m; i += 1024) { sk[i] = KEY(i); si[i] = i; }
-    } else {
-        // MSB-first radix select of the k-th smallest key.  Bits above the highest bit
-        // where the block's min and max keys differ are common and skipped; each pass
-        // histograms the next <= 8 bits of the keys still matching the fixed prefix.
-        // A pass whose chosen bin is taken whole ends the select early (inclusive bound
-        // hi); otherwise T = the exact k-th key and `need` ties to it are taken by
-        // position.
-        const uint64_t diff = s_min ^ s_max;
-        int lo_fixed = diff ? 64 - __clzll((long long)diff) : 0;    // bits below are free
-        uint64_t prefix = lo_fixed >= 64 ? 0ull : (s_min & ~((1ull << lo_fixed) - 1ull));
-        int need = k;
-        while (lo_fixed > 0) {
-            const int s = lo_fixed > 8 ? lo_fixed - 8 : 0;
-            const int w = lo_fixed - s;
-            for (int d = threadIdx.x; d < 256; d += 1024) hist[d] = 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t y = __shfl_xor(lmin, o), z = __shfl_xor(lmax, o);
+            lmin = y < lmin ? y : lmin;
+            lmax = z > lmax ? z : lmax;
+        }
+        if (lane == 0 && tid < m) { atomicMin(&s_min, lmin); atomicMax(&s_max, lmax); }
+        __syncthreads();
+        if (k == m) {
+#pragma unroll
+            for (int u = 0; u < KR; ++u) {
+                const int i = u * 1024 + tid;
+                if (i < m) { sk[i] = key[u]; si[i] = (uint32_t)i; }
+            }
+        } else {
+            const uint64_t diff = s_min ^ s_max;
+            const int lo_fixed = diff ? 64 - __clzll((long long)diff) : 0;
+            const int sh = lo_fixed > HB ? lo_fixed - HB : 0;
+            const uint32_t mask = (1u << (lo_fixed - sh)) - 1u;
+            // every key shares the bits above lo_fixed: its digit is (key >> sh) & mask
+#pragma unroll
+            for (int u = 0; u < KR; ++u)
+                if (u * 1024 + tid < m) atomicAdd(&hist[(key[u] >> sh) & mask], 1);
             __syncthreads();
-            for (int i = threadIdx.x; i < m; i += 1024) {
-                const uint64_t key = KEY(i);
-                if (lo_fixed >= 64 || (key >> lo_fixed) == (prefix >> lo_fixed))
-                    atomicAdd(&hist[(key >> s) & ((1u << w) - 1u)], 1);
+            // the digit B where the running count reaches k (4 bins per thread)
+            int h4[4], sum = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { h4[q] = hist[4 * tid + q]; sum += h4[q]; }
+            int tot;
+            const int ex = block_scan<1024, int>(sum, wsum, tot);
+            if (ex < k && ex + sum >= k) {
+                int acc = ex, q = 0;
+                for (; q < 3; ++q) {
+                    if (acc + h4[q] >= k) break;
+                    acc += h4[q];
+                }
+                s_bin = 4 * tid + q;
+                s_cum = acc + h4[q];
             }
             __syncthreads();
-            if (threadIdx.x < 64) {
-                // wave 0 finds the bin holding the need-th key: 4 bins per lane, a wave
-                // prefix sum, the first lane whose running count reaches `need`
-                const int l = threadIdx.x;
-                const int h0 = hist[4 * l], h1 = hist[4 * l + 1], h2 = hist[4 * l + 2],
-                          h3 = hist[4 * l + 3];
-                const int sum = h0 + h1 + h2 + h3;
-                int incl = sum;
+            const uint32_t B = (uint32_t)s_bin;
+            fast = s_cum <= SC;
+            if (fast) {
 #pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const int y = __shfl_up(incl, o);
-                    if (l >= o) incl += y;
-                }
-                const uint64_t hitm = __ballot(incl >= need);
-                if (l == __ffsll((unsigned long long)hitm) - 1) {
-                    int acc = incl - sum, q = 0;
-                    const int hs[4] = {h0, h1, h2, h3};
-                    for (; q < 3; ++q) {
-                        if (acc + hs[q] >= need) break;
-                        acc += hs[q];
+                for (int u = 0; u < KR; ++u) {
+                    const int i = u * 1024 + tid;
+                    if (i < m && ((key[u] >> sh) & mask) <= B) {
+                        const int p = atomicAdd(&s_cnt, 1);
+                        sk[p] = key[u];
+                        si[p] = (uint32_t)i;
                     }
-                    s_prefix = prefix | ((uint64_t)(4 * l + q) << s);
-                    s_need = need - acc;
-                    s_done = hs[q] == need - acc;          // the whole bin is selected
                 }
-            }
-            __syncthreads();
-            prefix = s_prefix;
-            need = s_need;
-            lo_fixed = s;
-            if (s_done) break;
-        }
-        if (lo_fixed > 0) {                  // early end: every key <= hi, exactly k of them
-            const uint64_t hi = prefix | ((1ull << lo_fixed) - 1ull);
-            for (int i = threadIdx.x; i < m; i += 1024) {
-                const uint64_t key = KEY(i);
-                if (key <= hi) {
-                    const int p = atomicAdd(&s_cnt, 1);
-                    sk[p] = key;
-                    si[p] = (uint32_t)i;
-                }
-            }
-            need = 0;
-        }
-        const uint64_t T = prefix;
-        if (need > 0) {
-            for (int i = threadIdx.x; i < m; i += 1024) {
-                const uint64_t key = KEY(i);
-                if (key < T) {
-                    const int p = atomicAdd(&s_cnt, 1);
-                    sk[p] = key;
-                    si[p] = (uint32_t)i;
+            } else {
+                // too many keys at the threshold digit: the exact select, from global
+#pragma unroll
+                for (int u = 0; u < KR; ++u) {
+                    const int i = u * 1024 + tid;
+                    if (i < m) a.scratch[off + i] = key[u];
                 }
             }
         }
         __syncthreads();
-        const int lt = s_cnt;                      // = k - need
-        int taken = 0;                             // ties to T: lowest positions first
-        for (int i0 = 0; i0 < m && taken < need; i0 += 1024) {
-            const int i = i0 + threadIdx.x;
-            const int f = (i < m && KEY(i) == T) ? 1 : 0;
-            int tot;
-            const int ex = block_scan<1024, int>(f, wsum, tot);
-            if (f && taken + ex < need) { sk[lt + taken + ex] = T; si[lt + taken + ex] = (uint32_t)i; }
-            taken += tot;
+    } else {
+        // larger blocks: keys through global scratch, four particles per thread per
+        // trip (their coordinate loads all in flight before the first radius)
+        uint64_t lmin = ~0ull, lmax = 0;
+        constexpr int RU = 4;
+        for (int i0 = tid; i0 < m; i0 += 1024 * RU) {
+            TX xs[RU][3];
+#pragma unroll
+            for (int u = 0; u < RU; ++u) {
+                const int i = i0 + u * 1024;
+                const int64_t p = off + (i < m ? i : 0);
+#pragma unroll
+                for (int d = 0; d < 3; ++d) xs[u][d] = x[3 * p + d];
+            }
+#pragma unroll
+            for (int u = 0; u < RU; ++u) {
+                const int i = i0 + u * 1024;
+                if (i >= m) break;
+                const uint64_t kk = radius_key<TX, TD>(xs[u], c, a);
+                lmin = kk < lmin ? kk : lmin;
+                lmax = kk > lmax ? kk : lmax;
+                a.scratch[off + i] = kk;
+            }
         }
+        if (tid < m) { atomicMin(&s_min, lmin); atomicMax(&s_max, lmax); }
+        __syncthreads();
     }
+    const int n_sorted = (fast && k < m) ? s_cnt : k;
+    if (!fast) {
+#define KEY(i) a.scratch[off + (i)]
+        if (k == m) {
+            for (int i = tid; i < m; i += 1024) { sk[i] = KEY(i); si[i] = i; }
+        } else {
+            // MSB-first radix select of the k-th smallest key.  Bits above the highest
+            // bit where the block's min and max keys differ are common and skipped; each
+            // pass histograms the next <= 8 bits of the keys still matching the fixed
+            // prefix.  A pass whose chosen bin is taken whole ends the select early
+            // (inclusive bound hi); otherwise T = the exact k-th key and `need` ties to
+            // it are taken by position.
+            const uint64_t diff = s_min ^ s_max;
+            int lo_fixed = diff ? 64 - __clzll((long long)diff) : 0;    // bits below are free
+            uint64_t prefix = lo_fixed >= 64 ? 0ull : (s_min & ~((1ull << lo_fixed) - 1ull));
+            int need = k;
+            while (lo_fixed > 0) {
+                const int s = lo_fixed > 8 ? lo_fixed - 8 : 0;
+                const int w = lo_fixed - s;
+                for (int d = tid; d < 256; d += 1024) hist[d] = 0;
+                __syncthreads();
+                for (int i = tid; i < m; i += 1024) {
+                    const uint64_t kk = KEY(i);
+                    if (lo_fixed >= 64 || (kk >> lo_fixed) == (prefix >> lo_fixed))
+                        atomicAdd(&hist[(kk >> s) & ((1u << w) - 1u)], 1);
+                }
+                __syncthreads();
+                if (tid < 64) {
+                    // wave 0 finds the bin holding the need-th key: 4 bins per lane, a
+                    // wave prefix sum, the first lane whose running count reaches `need`
+                    const int l = tid;
+                    const int h0 = hist[4 * l], h1 = hist[4 * l + 1], h2 = hist[4 * l + 2],
+                              h3 = hist[4 * l + 3];
+                    const int sum = h0 + h1 + h2 + h3;
+                    int incl = sum;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const int y = __shfl_up(incl, o);
+                        if (l >= o) incl += y;
+                    }
+                    const uint64_t hitm = __ballot(incl >= need);
+                    if (l == __ffsll((unsigned long long)hitm) - 1) {
+                        int acc = incl - sum, q = 0;
+                        const int hs[4] = {h0, h1, h2, h3};
+                        for (; q < 3; ++q) {
+                            if (acc + hs[q] >= need) break;
+                            acc += hs[q];
+                        }
+                        s_prefix = prefix | ((uint64_t)(4 * l + q) << s);
+                        s_need = need - acc;
+                        s_done = hs[q] == need - acc;          // the whole bin is selected
+                    }
+                }
+                __syncthreads();
+                prefix = s_prefix;
+                need = s_need;
+                lo_fixed = s;
+                if (s_done) break;
+            }
+            if (lo_fixed > 0) {                  // early end: every key <= hi, exactly k of them
+                const uint64_t hi = prefix | ((1ull << lo_fixed) - 1ull);
+                for (int i = tid; i < m; i += 1024) {
+                    const uint64_t kk = KEY(i);
+                    if (kk <= hi) {
+                        const int p = atomicAdd(&s_cnt, 1);
+                        sk[p] = kk;
+                        si[p] = (uint32_t)i;
+                    }
+                }
+                need = 0;
+            }
+            const uint64_t T = prefix;
+            if (need > 0) {
+                for (int i = tid; i < m; i += 1024) {
+                    const uint64_t kk = KEY(i);
+                    if (kk < T) {
+                        const int p = atomicAdd(&s_cnt, 1);
+                        sk[p] = kk;
+                        si[p] = (uint32_t)i;
+                    }
+                }
+            }
+            __syncthreads();
+            const int lt = s_cnt;                      // = k - need
+            int taken = 0;                             // ties to T: lowest positions first
+            for (int i0 = 0; i0 < m && taken < need; i0 += 1024) {
+                const int i = i0 + tid;
+                const int f = (i < m && KEY(i) == T) ? 1 : 0;
+                int tt;
+                const int e = block_scan<1024, int>(f, wsum, tt);
+                if (f && taken + e < need) { sk[lt + taken + e] = T; si[lt + taken + e] = (uint32_t)i; }
+                taken += tt;
+            }
+        }
 #undef KEY
+    }
     __syncthreads();
     int P = 1;
-    while (P < k) P <<= 1;
-    for (int i = k + threadIdx.x; i < P; i += 1024) { sk[i] = ~0ull; si[i] = 0xFFFFFFFFu; }
+    while (P < n_sorted) P <<= 1;
+    for (int i = n_sorted + tid; i < P; i += 1024) { sk[i] = ~0ull; si[i] = 0xFFFFFFFFu; }
     __syncthreads();
     bitonic_pairs<1024>(sk, si, P);
     const int64_t o = a.out_offsets[h];
-    for (int r = threadIdx.x; r < k; r += 1024) {
+    for (int r = tid; r < k; r += 1024) {
         const int64_t src = off + si[r];
         if (a.id_bytes == 8)
             static_cast<uint64_t *>(a.out_ids)[o + r] = static_cast<const uint64_t *>(a.ids)[src];

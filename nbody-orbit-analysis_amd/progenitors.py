@@ -89,10 +89,10 @@ class CentralIds:
         self.dev = dev = _device()
         pos = np.asarray([np.asarray(halo_positions[k], dtype=np.float64) for k in range(nh)])
         plan = _box_plan(snapshot['box_size'], dx_dtype) if 'box_size' in snapshot else []
-        big = int(np.diff(offsets).max(initial=0)) > 8192
-        # every device buffer is held by self until the kernel has run
+        # every device buffer is held by self until the kernel has run; the radius-key
+        # scratch is touched only by blocks the register fast path cannot take
         self.x_d, self.ids_d = _dev(x, dev), _dev(ids, dev)
-        self.scratch = torch.empty(len(ids) if big else 1, dtype=torch.int64, device=dev)
+        self.scratch = torch.empty(max(len(ids), 1), dtype=torch.int64, device=dev)
         self.out = torch.empty(max(self.total * ids.itemsize // 4, 1), dtype=torch.int32, device=dev)
         self.pos_d, self.off_d, self.oo_d = _dev(pos, dev), _dev(offsets, dev), _dev(out_off, dev)
         a = N.CentralArgs(coords=_ptr(self.x_d), coord_f64=int(x.dtype == np.float64),
