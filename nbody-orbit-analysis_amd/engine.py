@@ -251,13 +251,13 @@ def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=No
     if prev_sets is not None and prev_idx is not None:
         pc = np.asarray(prev_idx, dtype=np.int64)[h]
         ok = (pc >= 0) & (K > 0)
-        pk = np.where(ok, prev_sets['K'][np.maximum(pc, 0)], 0)
+        pk = np.where(ok, prev_sets.K[np.maximum(pc, 0)], 0)
         inh = ok & (pk > 0)
         gpart[inh, 3] = 1
-        gpart[inh, 4] = prev_sets['base'][pc[inh]]
+        gpart[inh, 4] = prev_sets.base[pc[inh]]
         gpart[inh, 5] = pk[inh]
-        gpart[inh, 6] = int(prev_sets['cap'])
-        gpart[inh, 7] = prev_sets['cbase'][pc[inh]]
+        gpart[inh, 6] = int(prev_sets.cap)
+        gpart[inh, 7] = prev_sets.cbase[pc[inh]]
     fresh = (K > 0) & ~inh
     mean = p / np.maximum(K, 1)
     cap2 = np.where(fresh, np.ceil(mean + 8 * np.sqrt(mean) + 64), 0).astype(np.int64)

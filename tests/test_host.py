@@ -258,3 +258,39 @@ def test_resume_without_checkpoint_raises():
         track_orbits([0, 1, 2], [[0], [0], [0]], lambda s, h: (np.zeros((1, 3)), np.ones(1), None),
                      lambda s, p, r: dict(snap), out, resume=True, verbose=False,
                      engine=StubEngine())
+
+
+def test_plan_part_bucket_sets():
+    """Partition plan of the large halos (engine.plan_part): power-of-two K, the current
+    set's layout, and a previous step's bucket set inherited halo by halo (any K ratio);
+    a halo without one gets a fresh previous set and counters after the current ones."""
+    from types import SimpleNamespace
+    from orbitanalysis_amd.engine import plan_part, PART_SPREAD, GPART_W
+    cur = np.array([30000, 200000, 5000, 90000, 0])
+    prev = np.array([29000, 190000, -1, 88000, 10])
+    glob = {'h0': np.array([0, 1, 2, 3, 4])}
+    prev_idx = np.array([3, 0, -1, 2, 1])                    # previous halo numbers
+    ps = SimpleNamespace(K=np.array([64, 0, 16, 32]), base=np.array([0, -1, 64 * 4096, 80 * 4096]),
+                         cbase=np.array([0, 0, 64, 80]), cap=4096)
+    pl = plan_part(glob, cur, prev, 4096, 4096, prev_idx, ps)
+    K, g = pl['K'], pl['gpart']
+    assert g.shape == (5, GPART_W)
+    assert all(k == 0 or (k & (k - 1)) == 0 for k in K)
+    assert K[0] == max(PART_SPREAD, 16) and K[2] == 0 and K[4] > 0
+    assert np.all(K[K > 0] * 4096 * 0.9 >= cur[K > 0])
+    # current set: consecutive K * part_e runs, counters consecutive
+    assert np.array_equal(g[:, 0], (np.cumsum(K) - K) * 4096)
+    assert np.array_equal(g[:, 2], np.cumsum(K) - K)
+    # halo 0 inherits previous halo 3 (K 32), halo 3 previous halo 2 (K 16); halo 1's
+    # progenitor (previous halo 0) is bucketed too; halo 4's (previous 1) is not
+    assert list(g[:, 3]) == [1, 1, 0, 1, 0]
+    assert g[0, 4] == 80 * 4096 and g[0, 5] == 32 and g[0, 6] == 4096 and g[0, 7] == 80
+    assert g[3, 4] == 64 * 4096 and g[3, 5] == 16 and g[3, 7] == 64
+    assert g[1, 5] == 64 and g[1, 7] == 0
+    # the fresh previous set of halo 4: K of its own, counters after the current ones
+    assert g[4, 5] == K[4] and g[4, 7] == K.sum() and g[4, 6] >= 10 / K[4]
+    assert pl['n_pcnt'] == K.sum() + K[4] and pl['n_prev'] == K[4] * g[4, 6]
+    assert list(pl['inherited']) == [True, True, False, True, False]
+    # every current partition listed once
+    pl_ok = pl['plist'][pl['plist'][:, 0] >= 0]
+    assert len(pl_ok) == K.sum() and len({tuple(r) for r in pl_ok}) == K.sum()
