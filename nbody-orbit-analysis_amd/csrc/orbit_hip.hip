@@ -2107,7 +2107,8 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
                 const TD dt = dot3(qrh[u].x, qrh[u].y, qrh[u].z, crh[u].x, crh[u].y, crh[u].z);
                 const uint16_t acc = angle_add((uint16_t)(qmeta[u] & 0xFFFFu), acos_td(dt));
                 cmeta[hit[u] & 0x3FFFFFFFu] = (uint32_t)(flag ? 0u : acc) | (sc << 16);
-                if (flag) mark[qpos[u]] = 0x10000u | acc;
+                // an inherited set's position words carry the sign in bits 30-31
+                if (flag) mark[qpos[u] & 0x3FFFFFFFu] = 0x10000u | acc;
             }
             if (j0 == 0 && q == 0) PSTAMP(4);
         }
