@@ -414,6 +414,9 @@ class SnapshotState:
 
 @dataclass
 class StepResult:
+    """A compare step's records.  They live in one of the engine's two workspaces and
+    are valid until the step after next reuses it: ``fetch`` / ``fetch_async`` of an
+    older result raise instead of returning another snapshot's records."""
     n_slots: int
     has_prog: np.ndarray                       # bool per current halo
     offsets: Optional[torch.Tensor] = None     # device int64 [n_slots+1]
@@ -423,6 +426,13 @@ class StepResult:
     halos: Optional[torch.Tensor] = None       # device halo table (bulk written on device)
     apsis_pos: Optional[torch.Tensor] = None   # device int32 previous-state rows (optional)
     extra: dict = field(default_factory=dict)
+    ws: object = None                          # the workspace holding the records
+    gen: int = 0                               # its launch count when they were written
+
+    def check_fresh(self):
+        if self.ws is not None and self.ws.gen != self.gen:
+            raise RuntimeError('StepResult is stale: its workspace was reused by a later '
+                               'step (fetch a result before the step after next)')
 
 
 @dataclass
@@ -478,6 +488,7 @@ class Workspace:
         self.halo_count = e(n_slots, torch.int32)
         self.item_count = e(n_items, torch.int32)
         self.status = e(1, torch.int32)
+        self.gen = 0                        # launches that wrote this workspace
         self.offsets = e(n_slots + 1, torch.int64)
         self.out_ids = e(n_prev, id_torch_dtype)
         self.out_ang = e(n_prev, torch.int16)
@@ -827,6 +838,8 @@ class OrbitEngine:
                                                     p.meta.data_ptr())
             a.n_prev = pr.n_prev
             ws.reset(res.n_slots)
+            ws.gen += 1
+            res.ws, res.gen = ws, ws.gen
             a.scratch_ids, a.scratch_ang = ws.scratch_ids.data_ptr(), ws.scratch_ang.data_ptr()
             a.seg_count = ws.seg_count.data_ptr()
             a.halo_count, a.item_count, a.status = (ws.halo_count.data_ptr(),
@@ -865,6 +878,7 @@ class OrbitEngine:
         next snapshot's kernels write the other workspace), so the records' transfer is
         off the per-snapshot critical path.  The result's workspace must not be reused
         before ``wait()``: ``step`` alternates two."""
+        res.check_fresh()
         dev = self.device
         if getattr(self, '_copy_stream', None) is None:
             self._copy_stream = torch.cuda.Stream(device=dev)
@@ -895,6 +909,7 @@ class OrbitEngine:
         through page-locked buffers from torch's caching host allocator: one DMA each
         at the link rate instead of the staged pageable copy (~8 GB/s).  The returned
         arrays own their buffers (a block is reused only once they are gone)."""
+        res.check_fresh()
         offsets = res.offsets.cpu().numpy()
         total = int(offsets[-1]) if len(offsets) else 0
         if not total:

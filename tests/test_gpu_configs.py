@@ -39,7 +39,7 @@ def _run(gen, steps, eng):
         res = eng.step(snap, c[0], c[2], H, cos['redshift'], ex, s > 0)
         if s > 0:
             offs, ids, ang = eng.fetch(res, np.dtype(np.int64))
-            out.append(dict(offs=offs, ids=ids, ang=ang, meta=eng.prev.meta.clone()))
+            out.append(dict(offs=offs, ids=ids, ang=ang, meta=eng.state_meta().clone()))
         out_snap = snap
     return out, out_snap, H
 
