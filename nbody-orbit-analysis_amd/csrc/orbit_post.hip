@@ -353,10 +353,34 @@ __device__ __forceinline__ uint64_t radius_key(const TX (&x)[3], const double *c
 constexpr int KR = 12;                     // k_central: radius keys per thread in registers
 constexpr int HB = 12;                     // k_central: digit bits of the threshold pass
 
+// rank of every candidate by (key, position) among the n of them (n <= 1024, one
+// candidate per thread, keys broadcast from LDS): the sorted order without a sorting
+// network's log^2 barriers
+__device__ __forceinline__ void rank_pairs(const uint64_t *s, const uint32_t *x, int n,
+                                           uint64_t *ds, uint32_t *dx) {
+    const int t = threadIdx.x;
+    if (t < n) {
+        const uint64_t k = s[t];
+        const uint32_t i = x[t];
+        int r = 0;
+        for (int j = 0; j < n; ++j) {
+            const uint64_t kj = s[j];
+            r += (kj < k || (kj == k && x[j] < i)) ? 1 : 0;
+        }
+        ds[r] = k;
+        dx[r] = i;
+    }
+}
+
+// <= 64 VGPRs: two 1024-thread work-groups per CU, so one's barriers and sort overlap
+// the other's loads
 template <typename TX, typename TD>
-__global__ __launch_bounds__(1024) void k_central(const oa_central_args a) {
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)))
+void k_central(const oa_central_args a) {
     __shared__ uint64_t sk[SC];
     __shared__ uint32_t si[SC];
+    __shared__ uint64_t rk[1024];              // candidates in rank order (n <= 1024)
+    __shared__ uint32_t ri[1024];
     __shared__ int hist[1 << HB];
     __shared__ int wsum[17];
     __shared__ uint64_t s_prefix;
@@ -381,20 +405,27 @@ __global__ __launch_bounds__(1024) void k_central(const oa_central_args a) {
         // smallest; when those are <= SC they are sorted by (key, position) in LDS and
         // the first k taken -- the same k keys, in the same order, as the exact select
         // below, in one pass over the keys instead of up to eight.
-        TX xs[KR][3];
-#pragma unroll
-        for (int u = 0; u < KR; ++u) {
-            const int i = u * 1024 + tid;
-            const int64_t p = off + (i < m ? i : 0);
-#pragma unroll
-            for (int d = 0; d < 3; ++d) xs[u][d] = x[3 * p + d];
-        }
         uint64_t lmin = ~0ull, lmax = 0;
+        constexpr int LU = 4;                  // particles per thread with loads in flight
 #pragma unroll
-        for (int u = 0; u < KR; ++u) {
-            const int i = u * 1024 + tid;
-            key[u] = i < m ? radius_key<TX, TD>(xs[u], c, a) : ~0ull;
-            if (i < m) { lmin = key[u] < lmin ? key[u] : lmin; lmax = key[u] > lmax ? key[u] : lmax; }
+        for (int u0 = 0; u0 < KR; u0 += LU) {
+            TX xs[LU][3];
+#pragma unroll
+            for (int u = 0; u < LU; ++u) {
+                const int i = (u0 + u) * 1024 + tid;
+                const int64_t p = off + (i < m ? i : 0);
+#pragma unroll
+                for (int d = 0; d < 3; ++d) xs[u][d] = x[3 * p + d];
+            }
+#pragma unroll
+            for (int u = 0; u < LU; ++u) {
+                const int i = (u0 + u) * 1024 + tid;
+                key[u0 + u] = i < m ? radius_key<TX, TD>(xs[u], c, a) : ~0ull;
+                if (i < m) {
+                    lmin = key[u0 + u] < lmin ? key[u0 + u] : lmin;
+                    lmax = key[u0 + u] > lmax ? key[u0 + u] : lmax;
+                }
+            }
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
@@ -582,14 +613,21 @@ __global__ __launch_bounds__(1024) void k_central(const oa_central_args a) {
 #undef KEY
     }
     __syncthreads();
-    int P = 1;
-    while (P < n_sorted) P <<= 1;
-    for (int i = n_sorted + tid; i < P; i += 1024) { sk[i] = ~0ull; si[i] = 0xFFFFFFFFu; }
+    const uint32_t *order = si;
+    if (n_sorted <= 1024) {
+        rank_pairs(sk, si, n_sorted, rk, ri);
+        order = ri;
+    } else {
+        int P = 1;
+        while (P < n_sorted) P <<= 1;
+        for (int i = n_sorted + tid; i < P; i += 1024) { sk[i] = ~0ull; si[i] = 0xFFFFFFFFu; }
+        __syncthreads();
+        bitonic_pairs<1024>(sk, si, P);
+    }
     __syncthreads();
-    bitonic_pairs<1024>(sk, si, P);
     const int64_t o = a.out_offsets[h];
     for (int r = tid; r < k; r += 1024) {
-        const int64_t src = off + si[r];
+        const int64_t src = off + order[r];
         if (a.id_bytes == 8)
             static_cast<uint64_t *>(a.out_ids)[o + r] = static_cast<const uint64_t *>(a.ids)[src];
         else
