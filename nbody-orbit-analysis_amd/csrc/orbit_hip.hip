@@ -1715,6 +1715,9 @@ constexpr int GPART_W = 16;             // int64 per gpart row (orbit_hip.h)
 #ifndef OA_SCAT_PER
 #define OA_SCAT_PER 4       // k_part_scatter: particles per thread per staged sub-chunk
 #endif
+#ifndef OA_SCAT_NT
+#define OA_SCAT_NT 1        // k_part_scatter: bucket IDs / position / state words stored non-temporally
+#endif
 constexpr int SCAT_WG = 256, SCAT_PER = OA_SCAT_PER, SCAT_NS = SCAT_WG * SCAT_PER;
 static_assert(PART_E - 1 <= (int)MAX_POS, "partition entries must fit the slot position field");
 static_assert(PART_KMAX <= 65536, "staged partition numbers are 16-bit");
@@ -1887,10 +1890,14 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
             const uint32_t e = gres[k] + (uint32_t)(s - lrun[k]);
             if (e < bcap) {                             // an overflow is reported by the join
                 const int64_t o = (int64_t)k * bcap + e;
-                __builtin_nontemporal_store(skey[s], &bkey[o]);
-                __builtin_nontemporal_store(spw[s], &bpos[o]);
-                __builtin_nontemporal_store(smeta[s], &bmeta[o]);
                 TD *d = brh + 3 * o;
+                if (OA_SCAT_NT) {
+                    __builtin_nontemporal_store(skey[s], &bkey[o]);
+                    __builtin_nontemporal_store(spw[s], &bpos[o]);
+                    __builtin_nontemporal_store(smeta[s], &bmeta[o]);
+                } else {
+                    bkey[o] = skey[s]; bpos[o] = spw[s]; bmeta[o] = smeta[s];
+                }
                 d[0] = srh[3 * s]; d[1] = srh[3 * s + 1]; d[2] = srh[3 * s + 2];
             }
         }

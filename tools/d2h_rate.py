@@ -1,0 +1,75 @@
+"""D2H rate of device -> page-locked host copies on this box (why the batch driver's
+record fetch runs at ~20-26 GB/s): torch's pinned tensors
+(hipHostMalloc default flags: coherent) against hipHostMalloc(..., NonCoherent), one
+copy alone and back to back, for the sizes one snapshot's apsis records take.
+
+  python tools/d2h_rate.py
+"""
+import ctypes
+import json
+import time
+
+import torch
+
+HIP_NONCOHERENT = 0x80000000
+HIP_D2H = 2
+
+
+def main():
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    hip = ctypes.CDLL('libamdhip64.so')
+    hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                   ctypes.c_void_p]
+    hip.hipHostFree.argtypes = [ctypes.c_void_p]
+    out = []
+    for mb in (4, 16, 64, 100, 256):
+        n = mb << 20
+        src = torch.empty(n, dtype=torch.uint8, device=dev).fill_(7)
+        res = {'MiB': mb}
+        pin = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        for rep in range(4):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            pin.copy_(src, non_blocking=True)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+        res['torch_pinned_GBs'] = n / dt / 1e9
+        p = ctypes.c_void_p()
+        assert hip.hipHostMalloc(ctypes.byref(p), n, HIP_NONCOHERENT) == 0
+        st = torch.cuda.current_stream().cuda_stream
+        for rep in range(4):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            assert hip.hipMemcpyAsync(p, src.data_ptr(), n, HIP_D2H, st) == 0
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+        res['noncoherent_GBs'] = n / dt / 1e9
+        # two halves on two streams at once (two DMA engines?)
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        for rep in range(4):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            with torch.cuda.stream(s1):
+                pin[:n // 2].copy_(src[:n // 2], non_blocking=True)
+            with torch.cuda.stream(s2):
+                pin[n // 2:].copy_(src[n // 2:], non_blocking=True)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+        res['torch_pinned_2streams_GBs'] = n / dt / 1e9
+        # H2D for comparison
+        for rep in range(4):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            src.copy_(pin, non_blocking=True)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+        res['h2d_pinned_GBs'] = n / dt / 1e9
+        hip.hipHostFree(p)
+        out.append(res)
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == '__main__':
+    main()

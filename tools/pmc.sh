@@ -7,7 +7,7 @@ i=0
 while read -r counters; do
   [ -z "$counters" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $counters --kernel-include-regex 'k_step' --output-format csv \
+  timeout -k 10 300 rocprofv3 --pmc $counters --kernel-include-regex "${KREGEX:-k_step}" --output-format csv \
       -d "$O/p$i" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} \
       > "$O/p$i.out" 2> "$O/p$i.err"
   rc=$?; echo "pass $i ($counters) rc=$rc"
