@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OA_ABI_VERSION 10
+#define OA_ABI_VERSION 11
 
 #define OA_OK 0
 #define OA_E_ARG (-1)       /* invalid argument / unsupported dtype plan */
@@ -217,6 +217,10 @@ typedef struct oa_step_args {
                                    zeroed by oa_step                                  */
     int64_t gmark_base;         /* scratch_off of the first global item (gmark[0])    */
     int64_t gmark_n;            /* marks (padded previous positions of global items)  */
+    const int64_t *gchunk3;     /* the previous chunks k_part_scatter reads: those of
+                                   halos with a fresh previous set (NULL: gchunk2)    */
+    int32_t n_gchunk3;
+    int32_t reserved3;
 } oa_step_args;
 
 /* Arguments of oa_part_unbucket: a bucket set's entries back to position order. */

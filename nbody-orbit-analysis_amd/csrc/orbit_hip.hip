@@ -1705,12 +1705,18 @@ __global__ __launch_bounds__(BIG_WG) void k_big_join(const oa_step_args a) {
 //                   previous position
 //   k_part_emit     64-position segments of the previous blocks: marks -> records in
 //                   previous-block order (:315-316), packed per segment as k_big_join
-constexpr int PART_E = 4096;            // current entries of one partition, at most
-constexpr int PART_S = 6144;            // LDS table slots, at most
+#ifndef OA_PART_E
+#define OA_PART_E 4096
+#endif
+constexpr int PART_E = OA_PART_E;       // current entries of one partition, at most
+constexpr int PART_S = PART_E + PART_E / 2;   // LDS table slots, at most
 // 512 threads, <= 128 VGPRs and ~58 KB of LDS: two join work-groups per CU, so one's
 // table build overlaps the other's streaming
 constexpr int PART_KMAX = 4096;         // partitions of one halo (scatter's LDS counters)
-constexpr int PART_WG = 512;
+#ifndef OA_PART_WG
+#define OA_PART_WG 512
+#endif
+constexpr int PART_WG = OA_PART_WG;
 constexpr int GPART_W = 16;             // int64 per gpart row (orbit_hip.h)
 #ifndef OA_SCAT_PER
 #define OA_SCAT_PER 4       // k_part_scatter: particles per thread per staged sub-chunk
@@ -1769,7 +1775,7 @@ template <typename TX, typename TV, typename TD, int IDB, bool CUR>
 __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK &fk, char *lds,
                                              int64_t chunk) {
     typedef typename IdT<IDB>::T ID;
-    const int64_t *ch = (CUR ? a.gchunk1 : a.gchunk2) + 3 * chunk;
+    const int64_t *ch = (CUR ? a.gchunk1 : (a.gchunk3 ? a.gchunk3 : a.gchunk2)) + 3 * chunk;
     const int64_t gi = ch[0], start = ch[1], cnt = ch[2];
     const oa_item it = a.items[gi];
     const oa_halo &h = a.halos[it.h0];
@@ -1911,7 +1917,8 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
 template <typename TX, typename TV, typename TD, int IDB>
 __global__ __launch_bounds__(SCAT_WG) void k_part_scatter(const oa_step_args a, const FrameK fk) {
     extern __shared__ __attribute__((aligned(16))) char slds[];
-    const int64_t b = blockIdx.x, n1 = a.n_gchunk1, n2 = a.n_gchunk2;
+    const int64_t b = blockIdx.x, n1 = a.n_gchunk1,
+                  n2 = a.gchunk3 ? a.n_gchunk3 : a.n_gchunk2;
     const int64_t m = n1 < n2 ? n1 : n2;
     bool cur;
     int64_t c;
@@ -2210,11 +2217,13 @@ int launch_part(const oa_step_args &a, hipStream_t st) {
     if (hipMemsetAsync(a.pcnt, 0, (size_t)a.n_pcnt * 4, st) != hipSuccess ||
         (a.gmark_n > 0 && hipMemsetAsync(a.gmark, 0, (size_t)a.gmark_n * 4, st) != hipSuccess))
         return fail(OA_E_LAUNCH, "oa_step: partition counters / marks reset");
-    if (a.n_gchunk1 + a.n_gchunk2 > 0) {
+    // previous chunks to scatter: those of halos without an inherited set (gchunk3)
+    const int64_t n_scat = a.n_gchunk1 + (a.gchunk3 ? a.n_gchunk3 : a.n_gchunk2);
+    if (n_scat > 0) {
         auto k = k_part_scatter<TX, TV, TD, IDB>;
         const int64_t lds = scat_lds_bytes(a.part_kmax, (int)sizeof(TD));
         if (int rc = set_lds(k, lds)) return rc;
-        hipLaunchKernelGGL(k, dim3((unsigned)(a.n_gchunk1 + a.n_gchunk2)), dim3(SCAT_WG), (size_t)lds,
+        hipLaunchKernelGGL(k, dim3((unsigned)n_scat), dim3(SCAT_WG), (size_t)lds,
                            st, a, make_frame_k(a));
         if (int rc = check_launch("k_part_scatter")) return rc;
     }

@@ -754,6 +754,12 @@ class OrbitEngine:
                                        cbase=cbase, cap=self.part_e, td_f64=plan.dx == F64)
                 if prev_sets is not None and pl['inherited'].any():
                     g['inherit'] = prev_sets           # keeps the previous set alive
+                    # the scatter reads only the previous chunks of fresh sets
+                    gi = np.asarray(ch2[:, 0], dtype=np.int64) - len(items)
+                    ch3 = ch2[~pl['inherited'][gi]]
+                    g['ch3'] = torch.from_numpy(np.ascontiguousarray(ch3)).to(dev) \
+                        if len(ch3) else None
+                    g['n3'] = len(ch3)
             elif compare:
                 g['keys'] = torch.empty(2 * total, dtype=torch.int64, device=dev)
             g['n1'], g['n2'] = len(ch1), len(ch2)
@@ -803,6 +809,11 @@ class OrbitEngine:
                 a.pcnt, a.n_pcnt = g['pcnt'].data_ptr(), int(g['pcnt'].numel())
                 a.gmark, a.gmark_base, a.gmark_n = (g['gmark'].data_ptr(), g['gmark_base'],
                                                     g['gmark_n'])
+                if 'n3' in g:
+                    # a non-NULL pointer marks the list as given, even when empty
+                    a.gchunk3 = g['ch3'].data_ptr() if g['ch3'] is not None else \
+                        g['gpart'].data_ptr()
+                    a.n_gchunk3 = g['n3']
         a.H, a.one_plus_z = float(H), float(1 + z)
         a.n_box_dims = len(plan.box)
         for d, L in enumerate(plan.box):

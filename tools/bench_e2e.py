@@ -72,7 +72,8 @@ def main():
     torch.cuda.empty_cache()
     # per-phase host time of the driver's engine calls (tool-side instrumentation)
     from orbitanalysis_amd.engine import OrbitEngine
-    phase = {'prepare': [], 'launch+status': [], 'fetch': []}
+    phase = {'prepare': [], 'launch+status': [], 'fetch': [], 'fetch_async': [],
+             'wait': [], 'save': []}
 
     def timed(name, fn):
         def w(*a, **k):
@@ -83,6 +84,10 @@ def main():
         return w
     OrbitEngine.prepare = timed('prepare', OrbitEngine.prepare)
     OrbitEngine.fetch = timed('fetch', OrbitEngine.fetch)
+    OrbitEngine.fetch_async = timed('fetch_async', OrbitEngine.fetch_async)
+    from orbitanalysis_amd import engine as E, track_orbits as TO
+    E.PendingFetch.wait = timed('wait', E.PendingFetch.wait)
+    TO.save_to_file = timed('save', TO.save_to_file)
     _launch = OrbitEngine.launch
 
     def launch(self, pr, ws, *a, **k):
