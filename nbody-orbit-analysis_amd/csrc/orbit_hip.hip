@@ -1930,9 +1930,16 @@ __global__ __launch_bounds__(SCAT_WG) void k_part_scatter(const oa_step_args a, 
     SSTAMP(1);
 }
 
+#ifndef OA_JOIN_RSTAGE
+#define OA_JOIN_RSTAGE 0    // k_part_join: the current bucket's r̂ staged in LDS (not gathered)
+#endif
+constexpr bool JRS = OA_JOIN_RSTAGE != 0;
+
 // LDS of one k_part_join work-group for a partition capacity of e entries, s slots
-__host__ __device__ inline int64_t part_lds_bytes(int e, int sl) {
-    return (int64_t)sl * 8 + (int64_t)(e / 4) * 8 + (int64_t)STASH * 8 + 16;
+// (td_bytes: the r̂ dtype, for the staged current r̂ of JRS builds)
+__host__ __device__ inline int64_t part_lds_bytes(int e, int sl, int td_bytes = 8) {
+    return (int64_t)sl * 8 + (int64_t)(e / 4) * 8 + (int64_t)STASH * 8 + 16 +
+           (JRS ? (int64_t)3 * e * td_bytes : 0);
 }
 
 // One work-group per current partition: LDS cuckoo table of its current bucket, then
@@ -1948,6 +1955,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     uint64_t *pend = slots + PS;                                        // [PE / 4]
     uint64_t *stash = pend + PE / 4;                                    // [STASH]
     uint32_t *flags = reinterpret_cast<uint32_t *>(stash + STASH);      // npend, nstash, overflow, nonuniform
+    TD *crl = reinterpret_cast<TD *>(flags + 4);                        // [3 PE] (JRS)
     const int tid = threadIdx.x;
     PSTAMP(0);
     const int32_t g = a.plist[2 * blockIdx.x], pp = a.plist[2 * blockIdx.x + 1];
@@ -1987,6 +1995,11 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
         ckey[u] = i < nc ? ck[i] : 0ull;
         cpw[u] = i < nc ? cp[i] : 0u;
     }
+    const TD *crh0 = static_cast<const TD *>(a.prh_cur) + 3 * cb;
+    if (JRS) {
+        // the bucket's current r̂, one coalesced sweep, straight into LDS
+        for (uint32_t w = tid; w < 3 * nc; w += PART_WG) crl[w] = crh0[w];
+    }
     uint64_t qkey[PU];
     uint32_t qpos[PU], qmeta[PU];
     V3<TD> qrh[PU];
@@ -2003,7 +2016,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     };
     load_prev(qk0 + (int64_t)q0 * pcap, qp0 + (int64_t)q0 * pcap, qm0 + (int64_t)q0 * pcap,
               qr0 + 3 * (int64_t)q0 * pcap, qcnt[q0], 0u);
-    uint32_t nsl = nc + nc / 2u + 64u;
+    uint32_t nsl = 2u * nc + 64u;                      // load <= 1/2 where the LDS allows
     nsl = nsl < PS ? nsl : PS;
     for (uint32_t w = tid; w < nsl; w += PART_WG) slots[w] = 0ull;
     if (tid < 4) flags[tid] = 0u;
@@ -2069,7 +2082,6 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     }
     const bool nonuniform = IDB == 8 && flags[3] != 0u;
     const uint32_t nstash = min(flags[1], (uint32_t)STASH);
-    const TD *crh0 = static_cast<const TD *>(a.prh_cur) + 3 * cb;
     uint32_t *cmeta = a.pmeta_cur + cb;
     uint32_t *mark = a.gmark + (it.scratch_off - a.gmark_base);
     // previous entries, PU per thread: lookups, then the gathers of the matched current
@@ -2109,7 +2121,11 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
             V3<TD> crh[PU];
 #pragma unroll
             for (int u = 0; u < PU; ++u)
-                if (hit[u] != 0xFFFFFFFFu) crh[u] = ld3(crh0, hit[u] & 0x3FFFFFFFu);
+                if (hit[u] != 0xFFFFFFFFu) {
+                    const uint32_t e = hit[u] & 0x3FFFFFFFu;
+                    if (JRS) crh[u] = V3<TD>{crl[3 * e], crl[3 * e + 1], crl[3 * e + 2]};
+                    else crh[u] = ld3(crh0, e);
+                }
 #pragma unroll
             for (int u = 0; u < PU; ++u) {
                 if (hit[u] == 0xFFFFFFFFu) continue;
@@ -2229,7 +2245,7 @@ int launch_part(const oa_step_args &a, hipStream_t st) {
     }
     if (a.n_parts > 0) {
         auto k = k_part_join<TD, IDB>;
-        const int64_t lds = part_lds_bytes(a.part_e, a.part_slots);
+        const int64_t lds = part_lds_bytes(a.part_e, a.part_slots, (int)sizeof(TD));
         if (int rc = set_lds(k, lds)) return rc;
         hipLaunchKernelGGL(k, dim3((unsigned)a.n_parts), dim3(PART_WG), (size_t)lds, st, a);
         if (int rc = check_launch("k_part_join")) return rc;
