@@ -1900,9 +1900,11 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
                 if (OA_SCAT_NT) {
                     __builtin_nontemporal_store(skey[s], &bkey[o]);
                     __builtin_nontemporal_store(spw[s], &bpos[o]);
-                    __builtin_nontemporal_store(smeta[s], &bmeta[o]);
+                    // a current entry's state word is the join's (k_part_join stages them)
+                    if (!CUR) __builtin_nontemporal_store(smeta[s], &bmeta[o]);
                 } else {
-                    bkey[o] = skey[s]; bpos[o] = spw[s]; bmeta[o] = smeta[s];
+                    bkey[o] = skey[s]; bpos[o] = spw[s];
+                    if (!CUR) bmeta[o] = smeta[s];
                 }
                 d[0] = srh[3 * s]; d[1] = srh[3 * s + 1]; d[2] = srh[3 * s + 2];
             }
@@ -1938,7 +1940,9 @@ constexpr bool JRS = OA_JOIN_RSTAGE != 0;
 // LDS of one k_part_join work-group for a partition capacity of e entries, s slots
 // (td_bytes: the r̂ dtype, for the staged current r̂ of JRS builds)
 __host__ __device__ inline int64_t part_lds_bytes(int e, int sl, int td_bytes = 8) {
-    return (int64_t)sl * 8 + (int64_t)(e / 4) * 8 + (int64_t)STASH * 8 + 16 +
+    // slots, then max(deferral list, the partition's state words), stash, flags
+    const int64_t mid = (int64_t)e * 4 > (int64_t)(e / 4) * 8 ? (int64_t)e * 4 : (int64_t)(e / 4) * 8;
+    return (int64_t)sl * 8 + mid + (int64_t)STASH * 8 + 16 +
            (JRS ? (int64_t)3 * e * td_bytes : 0);
 }
 
@@ -1953,7 +1957,9 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     const uint32_t PE = (uint32_t)a.part_e, PS = (uint32_t)a.part_slots;
     uint64_t *slots = reinterpret_cast<uint64_t *>(psm);               // [PS]
     uint64_t *pend = slots + PS;                                        // [PE / 4]
-    uint64_t *stash = pend + PE / 4;                                    // [STASH]
+    // after the walks: the partition's state words, over the deferral list
+    uint32_t *mlds = reinterpret_cast<uint32_t *>(pend);                // [PE]
+    uint64_t *stash = pend + (PE * 4 > (PE / 4) * 8 ? PE / 2 : PE / 4); // [STASH]
     uint32_t *flags = reinterpret_cast<uint32_t *>(stash + STASH);      // npend, nstash, overflow, nonuniform
     TD *crl = reinterpret_cast<TD *>(flags + 4);                        // [3 PE] (JRS)
     const int tid = threadIdx.x;
@@ -2080,6 +2086,14 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
         if (tid == 0) atomicOr(a.status, OA_STATUS_PART_OVERFLOW);
         return;
     }
+    // every current entry's state word starts as angle 0 | its sign (an entered
+    // particle keeps it, calc_angles :348-349); a match overwrites it below
+#pragma unroll
+    for (int u = 0; u < CU; ++u) {
+        const uint32_t i = (uint32_t)u * PART_WG + tid;
+        if (i < nc) mlds[i] = (cpw[u] >> 30) << 16;
+    }
+    __syncthreads();
     const bool nonuniform = IDB == 8 && flags[3] != 0u;
     const uint32_t nstash = min(flags[1], (uint32_t)STASH);
     uint32_t *cmeta = a.pmeta_cur + cb;
@@ -2136,13 +2150,16 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
                                                                 : (sp == 1u && sc == 2u);
                 const TD dt = dot3(qrh[u].x, qrh[u].y, qrh[u].z, crh[u].x, crh[u].y, crh[u].z);
                 const uint16_t acc = angle_add((uint16_t)(qmeta[u] & 0xFFFFu), acos_td(dt));
-                cmeta[hit[u] & 0x3FFFFFFFu] = (uint32_t)(flag ? 0u : acc) | (sc << 16);
+                mlds[hit[u] & 0x3FFFFFFFu] = (uint32_t)(flag ? 0u : acc) | (sc << 16);
                 // an inherited set's position words carry the sign in bits 30-31
                 if (flag) mark[qpos[u] & 0x3FFFFFFFu] = 0x10000u | acc;
             }
             if (j0 == 0 && q == 0) PSTAMP(4);
         }
     }
+    __syncthreads();
+    // the partition's state words leave as one coalesced run
+    for (uint32_t i = tid; i < nc; i += PART_WG) cmeta[i] = mlds[i];
     PSTAMP(5);
 }
 

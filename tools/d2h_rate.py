@@ -71,5 +71,38 @@ def main():
         print(json.dumps(res), flush=True)
 
 
-if __name__ == '__main__':
+if __name__ == '__main__' and 'pattern' not in __import__('sys').argv:
     main()
+
+
+def alloc_pattern():
+    """The batch driver's fetch pattern: per snapshot a pinned block of a slightly
+    different size (engine._pinned rounds to 4 MiB), filled by one D2H, freed a
+    snapshot later.  Times the allocation and the copy separately."""
+    import numpy as np
+    from orbitanalysis_amd.engine import _pinned
+    dev = torch.device('cuda', 0)
+    src = torch.empty(12_000_000, dtype=torch.int64, device=dev).fill_(3)
+    rng = np.random.default_rng(0)
+    keep = None
+    for it in range(8):
+        n = int(10_000_000 + rng.integers(-200_000, 200_000))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        h = _pinned(n, torch.int64)
+        t1 = time.perf_counter()
+        h.copy_(src[:n], non_blocking=True)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        print(json.dumps({'pattern_iter': it, 'n': n, 'alloc_ms': (t1 - t0) * 1e3,
+                          'copy_ms': (t2 - t1) * 1e3, 'GBs': n * 8 / (t2 - t1) / 1e9}), flush=True)
+        keep = h                     # freed at the next iteration, as the driver's
+    del keep
+
+
+if __name__ == '__main__' and 'pattern' in __import__('sys').argv:
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import orbitanalysis_amd  # noqa: F401
+    alloc_pattern()
