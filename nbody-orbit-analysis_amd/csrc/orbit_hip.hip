@@ -61,6 +61,9 @@ namespace {
 #ifndef OA_PF2
 #define OA_PF2 5            // phase 2b: rows of previous r̂ loads in flight ahead (A/B r02: 2 +3.5 %, 4 = 3, 5 -0.4 %)
 #endif
+#ifndef OA_PFEARLY
+#define OA_PFEARLY 0        // 1: those loads issued with the 2a loads, before the walks and lookups
+#endif
 #ifndef OA_HMAX
 #define OA_HMAX 32
 #endif
@@ -894,6 +897,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // up to 2 * KROWS loads in flight per wave hide the HBM latency behind them.
     ID pid[KROWS];
     uint32_t pk[KROWS];
+    V3<TD> prh[KROWS];
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < KROWS; ++k) {
@@ -905,6 +909,17 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         row_of(wave + NWAVE * k, nv, hs, kb);
         pid[k] = bld<ID, AUX_NT>(make_rsrc(ids_prev + kb, nv * IDB), lane * IDB);
         pk[k] = bld<uint32_t, AUX_NT>(make_rsrc(a.meta_prev + kb, nv * 4u), lane * 4u);
+    }
+    if (OA_PFEARLY) {
+        // the first PF2 rows' previous r̂ loads right behind the 2a loads: their HBM
+        // transfer overlaps the walks and the LDS lookups instead of following them
+#pragma unroll
+        for (int k = 0; k < PF2 && k < KROWS; ++k) {
+            uint32_t nv, hs;
+            int64_t kb;
+            row_of(wave + NWAVE * k, nv, hs, kb);
+            prh[k] = bld3<TD, AUX_NT>(make_rsrc(rhat_prev + 3 * kb, nv * SD), lane * SD);
+        }
     }
     __builtin_amdgcn_sched_barrier(0);
     // one deferred insert's eviction walk (atomic exchanges: safe beside the first-try
@@ -1064,10 +1079,10 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // ---- phase 2b: angles from the current r̂ staged in LDS, apsis records ------
     // The first PF2 rows' previous r̂ loads go out before the barrier (their HBM
     // latency behind the staging), which waits for LDS traffic only.
-    V3<TD> prh[KROWS];
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < PF2 && k < KROWS; ++k) {
+        if (OA_PFEARLY) break;
         if (OA_ROWGUARD && (uint32_t)(wave + NWAVE * k) >= nrow) continue;      // uniform
         uint32_t nv, hs;
         int64_t kb;
