@@ -700,6 +700,12 @@ __device__ __forceinline__ int64_t mp_find(const MpSlot *tab, uint64_t cap, uint
 #ifndef OA_MP_U
 #define OA_MP_U 8
 #endif
+#ifndef OA_MP_NT
+#define OA_MP_NT 0          // non-temporal member loads (A/B)
+#endif
+#ifndef OA_MP_DIAG
+#define OA_MP_DIAG 0        // 1, 2: timing diagnostics with wrong results (variants only)
+#endif
 constexpr int MP_U = OA_MP_U;
 __global__ __launch_bounds__(256) void k_mp_probe(const void *hp, int kind, int64_t n,
                                                   MpSlot *tab, uint64_t cap, uint32_t *neg1,
@@ -711,13 +717,23 @@ __global__ __launch_bounds__(256) void k_mp_probe(const void *hp, int kind, int6
 #pragma unroll
     for (int u = 0; u < MP_U; ++u) {
         const int64_t p = p0 + u * stride;
+#if OA_MP_NT
+        v[u] = p < n ? (kind == OA_ID_I64 ? (uint64_t)__builtin_nontemporal_load(
+                            static_cast<const unsigned long long *>(hp) + p)
+                                          : load_val(hp, p, kind)) : 0ull;
+#else
         v[u] = p < n ? load_val(hp, p, kind) : 0ull;
+#endif
     }
 #pragma unroll
     for (int u = 0; u < MP_U; ++u) {
         const uint64_t h = mix64(v[u]);
         m[u] = filt_mask(h);
+#if OA_MP_DIAG == 2                        // timing only: stream, no filter / table
+        w[u] = 0u;
+#else
         w[u] = p0 + u * stride < n ? filt[filt_word(h, fbits)] : 0u;
+#endif
     }
 #pragma unroll
     for (int u = 0; u < MP_U; ++u) {
@@ -725,6 +741,9 @@ __global__ __launch_bounds__(256) void k_mp_probe(const void *hp, int kind, int6
         if (p >= n) continue;
         if (v[u] == ~0ull) atomicMin(neg1, (uint32_t)p);
         if ((w[u] & m[u]) != m[u]) continue;
+#if OA_MP_DIAG == 1                        // timing only: filter, no table probe
+        continue;
+#endif
         const int64_t s = mp_find(tab, cap, v[u]);
         if (s >= 0) atomicMin(&tab[s].hpos, (uint32_t)p);
     }

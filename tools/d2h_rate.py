@@ -71,7 +71,7 @@ def main():
         print(json.dumps(res), flush=True)
 
 
-if __name__ == '__main__' and 'pattern' not in __import__('sys').argv:
+if __name__ == '__main__' and len(__import__('sys').argv) == 1:
     main()
 
 
@@ -106,3 +106,51 @@ if __name__ == '__main__' and 'pattern' in __import__('sys').argv:
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import orbitanalysis_amd  # noqa: F401
     alloc_pattern()
+
+
+def issue_cost():
+    """Host time to ISSUE one ~100 MB D2H (as fetch_async does: on a side stream after an
+    event) against the time until it completes: if the issue itself takes the copy's
+    duration, the copy blocks the host and cannot overlap the next snapshot."""
+    import numpy as np
+    from orbitanalysis_amd.engine import _pinned
+    dev = torch.device('cuda', 0)
+    hip = ctypes.CDLL('libamdhip64.so')
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                   ctypes.c_void_p]
+    hip.hipMemcpyDtoHAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                       ctypes.c_void_p]
+    n = 10_000_000
+    src = torch.empty(n, dtype=torch.int64, device=dev).fill_(3)
+    busy = torch.empty(1 << 26, dtype=torch.float32, device=dev)
+    cs = torch.cuda.Stream(device=dev)
+    h = _pinned(n, torch.int64)
+    for mode in ('torch_side', 'torch_side_busy', 'hip_side', 'hip_side_busy', 'torch_cur'):
+        for rep in range(4):
+            torch.cuda.synchronize()
+            if mode.endswith('busy'):
+                for _ in range(20):
+                    busy.mul_(1.0001)          # ~ms of compute queued on the current stream
+            t0 = time.perf_counter()
+            if mode.startswith('torch_side'):
+                with torch.cuda.stream(cs):
+                    h.copy_(src, non_blocking=True)
+            elif mode.startswith('hip_side'):
+                assert hip.hipMemcpyAsync(h.data_ptr(), src.data_ptr(), n * 8, HIP_D2H,
+                                          cs.cuda_stream) == 0
+            else:
+                h.copy_(src, non_blocking=True)
+            t1 = time.perf_counter()
+            cs.synchronize()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+        print(json.dumps({'mode': mode, 'issue_ms': (t1 - t0) * 1e3, 'done_ms': (t2 - t0) * 1e3}),
+              flush=True)
+
+
+if __name__ == '__main__' and 'issue' in __import__('sys').argv:
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import orbitanalysis_amd  # noqa: F401
+    issue_cost()

@@ -17,6 +17,7 @@
 #   post      tools/bench_post.py (+ rocprof)
 #   b2        bench.py --gpus 2 over gloo on this one GPU ($B2_SCALING, default strong)
 #   ab        alternating bench runs of library variants ($VARS, tools/variants.sh)
+#   pab       the same for tools/bench_post.py ($PAB_WHICH, default mainprog)
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; O=$R/gpurun_out; mkdir -p "$O"; T=${TAG:-x}
 ok() { local rc=$1; echo "[$2] rc=$rc"; [ "$rc" = 0 ] || exit "$rc"; }
@@ -81,6 +82,17 @@ ab)
         ${BENCH_ARGS:-} > "$O/ab_${T}_${v}_$rep.json" 2> "$O/ab_${T}_${v}_$rep.err"
       rc=$?; echo "$v rep$rep $(grep -o 'k_step [0-9.]* ms' "$O/ab_${T}_${v}_$rep.err") \
 $(grep -o '"ms_per_step": [0-9.]*' "$O/ab_${T}_${v}_$rep.json")"; ok $rc "ab $v"
+    done
+  done ;;
+pab)
+  D=$R/nbody-orbit-analysis_amd/variants
+  for rep in ${REPS:-1 2}; do
+    for v in ${VARS:-base}; do
+      lib=""; [ "$v" != base ] && lib="$D/lib_$v.so"
+      ORBIT_HIP_LIB=$lib timeout -k 10 300 python tools/bench_post.py --which ${PAB_WHICH:-mainprog} \
+        > "$O/pab_${T}_${v}_$rep.jsonl" 2> "$O/pab_${T}_${v}_$rep.err"
+      rc=$?; echo "$v rep$rep $(grep -o '"ms_per_[a-z]*": [0-9.]*' "$O/pab_${T}_${v}_$rep.jsonl" | tr '\n' ' ')"
+      ok $rc "pab $v"
     done
   done ;;
 *) echo "unknown step $step"; exit 2 ;;
