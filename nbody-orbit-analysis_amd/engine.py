@@ -341,6 +341,17 @@ def _upload(a, device):
     return h.to(device, non_blocking=True)
 
 
+def _up(a, device):
+    """``_upload`` of a typed host array: a device tensor of the same dtype and shape.
+    (A pageable ``torch.from_numpy(a).to(dev)`` would wait for the stream's queued
+    kernels, which a deferred step is still running.)"""
+    a = np.ascontiguousarray(a)
+    dt = torch.from_numpy(a[:0].reshape(-1)).dtype
+    if a.nbytes == 0:
+        return torch.empty(a.shape, dtype=dt, device=device)
+    return _upload(a, device).view(dt).reshape(a.shape)
+
+
 _PIN_GRAIN = 1 << 22
 
 
@@ -428,6 +439,8 @@ class StepResult:
     extra: dict = field(default_factory=dict)
     ws: object = None                          # the workspace holding the records
     gen: int = 0                               # its launch count when they were written
+    done: object = None                        # event after its kernels (compare steps)
+    pending: object = None                     # (ctx, prep) until OrbitEngine.settle
 
     def check_fresh(self):
         if self.ws is not None and self.ws.gen != self.gen:
@@ -497,6 +510,11 @@ class Workspace:
         self.scratch_pos = e(scratch, torch.int32) if positions else None
         self.out_pos = e(n_prev, torch.int32) if positions else None
         self.status.zero_()
+        # the status word and record count of the last launch, copied to the host
+        # behind the step's event (OrbitEngine.settle reads them without a stream sync)
+        self.h_status = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self.h_total = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+        self.copy_done = None               # event after the last D2H of its records
 
     @staticmethod
     def need(pr):
@@ -545,6 +563,7 @@ class OrbitEngine:
         # snapshot's kernels write the other one
         self._wss = [None, None]
         self._wsi = 0
+        self._pending = None                # a deferred step not yet settled (step)
         # apsis records also carry their previous-state row (ShardedEngine's merge)
         self.emit_positions = False
         # large halos of compare steps: hash partitions joined in LDS (k_part_*);
@@ -575,19 +594,24 @@ class OrbitEngine:
     def _ws(self):
         return self._wss[self._wsi]
 
-    def workspace(self, pr):
-        """The engine's current compare-step workspace, grown to fit ``pr``."""
-        ws = self._wss[self._wsi]
+    def workspace(self, pr, idx=None):
+        """The engine's current compare-step workspace (or workspace ``idx``), grown to
+        fit ``pr``."""
+        idx = self._wsi if idx is None else idx
+        ws = self._wss[idx]
         if ws is None or not ws.fits(pr, self.emit_positions):
             old = ws.cap if ws is not None else {}
             need = Workspace.need(pr)
             cap = {k: max(need[k], old.get(k, 0)) for k in need}
             dt = torch.int64 if pr.plan.ids.itemsize == 8 else torch.int32
-            ws = self._wss[self._wsi] = Workspace(self.device, dt, positions=self.emit_positions,
-                                                  **cap)
+            nws = Workspace(self.device, dt, positions=self.emit_positions, **cap)
+            if ws is not None:
+                nws.gen, nws.copy_done = ws.gen, ws.copy_done
+            ws = self._wss[idx] = nws
         return ws
 
     def reset(self):
+        self.settle()
         self.prev = None
 
     # ------------------------------------------------------------------ tables
@@ -628,10 +652,17 @@ class OrbitEngine:
 
     # ------------------------------------------------------------------ step
     def step(self, snapshot, centres, bulk_cat, H, z, exists, compare, angles_in=None,
-             angles_layout=None):
+             angles_layout=None, defer=False):
         """Process one snapshot.  ``compare`` is the reference's ``i > istart``.
         ``angles_layout``: the row layout a resumed checkpoint was written in (None:
-        the snapshot's own rows, the only layout a single GPU reads)."""
+        the snapshot's own rows, the only layout a single GPU reads).
+
+        ``defer``: return without waiting for the kernels.  The step's status word (an
+        LDS table overflow asks for a re-planned re-run) is then checked by ``settle``:
+        the next ``step`` does it after planning its own snapshot on the host, so that
+        planning overlaps this snapshot's kernels; ``fetch*``, ``angles`` and
+        ``bulk_velocities`` settle first too.  A re-run replaces the step's records and
+        state in place (same workspace), exactly as the synchronous path would have."""
         exists = np.asarray(exists)
         if angles_in is not None and angles_layout is not None:
             from .sharding import check_layout
@@ -644,29 +675,96 @@ class OrbitEngine:
             snap[k] = to_device(snapshot[k], dev)
         if is_array(snapshot['masses']):
             snap['masses'] = to_device(snapshot['masses'], dev)
-        entries, part = None, True
-        for attempt in range(10):
-            prep = self.prepare(snap, centres, bulk_cat, H, z, exists, compare,
-                                angles_in=angles_in, plan_src=snapshot,
-                                entries=entries, part=part)
-            ws = self.workspace(prep) if compare else None
-            if ws is not None:
-                ws.status.zero_()
-            res = self.launch(prep, ws)
-            # one small read-back per snapshot (the driver fetches the results anyway)
-            st = int(ws.status[0].item()) if compare else 0
-            if not st:
-                break
-            entries, part = retry_plan(prep, st)
+        ctx = dict(snap=snap, centres=centres, bulk_cat=bulk_cat, H=H, z=z, exists=exists,
+                   compare=compare, angles_in=angles_in, plan_src=snapshot,
+                   prev=self.prev if compare else None)
+        prep = self._prepare_ctx(ctx, None, True)
+        if self._pending is not None and self.settle(self._pending):
+            # the previous step was re-planned: its layout / bucket sets changed
+            ctx['prev'] = self.prev if compare else None
+            prep = self._prepare_ctx(ctx, None, True)
+        if defer:
+            res = self._launch_ctx(ctx, prep)
+            if compare:
+                res.pending = (ctx, prep)
+                self._pending = res
         else:
-            raise RuntimeError('LDS hash tables kept overflowing')
-        self.prev = SnapshotState(ids=snap['ids'], rhat=prep.rhat, meta=prep.meta,
-                                  starts=prep.starts,
-                                  counts=prep.counts, exists=exists, plan=prep.plan,
-                                  buckets=prep.buckets)
+            res, prep = self._run_ctx(ctx, prep)
+        self._set_prev(ctx, prep)
         if compare:
             self._wsi ^= 1                  # the next snapshot writes the other workspace
         return res
+
+    def _prepare_ctx(self, ctx, entries, part):
+        p = ctx['prev']
+        layout = None if p is None else (p.starts, p.counts, p.exists, p.plan, p.ids.numel(),
+                                         p.buckets)
+        return self.prepare(ctx['snap'], ctx['centres'], ctx['bulk_cat'], ctx['H'], ctx['z'],
+                            ctx['exists'], ctx['compare'], angles_in=ctx['angles_in'],
+                            plan_src=ctx['plan_src'], prev_layout=layout, entries=entries,
+                            part=part)
+
+    def _launch_ctx(self, ctx, prep, ws=None):
+        """Launch a prepared step; a compare step also queues the copy of its status
+        word and record count to page-locked host memory behind an event."""
+        if not ctx['compare']:
+            return self.launch(prep, None)
+        ws = self.workspace(prep, None if ws is None else
+                            next(i for i, w in enumerate(self._wss) if w is ws))
+        ws.status.zero_()
+        if ws.copy_done is not None:
+            # the records of the last step in this workspace may still be crossing PCIe
+            torch.cuda.current_stream(self.device).wait_event(ws.copy_done)
+            ws.copy_done = None
+        res = self.launch(prep, ws, prev=ctx['prev'])
+        ws.h_status.copy_(ws.status, non_blocking=True)
+        ws.h_total.copy_(ws.total, non_blocking=True)
+        res.done = torch.cuda.Event()
+        res.done.record(torch.cuda.current_stream(self.device))
+        return res
+
+    def _run_ctx(self, ctx, prep, res=None):
+        """Launch, wait, and re-plan until the kernels report no overflow."""
+        for attempt in range(10):
+            ws = res.ws if res is not None else None
+            r = self._launch_ctx(ctx, prep, ws)
+            if not ctx['compare']:
+                return r, prep
+            r.done.synchronize()
+            st = int(r.ws.h_status[0])
+            if not st:
+                if res is not None:          # the deferred result object, now re-filled
+                    res.__dict__.update({k: v for k, v in r.__dict__.items()})
+                    r = res
+                r.pending = None
+                return r, prep
+            prep = self._prepare_ctx(ctx, *retry_plan(prep, st))
+        raise RuntimeError('LDS hash tables kept overflowing')
+
+    def _set_prev(self, ctx, prep):
+        self.prev = SnapshotState(ids=ctx['snap']['ids'], rhat=prep.rhat, meta=prep.meta,
+                                  starts=prep.starts, counts=prep.counts,
+                                  exists=ctx['exists'], plan=prep.plan, buckets=prep.buckets)
+
+    def settle(self, res=None):
+        """Wait for a deferred step (default: the pending one) and re-run it if its
+        kernels reported an overflow.  Returns True when it was re-run (its state
+        replaced).  Only the engine's latest step can be pending."""
+        res = self._pending if res is None else res
+        if res is None or getattr(res, 'pending', None) is None:
+            return False
+        ctx, prep = res.pending
+        res.done.synchronize()
+        if not int(res.ws.h_status[0]):
+            res.pending = None
+            if self._pending is res:
+                self._pending = None
+            return False
+        self._pending = None
+        _, prep = self._run_ctx(ctx, self._prepare_ctx(ctx, *retry_plan(prep, int(res.ws.h_status[0]))),
+                                res=res)
+        self._set_prev(ctx, prep)
+        return True
 
     def prepare(self, snap, centres, bulk_cat, H, z, exists, compare, angles_in=None,
                 plan_src=None, prev_layout=None, entries=None, part=True):
@@ -714,9 +812,9 @@ class OrbitEngine:
             ch1, ch2, tab, total = plan_global(glob, counts, halos['prev_cnt'], len(items),
                                                compare)
             g = pr.glob
-            g['ch1'] = torch.from_numpy(ch1).to(dev)
-            g['ch2'] = torch.from_numpy(ch2).to(dev) if len(ch2) else None
-            g['tab'] = torch.from_numpy(tab).to(dev)
+            g['ch1'] = _up(ch1, dev)
+            g['ch2'] = _up(ch2, dev) if len(ch2) else None
+            g['tab'] = _up(tab, dev)
             g['total'] = total
             pl = None
             if compare and part and self.part_large:
@@ -725,8 +823,8 @@ class OrbitEngine:
             if pl is not None:
                 pr.part = True
                 i32, i64 = torch.int32, torch.int64
-                g['plist'] = torch.from_numpy(pl['plist'].reshape(-1)).to(dev)
-                g['gpart'] = torch.from_numpy(pl['gpart'].reshape(-1)).to(dev)
+                g['plist'] = _up(pl['plist'].reshape(-1), dev)
+                g['gpart'] = _up(pl['gpart'].reshape(-1), dev)
                 # this step's current bucket set: the next step's previous state
                 g['pkey_cur'] = torch.empty(pl['n_cur'], dtype=i64, device=dev)
                 g['ppos_cur'] = torch.empty(pl['n_cur'], dtype=i32, device=dev)
@@ -757,7 +855,7 @@ class OrbitEngine:
                     # the scatter reads only the previous chunks of fresh sets
                     gi = np.asarray(ch2[:, 0], dtype=np.int64) - len(items)
                     ch3 = ch2[~pl['inherited'][gi]]
-                    g['ch3'] = torch.from_numpy(np.ascontiguousarray(ch3)).to(dev) \
+                    g['ch3'] = _up(ch3, dev) \
                         if len(ch3) else None
                     g['n3'] = len(ch3)
             elif compare:
@@ -889,18 +987,22 @@ class OrbitEngine:
         next snapshot's kernels write the other workspace), so the records' transfer is
         off the per-snapshot critical path.  The result's workspace must not be reused
         before ``wait()``: ``step`` alternates two."""
+        self.settle(res)
         res.check_fresh()
         dev = self.device
         if getattr(self, '_copy_stream', None) is None:
             self._copy_stream = torch.cuda.Stream(device=dev)
         cs = self._copy_stream
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(dev))
         n = res.n_slots + 1
-        # the record count (a 16-byte read; the status read already synchronised)
-        total = int(res.total.item()) if res.n_slots else 0
+        if res.done is None:                # a result of launch() itself, not of step()
+            res.done = torch.cuda.Event()
+            res.done.record(torch.cuda.current_stream(dev))
+            total = int(res.total.item()) if res.n_slots else 0
+        else:
+            # the record count came back with the status word (settle waited for it)
+            total = int(res.ws.h_total[0]) if res.n_slots else 0
         with torch.cuda.stream(cs):
-            cs.wait_event(ev)
+            cs.wait_event(res.done)
             h_off = _pinned(n, torch.int64)
             h_off.copy_(res.offsets[:n], non_blocking=True)
             h_ids = h_ang = None
@@ -911,6 +1013,7 @@ class OrbitEngine:
                 h_ang.copy_(res.apsis_ang[:total], non_blocking=True)
             done = torch.cuda.Event()
             done.record(cs)
+        res.ws.copy_done = done             # the workspace's next launch waits for it
         return PendingFetch(done, h_off, h_ids, h_ang, np.dtype(ids_dtype))
 
     def fetch(self, res, ids_dtype):
@@ -920,6 +1023,7 @@ class OrbitEngine:
         through page-locked buffers from torch's caching host allocator: one DMA each
         at the link rate instead of the staged pageable copy (~8 GB/s).  The returned
         arrays own their buffers (a block is reused only once they are gone)."""
+        self.settle(res)
         res.check_fresh()
         offsets = res.offsets.cpu().numpy()
         total = int(offsets[-1]) if len(offsets) else 0
@@ -973,6 +1077,7 @@ class OrbitEngine:
         return out.astype(plan.bulk)
 
     def bulk_velocities(self, res, plan):
+        self.settle(res)
         h = res.halos.cpu().numpy().view(N.HALO_DTYPE)
         return h['bulk'].astype(plan.bulk)
 
@@ -1008,6 +1113,7 @@ class OrbitEngine:
 
     def state_meta(self):
         """The current state words in position order (bucketed large halos restored)."""
+        self.settle()
         p = self.prev
         if p.buckets is not None:
             self.unbucket(p.buckets, np.arange(len(p.buckets.K)), p.starts, p.rhat, p.meta)

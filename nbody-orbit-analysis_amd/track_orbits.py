@@ -7,6 +7,7 @@ over all halos (``engine.OrbitEngine``); the previous snapshot's state stays in
 HBM.  ``npool`` is accepted for signature compatibility and ignored (halo
 parallelism is the GPU grid).
 """
+import inspect
 import time
 
 import numpy as np
@@ -67,19 +68,25 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
 
     istart, started = 0, False
     progen_exists = None
-    # a compare step's records come back while the next snapshot is loaded, planned
-    # and run (engine.fetch_async): its group is written at the next iteration, or
-    # after the loop.  Engines without it (sharded: a collective gather) fetch inline.
+    # A compare step's records come back while the next snapshot is loaded, planned
+    # and run (engine.fetch_async), and are written one or two iterations later (or
+    # after the loop).  With ``defer`` the engine does not even wait for a step's
+    # kernels: the next snapshot's host planning overlaps them, and the step's status
+    # is checked (and a re-plan run) before the next launch (OrbitEngine.step).
+    # Engines without fetch_async (sharded: a collective gather) fetch inline.
     pipelined = hasattr(eng, 'fetch_async')
-    pending = None
+    defer = pipelined and not verbose and 'defer' in inspect.signature(eng.step).parameters
+    groups = []                     # [res, ids dtype, fetched or None, save args, kw]
 
-    def flush():
-        nonlocal pending
-        if pending is not None:
-            fetched, args, kw = pending
-            pending = None
-            offsets, ids, angles = fetched.wait()
-            save_to_file(out, ids, offsets, angles, *args, **kw)
+    def flush(keep=0):
+        """Write the groups oldest first, leaving the newest ``keep`` in flight."""
+        while len(groups) > keep:
+            g = groups[0]
+            if g[2] is None:
+                g[2] = eng.fetch_async(g[0], g[1])
+            offsets, ids, angles = g[2].wait()
+            groups.pop(0)
+            save_to_file(out, ids, offsets, angles, *g[3], **g[4])
 
     try:
         for i, (halo_ids, snapshot_number) in enumerate(zip(main_branches, snapshot_numbers)):
@@ -125,6 +132,8 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
                 layout = read_checkpoint_layout(out)
                 if layout is not None:
                     step_kw['angles_layout'] = layout
+            if defer:
+                step_kw['defer'] = True
             # apsis IDs are the previous snapshot's IDs (ids_prev_[apsis_inds], :315-316):
             # they keep that snapshot's dtype
             ids_dtype_prev = eng.prev.plan.ids if compare else None
@@ -133,12 +142,19 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
                 t0 = time.time()
             res = eng.step(snapshot, region_positions, region_bulk_vels, H, snapshot['redshift'],
                            halo_exists, compare, angles_in=angles_in, **step_kw)
-            # the previous snapshot's group: its records crossed PCIe during this step
-            flush()
+            if defer:
+                # the previous step is settled now: its records cross PCIe during this
+                # step's kernels; the one before is written
+                if groups and groups[-1][2] is None:
+                    groups[-1][2] = eng.fetch_async(groups[-1][0], groups[-1][1])
+                flush(keep=1)
+            else:
+                flush()
             if compare and res.n_slots == 0:
                 # the reference concatenates an empty list here (track_orbits.py:216)
                 raise ValueError('need at least one array to concatenate')
-            if compare:
+            fetched = None
+            if compare and not defer:
                 fetched = eng.fetch_async(res, ids_dtype_prev) if pipelined else \
                     _Fetched(eng.fetch(res, ids_dtype_prev))
             if verbose:
@@ -156,17 +172,24 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
                 halo_ids_final = main_branches[-1][progen_exists] if \
                     snapshot_number != snapshot_numbers[-1] else None
                 # checkpoint angles now: the next step replaces the engine's state
-                pending = (fetched, (region_positions[hinds], region_radii[hinds], bulk[hinds],
-                                     halo_ids_[hinds], halo_ids_final, snapshot_number, mode,
-                                     checkpoint, eng.angles() if checkpoint else None, verbose),
-                           dict(layout=checkpoint_layout(eng) if checkpoint else None))
+                groups.append([res, ids_dtype_prev, fetched,
+                               (region_positions[hinds], region_radii[hinds], bulk[hinds],
+                                halo_ids_[hinds], halo_ids_final, snapshot_number, mode,
+                                checkpoint, eng.angles() if checkpoint else None, verbose),
+                               dict(layout=checkpoint_layout(eng) if checkpoint else None)])
                 if not pipelined:
                     flush()
 
             progen_exists = halo_exists
-    finally:
-        # an error leaves no computed group unwritten (the reference wrote it already)
-        flush()
+    except BaseException:
+        # an error leaves no computed group unwritten (the reference wrote it already);
+        # a group whose own step failed cannot be written, and the error propagates
+        try:
+            flush()
+        except Exception:
+            pass
+        raise
+    flush()
 
     if verbose:
         print('Finished pericenter detection for all snapshots in {} s\n'.format(

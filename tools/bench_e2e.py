@@ -72,7 +72,7 @@ def main():
     torch.cuda.empty_cache()
     # per-phase host time of the driver's engine calls (tool-side instrumentation)
     from orbitanalysis_amd.engine import OrbitEngine
-    phase = {'prepare': [], 'launch+status': [], 'fetch': [], 'fetch_async': [],
+    phase = {'prepare': [], 'launch': [], 'settle': [], 'fetch': [], 'fetch_async': [],
              'wait': [], 'save': []}
 
     def timed(name, fn):
@@ -83,21 +83,24 @@ def main():
             return r
         return w
     OrbitEngine.prepare = timed('prepare', OrbitEngine.prepare)
+    OrbitEngine.launch = timed('launch', OrbitEngine.launch)
     OrbitEngine.fetch = timed('fetch', OrbitEngine.fetch)
     OrbitEngine.fetch_async = timed('fetch_async', OrbitEngine.fetch_async)
     from orbitanalysis_amd import engine as E, track_orbits as TO
+    _settle = OrbitEngine.settle
+
+    def settle(self, res=None):
+        # only the calls that wait (a pending step), not the no-op checks
+        r = res if res is not None else self._pending
+        if r is None or getattr(r, 'pending', None) is None:
+            return _settle(self, res)
+        t = time.perf_counter()
+        out = _settle(self, res)
+        phase['settle'].append(time.perf_counter() - t)
+        return out
+    OrbitEngine.settle = settle
     E.PendingFetch.wait = timed('wait', E.PendingFetch.wait)
     TO.save_to_file = timed('save', TO.save_to_file)
-    _launch = OrbitEngine.launch
-
-    def launch(self, pr, ws, *a, **k):
-        t = time.perf_counter()
-        r = _launch(self, pr, ws, *a, **k)
-        if ws is not None:
-            ws.status.item()                # the driver's status read follows the launch
-        phase['launch+status'].append(time.perf_counter() - t)
-        return r
-    OrbitEngine.launch = launch
     log('setup %.1f s: %d host snapshots of %s particles' % (
         time.perf_counter() - t0, S, [len(h['ids']) for h in host]))
 
@@ -146,6 +149,7 @@ def main():
                                'public track_orbits, in-memory savefile' % (units // len(timed),
                                                                           args.halos)},
         'ms_per_snapshot': [round(p * 1e3, 2) for p in per],
+        'ms_per_snapshot_median': round(float(np.median(per)) * 1e3, 3),
         'h2d_bytes_per_snapshot': 0.0 if args.device_loader else b,
         'host_ms_per_snapshot': {k: round(float(np.mean(v[2:])) * 1e3, 3) if len(v) > 2 else None
                                  for k, v in phase.items()},

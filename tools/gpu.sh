@@ -55,7 +55,7 @@ big)
   rc=$?; cat "$O/big_$T.json"; python3 tools/kstats.py "$O/prof_big_$T"; ok $rc big ;;
 e2e)
   for m in "--device-loader" ""; do
-    timeout -k 10 400 python tools/bench_e2e.py --snapshots 7 $m \
+    timeout -k 10 400 python tools/bench_e2e.py --snapshots ${E2E_SNAPS:-12} $m \
       > "$O/e2e_$T${m:+_dev}.json" 2> "$O/e2e_$T${m:+_dev}.err"
     rc=$?; cat "$O/e2e_$T${m:+_dev}.json"; ok $rc "e2e $m"
   done ;;
