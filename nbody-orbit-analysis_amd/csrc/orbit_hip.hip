@@ -592,14 +592,18 @@ template <typename T, int AUX> __device__ __forceinline__ V3<T> bld3(Rsrc r, uin
 template <int AUX> __device__ __forceinline__ void bst32(Rsrc r, uint32_t o, uint32_t v) {
     rbs_i32((int32_t)v, r, (int32_t)o, 0, AUX);
 }
+#ifndef OA_RNT
+#define OA_RNT 1            // r̂ stores non-temporal (A/B r03: 1.540-1.548 vs 1.561-1.581 ms)
+#endif
+constexpr int AUX_R = OA_RNT ? AUX_NT : 0;
 template <typename T> __device__ __forceinline__ void bst3(Rsrc r, uint32_t o, const T v[3]) {
     if constexpr (sizeof(T) == 4) {
         const f32x3 w = {v[0], v[1], v[2]};
-        rbs_v3f32(w, r, (int32_t)o, 0, 0);
+        rbs_v3f32(w, r, (int32_t)o, 0, AUX_R);
     } else {
         const f64x2 w = {v[0], v[1]};
-        rbs_v2f64(w, r, (int32_t)o, 0, 0);
-        rbs_f64(v[2], r, (int32_t)(o + 16u), 0, 0);
+        rbs_v2f64(w, r, (int32_t)o, 0, AUX_R);
+        rbs_f64(v[2], r, (int32_t)(o + 16u), 0, AUX_R);
     }
 }
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }

@@ -696,7 +696,12 @@ __device__ __forceinline__ int64_t mp_find(const MpSlot *tab, uint64_t cap, uint
 // in1d(tracked, halo_pids) / myin1d(halo_pids, ...) join, :95-99); the position of a
 // member equal to -1 is kept apart for the de-duplicated tracked entries (:83).
 // MP_U members per thread, a grid stride apart (coalesced): all their loads and filter
-// reads are issued before any is used, so the random L2 filter reads overlap.
+// reads are issued before any is used, so the random L2 filter reads overlap.  A member
+// that passes the filter (tracked, or a ~1.4 % false positive) goes to the work-group's
+// own queue segment (an LDS counter, no global atomics) instead of being looked up
+// here: the table read behind the stream would stall whole waves for a few active
+// lanes.  k_mp_resolve looks the segments up with every lane busy; a full segment
+// falls back to the lookup in place.
 #ifndef OA_MP_U
 #define OA_MP_U 8
 #endif
@@ -706,12 +711,24 @@ __device__ __forceinline__ int64_t mp_find(const MpSlot *tab, uint64_t cap, uint
 #ifndef OA_MP_DIAG
 #define OA_MP_DIAG 0        // 1, 2: timing diagnostics with wrong results (variants only)
 #endif
+#ifndef OA_MP_QUEUE
+#define OA_MP_QUEUE 1       // 0: look candidates up in place (the previous kernel, A/B)
+#endif
+#ifndef OA_MP_SEG
+#define OA_MP_SEG 128       // queue entries per probe work-group (of 256 * MP_U members)
+#endif
 constexpr int MP_U = OA_MP_U;
+constexpr int MP_SEG = OA_MP_SEG;
 __global__ __launch_bounds__(256) void k_mp_probe(const void *hp, int kind, int64_t n,
                                                   MpSlot *tab, uint64_t cap, uint32_t *neg1,
-                                                  const uint32_t *filt, uint64_t fbits) {
+                                                  const uint32_t *filt, uint64_t fbits,
+                                                  uint32_t *q, uint32_t *qcnt) {
+    __shared__ uint32_t lcnt;
+    if (threadIdx.x == 0) lcnt = 0;
+    __syncthreads();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t p0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    uint32_t *seg = q + (uint64_t)blockIdx.x * MP_SEG;
     uint64_t v[MP_U];
     uint32_t m[MP_U], w[MP_U];
 #pragma unroll
@@ -738,14 +755,45 @@ __global__ __launch_bounds__(256) void k_mp_probe(const void *hp, int kind, int6
 #pragma unroll
     for (int u = 0; u < MP_U; ++u) {
         const int64_t p = p0 + u * stride;
-        if (p >= n) continue;
-        if (v[u] == ~0ull) atomicMin(neg1, (uint32_t)p);
-        if ((w[u] & m[u]) != m[u]) continue;
+        if (p < n && v[u] == ~0ull) atomicMin(neg1, (uint32_t)p);
+        bool cand = p < n && (w[u] & m[u]) == m[u];
 #if OA_MP_DIAG == 1                        // timing only: filter, no table probe
-        continue;
+        cand = false;
+#endif
+#if OA_MP_QUEUE
+        const uint64_t bal = __ballot(cand);
+        if (bal == 0ull) continue;                  // wave-uniform
+        const int lane = __lane_id();
+        const int leader = __ffsll((unsigned long long)bal) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&lcnt, (uint32_t)__popcll(bal));
+        base = __shfl(base, leader);
+        if (!cand) continue;
+        const uint32_t slot = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+        if (slot < (uint32_t)MP_SEG) { seg[slot] = (uint32_t)p; continue; }
+#else
+        if (!cand) continue;
 #endif
         const int64_t s = mp_find(tab, cap, v[u]);
         if (s >= 0) atomicMin(&tab[s].hpos, (uint32_t)p);
+    }
+#if OA_MP_QUEUE
+    __syncthreads();
+    if (threadIdx.x == 0) qcnt[blockIdx.x] = lcnt < (uint32_t)MP_SEG ? lcnt : (uint32_t)MP_SEG;
+#endif
+}
+
+// the queued candidates: table lookup, smallest member position per tracked key
+__global__ __launch_bounds__(256) void k_mp_resolve(const void *hp, int kind, MpSlot *tab,
+                                                    uint64_t cap, const uint32_t *q,
+                                                    const uint32_t *qcnt, uint32_t nseg) {
+    for (uint32_t g = blockIdx.x; g < nseg; g += gridDim.x) {
+        const uint32_t c = qcnt[g];
+        for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) {
+            const uint32_t p = q[(uint64_t)g * MP_SEG + i];
+            const int64_t s = mp_find(tab, cap, load_val(hp, p, kind));
+            if (s >= 0) atomicMin(&tab[s].hpos, p);
+        }
     }
 }
 
@@ -811,6 +859,10 @@ uint64_t pow2_at_least(uint64_t v, uint64_t lo) {
 #ifndef OA_MP_FB
 #define OA_MP_FB 16         // filter bits per tracked ID
 #endif
+// candidate queue: MP_SEG entries per probe work-group, and its per-segment counts
+uint64_t mp_segments(uint64_t n_halo_pids) {
+    return (n_halo_pids + 256 * MP_U - 1) / (256 * MP_U);
+}
 uint64_t mp_filter_bits(uint64_t n_tracked) {
     uint64_t b = pow2_at_least(OA_MP_FB * n_tracked, 1ull << 15);
     return b > (1ull << 25) ? (1ull << 25) : b;
@@ -911,10 +963,12 @@ int oa_central_ids(const oa_central_args *args, void *stream) {
 }
 
 int64_t oa_mainprog_workspace_bytes(int64_t n_halo_pids, int64_t n_tracked) {
-    (void)n_halo_pids;                     // the halo members are streamed, not tabled
+    // the halo members are streamed, not tabled: they size only the candidate queue
     const uint64_t nt = (uint64_t)(n_tracked > 0 ? n_tracked : 1);
+    const uint64_t nh = (uint64_t)(n_halo_pids > 0 ? n_halo_pids : 0);
     const uint64_t ct = pow2_at_least(2 * nt, 64);
-    return (int64_t)(ct * sizeof(MpSlot) + 64 + 4 * nt + 4 + mp_filter_bits(nt) / 8);
+    return (int64_t)(ct * sizeof(MpSlot) + 64 + 4 * nt + 4 + mp_filter_bits(nt) / 8 +
+                     4 * mp_segments(nh) * (MP_SEG + 1));
 }
 
 int oa_main_progenitors(const oa_mainprog_args *args, void *stream) {
@@ -949,10 +1003,17 @@ int oa_main_progenitors(const oa_mainprog_args *args, void *stream) {
                            st, a.tracked, a.tracked_kind, a.n_tracked, tab, ct, a.status, filt, fbits);
         if (int rc = check_launch("k_mp_insert")) return rc;
         if (a.n_halo_pids > 0) {
-            hipLaunchKernelGGL(k_mp_probe, dim3((unsigned)((a.n_halo_pids + 256 * MP_U - 1) / (256 * MP_U))), dim3(256),
-                               0, st, a.halo_pids, a.halo_kind, a.n_halo_pids, tab, ct, neg1, filt,
-                               fbits);
+            // the queue segments after the filter, then their counts
+            const uint64_t nseg = mp_segments((uint64_t)a.n_halo_pids);
+            uint32_t *q = filt + fwords, *qcnt = q + nseg * MP_SEG;
+            hipLaunchKernelGGL(k_mp_probe, dim3((unsigned)nseg), dim3(256), 0, st, a.halo_pids,
+                               a.halo_kind, a.n_halo_pids, tab, ct, neg1, filt, fbits, q, qcnt);
             if (int rc = check_launch("k_mp_probe")) return rc;
+#if OA_MP_QUEUE
+            hipLaunchKernelGGL(k_mp_resolve, dim3((unsigned)(nseg < 4096 ? nseg : 4096)), dim3(256), 0,
+                               st, a.halo_pids, a.halo_kind, tab, ct, q, qcnt, (uint32_t)nseg);
+            if (int rc = check_launch("k_mp_resolve")) return rc;
+#endif
         }
         hipLaunchKernelGGL(k_mp_lookup, dim3((unsigned)((a.n_tracked + 255) / 256)), dim3(256), 0,
                            st, a, tab, ct, neg1, hn);

@@ -441,6 +441,7 @@ class StepResult:
     gen: int = 0                               # its launch count when they were written
     done: object = None                        # event after its kernels (compare steps)
     pending: object = None                     # (ctx, prep) until OrbitEngine.settle
+    ws_idx: int = 0                            # which of the engine's two workspaces
 
     def check_fresh(self):
         if self.ws is not None and self.ws.gen != self.gen:
@@ -704,19 +705,21 @@ class OrbitEngine:
                             plan_src=ctx['plan_src'], prev_layout=layout, entries=entries,
                             part=part)
 
-    def _launch_ctx(self, ctx, prep, ws=None):
-        """Launch a prepared step; a compare step also queues the copy of its status
-        word and record count to page-locked host memory behind an event."""
+    def _launch_ctx(self, ctx, prep, idx=None):
+        """Launch a prepared step into workspace ``idx`` (default: the current one); a
+        compare step also queues the copy of its status word and record count to
+        page-locked host memory behind an event."""
         if not ctx['compare']:
             return self.launch(prep, None)
-        ws = self.workspace(prep, None if ws is None else
-                            next(i for i, w in enumerate(self._wss) if w is ws))
+        idx = self._wsi if idx is None else idx
+        ws = self.workspace(prep, idx)
         ws.status.zero_()
         if ws.copy_done is not None:
             # the records of the last step in this workspace may still be crossing PCIe
             torch.cuda.current_stream(self.device).wait_event(ws.copy_done)
             ws.copy_done = None
         res = self.launch(prep, ws, prev=ctx['prev'])
+        res.ws_idx = idx
         ws.h_status.copy_(ws.status, non_blocking=True)
         ws.h_total.copy_(ws.total, non_blocking=True)
         res.done = torch.cuda.Event()
@@ -725,9 +728,9 @@ class OrbitEngine:
 
     def _run_ctx(self, ctx, prep, res=None):
         """Launch, wait, and re-plan until the kernels report no overflow."""
+        idx = res.ws_idx if res is not None else None
         for attempt in range(10):
-            ws = res.ws if res is not None else None
-            r = self._launch_ctx(ctx, prep, ws)
+            r = self._launch_ctx(ctx, prep, idx)
             if not ctx['compare']:
                 return r, prep
             r.done.synchronize()

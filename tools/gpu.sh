@@ -53,9 +53,18 @@ big)
   prof "$O/prof_big_$T" 400 "$R/bench.py" --dtype float64 --particles 1e7 --halos 100 \
     --steps 10 --warmup 3 --no-cpu-baseline > "$O/big_$T.json" 2> "$O/big_$T.err"
   rc=$?; cat "$O/big_$T.json"; python3 tools/kstats.py "$O/prof_big_$T"; ok $rc big ;;
+bigsweep)
+  # configs[1] under environment settings ($BIG_ENVS: space-separated NAME=VALUE,NAME=VALUE)
+  for rep in ${REPS:-1 2}; do
+    for e in ${BIG_ENVS:-ORBIT_PART_ENTRIES=4096}; do
+      env ${e//,/ } timeout -k 10 300 python bench.py --dtype float64 --particles 1e7 --halos 100 \
+        --steps 10 --warmup 3 --no-cpu-baseline > "$O/bs_${T}_${e}_$rep.json" 2> "$O/bs_${T}_${e}_$rep.err"
+      rc=$?; echo "$e rep$rep $(grep -o 'k_step [0-9.]* ms' "$O/bs_${T}_${e}_$rep.err")"; ok $rc "bigsweep $e"
+    done
+  done ;;
 e2e)
   for m in "--device-loader" ""; do
-    timeout -k 10 400 python tools/bench_e2e.py --snapshots ${E2E_SNAPS:-12} $m \
+    timeout -k 10 400 python tools/bench_e2e.py --snapshots ${E2E_SNAPS:-14} $m \
       > "$O/e2e_$T${m:+_dev}.json" 2> "$O/e2e_$T${m:+_dev}.err"
     rc=$?; cat "$O/e2e_$T${m:+_dev}.json"; ok $rc "e2e $m"
   done ;;
@@ -91,7 +100,7 @@ pab)
       lib=""; [ "$v" != base ] && lib="$D/lib_$v.so"
       ORBIT_HIP_LIB=$lib timeout -k 10 300 python tools/bench_post.py --which ${PAB_WHICH:-mainprog} \
         > "$O/pab_${T}_${v}_$rep.jsonl" 2> "$O/pab_${T}_${v}_$rep.err"
-      rc=$?; echo "$v rep$rep $(grep -o '"ms_per_[a-z]*": [0-9.]*' "$O/pab_${T}_${v}_$rep.jsonl" | tr '\n' ' ')"
+      rc=$?; echo "$v rep$rep $(grep -o '"ms_per_[a-z]*": [0-9.]*\|identical to the GPU: [A-Za-z]*' "$O/pab_${T}_${v}_$rep.jsonl" | tr '\n' ' ')"
       ok $rc "pab $v"
     done
   done ;;
