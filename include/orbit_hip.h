@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OA_ABI_VERSION 11
+#define OA_ABI_VERSION 12
 
 #define OA_OK 0
 #define OA_E_ARG (-1)       /* invalid argument / unsupported dtype plan */
@@ -220,7 +220,10 @@ typedef struct oa_step_args {
     const int64_t *gchunk3;     /* the previous chunks k_part_scatter reads: those of
                                    halos with a fresh previous set (NULL: gchunk2)    */
     int32_t n_gchunk3;
-    int32_t reserved3;
+    int32_t mark_tag;           /* 1..32767: k_part_join tags the marks it writes, so a
+                                   gmark buffer kept between steps needs no clearing (the
+                                   caller zeroes it once, and again before a tag repeats);
+                                   0: oa_step clears gmark_n marks first                 */
 } oa_step_args;
 
 /* Arguments of oa_part_unbucket: a bucket set's entries back to position order. */
@@ -265,7 +268,11 @@ typedef struct oa_compact_args {
     int32_t n_packed;           /* items[0, n_packed) are k_step items (records
                                    contiguous from scratch_off), the rest global items
                                    (records in 64-position segments)                  */
-    int32_t reserved_c;
+    int32_t n_gchunks;
+    const int64_t *gchunks;     /* optional: oa_step_args.gchunk2 of the step (the global
+                                   items' previous-block chunks); their records are then
+                                   gathered one work-group per chunk instead of one per
+                                   item (NULL: per item)                                */
 } oa_compact_args;
 
 /* ABI version (OA_ABI_VERSION) — lets the host reject a stale library. */

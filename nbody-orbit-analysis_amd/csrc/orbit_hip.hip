@@ -1250,42 +1250,25 @@ __global__ __launch_bounds__(1024) void k_scan_slots(const int32_t *cnt, int32_t
 }
 
 // Packed (k_step) items hold their records contiguously: a coalesced copy.  Global
-// items (k_big_join) keep theirs in 64-position segments, packed at each segment's
-// base.  One work-group per item, segments in chunks of 256: a block-wide exclusive scan of the
-// chunk's row counts (LDS), then the chunk's records are copied flat -- thread t moves
+// items (k_big_join, k_part_emit) keep theirs in 64-position segments, packed at each
+// segment's base: segments in chunks of 256 get a block-wide exclusive scan of their
+// record counts (LDS), then the chunk's records are copied flat -- thread t moves
 // records t, t + 256, ... (consecutive records of consecutive rows: coalesced), each
 // finding its row by a binary search over the scanned offsets.
 template <int IDB>
-__global__ __launch_bounds__(256) void k_gather_items(const oa_compact_args a) {
+__device__ __forceinline__ void gather_segments(const oa_compact_args &a, const oa_item &it,
+                                                int64_t dst, int64_t s_lo, int64_t s_hi,
+                                                uint32_t *wsum, uint32_t *roff) {
     typedef typename IdT<IDB>::T ID;
-    __shared__ uint32_t wsum[4];
-    __shared__ uint32_t roff[257];
-    const oa_item it = a.items[blockIdx.x];
-    // an item holds at most one record per (padded) progenitor position
-    const int32_t n = min((int64_t)a.item_count[blockIdx.x], it.n_pv);
-    const int64_t slot = it.slot0;               // planned on the host: no halo walk
-    if (n <= 0 || slot < 0) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t dst = a.offsets_out[slot];
     const ID *src = reinterpret_cast<const ID *>(a.scratch_ids);
     ID *out = reinterpret_cast<ID *>(a.out_ids) + dst;
     uint16_t *oang = a.out_ang + dst;
-    if ((int32_t)blockIdx.x < a.n_packed) {
-        // k_step items: the records are already contiguous and in order
-        const int64_t s0 = it.scratch_off;
-        for (int32_t j = tid; j < n; j += 256) {
-            out[j] = src[s0 + j];
-            oang[j] = a.scratch_ang[s0 + j];
-            if (a.out_pos) a.out_pos[dst + j] = a.scratch_pos[s0 + j];
-        }
-        return;
-    }
-    const int64_t nseg = (it.n_pv + 63) >> 6;
     const uint8_t *sc = a.seg_count + (it.scratch_off >> 6);
     int64_t carry = 0;
-    for (int64_t c0 = 0; c0 < nseg; c0 += 256) {
+    for (int64_t c0 = s_lo; c0 < s_hi; c0 += 256) {
         const int64_t sg = c0 + tid;
-        const uint32_t cnt = sg < nseg ? sc[sg] : 0u;
+        const uint32_t cnt = sg < s_hi ? sc[sg] : 0u;
         uint32_t incl = cnt;
         for (int o = 1; o < 64; o <<= 1) {
             uint32_t y = __shfl_up(incl, o);
@@ -1298,7 +1281,7 @@ __global__ __launch_bounds__(256) void k_gather_items(const oa_compact_args a) {
         roff[tid] = pre + incl - cnt;
         if (tid == 255) roff[256] = tot;
         __syncthreads();
-        const uint32_t rows = (uint32_t)(nseg - c0 < 256 ? nseg - c0 : 256);
+        const uint32_t rows = (uint32_t)(s_hi - c0 < 256 ? s_hi - c0 : 256);
         for (uint32_t j = tid; j < tot; j += 256) {
             const uint32_t r = upper_find(roff, rows, j);      // roff[r] <= j < roff[r + 1]
             const int64_t from = it.scratch_off + ((c0 + r) << 6) + (j - roff[r]);
@@ -1309,6 +1292,62 @@ __global__ __launch_bounds__(256) void k_gather_items(const oa_compact_args a) {
         carry += tot;
         __syncthreads();
     }
+}
+
+template <int IDB>
+__global__ __launch_bounds__(256) void k_gather_items(const oa_compact_args a) {
+    typedef typename IdT<IDB>::T ID;
+    __shared__ uint32_t wsum[4];
+    __shared__ uint32_t roff[257];
+    const oa_item it = a.items[blockIdx.x];
+    // an item holds at most one record per (padded) progenitor position
+    const int32_t n = min((int64_t)a.item_count[blockIdx.x], it.n_pv);
+    const int64_t slot = it.slot0;               // planned on the host: no halo walk
+    if (n <= 0 || slot < 0) return;
+    const int tid = threadIdx.x;
+    const int64_t dst = a.offsets_out[slot];
+    if ((int32_t)blockIdx.x < a.n_packed) {
+        // k_step items: the records are already contiguous and in order
+        const ID *src = reinterpret_cast<const ID *>(a.scratch_ids);
+        ID *out = reinterpret_cast<ID *>(a.out_ids) + dst;
+        uint16_t *oang = a.out_ang + dst;
+        const int64_t s0 = it.scratch_off;
+        for (int32_t j = tid; j < n; j += 256) {
+            out[j] = src[s0 + j];
+            oang[j] = a.scratch_ang[s0 + j];
+            if (a.out_pos) a.out_pos[dst + j] = a.scratch_pos[s0 + j];
+        }
+        return;
+    }
+    if (a.gchunks) return;                       // k_gather_chunks moves these
+    gather_segments<IDB>(a, it, dst, 0, (it.n_pv + 63) >> 6, wsum, roff);
+}
+
+// Global items, one work-group per previous-block chunk (gchunks rows: item, start,
+// count; start a multiple of 64): the chunk's output offset is the item's plus the
+// records of the item's segments before it (a block reduction over those segment
+// counts, L2 hits), then its own segments as above.  A large halo's records move with
+// as many work-groups as it has chunks instead of one.
+template <int IDB>
+__global__ __launch_bounds__(256) void k_gather_chunks(const oa_compact_args a) {
+    __shared__ uint32_t wsum[4];
+    __shared__ uint32_t roff[257];
+    __shared__ uint32_t red[4];
+    const int64_t *ch = a.gchunks + 3 * (int64_t)blockIdx.x;
+    const int64_t gi = ch[0], start = ch[1], cnt = ch[2];
+    const oa_item it = a.items[gi];
+    const int64_t slot = it.slot0;
+    if (slot < 0 || a.item_count[gi] <= 0 || cnt <= 0) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t s_lo = start >> 6, s_hi = (start + cnt + 63) >> 6;
+    const uint8_t *sc = a.seg_count + (it.scratch_off >> 6);
+    uint32_t before = 0;
+    for (int64_t sg = tid; sg < s_lo; sg += 256) before += sc[sg];
+    for (int o = 32; o > 0; o >>= 1) before += __shfl_down(before, o);
+    if (lane == 0) red[wave] = before;
+    __syncthreads();
+    const int64_t dst = a.offsets_out[slot] + (int64_t)(red[0] + red[1] + red[2] + red[3]);
+    gather_segments<IDB>(a, it, dst, s_lo, s_hi, wsum, roff);
 }
 
 // ------------------------------------------------------------------ bulk velocity
@@ -1970,6 +2009,13 @@ __host__ __device__ inline int64_t part_lds_bytes(int e, int sl, int td_bytes = 
 // one, as K and the previous set's K compare) looked up; a match gathers the current
 // r̂ from its bucket entry and writes that entry's state word; an apsis also marks the
 // previous position.
+// an apsis mark of the previous position (k_part_join -> k_part_emit): bit 16 set, the
+// step's tag in bits 17-31 (mark_tag; 0: an untagged buffer cleared by oa_step), the
+// f16 angle in bits 0-15.  Marks of earlier steps carry other tags and read as unset.
+__device__ __forceinline__ uint32_t mark_word(int32_t tag) {
+    return 0x10000u | ((uint32_t)tag << 17);
+}
+
 template <typename TD, int IDB>
 __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     extern __shared__ __attribute__((aligned(16))) char psm[];
@@ -2117,6 +2163,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     const uint32_t nstash = min(flags[1], (uint32_t)STASH);
     uint32_t *cmeta = a.pmeta_cur + cb;
     uint32_t *mark = a.gmark + (it.scratch_off - a.gmark_base);
+    const uint32_t mtag = mark_word(a.mark_tag);
     // previous entries, PU per thread: lookups, then the gathers of the matched current
     // r̂ (the partition's own bucket entries), then the angle and state-word arithmetic
     for (uint32_t q = 0; q < nq; ++q) {
@@ -2171,7 +2218,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
                 const uint16_t acc = angle_add((uint16_t)(qmeta[u] & 0xFFFFu), acos_td(dt));
                 mlds[hit[u] & 0x3FFFFFFFu] = (uint32_t)(flag ? 0u : acc) | (sc << 16);
                 // an inherited set's position words carry the sign in bits 30-31
-                if (flag) mark[qpos[u] & 0x3FFFFFFFu] = 0x10000u | acc;
+                if (flag) mark[qpos[u] & 0x3FFFFFFFu] = mtag | acc;
             }
             if (j0 == 0 && q == 0) PSTAMP(4);
         }
@@ -2213,6 +2260,7 @@ __global__ __launch_bounds__(BIG_WG) void k_part_emit(const oa_step_args a) {
     const oa_halo &h = a.halos[it.h0];
     const ID *ids_prev = static_cast<const ID *>(a.ids_prev);
     const uint32_t *mark = a.gmark + (it.scratch_off - a.gmark_base);
+    const uint32_t mtag = mark_word(a.mark_tag);
     ID *scr_ids = static_cast<ID *>(a.scratch_ids);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t lanemask_lt = (1ull << lane) - 1ull;
@@ -2230,7 +2278,7 @@ __global__ __launch_bounds__(BIG_WG) void k_part_emit(const oa_step_args a) {
         const int64_t v0 = w0 + e * BIG_WG;
         const int64_t p = v0 + threadIdx.x;
         const uint32_t m = mk[e];
-        const bool flag = m != 0u;
+        const bool flag = (m & 0xFFFF0000u) == mtag;    // a mark of this step
         const uint64_t b = __ballot(flag);
         const int64_t segpos = v0 + wave * 64;
         if (segpos < start + cnt) {
@@ -2266,8 +2314,11 @@ __global__ __launch_bounds__(BIG_WG) void k_part_emit(const oa_step_args a) {
 
 template <typename TX, typename TV, typename TD, int IDB>
 int launch_part(const oa_step_args &a, hipStream_t st) {
+    if (a.mark_tag < 0 || a.mark_tag > 0x7FFF)
+        return fail(OA_E_ARG, "oa_step: mark_tag must be in [0, 32767]");
     if (hipMemsetAsync(a.pcnt, 0, (size_t)a.n_pcnt * 4, st) != hipSuccess ||
-        (a.gmark_n > 0 && hipMemsetAsync(a.gmark, 0, (size_t)a.gmark_n * 4, st) != hipSuccess))
+        (a.mark_tag == 0 && a.gmark_n > 0 &&
+         hipMemsetAsync(a.gmark, 0, (size_t)a.gmark_n * 4, st) != hipSuccess))
         return fail(OA_E_LAUNCH, "oa_step: partition counters / marks reset");
     // previous chunks to scatter: those of halos without an inherited set (gchunk3)
     const int64_t n_scat = a.n_gchunk1 + (a.gchunk3 ? a.n_gchunk3 : a.n_gchunk2);
@@ -2528,10 +2579,18 @@ int oa_compact(const oa_compact_args *args, void *stream) {
     hipLaunchKernelGGL(k_scan_slots, dim3(1), dim3(1024), 0, st, a.halo_count, a.n_slots,
                        a.offsets_out, a.total_out);
     if (int rc = check_launch("k_scan_slots")) return rc;
-    if (a.n_items > 0) {
-        if (a.id_bytes == 8) hipLaunchKernelGGL(k_gather_items<8>, dim3(a.n_items), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL(k_gather_items<4>, dim3(a.n_items), dim3(256), 0, st, a);
+    if (a.n_gchunks < 0 || (a.n_gchunks > 0 && !a.gchunks))
+        return fail(OA_E_ARG, "oa_compact: n_gchunks without gchunks");
+    const int32_t n_direct = a.gchunks ? a.n_packed : a.n_items;   // per-item launches
+    if (n_direct > 0) {
+        if (a.id_bytes == 8) hipLaunchKernelGGL(k_gather_items<8>, dim3(n_direct), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL(k_gather_items<4>, dim3(n_direct), dim3(256), 0, st, a);
         if (int rc = check_launch("k_gather_items")) return rc;
+    }
+    if (a.gchunks && a.n_gchunks > 0) {
+        if (a.id_bytes == 8) hipLaunchKernelGGL(k_gather_chunks<8>, dim3(a.n_gchunks), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL(k_gather_chunks<4>, dim3(a.n_gchunks), dim3(256), 0, st, a);
+        if (int rc = check_launch("k_gather_chunks")) return rc;
     }
     return OA_OK;
 }

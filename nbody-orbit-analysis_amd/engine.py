@@ -516,6 +516,7 @@ class Workspace:
         self.h_status = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         self.h_total = torch.zeros(1, dtype=torch.int64, pin_memory=True)
         self.copy_done = None               # event after the last D2H of its records
+        self.gmark, self.mark_tag = None, 0   # large-halo apsis marks (marks())
 
     @staticmethod
     def need(pr):
@@ -535,6 +536,19 @@ class Workspace:
     def reset(self, n_slots):
         """Per-launch zeroing (the status word accumulates: callers clear it)."""
         self.halo_count[:max(n_slots, 1)].zero_()
+
+    def marks(self, n):
+        """(pointer, tag) of the large-halo apsis marks for a launch needing ``n``: the
+        buffer is kept and each launch tags its marks (oa_step_args.mark_tag), so it is
+        zeroed only when it grows or its 15-bit tag would repeat."""
+        if self.gmark is None or self.gmark.numel() < n or self.mark_tag >= 0x7FFF:
+            if self.gmark is None or self.gmark.numel() < n:
+                self.gmark = torch.zeros(max(int(n), 1), dtype=torch.int32, device=self.device)
+            else:
+                self.gmark.zero_()
+            self.mark_tag = 0
+        self.mark_tag += 1
+        return self.gmark.data_ptr(), self.mark_tag
 
 
 class OrbitEngine:
@@ -608,6 +622,7 @@ class OrbitEngine:
             nws = Workspace(self.device, dt, positions=self.emit_positions, **cap)
             if ws is not None:
                 nws.gen, nws.copy_done = ws.gen, ws.copy_done
+                nws.gmark, nws.mark_tag = ws.gmark, ws.mark_tag
             ws = self._wss[idx] = nws
         return ws
 
@@ -841,7 +856,7 @@ class OrbitEngine:
                 g['pcnt'] = torch.empty(pl['n_pcnt'], dtype=i32, device=dev)
                 g['gmark_base'] = int(glob['scratch_off'][0])
                 g['gmark_n'] = max(scratch - g['gmark_base'], 1)
-                g['gmark'] = torch.empty(g['gmark_n'], dtype=i32, device=dev)
+                # the marks buffer comes from the launch's workspace (OrbitEngine.launch)
                 g['n_parts'], g['kmax'] = len(pl['plist']), pl['kmax']
                 nh = len(halos)
                 K = np.zeros(nh, np.int64)
@@ -908,8 +923,7 @@ class OrbitEngine:
                 a.imeta, a.irh, a.icnt = (_ptr(inh and inh.meta), _ptr(inh and inh.rh),
                                           _ptr(inh and inh.cnt))
                 a.pcnt, a.n_pcnt = g['pcnt'].data_ptr(), int(g['pcnt'].numel())
-                a.gmark, a.gmark_base, a.gmark_n = (g['gmark'].data_ptr(), g['gmark_base'],
-                                                    g['gmark_n'])
+                a.gmark_base, a.gmark_n = g['gmark_base'], g['gmark_n']
                 if 'n3' in g:
                     # a non-NULL pointer marks the list as given, even when empty
                     a.gchunk3 = g['ch3'].data_ptr() if g['ch3'] is not None else \
@@ -957,6 +971,8 @@ class OrbitEngine:
             a.halo_count, a.item_count, a.status = (ws.halo_count.data_ptr(),
                                                    ws.item_count.data_ptr(), ws.status.data_ptr())
             a.scratch_pos = _ptr(ws.scratch_pos)
+            if pr.part:
+                a.gmark, a.mark_tag = ws.marks(pr.glob['gmark_n'])
         if step_events is not None:
             step_events[0].record()
         N.check(lib.oa_step(a, st), 'oa_step')
@@ -976,6 +992,8 @@ class OrbitEngine:
                                                ws.out_ang.data_ptr())
         c.total_out = ws.total.data_ptr()
         c.scratch_pos, c.out_pos = _ptr(ws.scratch_pos), _ptr(ws.out_pos)
+        # global items' records: one gather work-group per previous-block chunk
+        c.gchunks, c.n_gchunks = (a.gchunk2, a.n_gchunk2) if a.n_global_items else (None, 0)
         N.check(lib.oa_compact(c, st), 'oa_compact')
         res.offsets = ws.offsets[:res.n_slots + 1]
         res.apsis_ids, res.apsis_ang, res.total = ws.out_ids, ws.out_ang, ws.total
