@@ -783,18 +783,18 @@ __global__ __launch_bounds__(256) void k_mp_probe(const void *hp, int kind, int6
 #endif
 }
 
-// the queued candidates: table lookup, smallest member position per tracked key
+// the queued candidates: table lookup, smallest member position per tracked key.  One
+// thread per queue slot (a segment's unused slots exit at once): every lookup chain
+// is in flight together, none waits behind another segment's
 __global__ __launch_bounds__(256) void k_mp_resolve(const void *hp, int kind, MpSlot *tab,
                                                     uint64_t cap, const uint32_t *q,
                                                     const uint32_t *qcnt, uint32_t nseg) {
-    for (uint32_t g = blockIdx.x; g < nseg; g += gridDim.x) {
-        const uint32_t c = qcnt[g];
-        for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) {
-            const uint32_t p = q[(uint64_t)g * MP_SEG + i];
-            const int64_t s = mp_find(tab, cap, load_val(hp, p, kind));
-            if (s >= 0) atomicMin(&tab[s].hpos, p);
-        }
-    }
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t g = i / (uint64_t)MP_SEG;
+    if (g >= nseg || (uint32_t)(i % (uint64_t)MP_SEG) >= qcnt[g]) return;
+    const uint32_t p = q[i];
+    const int64_t s = mp_find(tab, cap, load_val(hp, p, kind));
+    if (s >= 0) atomicMin(&tab[s].hpos, p);
 }
 
 // per tracked entry: duplicates become -1 (:83-84), then the halo number of the member
@@ -1010,7 +1010,7 @@ int oa_main_progenitors(const oa_mainprog_args *args, void *stream) {
                                a.halo_kind, a.n_halo_pids, tab, ct, neg1, filt, fbits, q, qcnt);
             if (int rc = check_launch("k_mp_probe")) return rc;
 #if OA_MP_QUEUE
-            hipLaunchKernelGGL(k_mp_resolve, dim3((unsigned)(nseg < 4096 ? nseg : 4096)), dim3(256), 0,
+            hipLaunchKernelGGL(k_mp_resolve, dim3((unsigned)((nseg * MP_SEG + 255) / 256)), dim3(256), 0,
                                st, a.halo_pids, a.halo_kind, tab, ct, q, qcnt, (uint32_t)nseg);
             if (int rc = check_launch("k_mp_resolve")) return rc;
 #endif

@@ -71,7 +71,7 @@ def main():
         import torch.distributed as dist
         if world == 1 and 'MASTER_ADDR' not in os.environ:
             os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT='29561')
-        if args.backend == 'gloo' or world == 1:
+        if args.backend == 'gloo':
             dist.init_process_group('gloo', rank=rank, world_size=world)
         else:
             dist.init_process_group('nccl', device_id=dev)
