@@ -304,7 +304,24 @@ def _sort_pairs(h, key):
     return o[o2]
 
 
-def merge_onthefly(parts, nh, prev_starts, p_has, ids_dtype):
+def _by_unique_key(v, g, n):
+    """``v`` ordered by its distinct keys ``g`` in [0, n): as they are when every rank's
+    rows arrive in order (world 1, or one contributing rank), else by a counting
+    placement (one n-bit mark array and its prefix sum), not a comparison sort of
+    the ~N matched rows."""
+    if g.numel() < 2 or bool((g[1:] > g[:-1]).all()):
+        return v
+    # the bound covers every key (an index past the mark array would fault the device)
+    n = max(int(n or 0), int(g.max()) + 1)
+    mark = torch.zeros(int(n), dtype=torch.int32, device=g.device)
+    mark[g] = 1
+    dest = torch.cumsum(mark, 0, dtype=torch.int32)[g].long() - 1
+    out = torch.empty_like(v)
+    out[dest] = v
+    return out
+
+
+def merge_onthefly(parts, nh, prev_starts, p_has, ids_dtype, n_prev=None):
     """Merge the ranks' on-the-fly records of one snapshot pair on the root rank
     (ShardedOnTheFly), on whatever device the tensors are on.
 
@@ -318,7 +335,8 @@ def merge_onthefly(parts, nh, prev_starts, p_has, ids_dtype):
     emits them (previous-block order, halos in order, :154-174).  Departed and entered
     IDs are per-halo sorted unique (setdiff1d, :145, :168), except the entered IDs of a
     halo without a progenitor block, which keep loader order (:178), i.e. global
-    current-row order.  Returns host arrays (IDs in ``ids_dtype``)."""
+    current-row order.  ``n_prev``: the previous snapshot's row count (bounds the
+    global previous rows).  Returns host arrays (IDs in ``ids_dtype``)."""
     ap = parts['apsis']
     dev = ap.device
     out = {}
@@ -330,7 +348,7 @@ def merge_onthefly(parts, nh, prev_starts, p_has, ids_dtype):
         torch.zeros(nh, dtype=torch.int64, device=dev)
     out['apsis_offsets'] = np.concatenate([[0], np.cumsum(cnt.cpu().numpy())]).astype(np.int64)
     out['apsis_ids'] = ids_to_host(ap[:, 1], ids_dtype)
-    out['angles'] = _pinned_host(parts['angle_v'][torch.argsort(parts['angle_g'])])
+    out['angles'] = _pinned_host(_by_unique_key(parts['angle_v'], parts['angle_g'], n_prev))
 
     def grouped(h, ids, second, uniq):
         o = _sort_pairs(h, second)
@@ -478,7 +496,8 @@ class ShardedOnTheFly:
             n_prev = int(np.max(sl1[:, 1])) if len(sl1) else 0
             merged = merge_onthefly(dict(apsis=apsis, angle_g=angle_g, angle_v=angle_v,
                                          departed=departed, entered=entered), nh,
-                                    _block_starts(sl1, max(n_prev, 0)), p_has, ids_dtype)
+                                    _block_starts(sl1, max(n_prev, 0)), p_has, ids_dtype,
+                                    n_prev=max(n_prev, 0))
             merged['angles'] = merged['angles'].astype(adt, copy=False)
         else:
             z = np.zeros(nh + 1, np.int64)

@@ -68,6 +68,9 @@ def test_merge_onthefly_restores_single_rank_order(ids_dtype):
     assert np.array_equal(got['apsis_offsets'],
                           np.concatenate([[0], np.cumsum(np.bincount(halo_of[arow], minlength=nh))]))
     assert np.array_equal(got['angles'], aval)
+    # the same with the previous row count given (the counting placement's bound)
+    again = merge_onthefly(parts, nh, pstart, p_has, dt, n_prev=n_prev)
+    assert np.array_equal(again['angles'], aval)
     want_d = [np.unique(did[dh == j]) for j in range(nh)]
     assert np.array_equal(got['departed_ids'], np.concatenate(want_d))
     assert np.array_equal(got['departed_offsets'], np.cumsum([0] + [len(x) for x in want_d]))

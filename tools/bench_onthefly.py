@@ -74,7 +74,7 @@ def main():
         if args.backend == 'gloo':
             dist.init_process_group('gloo', rank=rank, world_size=world)
         else:
-            dist.init_process_group('nccl', device_id=dev)
+            dist.init_process_group('nccl', rank=rank, world_size=world, device_id=dev)
     nh = max(1, int(args.particles) // args.per_halo)
     gen = DevicePlummer(n_halos=nh, n_particles=int(args.particles), seed=5, device=dev)
     S = args.snapshots
