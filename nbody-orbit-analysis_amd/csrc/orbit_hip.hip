@@ -2016,8 +2016,16 @@ __device__ __forceinline__ uint32_t mark_word(int32_t tag) {
     return 0x10000u | ((uint32_t)tag << 17);
 }
 
+#ifndef OA_JOIN_WPE
+#define OA_JOIN_WPE 0       // k_part_join: waves per SIMD asked of the register allocator (0: default)
+#endif
+#if OA_JOIN_WPE
+#define JOIN_ATTR __attribute__((amdgpu_waves_per_eu(OA_JOIN_WPE, 8)))
+#else
+#define JOIN_ATTR
+#endif
 template <typename TD, int IDB>
-__global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
+__global__ __launch_bounds__(PART_WG) JOIN_ATTR void k_part_join(const oa_step_args a) {
     extern __shared__ __attribute__((aligned(16))) char psm[];
     const uint32_t PE = (uint32_t)a.part_e, PS = (uint32_t)a.part_slots;
     uint64_t *slots = reinterpret_cast<uint64_t *>(psm);               // [PS]
@@ -2273,6 +2281,15 @@ __global__ __launch_bounds__(BIG_WG) void k_part_emit(const oa_step_args a) {
         const int64_t p = w0 + e * BIG_WG + threadIdx.x;
         mk[e] = p < start + cnt ? mark[p] : 0u;
     }
+    // the flagged positions' IDs, every load issued before any record is stored (the
+    // stores may alias ids_prev for the compiler, which would otherwise keep each load
+    // behind the previous row's stores)
+    ID idl[EU];
+#pragma unroll
+    for (int e = 0; e < EU; ++e) {
+        const int64_t p = w0 + e * BIG_WG + threadIdx.x;
+        idl[e] = (mk[e] & 0xFFFF0000u) == mtag ? ids_prev[h.prev_off + p] : (ID)0;
+    }
 #pragma unroll
     for (int e = 0; e < EU; ++e) {
         const int64_t v0 = w0 + e * BIG_WG;
@@ -2284,7 +2301,7 @@ __global__ __launch_bounds__(BIG_WG) void k_part_emit(const oa_step_args a) {
         if (segpos < start + cnt) {
             if (flag) {
                 const int64_t pos = it.scratch_off + segpos + __popcll(b & lanemask_lt);
-                scr_ids[pos] = ids_prev[h.prev_off + p];
+                scr_ids[pos] = idl[e];
                 a.scratch_ang[pos] = (uint16_t)(m & 0xFFFFu);
                 if (a.scratch_pos) a.scratch_pos[pos] = (int32_t)(h.prev_off + p);
             }

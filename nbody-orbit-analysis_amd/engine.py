@@ -587,7 +587,7 @@ class OrbitEngine:
         # partition capacity: 4096 entries in 6144 slots (~74 KB of LDS: two join
         # work-groups per CU); at most oa_build_info(4)
         self.part_e = min(int(env('ORBIT_PART_ENTRIES', 4096)), self.lib.oa_build_info(4))
-        self.part_slots = self.part_e + self.part_e // 2
+        self.part_slots = int(env('ORBIT_PART_SLOTS', 0)) or self.part_e + self.part_e // 2
         self.part_kmax = self.lib.oa_build_info(5)
 
     def table_sizes(self, dx_f64, entries=None):
