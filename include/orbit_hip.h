@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OA_ABI_VERSION 12
+#define OA_ABI_VERSION 13
 
 #define OA_OK 0
 #define OA_E_ARG (-1)       /* invalid argument / unsupported dtype plan */
@@ -224,6 +224,9 @@ typedef struct oa_step_args {
                                    gmark buffer kept between steps needs no clearing (the
                                    caller zeroes it once, and again before a tag repeats);
                                    0: oa_step clears gmark_n marks first                 */
+    int32_t items_single;       /* 1: every packed item holds one halo (the launch takes
+                                   k_step's one-halo specialisation); 0: any item plan */
+    int32_t reserved;
 } oa_step_args;
 
 /* Arguments of oa_part_unbucket: a bucket set's entries back to position order. */

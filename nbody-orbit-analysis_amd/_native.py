@@ -13,7 +13,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.abspath(__file__))
 # ORBIT_HIP_LIB selects an alternative build (kernel variants for tuning sweeps)
 LIB_PATH = os.environ.get('ORBIT_HIP_LIB') or os.path.join(PKG, 'liborbit_hip.so')
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -53,7 +53,8 @@ class StepArgs(ctypes.Structure):
                 ('pkey_prev', c_vp), ('ppos_prev', c_vp), ('pmeta_prev', c_vp), ('prh_prev', c_vp),
                 ('ikey', c_vp), ('ipos', c_vp), ('imeta', c_vp), ('irh', c_vp), ('icnt', c_vp),
                 ('pcnt', c_vp), ('n_pcnt', c_i64), ('gmark', c_vp), ('gmark_base', c_i64),
-                ('gmark_n', c_i64), ('gchunk3', c_vp), ('n_gchunk3', c_i32), ('mark_tag', c_i32)]
+                ('gmark_n', c_i64), ('gchunk3', c_vp), ('n_gchunk3', c_i32), ('mark_tag', c_i32),
+                ('items_single', c_i32), ('reserved', c_i32)]
 
 
 class UnbucketArgs(ctypes.Structure):

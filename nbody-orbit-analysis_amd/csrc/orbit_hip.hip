@@ -271,7 +271,9 @@ struct ItemHdr {
     int32_t seg_halo[HMAX];         // segment -> item-local halo
     int32_t halo_cnt[HMAX];         // apsis records per item halo
     uint16_t rowoff[OA_KROWS * (OA_WG / 64)];   // item-local offset of each progenitor
-    uint8_t rowcnt[OA_KROWS * (OA_WG / 64)];    //   row's apsis records, and their count
+    uint8_t rowcnt[OA_KROWS * (OA_WG / 64)];    //   row's apsis records, and their count;
+                                    // phase 1 of a packed item: the halo of each current
+                                    // row's first position (rowh)
     uint32_t hslot[HMAX];           // bit 0: joined (non-empty progenitor block);
                                     // bits 1-31: the halo's out_slot + 1 (0: none)
     uint32_t seg_cnt[HMAX];         // progenitor particles of each segment
@@ -281,13 +283,19 @@ struct ItemHdr {
 };
 constexpr int64_t HDR_BYTES = (sizeof(ItemHdr) + 255) & ~int64_t(255);
 
+#ifndef OA_ROWTAB
+#define OA_ROWTAB 1         // packed items: per-row halo / segment tables built in phase 0
+#endif
 #ifndef OA_PENDDIV
-#define OA_PENDDIV 8        // deferral list: lds_entries / OA_PENDDIV entries of 8 bytes
+#define OA_PENDDIV 9        // deferral list: lds_entries / OA_PENDDIV entries of 8 bytes
 #endif
 __host__ __device__ inline int64_t table_bytes(int entries, int slots) {
     int64_t b = (int64_t)slots * 8 + (int64_t)entries * 8 / OA_PENDDIV;
     return (b + 15) & ~int64_t(15);
 }
+// packed items: per progenitor row, segment << 8 | row within the segment (u16), in
+// region A past both the table and the staged r̂, so it lives through phases 0-2b
+constexpr int64_t PROW_BYTES = ((int64_t)OA_KROWS * (OA_WG / 64) * 2 + 15) & ~int64_t(15);
 
 __device__ __forceinline__ uint32_t upper_find(const uint32_t *starts, uint32_t n, uint32_t x) {
     // largest k in [0, n) with starts[k] <= x  (starts non-decreasing, starts[0] = 0)
@@ -533,10 +541,13 @@ __device__ __forceinline__ uint32_t slot_meta(uint64_t v) {
 }
 
 // Region A: max(table + deferral list, three r̂ component arrays), 16-B aligned.
-__host__ __device__ inline int64_t region_a_bytes(int entries, int slots, int td_bytes) {
+__host__ __device__ inline int64_t prow_offset(int entries, int slots, int td_bytes) {
     const int64_t t = table_bytes(entries, slots);
     const int64_t r = ((int64_t)3 * td_bytes * entries + 15) & ~int64_t(15);
     return t > r ? t : r;
+}
+__host__ __device__ inline int64_t region_a_bytes(int entries, int slots, int td_bytes) {
+    return prow_offset(entries, slots, td_bytes) + PROW_BYTES;
 }
 __host__ __device__ inline int64_t step_lds_bytes(int entries, int slots, int td_bytes) {
     return HDR_BYTES + region_a_bytes(entries, slots, td_bytes) + (((int64_t)entries + 15) & ~int64_t(15));
@@ -618,7 +629,9 @@ __device__ __forceinline__ int64_t uni64(int64_t x) {
 //   bits 16-31 the previous float16 angle
 constexpr uint32_t PK_HIT = 1u << 14, PK_FLAG = 1u << 15;
 
-template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
+// SINGLE: every item holds one halo (oa_step_args.items_single): the packed-item paths
+// (per-row halo and segment lookups) are compiled out
+template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF, bool SINGLE = false>
 __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK fk) {
     typedef typename IdT<IDB>::T ID;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -631,10 +644,12 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     TD *rcy = rcx + E, *rcz = rcy + E;
     uint8_t *sgn8 = reinterpret_cast<uint8_t *>(
         smem + HDR_BYTES + region_a_bytes((int)E, (int)nslots_max, (int)sizeof(TD)));
+    uint16_t *prow = reinterpret_cast<uint16_t *>(
+        smem + HDR_BYTES + prow_offset((int)E, (int)nslots_max, (int)sizeof(TD)));
 
     // the item (host-planned, oa_plan_items): scalar loads, uniform values
     const oa_item it = a.items[blockIdx.x];
-    const int nh = it.h1 - it.h0;
+    const int nh = SINGLE ? 1 : it.h1 - it.h0;
     const uint32_t nhu = (uint32_t)nh;
     const int64_t base = it.cur_off;
     const uint32_t n_span = (uint32_t)it.n_span, nslots = (uint32_t)it.n_slots;
@@ -735,6 +750,21 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
         }
         const uint32_t n_pv = (uint32_t)__shfl(vi, 63), nseg = (uint32_t)__shfl(si, 63);
+        if (!SINGLE && OA_ROWTAB && nh > 1) {
+            // per-row tables, so no row searches the halo or segment starts later: the
+            // halo of each current row's first position, and each progenitor row's
+            // segment and row within it (a lane per halo, its own rows)
+            const uint32_t c0 = in ? (uint32_t)(hrow.cur_off - base) : n_span;
+            uint32_t c1 = __shfl_down(c0, 1);
+            if (lane == nh - 1) c1 = n_span;
+            constexpr uint32_t NR = (uint32_t)(KROWS * NWAVE);
+            if (in)
+                for (uint32_t r = (c0 + 63u) >> 6; (r << 6) < c1 && r < NR; ++r) H.rowcnt[r] = (uint8_t)lane;
+            if (hp) {
+                const uint32_t r0 = (vi - pv) >> 6, sg = si - 1u;
+                for (uint32_t r = 0; r < (pv >> 6) && r0 + r < NR; ++r) prow[r0 + r] = (uint16_t)((sg << 8) | r);
+            }
+        }
         if (lane == 0) {
             H.lstart[nh] = n_span;
             H.vstart[nseg] = n_pv; H.nseg = nseg; H.n_pv = n_pv;
@@ -771,8 +801,9 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             // the row's halo (uniform search); rows that cross into later halos of a
             // packed item step each lane forward
             uint32_t hl = 0;
-            if (nhu > 1) {
-                hl = uni(upper_find(H.lstart, nhu, r0));
+            if (!SINGLE && nhu > 1) {
+                hl = OA_ROWTAB ? uni((uint32_t)H.rowcnt[r0 >> 6])    // rowh (phase 0)
+                               : uni(upper_find(H.lstart, nhu, r0));
                 if (r0 + 63u >= H.lstart[hl + 1])
                     while (hl + 1 < nhu && li >= H.lstart[hl + 1]) ++hl;
             }
@@ -857,7 +888,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // statically: wave w takes rows w, w + NWAVE, ... (<= KROWS of them, the host
     // planner caps n_pv), and keeps each row's IDs and packed link in registers from
     // phase 2a to phase 2b.
-    const uint32_t n_pv = uni(H.n_pv), nseg = uni(H.nseg);
+    const uint32_t n_pv = uni(H.n_pv), nseg = SINGLE ? min(uni(H.nseg), 1u) : uni(H.nseg);
     const uint32_t nrow = (n_pv + 63) / 64;
     // r̂ of every row this wave computed, from registers (RDEFER); rows past the
     // item fall outside r_rh and are dropped
@@ -887,9 +918,16 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         uint32_t ro = r0, cnt = cnt0;
         hs = hal0;
         int64_t off = off0;
-        if (nseg > 1) {
+        if (nseg > 1 && !OA_ROWTAB) {
             const uint32_t s = uni(upper_find(H.vstart, nseg, min(r0, n_pv - 1u)));
             ro = r0 - uni(H.vstart[s]);
+            cnt = uni(H.seg_cnt[s]);
+            hs = uni((uint32_t)H.seg_halo[s]);
+            off = uni64(H.seg_prev_off[s]);
+        } else if (nseg > 1) {
+            // the row's segment from the phase-0 table (rows past the item: none)
+            const uint32_t e = r < nrow ? uni((uint32_t)prow[r]) : 0u, s = e >> 8;
+            ro = r < nrow ? (e & 0xFFu) * 64u : cnt0;
             cnt = uni(H.seg_cnt[s]);
             hs = uni((uint32_t)H.seg_halo[s]);
             off = uni64(H.seg_prev_off[s]);
@@ -1032,7 +1070,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         id_split<IDB>(pid[k], lo, hi);
         const bool can = ((uint32_t)lane < nv) & (IDB != 8 || nonuniform || hi == hi0);
         uint32_t lmin = 0, lmax = n_span;                 // the halo's position span
-        if (nhu > 1) {
+        if (!SINGLE && nhu > 1) {
             lmin = uni(H.lstart[hs]);
             lmax = uni(H.lstart[hs + 1]) - lmin;
         }
@@ -1495,7 +1533,8 @@ int launch_step_c(const oa_step_args &a, hipStream_t st) {
         // a frame-only launch needs no table: several work-groups share a CU
         const int64_t lds = COMPARE ? step_lds_bytes(a.lds_entries, a.lds_slots, (int)sizeof(TD))
                                     : HDR_BYTES;
-        auto k = k_step<TX, TV, TD, IDB, COMPARE, OTF>;
+        auto k = (COMPARE && !OTF && a.items_single) ? k_step<TX, TV, TD, IDB, COMPARE, OTF, true>
+                                                     : k_step<TX, TV, TD, IDB, COMPARE, OTF, false>;
         if (int rc = set_lds(k, lds)) return rc;
         hipLaunchKernelGGL(k, dim3(a.n_items), dim3(WG), (size_t)lds, st, a, make_frame_k(a));
         if (int rc = check_launch("k_step")) return rc;

@@ -903,6 +903,9 @@ class OrbitEngine:
         a.angles_in = _ptr(pr.angles_in)
         a.halos, a.n_halos = pr.halos.data_ptr(), len(halos)
         a.items, a.n_items = pr.d_items.data_ptr(), len(items)
+        # one halo per packed item: k_step's one-halo specialisation
+        a.items_single = int(len(items) > 0 and bool(np.all(items['h1'] - items['h0'] == 1))
+                             and os.environ.get('ORBIT_SINGLE', '1') != '0')
         g = pr.glob
         a.n_global_items = len(glob)
         if len(glob):
