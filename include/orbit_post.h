@@ -139,6 +139,11 @@ typedef struct oa_mainprog_args {
 int64_t oa_mainprog_workspace_bytes(int64_t n_halo_pids, int64_t n_tracked);
 int oa_main_progenitors(const oa_mainprog_args *args, void *stream);
 
+/* Diagnostic builds only (-DOA_STAMPS=1): k_central's per-block phase timestamps of its
+ * last launch (8 per block, s_memrealtime at 100 MHz).  Returns the number of values
+ * copied, -1 in normal builds. */
+int64_t oa_debug_central_stamps(uint64_t *host, int64_t n);
+
 #ifdef __cplusplus
 }
 #endif

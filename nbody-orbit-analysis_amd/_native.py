@@ -120,6 +120,7 @@ SYMBOLS = {
     'oa_max_lds_bytes': (c_i64, []),
     'oa_debug_stamps': (c_i64, [c_vp, c_i64]),
     'oa_debug_part_stamps': (c_i64, [c_i32, c_vp, c_i64]),
+    'oa_debug_central_stamps': (c_i64, [c_vp, c_i64]),
     'oa_compact': (ctypes.c_int, [ctypes.POINTER(CompactArgs), c_vp]),
     'oa_part_unbucket': (ctypes.c_int, [ctypes.POINTER(UnbucketArgs), c_vp]),
     'oa_match_workspace_bytes': (c_i64, [c_i64]),

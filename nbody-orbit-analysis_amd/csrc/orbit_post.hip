@@ -326,7 +326,9 @@ __global__ __launch_bounds__(256) void k_retro_counts(const void *ids, int kind,
 // radius key of particle p about the halo centre: dx in the promoted dtype TD,
 // recenter_coordinates (utils.py:24-33) per dim in its comparison dtype, then
 // region_coords (float64, progenitors.py:41) and sqrt(einsum) with the host's f64 tree
-template <typename TX, typename TD>
+// (SQ = false: the bits of r^2 itself -- the same order, since sqrt is monotone, with
+// ties of r possibly split; r_of() turns such a key into the radius key)
+template <typename TX, typename TD, bool SQ = true>
 __device__ __forceinline__ uint64_t radius_key(const TX (&x)[3], const double *c,
                                                const oa_central_args &a) {
     TD d[3];
@@ -346,29 +348,94 @@ __device__ __forceinline__ uint64_t radius_key(const TX (&x)[3], const double *c
     }
     const double r0 = (double)d[0], r1 = (double)d[1], r2 = (double)d[2];
     const double p0 = r0 * r0, p1 = r1 * r1, p2 = r2 * r2;
-    const double r = sqrt((p0 + p2) + p1);
+    const double r = SQ ? sqrt((p0 + p2) + p1) : (p0 + p2) + p1;
     return (uint64_t)__double_as_longlong(r);   // r >= +0 or NaN: bit order = numeric order, NaN last
+}
+__device__ __forceinline__ uint64_t r_of(uint64_t k2) {
+    return (uint64_t)__double_as_longlong(sqrt(__longlong_as_double((long long)k2)));
+}
+
+#ifndef OA_STAMPS
+#define OA_STAMPS 0
+#endif
+#if OA_STAMPS
+// diagnostic builds: per-block s_memrealtime at k_central's phase boundaries
+constexpr int CST_N = 8, CST_MAX = 1 << 16;
+__device__ uint64_t g_cstamps[CST_MAX * CST_N];
+#define CSTAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < CST_MAX) \
+    g_cstamps[blockIdx.x * CST_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define CSTAMP(k) do { } while (0)
+#endif
+// Raw buffer loads (resource: 48-bit base, byte size; lanes past the size read 0), so a
+// block's coordinates are addressed by one 32-bit lane offset plus a scalar offset per
+// particle instead of a 64-bit address per load.
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x3 __attribute__((ext_vector_type(3)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+__device__ f32x3 pb_v3f32(i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.load.v3f32");
+__device__ f64x2 pb_v2f64(i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.load.v2f64");
+__device__ double pb_f64(i32x4, int32_t, int32_t, int32_t) __asm("llvm.amdgcn.raw.buffer.load.f64");
+__device__ __forceinline__ i32x4 post_rsrc(const void *p, uint32_t bytes) {
+    const uint64_t a = (uint64_t)p;
+    i32x4 r;
+    r.x = __builtin_amdgcn_readfirstlane((int32_t)(uint32_t)a);
+    r.y = __builtin_amdgcn_readfirstlane((int32_t)((uint32_t)(a >> 32) & 0xFFFFu));
+    r.z = __builtin_amdgcn_readfirstlane((int32_t)bytes);
+    r.w = 0x00020000;
+    return r;
+}
+template <typename TX>
+__device__ __forceinline__ void load_xyz(i32x4 r, uint32_t vo, uint32_t so, TX (&x)[3]) {
+    if constexpr (sizeof(TX) == 4) {
+        const f32x3 v = pb_v3f32(r, (int32_t)vo, (int32_t)so, 0);
+        x[0] = v.x; x[1] = v.y; x[2] = v.z;
+    } else {
+        const f64x2 v = pb_v2f64(r, (int32_t)vo, (int32_t)so, 0);
+        x[0] = v.x; x[1] = v.y; x[2] = pb_f64(r, (int32_t)(vo + 16u), (int32_t)so, 0);
+    }
 }
 
 constexpr int KR = 12;                     // k_central: radius keys per thread in registers
 constexpr int HB = 12;                     // k_central: digit bits of the threshold pass
 
-// rank of every candidate by (key, position) among the n of them (n <= 1024, one
-// candidate per thread, keys broadcast from LDS): the sorted order without a sorting
-// network's log^2 barriers
-__device__ __forceinline__ void rank_pairs(const uint64_t *s, const uint32_t *x, int n,
-                                           uint64_t *ds, uint32_t *dx) {
+// Rank of every candidate by (key, position) among the n of them (n <= 1024, keys
+// broadcast from LDS): the sorted order without a sorting network's log^2 barriers.
+// Every thread of the work-group at work: candidate c = t mod n
+// counts the candidates of one of G = 1024 / n slices of [0, n) and adds its partial
+// rank to acc[c] (LDS, zeroed here); then each candidate is placed.  Barriers inside.
+__device__ __forceinline__ void rank_pairs_split(const uint64_t *s, const uint32_t *x, int n,
+                                                 uint64_t *ds, uint32_t *dx, int *acc) {
     const int t = threadIdx.x;
-    if (t < n) {
-        const uint64_t k = s[t];
-        const uint32_t i = x[t];
-        int r = 0;
-        for (int j = 0; j < n; ++j) {
+    if (t < n) acc[t] = 0;
+    __syncthreads();
+    const int G = 1024 / n, L = (n + G - 1) / G;
+    const int c = t % n, g = t / n;
+    if (g < G) {
+        const uint64_t k = s[c];
+        const uint32_t i = x[c];
+        const int j1 = min(n, (g + 1) * L);
+        int r = 0, j = g * L;
+        constexpr int RU = 8;
+        for (; j + RU <= j1; j += RU) {
+            uint64_t kj[RU];
+            uint32_t xj[RU];
+#pragma unroll
+            for (int u = 0; u < RU; ++u) { kj[u] = s[j + u]; xj[u] = x[j + u]; }
+#pragma unroll
+            for (int u = 0; u < RU; ++u) r += (kj[u] < k || (kj[u] == k && xj[u] < i)) ? 1 : 0;
+        }
+        for (; j < j1; ++j) {
             const uint64_t kj = s[j];
             r += (kj < k || (kj == k && x[j] < i)) ? 1 : 0;
         }
-        ds[r] = k;
-        dx[r] = i;
+        if (r) atomicAdd(&acc[c], r);
+    }
+    __syncthreads();
+    if (t < n) {
+        const int r = acc[t];
+        ds[r] = s[t];
+        dx[r] = x[t];
     }
 }
 
@@ -393,6 +460,7 @@ void k_central(const oa_central_args a) {
     if (k <= 0) return;
     const TX *x = static_cast<const TX *>(a.coords);
     const double *c = a.positions + 3 * (int64_t)h;
+    CSTAMP(0);
     if (tid == 0) { s_min = ~0ull; s_max = 0; s_cnt = 0; s_done = 0; }
     for (int d = tid; d < (1 << HB); d += 1024) hist[d] = 0;
     __syncthreads();
@@ -406,21 +474,21 @@ void k_central(const oa_central_args a) {
         // the first k taken -- the same k keys, in the same order, as the exact select
         // below, in one pass over the keys instead of up to eight.
         uint64_t lmin = ~0ull, lmax = 0;
-        constexpr int LU = 4;                  // particles per thread with loads in flight
+        // every particle's loads in flight at once: one lane offset, a scalar offset per
+        // particle (1024 particles apart), past-the-block lanes read 0 (key ~0 below)
+        constexpr int LU = sizeof(TX) == 4 ? KR : 4;
+        const i32x4 rx = post_rsrc(x + 3 * off, (uint32_t)m * 3u * (uint32_t)sizeof(TX));
+        const uint32_t vo = (uint32_t)tid * 3u * (uint32_t)sizeof(TX);
 #pragma unroll
         for (int u0 = 0; u0 < KR; u0 += LU) {
             TX xs[LU][3];
 #pragma unroll
-            for (int u = 0; u < LU; ++u) {
-                const int i = (u0 + u) * 1024 + tid;
-                const int64_t p = off + (i < m ? i : 0);
-#pragma unroll
-                for (int d = 0; d < 3; ++d) xs[u][d] = x[3 * p + d];
-            }
+            for (int u = 0; u < LU; ++u)
+                load_xyz<TX>(rx, vo, (uint32_t)(u0 + u) * 1024u * 3u * (uint32_t)sizeof(TX), xs[u]);
 #pragma unroll
             for (int u = 0; u < LU; ++u) {
                 const int i = (u0 + u) * 1024 + tid;
-                key[u0 + u] = i < m ? radius_key<TX, TD>(xs[u], c, a) : ~0ull;
+                key[u0 + u] = i < m ? radius_key<TX, TD, false>(xs[u], c, a) : ~0ull;
                 if (i < m) {
                     lmin = key[u0 + u] < lmin ? key[u0 + u] : lmin;
                     lmax = key[u0 + u] > lmax ? key[u0 + u] : lmax;
@@ -433,13 +501,17 @@ void k_central(const oa_central_args a) {
             lmin = y < lmin ? y : lmin;
             lmax = z > lmax ? z : lmax;
         }
+        CSTAMP(1);
         if (lane == 0 && tid < m) { atomicMin(&s_min, lmin); atomicMax(&s_max, lmax); }
         __syncthreads();
+        CSTAMP(2);
+        // The keys here are r^2 (no sqrt per particle): they select, and only the
+        // selected get their radius, which orders them.
         if (k == m) {
 #pragma unroll
             for (int u = 0; u < KR; ++u) {
                 const int i = u * 1024 + tid;
-                if (i < m) { sk[i] = key[u]; si[i] = (uint32_t)i; }
+                if (i < m) { sk[i] = r_of(key[u]); si[i] = (uint32_t)i; }
             }
         } else {
             const uint64_t diff = s_min ^ s_max;
@@ -451,6 +523,7 @@ void k_central(const oa_central_args a) {
             for (int u = 0; u < KR; ++u)
                 if (u * 1024 + tid < m) atomicAdd(&hist[(key[u] >> sh) & mask], 1);
             __syncthreads();
+            CSTAMP(3);
             // the digit B where the running count reaches k (4 bins per thread)
             int h4[4], sum = 0;
 #pragma unroll
@@ -465,27 +538,44 @@ void k_central(const oa_central_args a) {
                 }
                 s_bin = 4 * tid + q;
                 s_cum = acc + h4[q];
+                // The cut: every r^2 key <= the bin's top E, and past it to the end of the
+                // run of keys whose sqrt equals sqrt(E) (a few more).  A key above the cut
+                // then has a radius > sqrt(E) >= the k-th smallest radius (at least k keys
+                // are <= E), so no particle left out can tie the k-th radius.
+                const uint64_t pre = s_min & ~((1ull << lo_fixed) - 1ull);
+                uint64_t e = pre | ((uint64_t)s_bin << sh) | ((1ull << sh) - 1ull);
+                if (e < 0x7FF0000000000000ull) {          // finite r^2: extend the plateau
+                    const uint64_t re = r_of(e);
+                    for (int t = 0; t < 8 && e + 1 < 0x7FF0000000000000ull && r_of(e + 1) == re; ++t) ++e;
+                }
+                s_prefix = e;
             }
             __syncthreads();
-            const uint32_t B = (uint32_t)s_bin;
+            CSTAMP(4);
+            const uint64_t cut = s_prefix;
             fast = s_cum <= SC;
             if (fast) {
 #pragma unroll
                 for (int u = 0; u < KR; ++u) {
                     const int i = u * 1024 + tid;
-                    if (i < m && ((key[u] >> sh) & mask) <= B) {
+                    if (i < m && key[u] <= cut) {
                         const int p = atomicAdd(&s_cnt, 1);
-                        sk[p] = key[u];
-                        si[p] = (uint32_t)i;
+                        if (p < SC) { sk[p] = r_of(key[u]); si[p] = (uint32_t)i; }
                     }
                 }
-            } else {
-                // too many keys at the threshold digit: the exact select, from global
+                __syncthreads();
+                fast = s_cnt <= SC;                       // the plateau added too many
+            }
+            if (!fast) {
+                // too many keys at the threshold: the exact select over radius keys, from
+                // global (its min / max: sqrt is monotone)
 #pragma unroll
                 for (int u = 0; u < KR; ++u) {
                     const int i = u * 1024 + tid;
-                    if (i < m) a.scratch[off + i] = key[u];
+                    if (i < m) a.scratch[off + i] = r_of(key[u]);
                 }
+                __syncthreads();
+                if (tid == 0) { s_min = r_of(s_min); s_max = r_of(s_max); s_cnt = 0; }
             }
         }
         __syncthreads();
@@ -613,9 +703,11 @@ void k_central(const oa_central_args a) {
 #undef KEY
     }
     __syncthreads();
+    CSTAMP(5);
     const uint32_t *order = si;
     if (n_sorted <= 1024) {
-        rank_pairs(sk, si, n_sorted, rk, ri);
+        // the histogram is dead here: it holds the partial ranks
+        rank_pairs_split(sk, si, n_sorted, rk, ri, hist);
         order = ri;
     } else {
         int P = 1;
@@ -625,6 +717,7 @@ void k_central(const oa_central_args a) {
         bitonic_pairs<1024>(sk, si, P);
     }
     __syncthreads();
+    CSTAMP(6);
     const int64_t o = a.out_offsets[h];
     for (int r = tid; r < k; r += 1024) {
         const int64_t src = off + order[r];
@@ -633,6 +726,7 @@ void k_central(const oa_central_args a) {
         else
             static_cast<uint32_t *>(a.out_ids)[o + r] = static_cast<const uint32_t *>(a.ids)[src];
     }
+    CSTAMP(7);
 }
 
 // ------------------------------------------------------------------ f4: main progenitors
@@ -871,6 +965,20 @@ uint64_t mp_filter_bits(uint64_t n_tracked) {
 }  // namespace
 
 extern "C" {
+
+// Diagnostic builds (-DOA_STAMPS=1): k_central's per-block phase stamps of its last
+// launch (8 per block, s_memrealtime at 100 MHz); returns the count copied or -1.
+int64_t oa_debug_central_stamps(uint64_t *host, int64_t n) {
+#if OA_STAMPS
+    const int64_t m = n < (int64_t)CST_MAX * CST_N ? n : (int64_t)CST_MAX * CST_N;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_cstamps), m * sizeof(uint64_t)) != hipSuccess) return -1;
+    return m;
+#else
+    (void)host; (void)n;
+    return -1;
+#endif
+}
+
 
 int64_t oa_post_struct_size(int32_t which) {
     switch (which) {

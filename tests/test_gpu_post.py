@@ -142,6 +142,35 @@ def test_central_ids_random_vs_oracle(n, sizes, dtype, box):
     assert_same(got[1], want[1], 'offsets')
 
 
+@pytest.mark.parametrize('dtype', [np.float64, np.float32])
+def test_central_ids_radius_ties_vs_oracle(dtype):
+    """k_central selects on r^2 and orders the selected by (r, position): the n-th radius
+    falls inside a shell of particles whose r^2 differ by a few ulps but whose radii
+    round to the same values (sqrt plateaus), and inside a group of identical
+    positions; the order must still be the stable (r, position) order."""
+    from orbitanalysis_amd.progenitors import get_central_particle_ids
+    rng = np.random.default_rng(5)
+    blocks = []
+    for R in (3.0, 1.0 + 2 ** -30, 7.25):
+        th = rng.uniform(0, 2 * np.pi, 400)
+        shell = np.stack([R * np.cos(th), R * np.sin(th), np.zeros_like(th)], 1)
+        inner = rng.uniform(-R / 4, R / 4, (60, 3))
+        same = np.tile(rng.uniform(-R, R, (1, 3)) * 0.5, (40, 1))
+        outer = rng.uniform(-3 * R, 3 * R, (3000, 3))
+        b = np.concatenate([outer[:1500], shell[:200], same, inner, shell[200:], outer[1500:]])
+        blocks.append(b[rng.permutation(len(b))] if R == 7.25 else b)
+    x = (np.concatenate(blocks) + 50.0).astype(dtype)
+    sizes = [len(b) for b in blocks]
+    snap = {'ids': rng.permutation(10 ** 6)[:sum(sizes)].astype(np.int64), 'coordinates': x,
+            'region_offsets': np.cumsum([0] + sizes[:-1])}
+    pos = np.full((len(sizes), 3), 50.0, dtype=dtype)
+    for n in (100, 130, 300):
+        want = PO.get_central_particle_ids(snap, pos, n=n)
+        got = get_central_particle_ids(snap, pos, n=n)
+        assert_same(got[0], want[0], 'ids n=%d' % n)
+        assert_same(got[1], want[1], 'offsets n=%d' % n)
+
+
 @pytest.mark.parametrize('case', mainprog_cases(), ids=lambda c: c[0])
 def test_main_progenitors_match_reference(case):
     from orbitanalysis_amd.progenitors import find_main_progenitors
