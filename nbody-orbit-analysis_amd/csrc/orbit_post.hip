@@ -266,17 +266,33 @@ __global__ __launch_bounds__(CT) void k_collate_merge(const oa_collate_args a) {
     for (int q = threadIdx.x; q < u; q += CT) { nk[q] = a.w_keys[base + q]; nfp[q] = a.w_fp[base + q]; }
     if (threadIdx.x == 0) nfp[u] = a.w_found[j];
     __syncthreads();
-    for (int64_t i = threadIdx.x; i < on; i += CT) {
-        const uint64_t key = a.old_keys[ob + i];
-        int L = 0, R = u;
-        while (L < R) {
-            const int mid = (L + R) >> 1;
-            if (nk[mid] < key) L = mid + 1; else R = mid;
+    // old elements MU per thread per trip, every load issued before any store (the
+    // stores may alias the old list for the compiler, which would otherwise hold each
+    // trip's loads behind the previous trip's stores)
+    constexpr int MU = 8;
+    for (int64_t i0 = threadIdx.x; i0 < on; i0 += (int64_t)CT * MU) {
+        uint64_t key[MU];
+        int64_t cnt[MU];
+#pragma unroll
+        for (int e = 0; e < MU; ++e) {
+            const int64_t i = i0 + (int64_t)e * CT;
+            key[e] = i < on ? a.old_keys[ob + i] : 0ull;
+            cnt[e] = i < on ? a.old_cnt[ob + i] : 0;
         }
-        const bool eq = L < u && nk[L] == key;
-        const int64_t pos = no + i + L - nfp[L];
-        a.new_keys[pos] = key;
-        a.new_cnt[pos] = a.old_cnt[ob + i] + (eq ? a.w_cnt[base + L] : 0);
+#pragma unroll
+        for (int e = 0; e < MU; ++e) {
+            const int64_t i = i0 + (int64_t)e * CT;
+            if (i >= on) break;
+            int L = 0, R = u;
+            while (L < R) {
+                const int mid = (L + R) >> 1;
+                if (nk[mid] < key[e]) L = mid + 1; else R = mid;
+            }
+            const bool eq = L < u && nk[L] == key[e];
+            const int64_t pos = no + i + L - nfp[L];
+            a.new_keys[pos] = key[e];
+            a.new_cnt[pos] = cnt[e] + (eq ? a.w_cnt[base + L] : 0);
+        }
     }
     for (int q = threadIdx.x; q < u; q += CT) {
         if (nfp[q + 1] != nfp[q]) continue;               // already in the old list
