@@ -294,6 +294,15 @@ def retry_plan(pr, st):
     return e, pr.part and not (st & N.STATUS_PART_OVERFLOW)
 
 
+def items_single(items):
+    """oa_step_args.items_single: 1 when every packed item holds one halo, so oa_step
+    launches k_step's one-halo specialisation (ORBIT_SINGLE=0 keeps the general kernel,
+    for A/B runs); 0 for any other plan."""
+    if len(items) == 0 or os.environ.get('ORBIT_SINGLE', '1') == '0':
+        return 0
+    return int(bool(np.all(np.asarray(items['h1']) - np.asarray(items['h0']) == 1)))
+
+
 def set_item_slots(items, out_slot):
     """items['slot0'] = the first output slot among each item's halos [h0, h1), or -1
     (k_gather_items then needs no serial walk over the halo table)."""
@@ -903,9 +912,7 @@ class OrbitEngine:
         a.angles_in = _ptr(pr.angles_in)
         a.halos, a.n_halos = pr.halos.data_ptr(), len(halos)
         a.items, a.n_items = pr.d_items.data_ptr(), len(items)
-        # one halo per packed item: k_step's one-halo specialisation
-        a.items_single = int(len(items) > 0 and bool(np.all(items['h1'] - items['h0'] == 1))
-                             and os.environ.get('ORBIT_SINGLE', '1') != '0')
+        a.items_single = items_single(items)
         g = pr.glob
         a.n_global_items = len(glob)
         if len(glob):

@@ -165,6 +165,22 @@ def test_plan_items_invariants():
         assert c2[:, 2].sum() == max(prev[g['h0']], 0) and np.all(c2[:, 1] % 64 == 0)
 
 
+def test_items_single_flag(monkeypatch):
+    """oa_step_args.items_single (ABI 13) is set only when every packed item holds one
+    halo (the one-halo k_step specialisation compiles the packed-item paths out), and
+    the plans that pack halos keep the general kernel."""
+    from orbitanalysis_amd.engine import plan_items, items_single
+    big = np.full(50, 9000)
+    items, _, _ = plan_items(big, big, 11776, hmax=32, max_pv=12288)
+    assert np.all(items['h1'] - items['h0'] == 1) and items_single(items) == 1
+    small = np.full(50, 900)
+    items, _, _ = plan_items(small, small, 11776, hmax=32, max_pv=12288)
+    assert np.any(items['h1'] - items['h0'] > 1) and items_single(items) == 0
+    assert items_single(items[:0]) == 0
+    monkeypatch.setenv('ORBIT_SINGLE', '0')
+    assert items_single(plan_items(big, big, 11776, hmax=32, max_pv=12288)[0]) == 0
+
+
 def test_synthetic_generator_is_deterministic():
     from orbitanalysis_amd.synthetic import PlummerSnapshots
     a = PlummerSnapshots(n_halos=2, n_per_halo=300, n_snapshots=3, seed=5).input_digest()
