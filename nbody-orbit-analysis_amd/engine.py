@@ -212,6 +212,11 @@ def _pow2_ceil(x):
     return np.left_shift(1, np.ceil(np.log2(x)).astype(np.int64))
 
 
+def _pow2_floor(x):
+    x = np.maximum(np.asarray(x, dtype=np.int64), 1)
+    return np.left_shift(1, np.floor(np.log2(x)).astype(np.int64))
+
+
 # partitions per large halo at least (a power of two): as many as one XCD's CUs run join
 # work-groups at once, so an XCD works on one halo at a time
 PART_SPREAD = int(_pow2_ceil(int(os.environ.get('ORBIT_PART_SPREAD', 32))))
@@ -237,7 +242,11 @@ def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=No
     h = np.asarray(glob['h0'], dtype=np.int64)
     c = np.asarray(cur_cnt, dtype=np.int64)[h]
     p = np.maximum(np.asarray(prev_cnt, dtype=np.int64)[h], 0)
-    K = np.maximum(_pow2_ceil(-(-c // int(part_e * PART_FILL))), PART_SPREAD)
+    # the spread floor scales with the halo (one partition per ~1024 particles, a power
+    # of two <= PART_SPREAD): a halo just past the item budget gets a few partitions, not
+    # PART_SPREAD * part_e entries
+    floor = np.minimum(PART_SPREAD, _pow2_floor(np.maximum(c // 1024, 1)))
+    K = np.maximum(_pow2_ceil(-(-c // int(part_e * PART_FILL))), floor)
     K = np.where(p > 0, K, 0).astype(np.int64)
     nk = int(K.sum())
     if nk == 0 or K.max() > kmax:
@@ -289,9 +298,13 @@ def retry_plan(pr, st):
     if st & N.STATUS_PLAN:
         raise RuntimeError('oa_step: an item exceeds the kernel limits (planner bug)')
     e = pr.entries
+    part = pr.part and not (st & N.STATUS_PART_OVERFLOW)
     if st & N.STATUS_TABLE_OVERFLOW:
         e = 0 if e <= 256 else max(256, e // 2)
-    return e, pr.part and not (st & N.STATUS_PART_OVERFLOW)
+        # smaller items turn more (and smaller) halos into global items: those take the
+        # global tables, sized by each halo, not partitions of part_e entries each
+        part = False
+    return e, part
 
 
 def items_single(items):
@@ -772,6 +785,16 @@ class OrbitEngine:
         self.prev = SnapshotState(ids=ctx['snap']['ids'], rhat=prep.rhat, meta=prep.meta,
                                   starts=prep.starts, counts=prep.counts,
                                   exists=ctx['exists'], plan=prep.plan, buckets=prep.buckets)
+
+    def step_ready(self, res):
+        """Without waiting: None while a step's kernels run, else whether its records
+        are final (False: its kernels asked for a re-planned re-run).  Error paths use
+        it to avoid blocking on, or launching more work after, a failure."""
+        if res.done is not None and not res.done.query():
+            return None
+        if getattr(res, 'pending', None) is not None:
+            return not int(res.ws.h_status[0])
+        return True
 
     def settle(self, res=None):
         """Wait for a deferred step (default: the pending one) and re-run it if its

@@ -26,13 +26,25 @@ from .utils import myin1d
 
 # ------------------------------------------------------------------ file access
 class _H5Store:
+    """An HDF5 file opened per access, as the reference opens it (postprocessing.py:
+    14, :89, :145, :198): a destination ('a') is created by its first group write,
+    not before."""
+
     def __init__(self, path, mode):
         import h5py
         self._h5py = h5py
         self.path = path
         self.mode = mode
-        with h5py.File(path, 'r' if mode == 'r' else mode) as hf:
-            self.attrs = dict(hf.attrs)
+        self._attrs = None
+        if mode in ('r', 'r+'):
+            self.attrs                    # a missing file fails here, as the reference's open
+
+    @property
+    def attrs(self):
+        if self._attrs is None:
+            with self._h5py.File(self.path, 'r') as hf:
+                self._attrs = {k: hf.attrs[k] for k in hf.attrs.keys()}
+        return self._attrs
 
     def group_names(self):
         with self._h5py.File(self.path, 'r') as hf:

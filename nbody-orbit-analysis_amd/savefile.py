@@ -85,15 +85,18 @@ class HDF5Savefile:
             return int(list(hf.keys())[-1].split('_')[1])
 
     def read_checkpoint(self):
-        import h5py
-        with h5py.File(self.path + '.checkpoint', 'r') as hf:
-            return hf['angles'][:]
-
-    def read_checkpoint_layout(self):
+        """The checkpoint angles (:229-232); the row layout attribute is read in the
+        same open, as the reference opens the checkpoint once."""
         import h5py
         with h5py.File(self.path + '.checkpoint', 'r') as hf:
             v = hf.attrs.get('row_layout')
-        return None if v is None else (v.decode() if isinstance(v, bytes) else str(v))
+            self._layout = None if v is None else (v.decode() if isinstance(v, bytes) else str(v))
+            return hf['angles'][:]
+
+    def read_checkpoint_layout(self):
+        if not hasattr(self, '_layout'):
+            self.read_checkpoint()
+        return self._layout
 
 
 class RankSink:

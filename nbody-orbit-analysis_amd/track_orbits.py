@@ -183,19 +183,51 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
                     flush()
 
             progen_exists = halo_exists
-    except BaseException:
-        # an error leaves no computed group unwritten (the reference wrote it already);
-        # a group whose own step failed cannot be written, and the error propagates
-        try:
-            flush()
-        except Exception:
-            pass
+    except Exception:
+        # the reference had written every group before the failing snapshot: write
+        # those whose records are available without re-running anything (a step that
+        # asks for a re-plan, a device that does not answer within a few seconds, or a
+        # failing query ends this); KeyboardInterrupt / SystemExit touch nothing
+        _salvage(groups, eng, out)
         raise
     flush()
 
     if verbose:
         print('Finished pericenter detection for all snapshots in {} s\n'.format(
             time.time() - tstart))
+
+
+def _poll(ready, t_end):
+    while not ready():
+        if time.time() > t_end:
+            return False
+        time.sleep(0.002)
+    return True
+
+
+def _salvage(groups, eng, out, timeout=10.0):
+    """Error path of track_orbits: write pending groups oldest first while each one's
+    records can be had without a re-run or an unbounded wait."""
+    t_end = time.time() + timeout
+    try:
+        while groups:
+            g = groups[0]
+            if g[2] is None:
+                ready = getattr(eng, 'step_ready', None)
+                if ready is None or not _poll(lambda: ready(g[0]) is not None, t_end) or \
+                        not ready(g[0]):
+                    return
+                g[2] = eng.fetch_async(g[0], g[1])
+            done = getattr(g[2], 'done', None)
+            if done is not None and not _poll(done.query, t_end):
+                return
+            offsets, ids, angles = g[2].wait()
+            groups.pop(0)
+            save_to_file(out, ids, offsets, angles, *g[3], **g[4])
+    except Exception as e:          # the original error propagates; this one is reported
+        import warnings
+        warnings.warn('track_orbits: pending groups not written after an error (%s: %s)'
+                      % (type(e).__name__, e), RuntimeWarning)
 
 
 class _Fetched:

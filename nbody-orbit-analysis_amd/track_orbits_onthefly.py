@@ -217,16 +217,20 @@ class OnTheFly:
             return torch.searchsorted(st, pos, right=True) - 1
         # departed: setdiff1d(previous, current) per halo (:145), i.e. the sorted unique
         # IDs of the unmatched previous rows (which already sit in halo order)
+        # rows before the first block are in no block (halo -1): the reference's slices
+        # start at region_offsets[0] and never see them (as the sharded stripes)
         dsel = torch.nonzero(~mp).squeeze(1)
         dh = halo_of(dsel, prev.starts)
+        dsel, dh = dsel[dh >= 0], dh[dh >= 0]
         departed, d_off = _sorted_unique_per_halo(
             eng.lib, eng.device, prev.ids[dsel],
             torch.bincount(dh, minlength=nh).cpu().numpy(), ids_dtype)
         # entered: setdiff1d(current, previous) per halo (:168); all of a halo's
         # particles, in loader order, when its progenitor block is empty (:178)
         esel = torch.nonzero(d.matched_cur == 0).squeeze(1)
-        e_ids = pc.snap['ids'][esel]
         eh = halo_of(esel, pc.starts)
+        esel, eh = esel[eh >= 0], eh[eh >= 0]
+        e_ids = pc.snap['ids'][esel]
         sorted_h = torch.from_numpy(p_has).to(eng.device)[eh]
         srt, s_off = _sorted_unique_per_halo(
             eng.lib, eng.device, e_ids[sorted_h],

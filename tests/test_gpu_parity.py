@@ -472,3 +472,59 @@ def test_onthefly_stream_carry_matches_fresh_calls(monkeypatch):
         assert sorted(a) == sorted(b)
         for k in a:
             assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=True), (s, k)
+
+
+class _LeadingRows:
+    """Loader wrapper: ``k`` rows before the first region block (region_offsets[0] = k).
+    The reference's slices start at region_offsets[0] (track_orbits.py:129-132,
+    track_orbits_onthefly.py:33-35), so those rows are never seen."""
+
+    def __init__(self, load, k=37, seed=5):
+        self.load, self.k, self.seed = load, k, seed
+
+    def __call__(self, s, pos, rad):
+        d = dict(self.load(s, pos, rad))
+        rng = np.random.default_rng(self.seed + int(s))
+        n = len(d['ids'])
+        pick = rng.integers(0, max(n, 1), self.k) if n else np.zeros(0, np.int64)
+        for key in ('ids', 'coordinates', 'velocities'):
+            a = np.asarray(d[key])
+            extra = a[pick] if n else np.zeros((self.k,) + a.shape[1:], a.dtype)
+            if key == 'coordinates':
+                extra = extra + 0.25
+            d[key] = np.concatenate([extra, a])
+        if isinstance(d['masses'], np.ndarray):
+            d['masses'] = np.concatenate([d['masses'][pick], d['masses']])
+        d['region_offsets'] = np.asarray(d['region_offsets']) + self.k
+        return d
+
+
+@pytest.mark.parametrize('mode', ['pericentric', 'apocentric'])
+def test_rows_before_the_first_block_are_ignored(mode):
+    """a loader whose region_offsets[0] > 0 (rows in no block) gives the
+    same outputs as without those rows, in the on-the-fly driver (single GPU) and the
+    batch driver."""
+    from orbitanalysis_amd.track_orbits_onthefly import track_orbits as otf, clear_carry
+    from orbitanalysis_amd.track_orbits import track_orbits
+    from orbitanalysis_amd.savefile import MemorySavefile
+    fix = load('g6_onthefly')
+    u, meta = universe(fix)
+    s = meta['snapshot']
+    outs = []
+    for loader in (u.load_snapshot_data, _LeadingRows(u.load_snapshot_data)):
+        clear_carry()
+        out = MemorySavefile()
+        otf(s, fix['links'], u.regions, loader, out, mode=mode, verbose=False)
+        outs.append(out.files[s][0])
+    assert sorted(outs[0]) == sorted(outs[1])
+    for k in outs[0]:
+        assert np.array_equal(outs[0][k], outs[1][k], equal_nan=outs[0][k].dtype.kind == 'f'), k
+    fix = load('g2_overlap_birth_massarray')
+    u, meta = universe(fix)
+    res = []
+    for loader in (u.load_snapshot_data, _LeadingRows(u.load_snapshot_data)):
+        out = MemorySavefile()
+        track_orbits(u.snapshot_numbers, u.main_branches(), u.regions, loader, out,
+                     verbose=False, mode=mode)
+        res.append(out.groups)
+    compare_groups(res[1], res[0], {})

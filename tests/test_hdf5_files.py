@@ -1,0 +1,378 @@
+"""the savefile contract at the file level.
+
+The fixture ``g12_hdf5_files`` holds every file the REFERENCE's own writers left
+(track_orbits.py:354-397 incl. the checkpoint and resume, track_orbits_onthefly.py:
+208-252, postprocessing.py:87-240) when run against the recording h5py stand-in
+(``tests/h5_standin.py``; ``tools/gen_golden.py:run_hdf5``): attributes, groups and
+datasets in creation order, dataset dtypes / shapes / values, and the sequence of
+``h5py.File`` opens.  Here the package's writers and readers run against the same
+stand-in and must leave the same trees.
+
+What this pins: the call-level layout (names, creation order, dtypes, shapes,
+values, attributes, open modes, resume lookup).  What it cannot pin: HDF5 bytes on
+disk, since h5py is not installed in this image — byte-level HDF5 parity stays
+"parity unpinned" (DESIGN.md §4).
+
+CPU tests feed the reference's own datasets through the package's writers
+(``savefile.HDF5Savefile``, the on-the-fly ``save_to_file``) and read the
+reference's files with the package's readers (resume lookup, checkpoint, the
+``Apsides`` constructor).  The ``-m gpu`` tests run the whole HIP path with path
+savefiles: ``track_orbits`` (run and resume), the on-the-fly driver and
+``Apsides.collate_apsides`` / ``save_final_apsis_counts``.
+"""
+import ast
+import json
+
+import numpy as np
+import pytest
+
+import h5_standin as H
+from golden_util import load, universe, ANGLE_TALLY
+
+FIX = 'g12_hdf5_files'
+WRITE_MODES = ('w', 'w-', 'x', 'a', 'r+')
+
+
+@pytest.fixture
+def h5():
+    prev = H.install()
+    H.reset()
+    yield H
+    H.reset()
+    H.uninstall(prev)
+
+
+def _fixture():
+    fix = load(FIX)
+    return fix, json.loads(str(fix['meta_json']))
+
+
+def want_tree(fix, meta, case, fname):
+    key = '%s|%s' % (case, fname)
+    m = meta['files'][key]
+    attrs = {}
+    for k, kind in m['attrs'].items():
+        v = fix['%s|@%s' % (key, k)]
+        attrs[k] = str(v) if kind == 'str' else v
+    order = [tuple(o) for o in m['order']]
+    arrays = {p: fix['%s|%s' % (key, p)] for kind, p in order if kind == 'dataset'}
+    return {'attrs': attrs, 'order': order, 'arrays': arrays}
+
+
+def case_files(meta, case):
+    pre = case + '|'
+    return sorted(k[len(pre):] for k in meta['files'] if k.startswith(pre))
+
+
+def _angle_rule(path, fname):
+    """How a dataset's values compare: 'f16' (apsis / checkpoint angles: 1 float16
+    ulp, counted), 'change' (on-the-fly angle changes: ulps of their dtype), else exact."""
+    leaf = path.rsplit('/', 1)[-1]
+    if leaf != 'angles':
+        return 'exact'
+    return 'f16' if fname.endswith('.checkpoint') or '/' in path else 'change'
+
+
+def compare_tree(got, want, fname, exact=False, report=None):
+    assert got['attrs'].keys() == want['attrs'].keys(), (fname, got['attrs'].keys(),
+                                                         want['attrs'].keys())
+    for k, w in want['attrs'].items():
+        v = got['attrs'][k]
+        if isinstance(w, str):
+            assert isinstance(v, str) and v == w, (fname, k, v, w)
+        else:
+            v = np.asarray(v)
+            assert v.dtype == w.dtype and v.shape == w.shape and np.array_equal(v, w), (fname, k)
+    assert [tuple(o) for o in got['order']] == want['order'], (fname, got['order'], want['order'])
+    for p, w in want['arrays'].items():
+        v = got['arrays'][p]
+        assert v.dtype == w.dtype and v.shape == w.shape, (fname, p, v.dtype, w.dtype, v.shape, w.shape)
+        rule = 'exact' if exact else _angle_rule(p, fname)
+        if rule == 'exact' or w.dtype.kind != 'f':
+            assert np.array_equal(v, w, equal_nan=w.dtype.kind == 'f'), (fname, p)
+            continue
+        a, b = v.astype(np.float64), w.astype(np.float64)
+        same = (a == b) | (np.isnan(a) & np.isnan(b))
+        assert np.array_equal(np.isnan(a), np.isnan(b)), (fname, p, 'NaN pattern')
+        if rule == 'f16':
+            ulp = np.spacing(np.maximum(np.abs(a), np.abs(b)).astype(np.float16)).astype(np.float64)
+            assert np.all(same | (np.abs(a - b) <= ulp)), (fname, p, 'off by more than 1 f16 ulp')
+            ANGLE_TALLY['angles'] += int(a.size)
+            ANGLE_TALLY['mismatch'] += int((~same).sum())
+            if report is not None:
+                report['f16'] = report.get('f16', 0) + int(a.size)
+                report['f16_off'] = report.get('f16_off', 0) + int((~same).sum())
+        else:
+            ok = ~np.isnan(b)
+            ulp = np.spacing(np.abs(w[ok])).astype(np.float64)
+            err = np.abs(a[ok] - b[ok]) / ulp
+            assert np.all(err <= 2), (fname, p, float(err.max()))
+            if report is not None:
+                report['change_ulp_max'] = max(report.get('change_ulp_max', 0.0),
+                                               float(err.max()) if err.size else 0.0)
+
+
+def write_opens(opens):
+    return [(f, m) for f, m in opens if m in WRITE_MODES]
+
+
+# ------------------------------------------------------------------ the stand-in itself
+def test_standin_follows_h5py_semantics(h5):
+    import h5py
+    with pytest.raises(FileNotFoundError):
+        h5py.File('/t/missing.hdf5', 'r+')
+    with h5py.File('/t/a.hdf5', 'w') as hf:
+        hf.attrs['mode'] = 'pericentric'
+        hf.attrs['box_size'] = [1.0, 2.0, 3.0]
+        g = hf.create_group('snapshot_010')
+        g.create_dataset('x', data=np.arange(3, dtype=np.int32))
+        hf.create_group('snapshot_002')
+        with pytest.raises(ValueError):
+            hf.create_group('snapshot_010')
+        with pytest.raises(ValueError):
+            g.create_dataset('x', data=[1])
+    with h5py.File('/t/a.hdf5', 'r') as hf:
+        assert list(hf.keys()) == ['snapshot_002', 'snapshot_010']     # name order
+        assert hf['snapshot_010']['x'][:].dtype == np.int32
+        assert np.array_equal(hf['snapshot_010/x'][1:], [1, 2])
+        assert isinstance(hf.attrs['mode'], str)
+        assert hf.attrs['box_size'].dtype == np.float64
+        with pytest.raises(ValueError):
+            hf.create_group('y')
+    with pytest.raises(FileExistsError):
+        h5py.File('/t/a.hdf5', 'w-')
+    t = H.tree('/t/a.hdf5')
+    assert t['order'] == [('group', 'snapshot_010'), ('dataset', 'snapshot_010/x'),
+                          ('group', 'snapshot_002')]
+
+
+def test_fixture_records_the_reference_contract():
+    """What the reference itself did, as recorded: one 'w' per savefile, then per
+    compared snapshot an 'r+' group write and (checkpoint=True) a 'w' checkpoint;
+    resume opens the savefile and the checkpoint once each with 'r'; the first-row
+    quirk fails its first 'r+' with FileNotFoundError."""
+    fix, meta = _fixture()
+    o = [tuple(x) for x in meta['opens']['g1_config1']['run']]
+    assert o == [('run.hdf5', 'w')] + [('run.hdf5', 'r+'), ('run.hdf5.checkpoint', 'w')] * 9
+    o = [tuple(x) for x in meta['opens']['g1_config1']['resume']]
+    assert o[5:7] == [('resume.hdf5', 'r'), ('resume.hdf5.checkpoint', 'r')]
+    o = [tuple(x) for x in meta['opens']['g1_config1']['collate']]
+    assert write_opens(o) == [('collated.hdf5', 'a')] * 9 + [('collated.hdf5', 'r+')]
+    assert meta['errors']['quirk_row0'] == 'FileNotFoundError'
+    assert [tuple(x) for x in meta['opens']['quirk_row0']] == [('run.hdf5', 'r+')]
+    t = want_tree(fix, meta, 'g1_config1', 'run.hdf5')
+    assert t['attrs'] == {'mode': 'pericentric'}
+    assert [p for k, p in t['order'] if k == 'group'] == ['snapshot_%03d' % s for s in range(1, 10)]
+
+
+# ------------------------------------------------------------------ writers (CPU)
+def _groups_in_order(tree):
+    out = []
+    for kind, p in tree['order']:
+        if kind == 'group':
+            out.append((p, {}))
+        else:
+            g, d = p.split('/')
+            assert out[-1][0] == g
+            out[-1][1][d] = tree['arrays'][p]
+    return out
+
+
+@pytest.mark.parametrize('case', ['g1_config1', 'g3_apo_periodic', 'g11_edges', 'g5_fp32_centre32'])
+def test_batch_writer_leaves_the_reference_tree(case, h5):
+    """savefile.HDF5Savefile through the driver's own initialize_savefile /
+    save_to_file, fed the reference's datasets: same file, same checkpoint, same
+    open sequence (track_orbits.py:354-397)."""
+    from orbitanalysis_amd.track_orbits import initialize_savefile, save_to_file
+    fix, meta = _fixture()
+    run = load(case)
+    mode = str(run['attr/mode'])
+    want = want_tree(fix, meta, case, 'run.hdf5')
+    box = want['attrs'].get('box_size')
+    ck = 'run.hdf5.checkpoint' in case_files(meta, case)
+    angles = want_tree(fix, meta, case, 'run.hdf5.checkpoint')['arrays']['angles'] if ck else None
+    path = '/p/%s/run.hdf5' % case
+    initialize_savefile(path, mode, box, verbose=False)
+    tag = '{}er_IDs'.format(mode[:-3])
+    for g, d in _groups_in_order(want):
+        save_to_file(path, d[tag], d['region_offsets'], d['angles'], d['region_positions'],
+                     d['region_radii'], d['bulk_velocities'], d['halo_IDs'],
+                     d.get('final_descendant_IDs'), int(g.split('_')[1]), mode, ck, angles,
+                     verbose=False)
+    compare_tree(H.tree(path), want, 'run.hdf5', exact=True)
+    if ck:
+        compare_tree(H.tree(path + '.checkpoint'),
+                     want_tree(fix, meta, case, 'run.hdf5.checkpoint'), 'ckpt', exact=True)
+    assert H.opens('/p/%s/' % case) == [tuple(x) for x in meta['opens'][case]['run']]
+
+
+@pytest.mark.parametrize('case', ['g1_config1', 'g3_apo_periodic', 'g11_edges'])
+def test_resume_reads_the_reference_files(case, h5):
+    """The resume lookup (`list(hf.keys())[-1]`, :93-101) and the checkpoint read
+    (:229-232) on the reference's own files, one 'r' open each."""
+    from orbitanalysis_amd.savefile import HDF5Savefile
+    fix, meta = _fixture()
+    for f in ('resume.hdf5', 'resume.hdf5.checkpoint'):
+        t = want_tree(fix, meta, case, f)
+        with H.File('/r/' + f, 'w') as hf:
+            for kind, p in t['order']:
+                if kind == 'group':
+                    hf.create_group(p)
+                else:
+                    hf.create_dataset(p, data=t['arrays'][p])
+            for k, v in t['attrs'].items():
+                hf.attrs[k] = v
+    H.OPENS.clear()
+    sf = HDF5Savefile('/r/resume.hdf5')
+    t = want_tree(fix, meta, case, 'resume.hdf5')
+    last = [p for k, p in t['order'] if k == 'group'][-1]
+    assert sf.last_snapshot_number() == int(last.split('_')[1])
+    a = sf.read_checkpoint()
+    w = want_tree(fix, meta, case, 'resume.hdf5.checkpoint')['arrays']['angles']
+    assert a.dtype == w.dtype and np.array_equal(a, w, equal_nan=True)
+    assert sf.read_checkpoint_layout() is None
+    assert H.opens('/r/') == [('resume.hdf5', 'r'), ('resume.hdf5.checkpoint', 'r')]
+
+
+def test_checkpoint_layout_attribute_round_trip(h5):
+    """A presharded run's checkpoint records its row layout as an attribute beside
+    the reference's 'angles' dataset; a plain checkpoint has none."""
+    from orbitanalysis_amd.savefile import HDF5Savefile
+    sf = HDF5Savefile('/c/x.hdf5')
+    sf.write_checkpoint(np.zeros(5, np.float16), layout='rank-major/world=2/blocks=ab')
+    t = H.tree('/c/x.hdf5.checkpoint')
+    assert t['order'] == [('dataset', 'angles')] and t['attrs'] == {'row_layout': 'rank-major/world=2/blocks=ab'}
+    assert HDF5Savefile('/c/x.hdf5').read_checkpoint_layout() == 'rank-major/world=2/blocks=ab'
+    sf.write_checkpoint(np.zeros(5, np.float16))
+    assert HDF5Savefile('/c/x.hdf5').read_checkpoint_layout() is None
+
+
+@pytest.mark.parametrize('case', ['g6_onthefly', 'g6d_onthefly_empty'])
+def test_onthefly_writer_leaves_the_reference_files(case, h5):
+    """The on-the-fly save_to_file (track_orbits_onthefly.py:208-252): one 'w' file
+    per snapshot, datasets in the reference's order, box_size attribute."""
+    from orbitanalysis_amd.track_orbits_onthefly import save_to_file
+    fix, meta = _fixture()
+    for f in case_files(meta, case):
+        want = want_tree(fix, meta, case, f)
+        mode, s = f[:-len('.hdf5')].rsplit('_', 1)
+        attrs = {k: v for k, v in want['attrs'].items()}
+        save_to_file('/o/%s/%s_{}.hdf5' % (case, mode), int(s),
+                     {p: a for p, a in want['arrays'].items()}, attrs, verbose=False)
+        compare_tree(H.tree('/o/%s/%s' % (case, f)), want, f, exact=True)
+    assert sorted(H.opens('/o/%s/' % case)) == sorted(tuple(x) for x in meta['opens'][case])
+
+
+@pytest.mark.parametrize('case', ['g1_config1', 'g3_apo_periodic', 'g11_edges'])
+def test_apsides_reads_the_reference_savefile(case, h5):
+    """Apsides(filename) on the reference's file (postprocessing.py:10-28): snapshot
+    numbers, final halo IDs, mode and box size, from 'r' opens only."""
+    from orbitanalysis_amd.postprocessing import Apsides
+    fix, meta = _fixture()
+    t = want_tree(fix, meta, case, 'run.hdf5')
+    _materialise('/a/run.hdf5', t)
+    H.OPENS.clear()
+    ap = Apsides('/a/run.hdf5')
+    groups = [p for k, p in t['order'] if k == 'group']
+    assert np.array_equal(ap.snapshot_numbers, [int(g.split('_')[1]) for g in groups])
+    w = t['arrays'][groups[-1] + '/halo_IDs']
+    assert ap.final_halo_ids.dtype == w.dtype and np.array_equal(ap.final_halo_ids, w)
+    assert ap.mode == t['attrs']['mode']
+    assert hasattr(ap, 'box_size') == ('box_size' in t['attrs'])
+    assert all(m == 'r' for _, m in H.opens('/a/'))
+
+
+def _materialise(path, tree):
+    with H.File(path, 'w') as hf:
+        for kind, p in tree['order']:
+            if kind == 'group':
+                hf.create_group(p)
+            else:
+                hf.create_dataset(p, data=tree['arrays'][p])
+        for k, v in tree['attrs'].items():
+            hf.attrs[k] = v
+
+
+# ------------------------------------------------------------------ whole HIP path (GPU)
+BATCH_H5 = ['g1_config1', 'g3_apo_periodic', 'g11_edges', 'g5_fp32_centre32']
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', BATCH_H5)
+def test_track_orbits_path_savefile_matches_reference_files(case, h5):
+    """track_orbits(..., savefile=<path>) on the HIP path, a run and a resume (the
+    reference's k-snapshot interruption), then Apsides.collate_apsides on the written
+    file: every file's tree equals the reference's, and the driver's open sequence is
+    the reference's (the pipelined writes keep its order)."""
+    from orbitanalysis_amd.track_orbits import track_orbits
+    from orbitanalysis_amd.postprocessing import Apsides
+    fix, meta = _fixture()
+    u, m = universe(load(case))
+    info = meta['batch'][case]
+    pre = '/g/%s/' % case
+    rep = {}
+    ref_opens = {ph: [tuple(x) for x in v] for ph, v in meta['opens'][case].items()}
+    track_orbits(u.snapshot_numbers, u.main_branches(), u.regions, u.load_snapshot_data,
+                 pre + 'run.hdf5', verbose=False, **m['run'])
+    assert H.opens(pre) == ref_opens['run']
+    k = info['resume_after']
+    if k is not None:
+        H.OPENS.clear()
+        track_orbits(u.snapshot_numbers[:k], u.main_branches()[:k], u.regions,
+                     u.load_snapshot_data, pre + 'resume.hdf5', verbose=False, **m['run'])
+        track_orbits(u.snapshot_numbers, u.main_branches(), u.regions, u.load_snapshot_data,
+                     pre + 'resume.hdf5', verbose=False, resume=True, **m['run'])
+        assert H.opens(pre) == ref_opens['resume']
+    if 'collate' in ref_opens:
+        H.OPENS.clear()
+        kw = {kk: ast.literal_eval(vv) for kk, vv in info['collate'].items()}
+        Apsides(pre + 'run.hdf5').collate_apsides(savefile=pre + 'collated.hdf5',
+                                                  verbose=False, **kw)
+        # the package reads per dataset, the reference per snapshot: the writes match
+        assert write_opens(H.opens(pre)) == write_opens(ref_opens['collate'])
+    assert H.files(pre) == case_files(meta, case)
+    for f in case_files(meta, case):
+        compare_tree(H.tree(pre + f), want_tree(fix, meta, case, f), f, report=rep)
+    if rep.get('f16'):
+        from test_gpu_parity import mismatch_ok
+        assert mismatch_ok(rep['f16_off'], rep['f16']), rep
+    print(case, rep)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', ['g6_onthefly', 'g6d_onthefly_empty'])
+def test_onthefly_path_savefile_matches_reference_files(case, h5):
+    """The on-the-fly driver with a path template, called snapshot after snapshot in
+    both modes (the second call reuses the first's device state): one file per call,
+    each equal to the reference's."""
+    from orbitanalysis_amd.track_orbits_onthefly import track_orbits as otf, clear_carry
+    fix, meta = _fixture()
+    u, m = universe(load(case))
+    pre = '/q/%s/' % case
+    rep = {}
+    for mode in ('pericentric', 'apocentric'):
+        clear_carry()
+        for s in meta['onthefly'][case]['snapshots']:
+            otf(s, load(case)['links'], u.regions, u.load_snapshot_data,
+                pre + mode + '_{}.hdf5', mode=mode, verbose=False)
+    assert H.opens(pre) == [tuple(x) for x in meta['opens'][case]]
+    for f in case_files(meta, case):
+        compare_tree(H.tree(pre + f), want_tree(fix, meta, case, f), f, report=rep)
+    print(case, rep)
+
+
+@pytest.mark.gpu
+def test_first_row_absent_quirk_fails_like_the_reference(h5):
+    """main_branches' first row all -1: the reference never initialises the savefile
+    (:140) and its first group write ('r+') fails; so does the drop-in, with the same
+    exception and the same single open."""
+    from orbitanalysis_amd.track_orbits import track_orbits
+    from orbitanalysis_amd.synthetic import PlummerSnapshots
+    fix, meta = _fixture()
+    q = meta['quirk_row0']
+    u = PlummerSnapshots(**q['gen'])
+    with pytest.raises(FileNotFoundError):
+        track_orbits(u.snapshot_numbers, u.main_branches(), u.regions, u.load_snapshot_data,
+                     '/z/run.hdf5', verbose=False, **q['run'])
+    assert meta['errors']['quirk_row0'] == 'FileNotFoundError'
+    assert H.opens('/z/') == [tuple(x) for x in meta['opens']['quirk_row0']]

@@ -292,7 +292,7 @@ def test_plan_part_bucket_sets():
     K, g = pl['K'], pl['gpart']
     assert g.shape == (5, GPART_W)
     assert all(k == 0 or (k & (k - 1)) == 0 for k in K)
-    assert K[0] == max(PART_SPREAD, 16) and K[2] == 0 and K[4] > 0
+    assert K[0] == 16 and K[1] == 64 and K[3] == PART_SPREAD and K[2] == 0 and K[4] > 0
     assert np.all(K[K > 0] * 4096 * 0.9 >= cur[K > 0])
     # current set: consecutive K * part_e runs, counters consecutive
     assert np.array_equal(g[:, 0], (np.cumsum(K) - K) * 4096)
@@ -310,3 +310,25 @@ def test_plan_part_bucket_sets():
     # every current partition listed once
     pl_ok = pl['plist'][pl['plist'][:, 0] >= 0]
     assert len(pl_ok) == K.sum() and len({tuple(r) for r in pl_ok}) == K.sum()
+
+
+def test_plan_part_memory_scales_with_halo_size():
+    """the partition floor scales with the halo, so many global halos just
+    past the item budget do not each take PART_SPREAD * part_e bucket entries; and a
+    re-plan after an LDS table overflow leaves the partitioned path (its smaller items
+    would turn every halo into a global item)."""
+    from types import SimpleNamespace
+    from orbitanalysis_amd import _native as N
+    from orbitanalysis_amd.engine import plan_part, retry_plan, PART_SPREAD
+    n = 2000
+    cur = np.full(n, 6200)
+    glob = {'h0': np.arange(n)}
+    pl = plan_part(glob, cur, cur, 4096, 4096)
+    assert pl['n_cur'] <= 3 * cur.sum(), pl['n_cur'] / cur.sum()
+    big = plan_part({'h0': np.arange(3)}, np.full(3, 100000), np.full(3, 100000), 4096, 4096)
+    assert np.all(big['K'] == PART_SPREAD)          # configs[1]'s halos keep the full spread
+    pr = SimpleNamespace(entries=6144, part=True)
+    assert retry_plan(pr, N.STATUS_TABLE_OVERFLOW) == (3072, False)
+    assert retry_plan(pr, N.STATUS_PART_OVERFLOW) == (6144, False)
+    pr.entries = 256
+    assert retry_plan(pr, N.STATUS_TABLE_OVERFLOW) == (0, False)

@@ -466,6 +466,117 @@ def run_progenitors(syn, P):
     return out
 
 
+# ------------------------------------------------- §8(f) row f2: the HDF5 files themselves
+# The reference's own writers and readers (track_orbits.py:93-101, :229-232, :354-397;
+# track_orbits_onthefly.py:208-252; postprocessing.py:10-28, :87-240) run against the
+# recording h5py stand-in of tests/h5_standin.py, and every file they leave is stored
+# as a tree: attributes, nodes in creation order, dataset values (dtype and shape
+# included), plus the sequence of File() opens.  tests/test_hdf5_files.py runs the
+# package's writers and readers against the same stand-in and compares the trees.
+HDF5_BATCH = {
+    # case: (BATCH_CASES entry, resume after k snapshots or None, collate kwargs or None)
+    'g1_config1': (3, dict(save_final_counts=True)),
+    'g3_apo_periodic': (3, dict(save_final_counts=True, angle_cut=0.0)),
+    'g11_edges': (4, dict()),         # final counts: the reference fails on its deaths
+    'g5_fp32_centre32': (None, None),
+}
+HDF5_ONTHEFLY = {
+    # case: snapshots called in turn (each writes one file), with the case's links
+    'g6_onthefly': [4, 5],
+    'g6d_onthefly_empty': [3],
+}
+# the reference never initialises the savefile when main_branches' first row is all
+# -1 (:140 runs only at i == 0), so its first 'r+' open fails
+HDF5_QUIRK = dict(gen=dict(n_halos=2, n_per_halo=[500, 400], n_snapshots=3, seed=41, dt=0.5,
+                           absent=[[0, 0], [0, 1]]),
+                  run=dict(mode='pericentric'))
+
+
+def _store_tree(out, meta, key, tree):
+    """tree (h5_standin.tree) -> arrays under 'key|...' + order/attr kinds in meta."""
+    meta[key] = {'order': tree['order'],
+                 'attrs': {k: ('str' if isinstance(v, str) else 'array')
+                           for k, v in tree['attrs'].items()}}
+    for k, v in tree['attrs'].items():
+        out['%s|@%s' % (key, k)] = np.array(v)
+    for p, a in tree['arrays'].items():
+        out['%s|%s' % (key, p)] = a
+
+
+def run_hdf5(syn, T, O, P):
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    import h5_standin as H
+    mods = (T, O, P)
+    saved = [m.h5py for m in mods]
+    for m in mods:
+        m.h5py = H
+    out, meta = {}, {'batch': {}, 'onthefly': {}, 'files': {}, 'opens': {}, 'errors': {}}
+    try:
+        for name, (k, ckw) in HDF5_BATCH.items():
+            case = BATCH_CASES[name]
+            u = syn.PlummerSnapshots(**gen_kwargs(case['gen']))
+            H.reset()
+            pre = '/h5/%s/' % name
+            phases = {}
+            T.track_orbits(u.snapshot_numbers, u.main_branches(), u.regions,
+                           u.load_snapshot_data, pre + 'run.hdf5', npool=None, verbose=False,
+                           **case['run'])
+            phases['run'] = H.opens(pre)
+            if k is not None:
+                H.OPENS.clear()
+                T.track_orbits(u.snapshot_numbers[:k], u.main_branches()[:k], u.regions,
+                               u.load_snapshot_data, pre + 'resume.hdf5', npool=None,
+                               verbose=False, **case['run'])
+                T.track_orbits(u.snapshot_numbers, u.main_branches(), u.regions,
+                               u.load_snapshot_data, pre + 'resume.hdf5', npool=None,
+                               verbose=False, resume=True, **case['run'])
+                phases['resume'] = H.opens(pre)
+            if ckw is not None:
+                H.OPENS.clear()
+                P.Apsides(pre + 'run.hdf5').collate_apsides(savefile=pre + 'collated.hdf5',
+                                                            verbose=False, **ckw)
+                phases['collate'] = H.opens(pre)
+            meta['batch'][name] = {'resume_after': k, 'collate': {
+                kk: repr(vv) for kk, vv in (ckw or {}).items()}}
+            meta['opens'][name] = phases
+            for f in H.files(pre):
+                _store_tree(out, meta['files'], '%s|%s' % (name, f), H.tree(pre + f))
+        for name, snaps in HDF5_ONTHEFLY.items():
+            case = ONTHEFLY_CASES[name]
+            g = dict(case['gen'])
+            for kk in ('dtype', 'centre_dtype', 'id_dtype'):
+                if kk in g:
+                    g[kk] = np.dtype(g[kk])
+            u = syn.PlummerSnapshots(**g)
+            H.reset()
+            pre = '/h5/%s/' % name
+            for mode in ('pericentric', 'apocentric'):
+                for s in snaps:
+                    O.track_orbits(s, np.array(case['links']), u.regions, u.load_snapshot_data,
+                                   pre + mode + '_{}.hdf5', mode=mode, verbose=False)
+            meta['onthefly'][name] = {'snapshots': snaps}
+            meta['opens'][name] = H.opens(pre)
+            for f in H.files(pre):
+                _store_tree(out, meta['files'], '%s|%s' % (name, f), H.tree(pre + f))
+        u = syn.PlummerSnapshots(**gen_kwargs(HDF5_QUIRK['gen']))
+        H.reset()
+        pre = '/h5/quirk_row0/'
+        try:
+            T.track_orbits(u.snapshot_numbers, u.main_branches(), u.regions,
+                           u.load_snapshot_data, pre + 'run.hdf5', npool=None, verbose=False,
+                           **HDF5_QUIRK['run'])
+            meta['errors']['quirk_row0'] = None
+        except Exception as e:                      # recorded: the reference's own failure
+            meta['errors']['quirk_row0'] = type(e).__name__
+        meta['opens']['quirk_row0'] = H.opens(pre)
+        meta['quirk_row0'] = HDF5_QUIRK
+    finally:
+        for m, h in zip(mods, saved):
+            m.h5py = h
+    out['meta_json'] = np.array(json.dumps(meta))
+    return out
+
+
 def main():
     install_stubs()
     import orbitanalysis.track_orbits as T
@@ -476,6 +587,11 @@ def main():
     syn = load_synthetic()
     os.makedirs(OUT, exist_ok=True)
     only = set(sys.argv[1:])          # optional: regenerate just the named fixtures
+    if not only or 'g12_hdf5_files' in only:
+        np.savez_compressed(os.path.join(OUT, 'g12_hdf5_files.npz'), **run_hdf5(syn, T, O, P))
+        print('wrote g12_hdf5_files')
+    if only == {'g12_hdf5_files'}:
+        return
     for name, case in BATCH_CASES.items():
         if only and name not in only:
             continue
