@@ -49,6 +49,16 @@ def step_bytes(pr, n_prev, n_apsis):
     return pr.n * cur + n_prev * prev + n_apsis * (p.ids.itemsize + 2)
 
 
+def kernel_label(pr):
+    """The kernels the oa_step HIP events bracket for this workload."""
+    if pr.n_global and pr.part:
+        return ('oa_step: k_part_scatter + k_part_join' +
+                (' + k_step' if pr.n_small else ''))
+    if pr.n_global:
+        return 'oa_step: k_big_frame + k_big_join' + (' + k_step' if pr.n_small else '')
+    return 'k_step'
+
+
 def cpu_baseline(snap_cur, snap_prev, cat_cur, cat_prev, H, z, gpu_prev_angles,
                  gpu_ids, gpu_offs, n_halos, mode, workers):
     """Time the reference's per-halo path on the CPU (oracle/cpu_baseline.py, a child
@@ -322,7 +332,7 @@ def main():
                        'host_prepare_ms': float(np.median(prep_s)) * 1e3},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
-                         'traffic': traffic, 'kernel': 'k_step', 'kernel_ms': kern_ms,
+                         'traffic': traffic, 'kernel': kernel_label(last), 'kernel_ms': kern_ms,
                          'alg_bytes_per_launch': bytes_launch},
             'cpu_baseline': cpu,
         }

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OA_ABI_VERSION 13
+#define OA_ABI_VERSION 14
 
 #define OA_OK 0
 #define OA_E_ARG (-1)       /* invalid argument / unsupported dtype plan */
@@ -46,6 +46,12 @@ extern "C" {
 #define OA_STATUS_PART_OVERFLOW 8u    /* a large-halo hash partition outgrew its bucket
                                          or LDS table: re-run the snapshot on the
                                          global-table path (n_parts = 0)             */
+#define OA_STATUS_PART_KEYS 32u       /* part_key4: a large-halo ID's high word differs
+                                         from part_hi: re-run on the global-table path
+                                         and keep 8-byte bucket keys                 */
+#define OA_STATUS_LOOKBACK 16u        /* direct records: an item's look-back found no
+                                         predecessor prefix within its spin budget
+                                         (records invalid): re-run with direct = 0   */
 
 #define OA_MODE_PERICENTRIC 0
 #define OA_MODE_APOCENTRIC 1
@@ -163,20 +169,22 @@ typedef struct oa_step_args {
      * global-table path above).  Each global item's IDs are cut into K hash partitions
      * (K a power of two, partition = mulhi64(mix64(ID), K)) so one partition's current
      * particles fit an LDS table of oa_build_info(4) entries.  A *bucket set* holds one
-     * snapshot's state of those halos by partition: per entry the ID, the position in
-     * the halo's block (| sign(v_r) << 30 in a current set), the state word and r̂.
-     * The current set of one step is the previous set of the next (inherited), so the
-     * previous state is streamed from its buckets, never scattered again:
+     * snapshot's state of those halos by partition: per entry the ID (its low word
+     * only with part_key4), the position in the halo's block (| sign(v_r) << 30 in a
+     * current set), the state word and r̂.  The current set of one step is the previous
+     * set of the next (inherited), so the previous state is streamed from its buckets,
+     * never scattered again:
      *   k_part_scatter  frame of the current chunks (gchunk1) into the current set
      *                   (LDS-staged: each partition's entries leave as one run); the
      *                   previous chunks (gchunk2) of halos without an inherited set
      *                   into a fresh previous set, from the position-order state
      *   k_part_join     one work-group per plist row (LDS: oa_part_lds_bytes): LDS table
      *                   of a current bucket, lookups of the previous bucket(s) holding
-     *                   its IDs, the state word of every matched current entry, apsis
-     *                   marks at previous positions
-     *   k_part_emit     previous chunks: marks -> records packed per 64-position
-     *                   segment (the layout k_big_join writes)
+     *                   its IDs, the state word of every matched current entry; each
+     *                   apsis record is appended to its previous-block chunk (gchunk2
+     *                   row: 4096 positions, oa_build_info(7)) in the item's scratch
+     *                   range with its position in the chunk (scratch_rk)
+     *   oa_compact      ranks each chunk's records by position (k_gather_recs)
      * The position-order rhat_out / meta_out of these halos are NOT written
      * (oa_part_unbucket restores them from the set when a caller needs them).      */
     int32_t n_parts;            /* rows of plist (padding rows included)              */
@@ -194,39 +202,59 @@ typedef struct oa_step_args {
                                    i* arrays, counters in icnt), [4] previous set base,
                                    [5] its K (a power of two), [6] its entries per
                                    partition, [7] index of its first counter,
-                                   [8..15] 0                                          */
-    uint64_t *pkey_cur;         /* current set: IDs (zero-extended 4-byte IDs)        */
+                                   [8] index in pcnt of the record counter of its
+                                   first previous-block chunk (one per gchunk2 row of
+                                   the item, in order), [9..15] 0                     */
+    void *pkey_cur;             /* current set: IDs (uint64; uint32 low words with
+                                   part_key4)                                         */
     uint32_t *ppos_cur;         /*   position in the halo's block | sign(v_r) << 30   */
     uint32_t *pmeta_cur;        /*   state word (f16 angle | sign << 16)              */
     void *prh_cur;              /*   r̂ (3 values of the r̂ dtype)                      */
-    uint64_t *pkey_prev;        /* fresh previous set: IDs                            */
+    void *pkey_prev;            /* fresh previous set: IDs (as pkey_cur)              */
     uint32_t *ppos_prev;        /*   position in the halo's previous block            */
     uint32_t *pmeta_prev;       /*   its previous state word                          */
     void *prh_prev;             /*   its previous r̂ (3 values of the r̂ dtype)         */
-    const uint64_t *ikey;       /* inherited previous set (the previous step's current
-                                   set; any of these may be NULL when none is used)   */
+    const void *ikey;           /* inherited previous set (the previous step's current
+                                   set, keys of the same width; any of these may be
+                                   NULL when none is used)                            */
     const uint32_t *ipos;
     const uint32_t *imeta;
     const void *irh;
     const uint32_t *icnt;       /*   its fill counters                                */
     uint32_t *pcnt;             /* [n_pcnt] fill counters of the current set and of the
-                                   fresh previous set, zeroed by oa_step              */
+                                   fresh previous set, then the record counters of the
+                                   previous-block chunks; zeroed by oa_step           */
     int64_t n_pcnt;
-    uint32_t *gmark;            /* apsis marks, one per padded previous position of
-                                   the global items: 0 or 1 << 16 | float16 angle;
-                                   zeroed by oa_step                                  */
-    int64_t gmark_base;         /* scratch_off of the first global item (gmark[0])    */
-    int64_t gmark_n;            /* marks (padded previous positions of global items)  */
+    uint16_t *scratch_rk;       /* per apsis record of a partitioned halo: its position
+                                   in its 4096-position chunk (beside scratch_ids)    */
+    int32_t part_key4;          /* 1: bucket keys are the IDs' low words; every
+                                   large-halo ID's high word must equal part_hi, else
+                                   OA_STATUS_PART_KEYS (4-byte IDs: always 1)         */
+    uint32_t part_hi;
     const int64_t *gchunk3;     /* the previous chunks k_part_scatter reads: those of
                                    halos with a fresh previous set (NULL: gchunk2)    */
     int32_t n_gchunk3;
-    int32_t mark_tag;           /* 1..32767: k_part_join tags the marks it writes, so a
-                                   gmark buffer kept between steps needs no clearing (the
-                                   caller zeroes it once, and again before a tag repeats);
-                                   0: oa_step clears gmark_n marks first                 */
     int32_t items_single;       /* 1: every packed item holds one halo (the launch takes
                                    k_step's one-halo specialisation); 0: any item plan */
-    int32_t reserved;
+    /* Direct records (replaces oa_compact for a compare step with packed items only,
+     * not on-the-fly): k_step writes every apsis record at its final output offset
+     * and the per-halo offsets (track_orbits.py:199-227), each item finding its
+     * record prefix by a decoupled look-back over the items before it.            */
+    int32_t direct;             /* 1: on (n_global_items must be 0); 0: scratch +
+                                   oa_compact                                        */
+    uint64_t *lookback;         /* [n_items] item prefix words: lb_epoch << 48 | state
+                                   << 46 | records (state 1: the item's own count,
+                                   2: inclusive prefix); words of other epochs read as
+                                   unpublished, so the buffer is zeroed only once and
+                                   again before an epoch repeats                      */
+    int32_t lb_epoch;           /* 1..65535 */
+    int32_t n_slots;            /* halos with a progenitor (out_slot range)           */
+    int64_t *offsets_out;       /* [n_slots + 1] apsis region offsets                 */
+    void *out_ids;              /* capacity >= records (<= n_prev), ID dtype           */
+    uint16_t *out_ang;          /* float16 bits                                        */
+    int32_t *out_pos;           /* optional: each record's previous-state row (the
+                                   oa_compact_args.out_pos of a scratch_pos step)     */
+    int64_t *total_out;         /* device scalar: number of records                    */
 } oa_step_args;
 
 /* Arguments of oa_part_unbucket: a bucket set's entries back to position order. */
@@ -276,6 +304,12 @@ typedef struct oa_compact_args {
                                    items' previous-block chunks); their records are then
                                    gathered one work-group per chunk instead of one per
                                    item (NULL: per item)                                */
+    const uint32_t *chunk_count;/* partitioned steps (with gchunks): the record count of
+                                   each gchunk2 row (oa_step_args.pcnt + gpart[8] of its
+                                   item's first row ...); the records of a chunk sit
+                                   unordered at its scratch base and are ranked by
+                                   scratch_rk.  NULL: 64-position segments (seg_count) */
+    const uint16_t *scratch_rk;
 } oa_compact_args;
 
 /* ABI version (OA_ABI_VERSION) — lets the host reject a stale library. */
@@ -289,7 +323,8 @@ int64_t oa_struct_size(int32_t which);
 /* Compile-time configuration: 0 work-group size, 1 max halos per item,
  * 2 phase-1 unroll, 3 progenitor rows (64 positions) per wave of an item, 4 current
  * entries per large-halo partition (k_part_join's LDS table), 5 largest K per halo
- * (k_part_scatter's LDS counters), 6 int64 per gpart row; -1 otherwise. */
+ * (k_part_scatter's LDS counters), 6 int64 per gpart row, 7 previous-block positions
+ * per large-halo chunk (gchunk2 rows; the record chunks of k_part_join); -1 otherwise. */
 int32_t oa_build_info(int32_t which);
 
 /* LDS bytes of one k_part_join work-group for a partition of `entries` current

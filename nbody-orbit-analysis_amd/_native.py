@@ -13,7 +13,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.abspath(__file__))
 # ORBIT_HIP_LIB selects an alternative build (kernel variants for tuning sweeps)
 LIB_PATH = os.environ.get('ORBIT_HIP_LIB') or os.path.join(PKG, 'liborbit_hip.so')
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -29,6 +29,8 @@ MODE = {'pericentric': 0, 'apocentric': 1}
 STATUS_TABLE_OVERFLOW = 2
 STATUS_PLAN = 4
 STATUS_PART_OVERFLOW = 8
+STATUS_LOOKBACK = 16
+STATUS_PART_KEYS = 32
 
 
 class StepArgs(ctypes.Structure):
@@ -52,9 +54,11 @@ class StepArgs(ctypes.Structure):
                 ('pkey_cur', c_vp), ('ppos_cur', c_vp), ('pmeta_cur', c_vp), ('prh_cur', c_vp),
                 ('pkey_prev', c_vp), ('ppos_prev', c_vp), ('pmeta_prev', c_vp), ('prh_prev', c_vp),
                 ('ikey', c_vp), ('ipos', c_vp), ('imeta', c_vp), ('irh', c_vp), ('icnt', c_vp),
-                ('pcnt', c_vp), ('n_pcnt', c_i64), ('gmark', c_vp), ('gmark_base', c_i64),
-                ('gmark_n', c_i64), ('gchunk3', c_vp), ('n_gchunk3', c_i32), ('mark_tag', c_i32),
-                ('items_single', c_i32), ('reserved', c_i32)]
+                ('pcnt', c_vp), ('n_pcnt', c_i64), ('scratch_rk', c_vp), ('part_key4', c_i32),
+                ('part_hi', ctypes.c_uint32), ('gchunk3', c_vp), ('n_gchunk3', c_i32),
+                ('items_single', c_i32), ('direct', c_i32), ('lookback', c_vp),
+                ('lb_epoch', c_i32), ('n_slots', c_i32), ('offsets_out', c_vp), ('out_ids', c_vp),
+                ('out_ang', c_vp), ('out_pos', c_vp), ('total_out', c_vp)]
 
 
 class UnbucketArgs(ctypes.Structure):
@@ -70,7 +74,8 @@ class CompactArgs(ctypes.Structure):
                 ('halo_count', c_vp), ('item_count', c_vp), ('n_slots', c_i32),
                 ('offsets_out', c_vp), ('out_ids', c_vp), ('out_ang', c_vp),
                 ('total_out', c_vp), ('scratch_pos', c_vp), ('out_pos', c_vp),
-                ('n_packed', c_i32), ('n_gchunks', c_i32), ('gchunks', c_vp)]
+                ('n_packed', c_i32), ('n_gchunks', c_i32), ('gchunks', c_vp),
+                ('chunk_count', c_vp), ('scratch_rk', c_vp)]
 
 
 class CollateArgs(ctypes.Structure):

@@ -5,9 +5,11 @@
 //   region_frame               track_orbits.py:247-290    -> k_step phase 1
 //   compare_radial_velocities  track_orbits.py:293-327    -> k_step phase 2
 //   calc_angles                track_orbits.py:330-351    -> k_step phase 2
-//   result assembly            track_orbits.py:199-227    -> k_scan_slots, k_gather_items
+//   result assembly            track_orbits.py:199-227    -> k_step (direct records), or
+//                                                            k_scan_slots, k_gather_*
 //   bulk velocity (sum/mean)   track_orbits.py:262-284    -> k_bulk
-//   large halos                (same functions)           -> k_big_frame, k_big_join
+//   large halos                (same functions)           -> k_part_scatter, k_part_join;
+//                                                            k_big_frame, k_big_join
 //   on-the-fly driver          track_orbits_onthefly.py   -> k_step<..., OTF>, k_big_*
 //   module-level helpers       track_orbits.py:293-351    -> k_match_*, k_compare_pairs,
 //                                                            k_angle_add
@@ -260,7 +262,7 @@ __device__ __forceinline__ void id_split(typename IdT<IDB>::T id, uint32_t &lo, 
 
 // ------------------------------------------------------------------ LDS layout
 struct ItemHdr {
-    int64_t cur_base;
+    int64_t prefix;                 // direct records: the item's first output record
     uint32_t nonuniform, hi0, pad0, overflow;
     uint32_t nh, nseg, n_span, n_pv;
     uint32_t chunk_total, nsl, nstash, npend;
@@ -282,6 +284,67 @@ struct ItemHdr {
     float cf[HMAX][6];              // the same, rounded to float32
 };
 constexpr int64_t HDR_BYTES = (sizeof(ItemHdr) + 255) & ~int64_t(255);
+
+// ------------------------------------------------------------------ direct records
+// Decoupled look-back over items (oa_step_args.direct): item b publishes its record
+// count as soon as phase 2a knows it, then sums the counts of the items before it back
+// to the nearest published inclusive prefix, and publishes its own inclusive prefix.
+// A word is one 8-byte granule {epoch, state, value} written by one sc1 store and
+// polled with sc1 loads (MI355X_MICROARCH.md, inter-workgroup hand-off R2): no fence.
+// An item waits only on lower-numbered items, which publish their counts without
+// waiting on anyone, so the chain always resolves; the spin is still bounded (a
+// status bit asks the host for a re-run without direct records).
+constexpr uint64_t LB_AGG = 1ull << 46, LB_INC = 2ull << 46, LB_VAL = (1ull << 46) - 1ull;
+constexpr uint32_t LB_SPIN_MAX = 1u << 20;
+
+__device__ __forceinline__ void lb_publish(uint64_t *w, uint64_t v) {
+    __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lb_poll(const uint64_t *w) {
+    return __hip_atomic_load(const_cast<uint64_t *>(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One whole wave: publish `count` for item b, return the item's exclusive prefix (and
+// publish the inclusive one).  Lane l of a window reads item j0 - l.
+__device__ int64_t item_lookback(const oa_step_args &a, uint32_t b, uint32_t count) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t tag = (uint64_t)(uint32_t)a.lb_epoch << 48;
+    if (lane == 0) lb_publish(&a.lookback[b], tag | LB_AGG | count);
+    int64_t excl = 0, j0 = (int64_t)b - 1;
+    uint32_t spins = 0;
+    while (j0 >= 0) {
+        const int64_t j = j0 - lane;
+        // before item 0: an inclusive prefix of 0
+        const uint64_t w = j >= 0 ? lb_poll(&a.lookback[j]) : (tag | LB_INC);
+        const bool ready = (w >> 48) == (tag >> 48) && (w & (3ull << 46)) != 0ull;
+        const uint64_t inc = __ballot(ready && (w & LB_INC) != 0ull);
+        const uint64_t notready = __ballot(!ready);
+        // lanes 0 .. the nearest inclusive word are needed, all of them published
+        const int f = inc ? __builtin_ctzll(inc) : 64;
+        const uint64_t need = f == 64 ? ~0ull : ((2ull << f) - 1ull);
+        if (notready & need) {
+            if (++spins > LB_SPIN_MAX) {
+                if (lane == 0) atomicOr(a.status, OA_STATUS_LOOKBACK);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        int64_t v = lane <= f ? (int64_t)(w & LB_VAL) : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        excl += v;
+        if (f < 64) break;
+        j0 -= 64;
+    }
+    {   // uniform (every lane holds the same sum): keep it in SGPRs
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)excl);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)excl >> 32));
+        excl = (int64_t)(((uint64_t)hi << 32) | lo);
+    }
+    if (lane == 0) lb_publish(&a.lookback[b], tag | LB_INC | (uint64_t)(excl + count));
+    return excl;
+}
 
 #ifndef OA_ROWTAB
 #define OA_ROWTAB 1         // packed items: per-row halo / segment tables built in phase 0
@@ -902,12 +965,31 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             bst3<TD>(r_rh, li * SD, w);
         }
     };
+    // direct records (oa_step_args.direct), wave 0 at the item's end: every halo of the
+    // item with an output slot gets its offset (the item's prefix + the records of its
+    // earlier halos, in halo order = slot order), and the last item writes the total
+    auto direct_tail = [&](int64_t P, uint32_t total) __attribute__((always_inline)) {
+        const int32_t c = lane < nh ? H.halo_cnt[lane] : 0;
+        int32_t incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const uint32_t os = lane < nh ? H.hslot[lane] >> 1 : 0u;
+        if (os) a.offsets_out[os - 1u] = P + (incl - c);
+        if (lane == 0 && blockIdx.x == gridDim.x - 1) {
+            a.offsets_out[a.n_slots] = P + total;
+            *a.total_out = P + total;
+        }
+    };
     if (n_pv == 0) {                                 // nothing to join: state words only
         if (RD) store_rhat();
         __syncthreads();
         for (uint32_t li = tid; li < n_span; li += WG)
             bst32<AUX_NT>(r_mt, li * 4u, (uint32_t)(sgn8[li] & 3u) << 16);
         if (tid == 0) a.item_count[blockIdx.x] = 0;
+        if (a.direct && wave == 0) direct_tail(item_lookback(a, blockIdx.x, 0u), 0u);
         return;
     }
     const uint32_t cnt0 = uni(H.seg_cnt[0]), hal0 = uni((uint32_t)H.seg_halo[0]);
@@ -1048,6 +1130,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             atomicOr(a.status, H.overflow ? OA_STATUS_TABLE_OVERFLOW : OA_STATUS_PLAN);
             a.item_count[blockIdx.x] = 0;
         }
+        // the later items' look-backs must still resolve (the step is re-run anyway)
+        if (a.direct && wave == 0) item_lookback(a, blockIdx.x, 0u);
         return;
     }
     const bool nonuniform = IDB == 8 && uni(H.nonuniform) != 0;
@@ -1151,6 +1235,11 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             carry += (uint32_t)__shfl(incl, 63);
         }
         if (lane == 0) H.chunk_total = carry;
+        // direct records: the item's output prefix, while the other waves stage r̂
+        if (a.direct) {
+            const int64_t P = item_lookback(a, blockIdx.x, uni(carry));
+            if (lane == 0) H.prefix = P;
+        }
     }
     // the item's current r̂, from the registers phase 1 left it in
 #pragma unroll
@@ -1167,7 +1256,12 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     STAMP(5);
 
     const uint64_t lanemask_lt = (1ull << lane) - 1ull;
-    ID *scr_ids = reinterpret_cast<ID *>(a.scratch_ids);
+    // records go to the item's scratch range, or (direct) straight to the output
+    const bool direct = a.direct != 0;
+    ID *scr_ids = reinterpret_cast<ID *>(direct ? a.out_ids : a.scratch_ids);
+    uint16_t *scr_ang = direct ? a.out_ang : a.scratch_ang;
+    int32_t *scr_pos = direct ? a.out_pos : a.scratch_pos;
+    const int64_t rec0 = direct ? uni64(H.prefix) : it.scratch_off;
     uint32_t *rcw = reinterpret_cast<uint32_t *>(rcx);        // new angles over rc_x
     constexpr uint32_t RCW = sizeof(TD) / 4;
 #pragma unroll
@@ -1208,12 +1302,12 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         // item's records are contiguous and in order (k_gather_items copies them)
         const uint64_t mk = __ballot(flag);
         const uint32_t cnt = (uint32_t)__popcll(mk);
-        const int64_t sb = it.scratch_off + uni(H.rowoff[r]);
+        const int64_t sb = rec0 + uni(H.rowoff[r]);
         if (flag) {
             const uint32_t q = (uint32_t)__popcll(mk & lanemask_lt);
             __builtin_nontemporal_store(pid[k], &scr_ids[sb + q]);
-            __builtin_nontemporal_store(a16, &a.scratch_ang[sb + q]);
-            if (a.scratch_pos) a.scratch_pos[sb + q] = (int32_t)(kb + lane);
+            __builtin_nontemporal_store(a16, &scr_ang[sb + q]);
+            if (scr_pos) scr_pos[sb + q] = (int32_t)(kb + lane);
         }
         if (lane == 0 && cnt) atomicAdd(&H.halo_cnt[hs], (int)cnt);
     }
@@ -1250,7 +1344,9 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         const uint32_t ang = (s & 4u) ? (rcw[RCW * li] & 0xFFFFu) : 0u;
         bst32<AUX_NT>(r_mt, li * 4u, ang | ((s & 3u) << 16));
     }
-    if (tid < nh) {
+    if (direct) {
+        if (wave == 0) direct_tail(rec0, uni(H.chunk_total));
+    } else if (tid < nh) {
         const uint32_t os = H.hslot[tid] >> 1;
         if (os) a.halo_count[os - 1u] = H.halo_cnt[tid];
     }
@@ -1259,6 +1355,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
 }
 
 // ------------------------------------------------------------------ compaction
+// previous-block positions per record chunk of a partitioned halo (k_part_join's RCHUNK)
+constexpr int RCHUNK_GATHER = 4096;
 __global__ __launch_bounds__(1024) void k_scan_slots(const int32_t *cnt, int32_t n,
                                                      int64_t *off, int64_t *total) {
     // exclusive scan of the per-halo record counts (one work-group).  Thread t owns the
@@ -1288,8 +1386,8 @@ __global__ __launch_bounds__(1024) void k_scan_slots(const int32_t *cnt, int32_t
 }
 
 // Packed (k_step) items hold their records contiguously: a coalesced copy.  Global
-// items (k_big_join, k_part_emit) keep theirs in 64-position segments, packed at each
-// segment's base: segments in chunks of 256 get a block-wide exclusive scan of their
+// items of the global-table path (k_big_join) keep theirs in 64-position segments,
+// packed at each segment's base: segments in chunks of 256 get a block-wide exclusive scan of their
 // record counts (LDS), then the chunk's records are copied flat -- thread t moves
 // records t, t + 256, ... (consecutive records of consecutive rows: coalesced), each
 // finding its row by a binary search over the scanned offsets.
@@ -1386,6 +1484,68 @@ __global__ __launch_bounds__(256) void k_gather_chunks(const oa_compact_args a) 
     __syncthreads();
     const int64_t dst = a.offsets_out[slot] + (int64_t)(red[0] + red[1] + red[2] + red[3]);
     gather_segments<IDB>(a, it, dst, s_lo, s_hi, wsum, roff);
+}
+
+// Partitioned large halos (k_part_join): one work-group per previous-block chunk (gchunks
+// rows, RCHUNK positions each); its records sit unordered at the chunk's scratch base,
+// each with its position in the chunk (scratch_rk).  Positions are distinct, so a record's
+// rank in previous-block order is the number of set bits below its own in a bitmap of the
+// chunk's record positions; the chunk's output offset is the item's plus the records of
+// the item's earlier chunks.
+template <int IDB>
+__global__ __launch_bounds__(256) void k_gather_recs(const oa_compact_args a) {
+    typedef typename IdT<IDB>::T ID;
+    constexpr int NW = RCHUNK_GATHER / 32;
+    __shared__ uint32_t bm[NW], wpre[NW], red[4];
+    const int64_t row = blockIdx.x;
+    const int64_t *ch = a.gchunks + 3 * row;
+    const int64_t gi = ch[0], start = ch[1], cnt = ch[2];
+    const oa_item it = a.items[gi];
+    const int64_t slot = it.slot0;
+    if (slot < 0 || cnt <= 0) return;                   // uniform
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t n = a.chunk_count[row];
+    uint32_t before = 0;
+    for (int64_t r = row - start / RCHUNK_GATHER + tid; r < row; r += 256) before += a.chunk_count[r];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) before += __shfl_down(before, o);
+    if (lane == 0) red[wave] = before;
+    for (int w = tid; w < NW; w += 256) bm[w] = 0u;
+    __syncthreads();
+    if (n == 0) return;                                 // uniform
+    const int64_t s0 = it.scratch_off + start;
+    for (uint32_t j = tid; j < n; j += 256) {
+        const uint32_t rk = a.scratch_rk[s0 + j];
+        atomicOr(&bm[rk >> 5], 1u << (rk & 31u));
+    }
+    __syncthreads();
+    if (wave == 0) {                                    // exclusive popcount prefix of the words
+        uint32_t c[NW / 64], t = 0;
+#pragma unroll
+        for (int q = 0; q < NW / 64; ++q) { c[q] = __popc(bm[lane * (NW / 64) + q]); t += c[q]; }
+        uint32_t incl = t;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        uint32_t e = incl - t;
+#pragma unroll
+        for (int q = 0; q < NW / 64; ++q) { wpre[lane * (NW / 64) + q] = e; e += c[q]; }
+    }
+    __syncthreads();
+    const int64_t dst = a.offsets_out[slot] + (int64_t)(red[0] + red[1] + red[2] + red[3]);
+    const ID *src = reinterpret_cast<const ID *>(a.scratch_ids);
+    ID *out = reinterpret_cast<ID *>(a.out_ids) + dst;
+    uint16_t *oang = a.out_ang + dst;
+    const int64_t pbase = a.out_pos ? a.halos[it.h0].prev_off + start : 0;
+    for (uint32_t j = tid; j < n; j += 256) {
+        const uint32_t rk = a.scratch_rk[s0 + j], w = rk >> 5;
+        const uint32_t rank = wpre[w] + __popc(bm[w] & ((1u << (rk & 31u)) - 1u));
+        out[rank] = src[s0 + j];
+        oang[rank] = a.scratch_ang[s0 + j];
+        if (a.out_pos) a.out_pos[dst + rank] = (int32_t)(pbase + rk);
+    }
 }
 
 // ------------------------------------------------------------------ bulk velocity
@@ -1787,21 +1947,19 @@ __global__ __launch_bounds__(BIG_WG) void k_big_join(const oa_step_args a) {
 // The default large-halo path of compare steps.  A halo too large for one work-group's
 // LDS table is cut into K partitions by a hash of the full ID, each small enough for an
 // LDS cuckoo table, so the join is LDS-local like k_step's and every HBM stream is
-// coalesced (the global-table path above pays a random HBM access per insert and probe):
-//   k_part_scatter  chunks of the current blocks: the frame (r̂ and the state word with
-//                   angle 0 in position order, as k_big_frame) plus each particle's
-//                   {ID, position | sign << 30} appended to its partition's bucket;
-//                   chunks of the previous blocks: {ID, position} appended, and the
-//                   apsis marks of those positions cleared.  A chunk counts its
-//                   partitions in LDS and reserves each bucket range with one atomic.
+// coalesced (the global-table path above pays a random HBM access per insert and probe).
+// A halo's state lives between snapshots as a *bucket set* (per partition: key, position
+// word, state word, r̂), so a step streams the previous state from its buckets:
+//   k_part_scatter  chunks of the current blocks: the frame, each particle's entry
+//                   {key, position | sign << 30, r̂} staged in LDS in partition order and
+//                   copied to its bucket as contiguous runs (one device atomic per
+//                   partition and chunk reserves the range); previous chunks only for
+//                   halos without an inherited set
 //   k_part_join     one work-group per partition: LDS cuckoo table of the current
-//                   bucket, then every previous entry looked up; a match gathers the
-//                   two r̂ rows and the previous state word (the halo's blocks are
-//                   shared by its partitions, which plist keeps on one XCD), writes the
-//                   current particle's state word and, for an apsis, the mark at the
-//                   previous position
-//   k_part_emit     64-position segments of the previous blocks: marks -> records in
-//                   previous-block order (:315-316), packed per segment as k_big_join
+//                   bucket, then every previous entry of the partition looked up; a match
+//                   gathers the current r̂ from the bucket, writes the current state word
+//                   and, for an apsis, appends the record {ID, angle, position in chunk}
+//                   to its previous-block chunk (oa_compact's k_gather_recs orders them)
 #ifndef OA_PART_E
 #define OA_PART_E 4096
 #endif
@@ -1868,10 +2026,12 @@ __device__ __forceinline__ void block_scan_excl(uint32_t *v, uint32_t n, uint32_
 // entries), state word, r̂ -- so the join streams it and a current bucket set is the
 // next snapshot's previous one.  Previous chunks of halos whose previous state is
 // already such a set (gpart[3] = 1, inherited) are skipped.
-template <typename TX, typename TV, typename TD, int IDB, bool CUR>
+// KB: bucket key bytes (4: the IDs' low words, oa_step_args.part_key4)
+template <typename TX, typename TV, typename TD, int IDB, bool CUR, int KB>
 __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK &fk, char *lds,
                                              int64_t chunk) {
     typedef typename IdT<IDB>::T ID;
+    typedef typename IdT<KB>::T KEY;
     const int64_t *ch = (CUR ? a.gchunk1 : (a.gchunk3 ? a.gchunk3 : a.gchunk2)) + 3 * chunk;
     const int64_t gi = ch[0], start = ch[1], cnt = ch[2];
     const oa_item it = a.items[gi];
@@ -1899,7 +2059,8 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
     uint32_t *ctr = a.pcnt + (CUR ? gp[2] : gp[7]);
     const uint32_t bcap = CUR ? (uint32_t)a.part_e : (uint32_t)gp[6];
     const int64_t bb = CUR ? gp[0] : gp[4];
-    uint64_t *bkey = (CUR ? a.pkey_cur : a.pkey_prev) + bb;
+    KEY *bkey = static_cast<KEY *>(CUR ? a.pkey_cur : a.pkey_prev) + bb;
+    bool badhi = false;                                 // part_key4: a foreign high word
     uint32_t *bpos = (CUR ? a.ppos_cur : a.ppos_prev) + bb;
     uint32_t *bmeta = (CUR ? a.pmeta_cur : a.pmeta_prev) + bb;
     TD *brh = static_cast<TD *>(CUR ? a.prh_cur : a.prh_prev) + 3 * bb;
@@ -1931,6 +2092,7 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
             if (j >= n0) continue;
             const int64_t i = base + s0 + j;
             key[q] = (uint64_t)lds_nt(&ids[i]);
+            if (IDB == 8 && KB == 4 && part) badhi |= (uint32_t)(key[q] >> 32) != a.part_hi;
             if (!CUR) {
                 pm[q] = lds_nt(&a.meta_prev[i]);
                 rh[q] = ld3_nt(rhat_prev, i);
@@ -1995,12 +2157,12 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
                 const int64_t o = (int64_t)k * bcap + e;
                 TD *d = brh + 3 * o;
                 if (OA_SCAT_NT) {
-                    __builtin_nontemporal_store(skey[s], &bkey[o]);
+                    __builtin_nontemporal_store((KEY)skey[s], &bkey[o]);
                     __builtin_nontemporal_store(spw[s], &bpos[o]);
                     // a current entry's state word is the join's (k_part_join stages them)
                     if (!CUR) __builtin_nontemporal_store(smeta[s], &bmeta[o]);
                 } else {
-                    bkey[o] = skey[s]; bpos[o] = spw[s];
+                    bkey[o] = (KEY)skey[s]; bpos[o] = spw[s];
                     if (!CUR) bmeta[o] = smeta[s];
                 }
                 d[0] = srh[3 * s]; d[1] = srh[3 * s + 1]; d[2] = srh[3 * s + 2];
@@ -2008,12 +2170,14 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
         }
         __syncthreads();
     }
+    if (IDB == 8 && KB == 4 && __ballot(badhi) && (threadIdx.x & 63) == 0)
+        atomicOr(a.status, OA_STATUS_PART_KEYS);
 }
 
 // Current and previous chunks interleaved in one grid (their latencies overlap):
 // even work-groups take current chunks, odd ones previous chunks, then the longer
 // list's remainder.
-template <typename TX, typename TV, typename TD, int IDB>
+template <typename TX, typename TV, typename TD, int IDB, int KB>
 __global__ __launch_bounds__(SCAT_WG) void k_part_scatter(const oa_step_args a, const FrameK fk) {
     extern __shared__ __attribute__((aligned(16))) char slds[];
     const int64_t b = blockIdx.x, n1 = a.n_gchunk1,
@@ -2024,47 +2188,36 @@ __global__ __launch_bounds__(SCAT_WG) void k_part_scatter(const oa_step_args a, 
     if (b < 2 * m) { cur = (b & 1) == 0; c = b >> 1; }
     else { cur = n1 > n2; c = b - m; }
     SSTAMP(0);
-    if (cur) part_scatter<TX, TV, TD, IDB, true>(a, fk, slds, c);
-    else part_scatter<TX, TV, TD, IDB, false>(a, fk, slds, c);
+    if (cur) part_scatter<TX, TV, TD, IDB, true, KB>(a, fk, slds, c);
+    else part_scatter<TX, TV, TD, IDB, false, KB>(a, fk, slds, c);
     SSTAMP(1);
 }
 
-#ifndef OA_JOIN_RSTAGE
-#define OA_JOIN_RSTAGE 0    // k_part_join: the current bucket's r̂ staged in LDS (not gathered)
-#endif
-constexpr bool JRS = OA_JOIN_RSTAGE != 0;
-
-// LDS of one k_part_join work-group for a partition capacity of e entries, s slots
-// (td_bytes: the r̂ dtype, for the staged current r̂ of JRS builds)
-__host__ __device__ inline int64_t part_lds_bytes(int e, int sl, int td_bytes = 8) {
-    // slots, then max(deferral list, the partition's state words), stash, flags
+// LDS of one k_part_join work-group for a partition capacity of e entries, s slots:
+// the slots, then max(deferral list, the partition's state words), the stash, flags
+__host__ __device__ inline int64_t part_lds_bytes(int e, int sl) {
     const int64_t mid = (int64_t)e * 4 > (int64_t)(e / 4) * 8 ? (int64_t)e * 4 : (int64_t)(e / 4) * 8;
-    return (int64_t)sl * 8 + mid + (int64_t)STASH * 8 + 16 +
-           (JRS ? (int64_t)3 * e * td_bytes : 0);
+    return (int64_t)sl * 8 + mid + (int64_t)STASH * 8 + 16 + 16;
 }
+
+// The apsis records of a partitioned halo (k_part_join -> oa_compact): a record is
+// appended to the chunk of RCHUNK previous-block positions holding its particle (the
+// gchunk2 rows of the item, engine.GCHUNK), at the chunk's scratch base + a slot from
+// the chunk's counter, with its position in the chunk (scratch_rk); k_gather_recs ranks
+// a chunk's records by that position, so they leave in previous-block order (:315-316).
+constexpr int RCHUNK_LOG2 = 12, RCHUNK = 1 << RCHUNK_LOG2;
+static_assert(RCHUNK == RCHUNK_GATHER, "record chunks of the join and the gather");
 
 // One work-group per current partition: LDS cuckoo table of its current bucket, then
 // every entry of the previous partitions that hold its IDs (one, several or a share of
 // one, as K and the previous set's K compare) looked up; a match gathers the current
-// r̂ from its bucket entry and writes that entry's state word; an apsis also marks the
-// previous position.
-// an apsis mark of the previous position (k_part_join -> k_part_emit): bit 16 set, the
-// step's tag in bits 17-31 (mark_tag; 0: an untagged buffer cleared by oa_step), the
-// f16 angle in bits 0-15.  Marks of earlier steps carry other tags and read as unset.
-__device__ __forceinline__ uint32_t mark_word(int32_t tag) {
-    return 0x10000u | ((uint32_t)tag << 17);
-}
-
-#ifndef OA_JOIN_WPE
-#define OA_JOIN_WPE 0       // k_part_join: waves per SIMD asked of the register allocator (0: default)
-#endif
-#if OA_JOIN_WPE
-#define JOIN_ATTR __attribute__((amdgpu_waves_per_eu(OA_JOIN_WPE, 8)))
-#else
-#define JOIN_ATTR
-#endif
-template <typename TD, int IDB>
-__global__ __launch_bounds__(PART_WG) JOIN_ATTR void k_part_join(const oa_step_args a) {
+// r̂ from its bucket entry and writes that entry's state word; an apsis appends its
+// record to its previous-block chunk.  KB: bucket key bytes (4: low words, every ID's
+// high word is part_hi).
+template <typename TD, int IDB, int KB>
+__global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
+    typedef typename IdT<IDB>::T ID;
+    typedef typename IdT<KB>::T KEY;
     extern __shared__ __attribute__((aligned(16))) char psm[];
     const uint32_t PE = (uint32_t)a.part_e, PS = (uint32_t)a.part_slots;
     uint64_t *slots = reinterpret_cast<uint64_t *>(psm);               // [PS]
@@ -2073,12 +2226,13 @@ __global__ __launch_bounds__(PART_WG) JOIN_ATTR void k_part_join(const oa_step_a
     uint32_t *mlds = reinterpret_cast<uint32_t *>(pend);                // [PE]
     uint64_t *stash = pend + (PE * 4 > (PE / 4) * 8 ? PE / 2 : PE / 4); // [STASH]
     uint32_t *flags = reinterpret_cast<uint32_t *>(stash + STASH);      // npend, nstash, overflow, nonuniform
-    TD *crl = reinterpret_cast<TD *>(flags + 4);                        // [3 PE] (JRS)
+    uint32_t *nrec = flags + 4;                                         // records of the work-group
     const int tid = threadIdx.x;
     PSTAMP(0);
     const int32_t g = a.plist[2 * blockIdx.x], pp = a.plist[2 * blockIdx.x + 1];
     if (g < 0) return;                                  // padding row
-    const oa_item it = a.items[a.n_items + g];
+    const int64_t gi = a.n_items + g;
+    const oa_item it = a.items[gi];
     const int64_t *gp = a.gpart + GPART_W * (int64_t)g;
     const uint32_t K = (uint32_t)gp[1];
     const int64_t cb = gp[0] + (int64_t)pp * PE;
@@ -2086,7 +2240,7 @@ __global__ __launch_bounds__(PART_WG) JOIN_ATTR void k_part_join(const oa_step_a
     const bool inh = gp[3] != 0;
     const uint32_t Kp = (uint32_t)gp[5], pcap = (uint32_t)gp[6];
     const uint32_t *qcnt = (inh ? a.icnt : a.pcnt) + gp[7];
-    const uint64_t *qk0 = (inh ? a.ikey : a.pkey_prev) + gp[4];
+    const KEY *qk0 = static_cast<const KEY *>(inh ? a.ikey : a.pkey_prev) + gp[4];
     const uint32_t *qp0 = (inh ? a.ipos : a.ppos_prev) + gp[4];
     const uint32_t *qm0 = (inh ? a.imeta : a.pmeta_prev) + gp[4];
     const TD *qr0 = static_cast<const TD *>(inh ? a.irh : a.prh_prev) + 3 * gp[4];
@@ -2100,33 +2254,29 @@ __global__ __launch_bounds__(PART_WG) JOIN_ATTR void k_part_join(const oa_step_a
         if (tid == 0) atomicOr(a.status, OA_STATUS_PART_OVERFLOW);
         return;
     }
-    const uint64_t *ck = a.pkey_cur + cb;
+    const KEY *ck = static_cast<const KEY *>(a.pkey_cur) + cb;
     const uint32_t *cp = a.ppos_cur + cb;
     // Every load of the partition goes out first (both buckets are streamed once):
     // their HBM latency hides behind the table clear, the inserts and the walks.
     constexpr int CU = PART_E / PART_WG, PU = OA_PU;
-    uint64_t ckey[CU];
+    KEY ckey[CU];
     uint32_t cpw[CU];
 #pragma unroll
     for (int u = 0; u < CU; ++u) {
         const uint32_t i = (uint32_t)u * PART_WG + tid;
-        ckey[u] = i < nc ? ck[i] : 0ull;
+        ckey[u] = i < nc ? ck[i] : (KEY)0;
         cpw[u] = i < nc ? cp[i] : 0u;
     }
     const TD *crh0 = static_cast<const TD *>(a.prh_cur) + 3 * cb;
-    if (JRS) {
-        // the bucket's current r̂, one coalesced sweep, straight into LDS
-        for (uint32_t w = tid; w < 3 * nc; w += PART_WG) crl[w] = crh0[w];
-    }
-    uint64_t qkey[PU];
+    KEY qkey[PU];
     uint32_t qpos[PU], qmeta[PU];
     V3<TD> qrh[PU];
-    auto load_prev = [&](const uint64_t *qk, const uint32_t *qp, const uint32_t *qm, const TD *qr,
+    auto load_prev = [&](const KEY *qk, const uint32_t *qp, const uint32_t *qm, const TD *qr,
                          uint32_t np, uint32_t j0) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < PU; ++u) {
             const uint32_t j = j0 + (uint32_t)u * PART_WG + tid;
-            qkey[u] = j < np ? qk[j] : 0ull;
+            qkey[u] = j < np ? qk[j] : (KEY)0;
             qpos[u] = j < np ? qp[j] : 0u;
             qmeta[u] = j < np ? qm[j] : 0u;
             if (j < np) qrh[u] = ld3(qr, j);
@@ -2137,8 +2287,8 @@ __global__ __launch_bounds__(PART_WG) JOIN_ATTR void k_part_join(const oa_step_a
     uint32_t nsl = 2u * nc + 64u;                      // load <= 1/2 where the LDS allows
     nsl = nsl < PS ? nsl : PS;
     for (uint32_t w = tid; w < nsl; w += PART_WG) slots[w] = 0ull;
-    if (tid < 4) flags[tid] = 0u;
-    const uint32_t hi0 = nc ? (uint32_t)(ck[0] >> 32) : 0u;
+    if (tid < 5) flags[tid] = 0u;
+    const uint32_t hi0 = (KB == 8 && nc) ? (uint32_t)((uint64_t)ck[0] >> 32) : 0u;
     __syncthreads();
     PSTAMP(1);
     // current bucket -> LDS table: lo32(ID) | (sign << 16 | (entry + 1) << 18) << 32
@@ -2147,8 +2297,8 @@ __global__ __launch_bounds__(PART_WG) JOIN_ATTR void k_part_join(const oa_step_a
     for (int u = 0; u < CU; ++u) {
         const uint32_t i = (uint32_t)u * PART_WG + tid;
         if (i >= nc) continue;
-        const uint64_t key = ckey[u];
-        if ((uint32_t)(key >> 32) != hi0) flags[3] = 1u;        // benign race: all write 1
+        const uint64_t key = (uint64_t)ckey[u];
+        if (KB == 8 && (uint32_t)(key >> 32) != hi0) flags[3] = 1u;   // benign race: all write 1
         const uint64_t val = slot_pack((uint32_t)key, (cpw[u] >> 30) << 16, i);
         uint32_t cs[NCAND];
         cuckoo_slots((uint32_t)key, nsl, cs);
@@ -2206,16 +2356,20 @@ __global__ __launch_bounds__(PART_WG) JOIN_ATTR void k_part_join(const oa_step_a
         if (i < nc) mlds[i] = (cpw[u] >> 30) << 16;
     }
     __syncthreads();
-    const bool nonuniform = IDB == 8 && flags[3] != 0u;
+    const bool nonuniform = KB == 8 && flags[3] != 0u;
     const uint32_t nstash = min(flags[1], (uint32_t)STASH);
     uint32_t *cmeta = a.pmeta_cur + cb;
-    uint32_t *mark = a.gmark + (it.scratch_off - a.gmark_base);
-    const uint32_t mtag = mark_word(a.mark_tag);
+    // record chunks of this item: counters in pcnt from gp[8], slots at the item's
+    // scratch base + chunk * RCHUNK
+    uint32_t *rcnt = a.pcnt + gp[8];
+    ID *scr_ids = static_cast<ID *>(a.scratch_ids);
+    const uint64_t hiw = KB == 4 ? (uint64_t)a.part_hi << 32 : 0ull;
+    uint32_t mine = 0;                                  // records of this thread
     // previous entries, PU per thread: lookups, then the gathers of the matched current
     // r̂ (the partition's own bucket entries), then the angle and state-word arithmetic
     for (uint32_t q = 0; q < nq; ++q) {
         const int64_t qo = (int64_t)(q0 + q) * pcap;
-        const uint64_t *qk = qk0 + qo;
+        const KEY *qk = qk0 + qo;
         const uint32_t *qp = qp0 + qo, *qm = qm0 + qo;
         const TD *qr = qr0 + 3 * qo;
         const uint32_t np = qcnt[q0 + q];
@@ -2226,9 +2380,10 @@ __global__ __launch_bounds__(PART_WG) JOIN_ATTR void k_part_join(const oa_step_a
             for (int u = 0; u < PU; ++u) {
                 hit[u] = 0xFFFFFFFFu;
                 const uint32_t j = j0 + (uint32_t)u * PART_WG + tid;
-                const uint32_t lo = (uint32_t)qkey[u];
-                if (j >= np || (IDB == 8 && !nonuniform && (uint32_t)(qkey[u] >> 32) != hi0)) continue;
-                if (filt && part_of(qkey[u], K) != (uint32_t)pp) continue;
+                const uint64_t key = (uint64_t)qkey[u] | hiw;
+                const uint32_t lo = (uint32_t)key;
+                if (j >= np || (KB == 8 && !nonuniform && (uint32_t)(key >> 32) != hi0)) continue;
+                if (filt && part_of(key, K) != (uint32_t)pp) continue;
                 uint32_t cs[NCAND];
                 cuckoo_slots(lo, nsl, cs);
                 uint64_t m = 0ull;
@@ -2236,25 +2391,24 @@ __global__ __launch_bounds__(PART_WG) JOIN_ATTR void k_part_join(const oa_step_a
                 for (int c = 0; c < NCAND; ++c) {
                     const uint64_t v = slots[cs[c]];
                     if (!m && v && (uint32_t)v == lo && slot_pos(v) < nc &&
-                        (!nonuniform || ck[slot_pos(v)] == qkey[u]))
+                        (!nonuniform || (uint64_t)ck[slot_pos(v)] == key))
                         m = v;
                 }
                 for (uint32_t e = 0; !m && e < nstash; ++e) {
                     const uint64_t v = stash[e];
-                    if ((uint32_t)v == lo && (!nonuniform || ck[slot_pos(v)] == qkey[u])) m = v;
+                    if ((uint32_t)v == lo && (!nonuniform || (uint64_t)ck[slot_pos(v)] == key)) m = v;
                 }
                 if (m) hit[u] = slot_pos(m) | ((slot_meta(m) >> 16) << 30);
             }
             V3<TD> crh[PU];
 #pragma unroll
             for (int u = 0; u < PU; ++u)
-                if (hit[u] != 0xFFFFFFFFu) {
-                    const uint32_t e = hit[u] & 0x3FFFFFFFu;
-                    if (JRS) crh[u] = V3<TD>{crl[3 * e], crl[3 * e + 1], crl[3 * e + 2]};
-                    else crh[u] = ld3(crh0, e);
-                }
+                if (hit[u] != 0xFFFFFFFFu) crh[u] = ld3(crh0, hit[u] & 0x3FFFFFFFu);
+            uint16_t rang[PU];
+            uint32_t rslot[PU];
 #pragma unroll
             for (int u = 0; u < PU; ++u) {
+                rslot[u] = 0xFFFFFFFFu;
                 if (hit[u] == 0xFFFFFFFFu) continue;
                 const uint32_t sc = hit[u] >> 30, sp = qmeta[u] >> 16;
                 // strict sign test (:311-314), arccos of the r̂ dot product (:324-325),
@@ -2264,15 +2418,37 @@ __global__ __launch_bounds__(PART_WG) JOIN_ATTR void k_part_join(const oa_step_a
                 const TD dt = dot3(qrh[u].x, qrh[u].y, qrh[u].z, crh[u].x, crh[u].y, crh[u].z);
                 const uint16_t acc = angle_add((uint16_t)(qmeta[u] & 0xFFFFu), acos_td(dt));
                 mlds[hit[u] & 0x3FFFFFFFu] = (uint32_t)(flag ? 0u : acc) | (sc << 16);
+                rang[u] = acc;
                 // an inherited set's position words carry the sign in bits 30-31
-                if (flag) mark[qpos[u] & 0x3FFFFFFFu] = mtag | acc;
+                if (flag) rslot[u] = atomicAdd(&rcnt[(qpos[u] & 0x3FFFFFFFu) >> RCHUNK_LOG2], 1u);
+            }
+            // the records: every slot claimed above first, then the stores
+#pragma unroll
+            for (int u = 0; u < PU; ++u) {
+                if (rslot[u] == 0xFFFFFFFFu) continue;
+                const uint32_t p = qpos[u] & 0x3FFFFFFFu;
+                const int64_t s = it.scratch_off + (int64_t)(p & ~(uint32_t)(RCHUNK - 1)) + rslot[u];
+                scr_ids[s] = (ID)((uint64_t)qkey[u] | hiw);
+                a.scratch_ang[s] = rang[u];
+                a.scratch_rk[s] = (uint16_t)(p & (RCHUNK - 1));
+                ++mine;
             }
             if (j0 == 0 && q == 0) PSTAMP(4);
         }
     }
+    // the work-group's record count: one pair of device atomics (halo and item counts)
+    uint32_t wc = mine;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wc += __shfl_xor(wc, o);
+    if ((tid & 63) == 0 && wc) atomicAdd(nrec, wc);
     __syncthreads();
     // the partition's state words leave as one coalesced run
     for (uint32_t i = tid; i < nc; i += PART_WG) cmeta[i] = mlds[i];
+    if (tid == 0 && *nrec) {
+        const oa_halo &h = a.halos[it.h0];
+        atomicAdd(&a.halo_count[h.out_slot], (int32_t)*nrec);
+        atomicAdd(&a.item_count[gi], (int32_t)*nrec);
+    }
     PSTAMP(5);
 }
 
@@ -2298,88 +2474,12 @@ __global__ __launch_bounds__(256) void k_part_unbucket(const oa_unbucket_args a)
     }
 }
 
-template <int IDB>
-__global__ __launch_bounds__(BIG_WG) void k_part_emit(const oa_step_args a) {
-    typedef typename IdT<IDB>::T ID;
-    const int64_t *ch = a.gchunk2 + 3 * blockIdx.x;
-    const int64_t gi = ch[0], start = ch[1], cnt = ch[2];
-    const oa_item it = a.items[gi];
-    const oa_halo &h = a.halos[it.h0];
-    const ID *ids_prev = static_cast<const ID *>(a.ids_prev);
-    const uint32_t *mark = a.gmark + (it.scratch_off - a.gmark_base);
-    const uint32_t mtag = mark_word(a.mark_tag);
-    ID *scr_ids = static_cast<ID *>(a.scratch_ids);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t lanemask_lt = (1ull << lane) - 1ull;
-    int32_t tot = 0;
-    constexpr int EU = 8;                       // marks of EU rows loaded before any is used
-    uint32_t mk[EU];
-    for (int64_t w0 = start; w0 < start + cnt; w0 += BIG_WG * EU) {
-#pragma unroll
-    for (int e = 0; e < EU; ++e) {
-        const int64_t p = w0 + e * BIG_WG + threadIdx.x;
-        mk[e] = p < start + cnt ? mark[p] : 0u;
-    }
-    // the flagged positions' IDs, every load issued before any record is stored (the
-    // stores may alias ids_prev for the compiler, which would otherwise keep each load
-    // behind the previous row's stores)
-    ID idl[EU];
-#pragma unroll
-    for (int e = 0; e < EU; ++e) {
-        const int64_t p = w0 + e * BIG_WG + threadIdx.x;
-        idl[e] = (mk[e] & 0xFFFF0000u) == mtag ? ids_prev[h.prev_off + p] : (ID)0;
-    }
-#pragma unroll
-    for (int e = 0; e < EU; ++e) {
-        const int64_t v0 = w0 + e * BIG_WG;
-        const int64_t p = v0 + threadIdx.x;
-        const uint32_t m = mk[e];
-        const bool flag = (m & 0xFFFF0000u) == mtag;    // a mark of this step
-        const uint64_t b = __ballot(flag);
-        const int64_t segpos = v0 + wave * 64;
-        if (segpos < start + cnt) {
-            if (flag) {
-                const int64_t pos = it.scratch_off + segpos + __popcll(b & lanemask_lt);
-                scr_ids[pos] = idl[e];
-                a.scratch_ang[pos] = (uint16_t)(m & 0xFFFFu);
-                if (a.scratch_pos) a.scratch_pos[pos] = (int32_t)(h.prev_off + p);
-            }
-            if (lane == 0) {
-                const uint32_t c = (uint32_t)__popcll(b);
-                a.seg_count[(it.scratch_off + segpos) >> 6] = (uint8_t)c;
-                tot += (int32_t)c;
-            }
-        }
-    }
-    }
-    // one pair of device atomics per work-group (per-wave atomics on the halo's two
-    // counters serialise across the chunks of a large halo)
-    __shared__ int32_t wtot[BIG_WG / 64];
-    if (lane == 0) wtot[wave] = tot;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int32_t t = 0;
-#pragma unroll
-        for (int w = 0; w < BIG_WG / 64; ++w) t += wtot[w];
-        if (t) {
-            atomicAdd(&a.halo_count[h.out_slot], t);
-            atomicAdd(&a.item_count[gi], t);
-        }
-    }
-}
-
-template <typename TX, typename TV, typename TD, int IDB>
-int launch_part(const oa_step_args &a, hipStream_t st) {
-    if (a.mark_tag < 0 || a.mark_tag > 0x7FFF)
-        return fail(OA_E_ARG, "oa_step: mark_tag must be in [0, 32767]");
-    if (hipMemsetAsync(a.pcnt, 0, (size_t)a.n_pcnt * 4, st) != hipSuccess ||
-        (a.mark_tag == 0 && a.gmark_n > 0 &&
-         hipMemsetAsync(a.gmark, 0, (size_t)a.gmark_n * 4, st) != hipSuccess))
-        return fail(OA_E_LAUNCH, "oa_step: partition counters / marks reset");
+template <typename TX, typename TV, typename TD, int IDB, int KB>
+int launch_part_k(const oa_step_args &a, hipStream_t st) {
     // previous chunks to scatter: those of halos without an inherited set (gchunk3)
     const int64_t n_scat = a.n_gchunk1 + (a.gchunk3 ? a.n_gchunk3 : a.n_gchunk2);
     if (n_scat > 0) {
-        auto k = k_part_scatter<TX, TV, TD, IDB>;
+        auto k = k_part_scatter<TX, TV, TD, IDB, KB>;
         const int64_t lds = scat_lds_bytes(a.part_kmax, (int)sizeof(TD));
         if (int rc = set_lds(k, lds)) return rc;
         hipLaunchKernelGGL(k, dim3((unsigned)n_scat), dim3(SCAT_WG), (size_t)lds,
@@ -2387,17 +2487,22 @@ int launch_part(const oa_step_args &a, hipStream_t st) {
         if (int rc = check_launch("k_part_scatter")) return rc;
     }
     if (a.n_parts > 0) {
-        auto k = k_part_join<TD, IDB>;
-        const int64_t lds = part_lds_bytes(a.part_e, a.part_slots, (int)sizeof(TD));
+        auto k = k_part_join<TD, IDB, KB>;
+        const int64_t lds = part_lds_bytes(a.part_e, a.part_slots);
         if (int rc = set_lds(k, lds)) return rc;
         hipLaunchKernelGGL(k, dim3((unsigned)a.n_parts), dim3(PART_WG), (size_t)lds, st, a);
         if (int rc = check_launch("k_part_join")) return rc;
     }
-    if (a.n_gchunk2 > 0) {
-        hipLaunchKernelGGL((k_part_emit<IDB>), dim3((unsigned)a.n_gchunk2), dim3(BIG_WG), 0, st, a);
-        if (int rc = check_launch("k_part_emit")) return rc;
-    }
     return OA_OK;
+}
+
+template <typename TX, typename TV, typename TD, int IDB>
+int launch_part(const oa_step_args &a, hipStream_t st) {
+    if (hipMemsetAsync(a.pcnt, 0, (size_t)a.n_pcnt * 4, st) != hipSuccess)
+        return fail(OA_E_LAUNCH, "oa_step: partition / record counters reset");
+    // 4-byte IDs are their own low words
+    if (IDB == 4 || a.part_key4) return launch_part_k<TX, TV, TD, IDB, 4>(a, st);
+    return launch_part_k<TX, TV, TD, IDB, IDB>(a, st);
 }
 
 template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>
@@ -2439,6 +2544,7 @@ int32_t oa_build_info(int32_t which) {
         case 4: return PART_E;
         case 5: return PART_KMAX;
         case 6: return GPART_W;
+        case 7: return RCHUNK;
         default: return -1;
     }
 }
@@ -2585,7 +2691,8 @@ int oa_step(const oa_step_args *args, void *stream) {
         return fail(OA_E_ARG, "null large-halo chunk pointer");
     const bool part = a.compare && !a.onthefly && a.n_parts > 0;
     if (part && (!a.plist || !a.gpart || !a.pkey_cur || !a.ppos_cur || !a.pmeta_cur ||
-                 !a.prh_cur || !a.pcnt || !a.gmark || a.n_pcnt < 1 ||
+                 !a.prh_cur || !a.pcnt || !a.scratch_rk || a.n_pcnt < 1 ||
+                 (a.id_bytes == 4 && a.part_hi != 0) ||
                  (a.n_gchunk2 > 0 && (!a.pkey_prev || !a.ppos_prev || !a.pmeta_prev ||
                                       !a.prh_prev)) || a.part_kmax < 1 ||
                  a.part_e < 64 || a.part_e > PART_E || a.part_e % 64 ||
@@ -2594,6 +2701,17 @@ int oa_step(const oa_step_args *args, void *stream) {
         return fail(OA_E_ARG, "bad large-halo partition arguments");
     if (a.onthefly && a.n_parts > 0)
         return fail(OA_E_ARG, "the partitioned large-halo path is not for on-the-fly steps");
+    if (a.direct && (!a.compare || a.onthefly || a.n_global_items > 0 || !a.lookback ||
+                     !a.offsets_out || !a.out_ids || !a.out_ang || !a.total_out ||
+                     a.lb_epoch < 1 || a.lb_epoch > 0xFFFF || a.n_slots < 0))
+        return fail(OA_E_ARG, "direct records: a packed-only compare step with look-back "
+                              "words, epoch in [1, 65535] and output pointers");
+    if (a.direct && a.n_items == 0) {
+        // no item writes the (empty) output: offsets = [0], total = 0
+        if (hipMemsetAsync(a.offsets_out, 0, 8, reinterpret_cast<hipStream_t>(stream)) != hipSuccess ||
+            hipMemsetAsync(a.total_out, 0, 8, reinterpret_cast<hipStream_t>(stream)) != hipSuccess)
+            return fail(OA_E_LAUNCH, "oa_step: empty direct output");
+    }
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (a.compare && a.n_global_items > 0) {
         if ((!part && hipMemsetAsync(a.gkeys, 0, (size_t)a.gtab_total * 16, st) != hipSuccess) ||
@@ -2643,7 +2761,13 @@ int oa_compact(const oa_compact_args *args, void *stream) {
         else hipLaunchKernelGGL(k_gather_items<4>, dim3(n_direct), dim3(256), 0, st, a);
         if (int rc = check_launch("k_gather_items")) return rc;
     }
-    if (a.gchunks && a.n_gchunks > 0) {
+    if (a.chunk_count && (!a.gchunks || !a.scratch_rk))
+        return fail(OA_E_ARG, "oa_compact: chunk_count needs gchunks and scratch_rk");
+    if (a.gchunks && a.n_gchunks > 0 && a.chunk_count) {
+        if (a.id_bytes == 8) hipLaunchKernelGGL(k_gather_recs<8>, dim3(a.n_gchunks), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL(k_gather_recs<4>, dim3(a.n_gchunks), dim3(256), 0, st, a);
+        if (int rc = check_launch("k_gather_recs")) return rc;
+    } else if (a.gchunks && a.n_gchunks > 0) {
         if (a.id_bytes == 8) hipLaunchKernelGGL(k_gather_chunks<8>, dim3(a.n_gchunks), dim3(256), 0, st, a);
         else hipLaunchKernelGGL(k_gather_chunks<4>, dim3(a.n_gchunks), dim3(256), 0, st, a);
         if (int rc = check_launch("k_gather_chunks")) return rc;

@@ -204,6 +204,11 @@ def plan_global(glob, cur_cnt, prev_cnt, first_index, compare):
     return chunks(n1).reshape(-1, 3), chunks(n2).reshape(-1, 3), tab, int(cap.sum())
 
 
+# compare steps with packed items only write their records at their final offsets
+# from k_step (oa_step_args.direct: decoupled look-back over items), so the step needs
+# no oa_compact; ORBIT_DIRECT=0 keeps scratch + oa_compact
+DIRECT = os.environ.get('ORBIT_DIRECT', '1') != '0'
+
 PART_FILL = 0.9      # mean fill of a large-halo partition's LDS table at most (k_part_join)
 
 
@@ -223,9 +228,10 @@ PART_SPREAD = int(_pow2_ceil(int(os.environ.get('ORBIT_PART_SPREAD', 32))))
 GPART_W = 16         # int64 per gpart row (orbit_hip.h)
 
 
-def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=None, n_xcd=8):
+def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=None, n_xcd=8,
+              key4=False):
     """Partition layout of the global items for the partitioned large-halo path
-    (k_part_scatter / k_part_join / k_part_emit), vectorised.
+    (k_part_scatter / k_part_join), vectorised.
 
     A halo with a progenitor block gets K = a power of two >= C / (0.9 part_e) (and
     >= PART_SPREAD) hash partitions of its IDs: a partition's current count is binomial
@@ -236,9 +242,13 @@ def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=No
     step bucketed the progenitor block (``prev_sets``, indexed by the previous
     snapshot's halo number ``prev_idx``; any K: both are powers of two), else from a
     fresh previous set scattered from the position-order state (mean + 8 sqrt(mean) + 64
-    entries per partition).  plist deals the partitions to the 8 XCDs in contiguous runs
-    (work-group b runs on XCD b % 8), so one halo's partitions share an L2.  Returns None
-    when no halo needs the join or one needs more than ``kmax`` partitions."""
+    entries per partition).  A previous set is inherited only when its keys have the
+    step's width (``key4``: 4-byte low words).  plist deals the partitions to the 8 XCDs
+    in contiguous runs (work-group b runs on XCD b % 8), so one halo's partitions share
+    an L2.  The counters (pcnt) are the current set's, the fresh previous set's, then
+    one record counter per previous-block chunk (gchunk2 row, GCHUNK positions; gpart[8]
+    is the item's first).  Returns None when no halo needs the join or one needs more
+    than ``kmax`` partitions."""
     h = np.asarray(glob['h0'], dtype=np.int64)
     c = np.asarray(cur_cnt, dtype=np.int64)[h]
     p = np.maximum(np.asarray(prev_cnt, dtype=np.int64)[h], 0)
@@ -259,7 +269,7 @@ def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=No
     inh = np.zeros(ng, dtype=bool)
     if prev_sets is not None and prev_idx is not None:
         pc = np.asarray(prev_idx, dtype=np.int64)[h]
-        ok = (pc >= 0) & (K > 0)
+        ok = (pc >= 0) & (K > 0) & (bool(prev_sets.key4) == bool(key4))
         pk = np.where(ok, prev_sets.K[np.maximum(pc, 0)], 0)
         inh = ok & (pk > 0)
         gpart[inh, 3] = 1
@@ -276,6 +286,10 @@ def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=No
     gpart[fresh, 5] = K[fresh]
     gpart[fresh, 6] = cap2[fresh]
     gpart[fresh, 7] = nk + (np.cumsum(fk) - fk)[fresh]
+    # record counters: one per previous-block chunk, in gchunk2 row order (plan_global)
+    nrow = -(-p // GCHUNK)
+    rc0 = nk + int(fk.sum())
+    gpart[:, 8] = rc0 + np.cumsum(nrow) - nrow
     g = np.repeat(np.arange(ng), K)
     pp = np.arange(nk) - np.repeat(np.cumsum(K) - K, K)
     per = -(-nk // n_xcd)
@@ -286,19 +300,24 @@ def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=No
     plist[:, 0] = -1
     plist[okb, 0], plist[okb, 1] = g[idx[okb]], pp[idx[okb]]
     return dict(gpart=gpart, plist=plist, n_cur=nk * int(part_e), n_prev=int(fsz.sum()),
-                n_pcnt=nk + int(fk.sum()), kmax=int(K.max()), K=K, inherited=inh, h=h)
+                n_pcnt=rc0 + int(nrow.sum()), rc0=rc0, kmax=int(K.max()), K=K, inherited=inh,
+                h=h)
 
 
 def retry_plan(pr, st):
     """(entries, part) of the re-run of a step whose kernels reported status ``st``:
     a full LDS table halves the items (at the floor every halo takes the global-table
     path, which keys on the full 64-bit ID); an overflowing large-halo partition
-    moves the large halos to the global-table path."""
+    moves the large halos to the global-table path.  (A direct-records look-back
+    timeout re-runs the same plan: OrbitEngine.note_status switches direct records
+    off.)"""
     from . import _native as N
     if st & N.STATUS_PLAN:
         raise RuntimeError('oa_step: an item exceeds the kernel limits (planner bug)')
     e = pr.entries
-    part = pr.part and not (st & N.STATUS_PART_OVERFLOW)
+    # a partition overflow or a large-halo ID outside the 4-byte keys' high word: the
+    # re-run takes the global tables (OrbitEngine.note_status keeps 8-byte keys after)
+    part = pr.part and not (st & (N.STATUS_PART_OVERFLOW | N.STATUS_PART_KEYS))
     if st & N.STATUS_TABLE_OVERFLOW:
         e = 0 if e <= 256 else max(256, e // 2)
         # smaller items turn more (and smaller) halos into global items: those take the
@@ -429,6 +448,7 @@ class BucketSet:
     cbase: np.ndarray
     cap: int
     td_f64: bool
+    key4: bool = False                  # keys are the IDs' low words (oa_step_args.part_key4)
     restored: Optional[np.ndarray] = None
 
 
@@ -538,7 +558,8 @@ class Workspace:
         self.h_status = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         self.h_total = torch.zeros(1, dtype=torch.int64, pin_memory=True)
         self.copy_done = None               # event after the last D2H of its records
-        self.gmark, self.mark_tag = None, 0   # large-halo apsis marks (marks())
+        self.scratch_rk = None              # partitioned halos' record positions (rk())
+        self.lookback, self.lb_epoch = None, 0  # direct records' item words (lookback())
 
     @staticmethod
     def need(pr):
@@ -559,18 +580,26 @@ class Workspace:
         """Per-launch zeroing (the status word accumulates: callers clear it)."""
         self.halo_count[:max(n_slots, 1)].zero_()
 
-    def marks(self, n):
-        """(pointer, tag) of the large-halo apsis marks for a launch needing ``n``: the
-        buffer is kept and each launch tags its marks (oa_step_args.mark_tag), so it is
-        zeroed only when it grows or its 15-bit tag would repeat."""
-        if self.gmark is None or self.gmark.numel() < n or self.mark_tag >= 0x7FFF:
-            if self.gmark is None or self.gmark.numel() < n:
-                self.gmark = torch.zeros(max(int(n), 1), dtype=torch.int32, device=self.device)
+    def lookback_words(self, n):
+        """(pointer, epoch) of the direct records' look-back words for a launch of ``n``
+        items: kept between launches and tagged per launch (oa_step_args.lb_epoch), so
+        they are zeroed only when the buffer grows or the 16-bit epoch would repeat."""
+        if self.lookback is None or self.lookback.numel() < n or self.lb_epoch >= 0xFFFF:
+            if self.lookback is None or self.lookback.numel() < n:
+                self.lookback = torch.zeros(max(int(n), 1), dtype=torch.int64, device=self.device)
             else:
-                self.gmark.zero_()
-            self.mark_tag = 0
-        self.mark_tag += 1
-        return self.gmark.data_ptr(), self.mark_tag
+                self.lookback.zero_()
+            self.lb_epoch = 0
+        self.lb_epoch += 1
+        return self.lookback.data_ptr(), self.lb_epoch
+
+    def rk(self):
+        """Per apsis-scratch slot, the position of a partitioned halo's record in its
+        previous-block chunk (oa_step_args.scratch_rk), allocated on first use."""
+        n = self.cap['scratch']
+        if self.scratch_rk is None or self.scratch_rk.numel() < n:
+            self.scratch_rk = torch.empty(max(n, 1), dtype=torch.int16, device=self.device)
+        return self.scratch_rk.data_ptr()
 
 
 class OrbitEngine:
@@ -611,6 +640,21 @@ class OrbitEngine:
         self.part_e = min(int(env('ORBIT_PART_ENTRIES', 4096)), self.lib.oa_build_info(4))
         self.part_slots = int(env('ORBIT_PART_SLOTS', 0)) or self.part_e + self.part_e // 2
         self.part_kmax = self.lib.oa_build_info(5)
+        if self.lib.oa_build_info(7) != GCHUNK:
+            raise N.NativeUnavailable('record chunk %d != engine.GCHUNK %d'
+                                      % (self.lib.oa_build_info(7), GCHUNK))
+        # 4-byte bucket keys (the IDs' low words) while every large-halo ID's high word
+        # is 0; a step that meets another one re-runs and the engine keeps 8-byte keys
+        self.part_key4 = env('ORBIT_PART_KEY4', '1') != '0'
+        # packed-only compare steps write their records from k_step (direct records)
+        self.direct = DIRECT
+
+    def note_status(self, st):
+        """Run-wide switches a step's status word turns off before its re-run."""
+        if st & N.STATUS_LOOKBACK:
+            self.direct = False
+        if st & N.STATUS_PART_KEYS:
+            self.part_key4 = False
 
     def table_sizes(self, dx_f64, entries=None):
         """(entries, slots) of one k_step item for a float32 / float64 r̂."""
@@ -644,7 +688,7 @@ class OrbitEngine:
             nws = Workspace(self.device, dt, positions=self.emit_positions, **cap)
             if ws is not None:
                 nws.gen, nws.copy_done = ws.gen, ws.copy_done
-                nws.gmark, nws.mark_tag = ws.gmark, ws.mark_tag
+                nws.lookback, nws.lb_epoch = ws.lookback, ws.lb_epoch
             ws = self._wss[idx] = nws
         return ws
 
@@ -778,6 +822,7 @@ class OrbitEngine:
                     r = res
                 r.pending = None
                 return r, prep
+            self.note_status(st)
             prep = self._prepare_ctx(ctx, *retry_plan(prep, st))
         raise RuntimeError('LDS hash tables kept overflowing')
 
@@ -811,8 +856,9 @@ class OrbitEngine:
                 self._pending = None
             return False
         self._pending = None
-        _, prep = self._run_ctx(ctx, self._prepare_ctx(ctx, *retry_plan(prep, int(res.ws.h_status[0]))),
-                                res=res)
+        st = int(res.ws.h_status[0])
+        self.note_status(st)
+        _, prep = self._run_ctx(ctx, self._prepare_ctx(ctx, *retry_plan(prep, st)), res=res)
         self._set_prev(ctx, prep)
         return True
 
@@ -868,27 +914,28 @@ class OrbitEngine:
             g['total'] = total
             pl = None
             if compare and part and self.part_large:
+                key4 = self.part_key4 or plan.ids.itemsize == 4
                 pl = plan_part(glob, counts, halos['prev_cnt'], self.part_e, self.part_kmax,
-                               prev_idx, prev_sets)
+                               prev_idx, prev_sets, key4=key4)
             if pl is not None:
                 pr.part = True
                 i32, i64 = torch.int32, torch.int64
                 g['plist'] = _up(pl['plist'].reshape(-1), dev)
                 g['gpart'] = _up(pl['gpart'].reshape(-1), dev)
                 # this step's current bucket set: the next step's previous state
-                g['pkey_cur'] = torch.empty(pl['n_cur'], dtype=i64, device=dev)
+                kt = i32 if key4 else i64
+                g['key4'] = key4
+                g['pkey_cur'] = torch.empty(pl['n_cur'], dtype=kt, device=dev)
                 g['ppos_cur'] = torch.empty(pl['n_cur'], dtype=i32, device=dev)
                 g['pmeta_cur'] = torch.empty(pl['n_cur'], dtype=i32, device=dev)
                 g['prh_cur'] = torch.empty(3 * pl['n_cur'], dtype=plan.torch_dx, device=dev)
-                g['pkey_prev'] = torch.empty(max(pl['n_prev'], 1), dtype=i64, device=dev)
+                g['pkey_prev'] = torch.empty(max(pl['n_prev'], 1), dtype=kt, device=dev)
                 g['ppos_prev'] = torch.empty(max(pl['n_prev'], 1), dtype=i32, device=dev)
                 g['pmeta_prev'] = torch.empty(max(pl['n_prev'], 1), dtype=i32, device=dev)
                 g['prh_prev'] = torch.empty(3 * max(pl['n_prev'], 1), dtype=plan.torch_dx,
                                             device=dev)
                 g['pcnt'] = torch.empty(pl['n_pcnt'], dtype=i32, device=dev)
-                g['gmark_base'] = int(glob['scratch_off'][0])
-                g['gmark_n'] = max(scratch - g['gmark_base'], 1)
-                # the marks buffer comes from the launch's workspace (OrbitEngine.launch)
+                g['rc0'] = pl['rc0']
                 g['n_parts'], g['kmax'] = len(pl['plist']), pl['kmax']
                 nh = len(halos)
                 K = np.zeros(nh, np.int64)
@@ -899,7 +946,8 @@ class OrbitEngine:
                 cbase[pl['h']] = pl['gpart'][:, 2]
                 pr.buckets = BucketSet(key=g['pkey_cur'], pos=g['ppos_cur'], meta=g['pmeta_cur'],
                                        rh=g['prh_cur'], cnt=g['pcnt'], K=K, base=base,
-                                       cbase=cbase, cap=self.part_e, td_f64=plan.dx == F64)
+                                       cbase=cbase, cap=self.part_e, td_f64=plan.dx == F64,
+                                       key4=key4)
                 if prev_sets is not None and pl['inherited'].any():
                     g['inherit'] = prev_sets           # keeps the previous set alive
                     # the scatter reads only the previous chunks of fresh sets
@@ -956,7 +1004,7 @@ class OrbitEngine:
                 a.imeta, a.irh, a.icnt = (_ptr(inh and inh.meta), _ptr(inh and inh.rh),
                                           _ptr(inh and inh.cnt))
                 a.pcnt, a.n_pcnt = g['pcnt'].data_ptr(), int(g['pcnt'].numel())
-                a.gmark_base, a.gmark_n = g['gmark_base'], g['gmark_n']
+                a.part_key4, a.part_hi = int(g['key4']), 0
                 if 'n3' in g:
                     # a non-NULL pointer marks the list as given, even when empty
                     a.gchunk3 = g['ch3'].data_ptr() if g['ch3'] is not None else \
@@ -996,7 +1044,10 @@ class OrbitEngine:
             a.ids_prev, a.rhat_prev, a.meta_prev = (p.ids.data_ptr(), p.rhat.data_ptr(),
                                                     p.meta.data_ptr())
             a.n_prev = pr.n_prev
-            ws.reset(res.n_slots)
+            # packed items only: k_step writes the records, offsets and total itself
+            direct = self.direct and pr.n_global == 0 and not a.onthefly
+            if not direct:
+                ws.reset(res.n_slots)
             ws.gen += 1
             res.ws, res.gen = ws, ws.gen
             a.scratch_ids, a.scratch_ang = ws.scratch_ids.data_ptr(), ws.scratch_ang.data_ptr()
@@ -1005,13 +1056,25 @@ class OrbitEngine:
                                                    ws.item_count.data_ptr(), ws.status.data_ptr())
             a.scratch_pos = _ptr(ws.scratch_pos)
             if pr.part:
-                a.gmark, a.mark_tag = ws.marks(pr.glob['gmark_n'])
+                a.scratch_rk = ws.rk()
+            a.direct = int(direct)
+            if direct:
+                a.lookback, a.lb_epoch = ws.lookback_words(len(pr.items))
+                a.n_slots = res.n_slots
+                a.offsets_out, a.out_ids = ws.offsets.data_ptr(), ws.out_ids.data_ptr()
+                a.out_ang, a.out_pos = ws.out_ang.data_ptr(), _ptr(ws.out_pos)
+                a.total_out = ws.total.data_ptr()
         if step_events is not None:
             step_events[0].record()
         N.check(lib.oa_step(a, st), 'oa_step')
         if step_events is not None:
             step_events[1].record()
         if not pr.compare:
+            return res
+        if a.direct:
+            res.offsets = ws.offsets[:res.n_slots + 1]
+            res.apsis_ids, res.apsis_ang, res.total = ws.out_ids, ws.out_ang, ws.total
+            res.apsis_pos = ws.out_pos
             return res
         c = pr.cargs
         c.halos, c.n_halos = a.halos, a.n_halos
@@ -1027,6 +1090,9 @@ class OrbitEngine:
         c.scratch_pos, c.out_pos = _ptr(ws.scratch_pos), _ptr(ws.out_pos)
         # global items' records: one gather work-group per previous-block chunk
         c.gchunks, c.n_gchunks = (a.gchunk2, a.n_gchunk2) if a.n_global_items else (None, 0)
+        # partitioned steps: the join's per-chunk record counters, ranked by scratch_rk
+        c.chunk_count = (a.pcnt + 4 * pr.glob['rc0']) if pr.part else None
+        c.scratch_rk = a.scratch_rk if pr.part else None
         N.check(lib.oa_compact(c, st), 'oa_compact')
         res.offsets = ws.offsets[:res.n_slots + 1]
         res.apsis_ids, res.apsis_ang, res.total = ws.out_ids, ws.out_ang, ws.total

@@ -700,6 +700,7 @@ class EngineLocal:
             if not st:
                 break
             # re-plan: smaller items / large halos on the global-table path
+            eng.note_status(st)
             entries, part = retry_plan(lp, st)
             shard, centres, bulk, H, z, exists, compare, angles_in, layout = lp.src
             hv = lp.halos.view(torch.float64).view(-1, 12)[:, 4:10].clone()

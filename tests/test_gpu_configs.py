@@ -2,7 +2,7 @@
 
 configs[2]: 1e8 particles in 1e4 halos, float32, every halo on the packed k_step path.
 configs[1]: 1e7 particles in 1e2 halos, float64, every halo (1e5 particles) on the
-partitioned large-halo path (k_part_scatter / k_part_join / k_part_emit).  Three
+partitioned large-halo path (k_part_scatter / k_part_join / k_gather_recs).  Three
 snapshots each, device-generated (synthetic_device.DevicePlummer), run through
 OrbitEngine (the path track_orbits uses).
 

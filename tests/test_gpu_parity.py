@@ -128,7 +128,7 @@ def _recording(eng):
 @pytest.mark.parametrize('mode', ['pericentric', 'apocentric'])
 def test_partitioned_large_halos(mode, monkeypatch):
     """Halos larger than a k_step item (30000 particles) through the partitioned path
-    (k_part_scatter / k_part_join / k_part_emit), through the global tables (k_big_*),
+    (k_part_scatter / k_part_join, records ranked by k_gather_recs), through the global tables (k_big_*),
     and with partitions forced past their LDS capacity (the kernel reports it and the
     snapshot re-runs on the global tables): all three equal the oracle."""
     from orbitanalysis_amd import engine as E
@@ -211,6 +211,59 @@ def test_bucket_sets_carried_between_steps(mode, monkeypatch):
     assert sum(x['inherit'] for x in seen) >= 4, seen          # sets carried over
     assert any(x['unbucket'] for x in seen), seen              # a halo turned small
     assert len({x['glob'] for x in seen}) > 1, seen            # ... and large again
+
+
+@pytest.mark.parametrize('ids', ['high_word', 'key8', 'int32'])
+def test_partition_key_widths(ids, monkeypatch):
+    """Bucket keys of the partitioned path: 4-byte low words while every large-halo ID's
+    high word is 0 (the default), else 8-byte keys.  'high_word': IDs past 2^40, so the
+    first compare step reports OA_STATUS_PART_KEYS, re-runs on the global tables and
+    the engine keeps 8-byte keys (fresh, then inherited sets); 'key8': 8-byte keys from
+    the start (ORBIT_PART_KEY4=0); 'int32': 4-byte IDs are their own keys.  All equal
+    the oracle, with checkpoint angles."""
+    from orbitanalysis_amd.engine import OrbitEngine
+    from orbitanalysis_amd.synthetic import PlummerSnapshots
+    from oracle import orbit_oracle as O
+    kw = dict(n_halos=5, n_per_halo=[30000, 20000, 30000, 5000, 26000], n_snapshots=5,
+              seed=47, box_size=150.0)
+    if ids == 'high_word':
+        kw['id_offset'] = 2 ** 40 + 7
+    elif ids == 'int32':
+        kw['id_dtype'] = np.int32
+    u = PlummerSnapshots(**kw)
+    mode = 'pericentric'
+    rec = O.MemoryRecord()
+    want = O.track_orbits(u.snapshot_numbers, u.main_branches(), u.regions, u.load_snapshot_data,
+                          rec, mode=mode, checkpoint=True)
+    eng = OrbitEngine(mode=mode)
+    if ids == 'key8':
+        eng.part_key4 = False
+    seen = []
+    orig = eng.prepare
+
+    def prepare(*a, **k):
+        pr = orig(*a, **k)
+        if pr.compare:
+            seen.append((pr.part, pr.glob.get('key4'), pr.glob.get('inherit') is not None))
+        return pr
+    eng.prepare = prepare
+    rep = {}
+    out = run_driver(u, dict(mode=mode, checkpoint=True), engine=eng)
+    compare_groups(out.groups, want.groups, rep)
+    c, w = out.checkpoint, np.asarray(rec.checkpoint)
+    bad = int(np.sum((c != w) & ~(np.isnan(c) & np.isnan(w))))
+    assert c.shape == w.shape and mismatch_ok(bad, c.size), (bad, c.size)
+    assert rep['angles'] > 0
+    if ids == 'high_word':
+        # step 1: 4-byte keys, then its re-run on the global tables (when the next step
+        # settles it); every plan after that re-run: 8-byte keys, fresh then inherited
+        assert seen[0][:2] == (True, True), seen
+        i = max(j for j, (p, _, _) in enumerate(seen) if not p)
+        assert seen[i + 1:] and all(p and k is False for p, k, _ in seen[i + 1:]), seen
+        assert seen[-1][2] and not eng.part_key4, seen
+    else:
+        assert all(p and k == (ids == 'int32') for p, k, _ in seen), seen
+        assert any(i for _, _, i in seen), seen
 
 
 @pytest.mark.parametrize('mode', ['pericentric', 'apocentric'])
@@ -528,3 +581,44 @@ def test_rows_before_the_first_block_are_ignored(mode):
                      verbose=False, mode=mode)
         res.append(out.groups)
     compare_groups(res[1], res[0], {})
+
+
+@pytest.mark.parametrize('kw,hmax', [
+    # 40 small halos packed up to 7 per item (slots of halos without progenitors too)
+    (dict(n_halos=40, n_per_halo=400, n_snapshots=4, seed=61), 7),
+    # 3000 one-halo items: many look-back windows of 64 items and dispatch rounds
+    (dict(n_halos=3000, n_per_halo=150, n_snapshots=3, seed=62, dtype=np.float32,
+          centre_dtype=np.float32, bulk='catalogue', box_size=400.0), None),
+])
+@pytest.mark.parametrize('mode', ['pericentric', 'apocentric'])
+def test_direct_records_match_compaction(kw, hmax, mode, monkeypatch):
+    """Packed-only compare steps write their records, offsets and total from k_step
+    (oa_step_args.direct, a decoupled look-back over items): the savefile equals the
+    scratch + oa_compact path's bit for bit, and the oracle's."""
+    from orbitanalysis_amd import engine as E
+    from orbitanalysis_amd.synthetic import PlummerSnapshots
+    outs = []
+    for direct in (True, False):
+        monkeypatch.setattr(E, 'DIRECT', direct)
+        eng = E.OrbitEngine(mode=mode, hmax=hmax)
+        used = []
+        orig = eng.launch
+
+        def launch(pr, ws, *a, **k):
+            r = orig(pr, ws, *a, **k)
+            if pr.compare:
+                used.append(bool(pr.args.direct))
+            return r
+        eng.launch = launch
+        outs.append(run_driver(PlummerSnapshots(**kw), dict(mode=mode, checkpoint=True),
+                               engine=eng))
+        assert used and all(u == direct for u in used), used
+    d, c = outs
+    assert sorted(d.groups) == sorted(c.groups)
+    for g in c.groups:
+        for k, w in c.groups[g].items():
+            assert np.array_equal(np.asarray(d.groups[g][k]).view(np.uint8),
+                                  np.asarray(w).view(np.uint8)), (g, k)
+    rep = {}
+    compare_groups(d.groups, _oracle_run(PlummerSnapshots(**kw), mode), rep)
+    assert rep['angles'] > 0

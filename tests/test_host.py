@@ -287,8 +287,10 @@ def test_plan_part_bucket_sets():
     glob = {'h0': np.array([0, 1, 2, 3, 4])}
     prev_idx = np.array([3, 0, -1, 2, 1])                    # previous halo numbers
     ps = SimpleNamespace(K=np.array([64, 0, 16, 32]), base=np.array([0, -1, 64 * 4096, 80 * 4096]),
-                         cbase=np.array([0, 0, 64, 80]), cap=4096)
-    pl = plan_part(glob, cur, prev, 4096, 4096, prev_idx, ps)
+                         cbase=np.array([0, 0, 64, 80]), cap=4096, key4=True)
+    # a set with keys of another width is not inherited
+    assert not plan_part(glob, cur, prev, 4096, 4096, prev_idx, ps, key4=False)['inherited'].any()
+    pl = plan_part(glob, cur, prev, 4096, 4096, prev_idx, ps, key4=True)
     K, g = pl['K'], pl['gpart']
     assert g.shape == (5, GPART_W)
     assert all(k == 0 or (k & (k - 1)) == 0 for k in K)
@@ -305,7 +307,12 @@ def test_plan_part_bucket_sets():
     assert g[1, 5] == 64 and g[1, 7] == 0
     # the fresh previous set of halo 4: K of its own, counters after the current ones
     assert g[4, 5] == K[4] and g[4, 7] == K.sum() and g[4, 6] >= 10 / K[4]
-    assert pl['n_pcnt'] == K.sum() + K[4] and pl['n_prev'] == K[4] * g[4, 6]
+    # then one record counter per previous-block chunk (GCHUNK positions), item by item
+    from orbitanalysis_amd.engine import GCHUNK
+    rows = -(-np.maximum(prev, 0) // GCHUNK)
+    assert pl['rc0'] == K.sum() + K[4]
+    assert np.array_equal(g[:, 8], pl['rc0'] + np.cumsum(rows) - rows)
+    assert pl['n_pcnt'] == pl['rc0'] + rows.sum() and pl['n_prev'] == K[4] * g[4, 6]
     assert list(pl['inherited']) == [True, True, False, True, False]
     # every current partition listed once
     pl_ok = pl['plist'][pl['plist'][:, 0] >= 0]
@@ -330,5 +337,7 @@ def test_plan_part_memory_scales_with_halo_size():
     pr = SimpleNamespace(entries=6144, part=True)
     assert retry_plan(pr, N.STATUS_TABLE_OVERFLOW) == (3072, False)
     assert retry_plan(pr, N.STATUS_PART_OVERFLOW) == (6144, False)
+    assert retry_plan(pr, N.STATUS_PART_KEYS) == (6144, False)
+    assert retry_plan(pr, N.STATUS_LOOKBACK) == (6144, True)
     pr.entries = 256
     assert retry_plan(pr, N.STATUS_TABLE_OVERFLOW) == (0, False)

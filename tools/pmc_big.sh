@@ -3,7 +3,7 @@
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/pmcbig_${TAG:-x}; mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
-for k in ${KERNELS:-k_part_join k_part_scatter k_part_emit}; do
+for k in ${KERNELS:-k_part_join k_part_scatter k_gather_recs}; do
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 120 rocprofv3 --pmc $c --kernel-include-regex "$k" --output-format csv \
       -d "$O/${k}_$c" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline \
