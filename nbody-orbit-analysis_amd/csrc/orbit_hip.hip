@@ -48,23 +48,8 @@ namespace {
 #ifndef OA_KROWS
 #define OA_KROWS 12         // phase 2: progenitor rows held per wave (n_pv <= KROWS * WG)
 #endif
-#ifndef OA_PF1
-#define OA_PF1 1            // phase 1: trips of loads in flight ahead (static trips; 2: A/B r02 neutral)
-#endif
-#ifndef OA_RDEFER
-#define OA_RDEFER 1         // compare steps: r̂ stored in phase 2b from registers, not in phase 1
-#endif
-#ifndef OA_EWALK
-#define OA_EWALK 1          // waves done with phase 1 walk the deferred inserts appended so far
-#endif
-#ifndef OA_P3BAR
-#define OA_P3BAR 1          // 1: LDS-only barrier before phase 3 (the records' stores stay in flight)
-#endif
 #ifndef OA_PF2
 #define OA_PF2 5            // phase 2b: rows of previous r̂ loads in flight ahead (A/B r02: 2 +3.5 %, 4 = 3, 5 -0.4 %)
-#endif
-#ifndef OA_PFEARLY
-#define OA_PFEARLY 0        // 1: those loads issued with the 2a loads, before the walks and lookups
 #endif
 #ifndef OA_HMAX
 #define OA_HMAX 32
@@ -77,33 +62,17 @@ constexpr int NWAVE = WG / 64;
 constexpr int HMAX = OA_HMAX;       // halos per item
 constexpr int UNR1 = OA_UNR1;       // phase-1 particles per thread per loop trip
 constexpr int KROWS = OA_KROWS;
-constexpr int PF1 = OA_PF1;
-constexpr bool RDEFER = OA_RDEFER != 0;
-constexpr bool EWALK = OA_EWALK != 0;
 constexpr int PF2 = OA_PF2;
-static_assert(PF1 == 1 || PF1 == 2, "phase-1 prefetch depth is 1 or 2 trips");
 constexpr int BULK_CHUNK = 8192;    // numpy pairwise-sum buffer chunk
 constexpr int STASH = 64;           // cuckoo stash entries per item
 #ifndef OA_MAXEV
 #define OA_MAXEV 48
 #endif
-#ifndef OA_ROWGUARD
-#define OA_ROWGUARD 0       // 1: no loads for rows past the item (A/B r02 gp: +30 us, off)
-#endif
-#ifndef OA_P3V
-#define OA_P3V 1            // phase 3: four state words per 16-byte store
-#endif
 #ifndef OA_PU
 #define OA_PU 4             // k_part_join: previous entries per thread loaded up front
 #endif
-#ifndef OA_RWALK
-#define OA_RWALK 0
-#endif
 constexpr int MAX_EVICT = OA_MAXEV; // eviction-chain length before an entry is stashed
-#ifndef OA_NCAND
-#define OA_NCAND 3
-#endif
-constexpr int NCAND = OA_NCAND;     // cuckoo candidate slots per key (3 or 4)
+constexpr int NCAND = 3;            // cuckoo candidate slots per key
 static_assert(WG % 64 == 0 && WG <= 1024, "work-group must be whole waves");
 static_assert(HMAX < WG, "halo table is staged by one thread per halo");
 
@@ -247,7 +216,6 @@ __device__ __forceinline__ void cuckoo_slots(uint32_t lo, uint32_t n, uint32_t s
     s[0] = __umul24(h1 >> 16, n) >> 16;
     s[1] = __umul24(h1 & 0xFFFFu, n) >> 16;
     s[2] = __umul24(h2 >> 16, n) >> 16;
-    if (NCAND > 3) s[3 % NCAND] = __umul24(h2 & 0xFFFFu, n) >> 16;
 }
 
 template <int IDB> struct IdT;
@@ -346,9 +314,6 @@ __device__ int64_t item_lookback(const oa_step_args &a, uint32_t b, uint32_t cou
     return excl;
 }
 
-#ifndef OA_ROWTAB
-#define OA_ROWTAB 1         // packed items: per-row halo / segment tables built in phase 0
-#endif
 #ifndef OA_PENDDIV
 #define OA_PENDDIV 9        // deferral list: lds_entries / OA_PENDDIV entries of 8 bytes
 #endif
@@ -666,10 +631,7 @@ template <typename T, int AUX> __device__ __forceinline__ V3<T> bld3(Rsrc r, uin
 template <int AUX> __device__ __forceinline__ void bst32(Rsrc r, uint32_t o, uint32_t v) {
     rbs_i32((int32_t)v, r, (int32_t)o, 0, AUX);
 }
-#ifndef OA_RNT
-#define OA_RNT 1            // r̂ stores non-temporal (A/B r03: 1.540-1.548 vs 1.561-1.581 ms)
-#endif
-constexpr int AUX_R = OA_RNT ? AUX_NT : 0;
+constexpr int AUX_R = AUX_NT;       // r̂ stores non-temporal (A/B r03: 1.540-1.548 vs 1.561-1.581 ms)
 template <typename T> __device__ __forceinline__ void bst3(Rsrc r, uint32_t o, const T v[3]) {
     if constexpr (sizeof(T) == 4) {
         const f32x3 w = {v[0], v[1], v[2]};
@@ -748,7 +710,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // into the LDS the table held -- no read-back of the rows it stored.
     constexpr int SU = sizeof(TD) == 4 ? STAGE_F32 : STAGE_F64;
     // float64 r̂ keeps its phase-1 stores (register budget)
-    constexpr bool RD = RDEFER && COMPARE && sizeof(TD) == 4;
+    constexpr bool RD = COMPARE && sizeof(TD) == 4;
     // float64 inputs: one row per trip (register budget of 1024-thread work-groups)
     constexpr int U1 = (sizeof(TX) == 8 || sizeof(TV) == 8) ? 1 : UNR1;
     constexpr int NTRIP = SU / U1;
@@ -770,19 +732,17 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         XA[u] = bld3<TX, AUX_NT>(r_x, li_ * SX);                                   \
         VA[u] = bld3<TV, AUX_NT>(r_v, li_ * SV);                                   \
     }
-    // static trips keep PF1 trips of loads in flight ahead of the one computing
-    constexpr int PF = DYN ? 1 : PF1;
-    ID idv[U1], idn[U1], idm[U1];
-    V3<TX> xv[U1], xn[U1], xm[U1];
-    V3<TV> vv[U1], vn[U1], vm[U1];
+    // one trip of loads in flight ahead of the one computing (two: A/B r02 neutral)
+    ID idv[U1], idn[U1];
+    V3<TX> xv[U1], xn[U1];
+    V3<TV> vv[U1], vn[U1];
     V3<TD> rr[SU];
     OA_LOAD1(idv, xv, vv, tp[0])
-    if (PF == 2) OA_LOAD1(idn, xn, vn, tp[1])
     __builtin_amdgcn_sched_barrier(0);
     if (COMPARE) {
         for (uint32_t w = tid; w < nslots; w += WG) slots[w] = 0ull;
         // early walks read appended entries: an unwritten one is still 0
-        if (EWALK) for (uint32_t w = tid; w < pend_cap; w += WG) pend[w] = 0ull;
+        for (uint32_t w = tid; w < pend_cap; w += WG) pend[w] = 0ull;
     }
     if (wave == 0) {
         // progenitor segments: every halo with a non-empty progenitor block, in halo
@@ -813,7 +773,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
         }
         const uint32_t n_pv = (uint32_t)__shfl(vi, 63), nseg = (uint32_t)__shfl(si, 63);
-        if (!SINGLE && OA_ROWTAB && nh > 1) {
+        if (!SINGLE && nh > 1) {
             // per-row tables, so no row searches the halo or segment starts later: the
             // halo of each current row's first position, and each progenitor row's
             // segment and row within it (a lane per halo, its own rows)
@@ -849,8 +809,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         const uint32_t tcur = DYN ? tp[kp] : (uint32_t)(wave + NWAVE * kp);
         uint32_t f = 0;
         if (DYN && kp + 2 < NTRIP && lane == 0) f = atomicAdd(&H.ctr1, 1u);   // trip kp + 2
-        if (PF == 1 && kp + 1 < NTRIP) OA_LOAD1(idn, xn, vn, (DYN ? tp[(kp + 1) % NTRIP] : (uint32_t)(wave + NWAVE * (kp + 1))))
-        if (PF == 2 && kp + 2 < NTRIP) OA_LOAD1(idm, xm, vm, (uint32_t)(wave + NWAVE * (kp + 2)))
+        if (kp + 1 < NTRIP) OA_LOAD1(idn, xn, vn, (DYN ? tp[(kp + 1) % NTRIP] : (uint32_t)(wave + NWAVE * (kp + 1))))
         uint64_t val[U1];
         uint32_t csu[U1][NCAND];
         bool ins[U1];
@@ -865,8 +824,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             // packed item step each lane forward
             uint32_t hl = 0;
             if (!SINGLE && nhu > 1) {
-                hl = OA_ROWTAB ? uni((uint32_t)H.rowcnt[r0 >> 6])    // rowh (phase 0)
-                               : uni(upper_find(H.lstart, nhu, r0));
+                hl = uni((uint32_t)H.rowcnt[r0 >> 6]);               // rowh (phase 0)
                 if (r0 + 63u >= H.lstart[hl + 1])
                     while (hl + 1 < nhu && li >= H.lstart[hl + 1]) ++hl;
             }
@@ -935,7 +893,6 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
 #pragma unroll
         for (int u = 0; u < U1; ++u) {
             idv[u] = idn[u]; xv[u] = xn[u]; vv[u] = vn[u];
-            if (PF == 2) { idn[u] = idm[u]; xn[u] = xm[u]; vn[u] = vm[u]; }
         }
         if (DYN && kp + 2 < NTRIP) tp[(kp + 2) % NTRIP] = __builtin_amdgcn_readfirstlane(f);
     }
@@ -1000,13 +957,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         uint32_t ro = r0, cnt = cnt0;
         hs = hal0;
         int64_t off = off0;
-        if (nseg > 1 && !OA_ROWTAB) {
-            const uint32_t s = uni(upper_find(H.vstart, nseg, min(r0, n_pv - 1u)));
-            ro = r0 - uni(H.vstart[s]);
-            cnt = uni(H.seg_cnt[s]);
-            hs = uni((uint32_t)H.seg_halo[s]);
-            off = uni64(H.seg_prev_off[s]);
-        } else if (nseg > 1) {
+        if (nseg > 1) {
             // the row's segment from the phase-0 table (rows past the item: none)
             const uint32_t e = r < nrow ? uni((uint32_t)prow[r]) : 0u, s = e >> 8;
             ro = r < nrow ? (e & 0xFFu) * 64u : cnt0;
@@ -1027,23 +978,11 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     for (int k = 0; k < KROWS; ++k) {
         pid[k] = 0;
         pk[k] = 0u;
-        if (OA_ROWGUARD && (uint32_t)(wave + NWAVE * k) >= nrow) continue;      // uniform
         uint32_t nv, hs;
         int64_t kb;
         row_of(wave + NWAVE * k, nv, hs, kb);
         pid[k] = bld<ID, AUX_NT>(make_rsrc(ids_prev + kb, nv * IDB), lane * IDB);
         pk[k] = bld<uint32_t, AUX_NT>(make_rsrc(a.meta_prev + kb, nv * 4u), lane * 4u);
-    }
-    if (OA_PFEARLY) {
-        // the first PF2 rows' previous r̂ loads right behind the 2a loads: their HBM
-        // transfer overlaps the walks and the LDS lookups instead of following them
-#pragma unroll
-        for (int k = 0; k < PF2 && k < KROWS; ++k) {
-            uint32_t nv, hs;
-            int64_t kb;
-            row_of(wave + NWAVE * k, nv, hs, kb);
-            prh[k] = bld3<TD, AUX_NT>(make_rsrc(rhat_prev + 3 * kb, nv * SD), lane * SD);
-        }
     }
     __builtin_amdgcn_sched_barrier(0);
     // one deferred insert's eviction walk (atomic exchanges: safe beside the first-try
@@ -1071,16 +1010,11 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             uint32_t nx = cs[0];
 #pragma unroll
             for (int j = NCAND - 2; j >= 0; --j) nx = cs[j] == t ? cs[j + 1] : nx;
-            if (OA_RWALK && NCAND == 3) {
-                // or, pseudo-randomly, to the other one (breaks walk cycles)
-                const uint32_t alt = cs[0] ^ cs[1] ^ cs[2] ^ t ^ nx;
-                if (((uint32_t)old ^ (uint32_t)it_) & 1u) nx = alt;
-            }
             t = nx;
             v = old;
         }
     };
-    if (EWALK) {
+    {
         // a wave done with phase 1 walks the deferred inserts appended so far, claimed
         // in runs of 64 from a cursor, while later waves still stream; the barrier
         // below leaves the rest to the whole work-group
@@ -1116,7 +1050,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     STAMP(2);
     {
         const uint32_t np = min(H.npend, pend_cap);
-        for (uint32_t e = (EWALK ? H.pad2 : 0u) + tid; e < np; e += WG) walk(pend[e]);
+        for (uint32_t e = H.pad2 + tid; e < np; e += WG) walk(pend[e]);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -1208,8 +1142,6 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < PF2 && k < KROWS; ++k) {
-        if (OA_PFEARLY) break;
-        if (OA_ROWGUARD && (uint32_t)(wave + NWAVE * k) >= nrow) continue;      // uniform
         uint32_t nv, hs;
         int64_t kb;
         row_of(wave + NWAVE * k, nv, hs, kb);
@@ -1266,7 +1198,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     constexpr uint32_t RCW = sizeof(TD) / 4;
 #pragma unroll
     for (int k = 0; k < KROWS; ++k) {
-        if (k + PF2 < KROWS && (!OA_ROWGUARD || (uint32_t)(wave + NWAVE * (k + PF2)) < nrow)) {
+        if (k + PF2 < KROWS) {
             uint32_t nv, hs;
             int64_t kb;
             row_of(wave + NWAVE * (k + PF2), nv, hs, kb);
@@ -1313,21 +1245,17 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     }
     WSTAMP(2);
     STAMP(6);
-    if (OA_P3BAR) {
-        // phase 3 reads LDS alone: the records' global stores stay in flight
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-    } else {
-        __syncthreads();
-    }
+    // phase 3 reads LDS alone: the records' global stores stay in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
 
     // ---- phase 3: every state word of the item, in position order ---------------
     // matched: the new angle phase 2b left in rc_x; entered or in a halo without a
     // progenitor block: angle 0 (calc_angles :348-349).  Nothing in this launch reads
     // them again, so the stores are non-temporal.
     // (four consecutive positions per thread: one 16-byte store)
-    const uint32_t n4 = OA_P3V ? n_span & ~3u : 0u;
+    const uint32_t n4 = n_span & ~3u;
     for (uint32_t l4 = (uint32_t)tid * 4u; l4 < n4; l4 += WG * 4u) {
         const uint32_t s4 = *reinterpret_cast<const uint32_t *>(sgn8 + l4);
         i32x4 w;
@@ -1976,9 +1904,6 @@ constexpr int GPART_W = 16;             // int64 per gpart row (orbit_hip.h)
 #ifndef OA_SCAT_PER
 #define OA_SCAT_PER 4       // k_part_scatter: particles per thread per staged sub-chunk
 #endif
-#ifndef OA_SCAT_NT
-#define OA_SCAT_NT 1        // k_part_scatter: bucket IDs / position / state words stored non-temporally
-#endif
 constexpr int SCAT_WG = 256, SCAT_PER = OA_SCAT_PER, SCAT_NS = SCAT_WG * SCAT_PER;
 static_assert(PART_E - 1 <= (int)MAX_POS, "partition entries must fit the slot position field");
 static_assert(PART_KMAX <= 65536, "staged partition numbers are 16-bit");
@@ -2156,15 +2081,11 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
             if (e < bcap) {                             // an overflow is reported by the join
                 const int64_t o = (int64_t)k * bcap + e;
                 TD *d = brh + 3 * o;
-                if (OA_SCAT_NT) {
-                    __builtin_nontemporal_store((KEY)skey[s], &bkey[o]);
-                    __builtin_nontemporal_store(spw[s], &bpos[o]);
-                    // a current entry's state word is the join's (k_part_join stages them)
-                    if (!CUR) __builtin_nontemporal_store(smeta[s], &bmeta[o]);
-                } else {
-                    bkey[o] = (KEY)skey[s]; bpos[o] = spw[s];
-                    if (!CUR) bmeta[o] = smeta[s];
-                }
+                // key, position and state words non-temporal; a current entry's state
+                // word is the join's (k_part_join stages them)
+                __builtin_nontemporal_store((KEY)skey[s], &bkey[o]);
+                __builtin_nontemporal_store(spw[s], &bpos[o]);
+                if (!CUR) __builtin_nontemporal_store(smeta[s], &bmeta[o]);
                 d[0] = srh[3 * s]; d[1] = srh[3 * s + 1]; d[2] = srh[3 * s + 2];
             }
         }

@@ -229,7 +229,7 @@ GPART_W = 16         # int64 per gpart row (orbit_hip.h)
 
 
 def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=None, n_xcd=8,
-              key4=False):
+              key4=False, td_f64=None):
     """Partition layout of the global items for the partitioned large-halo path
     (k_part_scatter / k_part_join), vectorised.
 
@@ -243,7 +243,7 @@ def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=No
     snapshot's halo number ``prev_idx``; any K: both are powers of two), else from a
     fresh previous set scattered from the position-order state (mean + 8 sqrt(mean) + 64
     entries per partition).  A previous set is inherited only when its keys have the
-    step's width (``key4``: 4-byte low words).  plist deals the partitions to the 8 XCDs
+    step's width (``key4``: 4-byte low words) and r̂ in the step's dtype (``td_f64``).  plist deals the partitions to the 8 XCDs
     in contiguous runs (work-group b runs on XCD b % 8), so one halo's partitions share
     an L2.  The counters (pcnt) are the current set's, the fresh previous set's, then
     one record counter per previous-block chunk (gchunk2 row, GCHUNK positions; gpart[8]
@@ -270,6 +270,8 @@ def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=No
     if prev_sets is not None and prev_idx is not None:
         pc = np.asarray(prev_idx, dtype=np.int64)[h]
         ok = (pc >= 0) & (K > 0) & (bool(prev_sets.key4) == bool(key4))
+        if td_f64 is not None:
+            ok &= bool(prev_sets.td_f64) == bool(td_f64)
         pk = np.where(ok, prev_sets.K[np.maximum(pc, 0)], 0)
         inh = ok & (pk > 0)
         gpart[inh, 3] = 1
@@ -418,8 +420,18 @@ class PendingFetch:
         offsets = self.h_off.numpy()
         if self.h_ids is None:
             return offsets, np.zeros(0, dtype=self.ids_dtype), np.zeros(0, dtype=np.float16)
-        return offsets, self.h_ids.numpy().view(self.ids_dtype), \
+        return offsets, ids_as(self.h_ids.numpy(), self.ids_dtype), \
             self.h_ang.numpy().view(np.float16)
+
+
+def ids_as(raw, ids_dtype):
+    """Records' IDs (the workspace's integer width) in the previous snapshot's ID dtype,
+    the dtype of the reference's ids_prev_[apsis_inds] (track_orbits.py:315-316): a
+    widened previous state (int32 -> int64 between snapshots) narrows back exactly."""
+    ids_dtype = np.dtype(ids_dtype)
+    if raw.dtype.itemsize == ids_dtype.itemsize:
+        return raw.view(ids_dtype)
+    return raw.view(np.dtype('%s%d' % (ids_dtype.kind, raw.dtype.itemsize))).astype(ids_dtype)
 
 
 def meta_angles(meta):
@@ -881,12 +893,16 @@ class OrbitEngine:
             prev_layout = (p.starts, p.counts, p.exists, p.plan, p.ids.numel(), p.buckets)
         prev_sets = prev_layout[5] if compare and len(prev_layout) > 5 else None
         if compare:
+            # a snapshot whose r̂ or ID dtype is wider than the previous one's compares in
+            # the wider dtype, as NumPy promotes (launch widens the previous state); a
+            # narrower one would need the previous state in two dtypes at once
             pplan = prev_layout[3]
-            if plan.dx != pplan.dx:
-                raise NotImplementedError('r̂ dtype changed between snapshots (%s -> %s)'
+            if np.dtype(plan.dx).itemsize < np.dtype(pplan.dx).itemsize:
+                raise NotImplementedError('r̂ dtype narrowed between snapshots (%s -> %s)'
                                           % (pplan.dx, plan.dx))
-            if plan.ids.itemsize != pplan.ids.itemsize:
-                raise NotImplementedError('ids dtype changed between snapshots')
+            if plan.ids.itemsize < pplan.ids.itemsize:
+                raise NotImplementedError('ids dtype narrowed between snapshots (%s -> %s)'
+                                          % (pplan.ids, plan.ids))
         n = snap['ids'].numel()
         if snap['coordinates'].numel() != 3 * n or snap['velocities'].numel() != 3 * n:
             raise ValueError('coordinates/velocities must be (N, 3) with N = len(ids)')
@@ -916,7 +932,7 @@ class OrbitEngine:
             if compare and part and self.part_large:
                 key4 = self.part_key4 or plan.ids.itemsize == 4
                 pl = plan_part(glob, counts, halos['prev_cnt'], self.part_e, self.part_kmax,
-                               prev_idx, prev_sets, key4=key4)
+                               prev_idx, prev_sets, key4=key4, td_f64=plan.dx == F64)
             if pl is not None:
                 pr.part = True
                 i32, i64 = torch.int32, torch.int64
@@ -1041,7 +1057,16 @@ class OrbitEngine:
                 # progenitor blocks this step reads in position order (packed items, the
                 # global tables) from the previous step's bucket set
                 self.unbucket(p.buckets, pr.unbucket_prev, p.starts, p.rhat, p.meta, st)
-            a.ids_prev, a.rhat_prev, a.meta_prev = (p.ids.data_ptr(), p.rhat.data_ptr(),
+            p_ids, p_rhat = p.ids, p.rhat
+            if p.plan.dx != pr.plan.dx:                  # float32 -> float64 r̂: exact
+                p_rhat = p.rhat.to(pr.plan.torch_dx)
+            if p.plan.ids.itemsize != pr.plan.ids.itemsize:
+                # 4-byte -> 8-byte IDs (unsigned ones zero-extended)
+                p_ids = p.ids.to(torch.int64)
+                if p.plan.ids.kind == 'u':
+                    p_ids &= 0xFFFFFFFF
+            res.extra['prev_widened'] = (p_ids, p_rhat)   # alive until the step is done
+            a.ids_prev, a.rhat_prev, a.meta_prev = (p_ids.data_ptr(), p_rhat.data_ptr(),
                                                     p.meta.data_ptr())
             a.n_prev = pr.n_prev
             # packed items only: k_step writes the records, offsets and total itself
@@ -1155,7 +1180,7 @@ class OrbitEngine:
         h_ids.copy_(ids_t, non_blocking=True)
         h_ang.copy_(res.apsis_ang[:total], non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
-        return offsets, h_ids.numpy().view(ids_dtype), h_ang.numpy().view(np.float16)
+        return offsets, ids_as(h_ids.numpy(), ids_dtype), h_ang.numpy().view(np.float16)
 
     def block_bulk(self, snapshot, halo_idx):
         """Bulk velocities (track_orbits.py:269-280) of the listed region blocks of a

@@ -18,17 +18,27 @@ def pytest_terminal_summary(terminalreporter):
     """Session total of f16 apsis angles that differ from the reference's by one ulp
     (test_gpu_parity.compare_groups; the per-test bound is ANGLE_MISMATCH_MAX)."""
     gu = sys.modules.get('golden_util')
+    ch = getattr(gu, 'CHANGE_TALLY', None)
+    if ch:
+        n = sum(ch.values())
+        terminalreporter.write_line('angle changes vs reference: %d compared, ulp distance histogram %s'
+                                    % (n, dict(sorted(ch.items()))))
+        _dump('angle_change_ulps.json', {str(k): v for k, v in sorted(ch.items())})
     t = getattr(gu, 'ANGLE_TALLY', None)
     if not t or not t['angles']:
         return
     rate = t['mismatch'] / t['angles']
     terminalreporter.write_line('f16 apsis angles vs reference fixtures: %d of %d differ by 1 ulp '
                                 '(%.4f %%)' % (t['mismatch'], t['angles'], 100 * rate))
+    _dump('angle_mismatch.json', dict(t, rate=rate))
+
+
+def _dump(name, obj):
     out = os.path.join(ROOT, 'gpurun_out')
     try:
         import json
         os.makedirs(out, exist_ok=True)
-        with open(os.path.join(out, 'angle_mismatch.json'), 'w') as f:
-            json.dump(dict(t, rate=rate), f)
+        with open(os.path.join(out, name), 'w') as f:
+            json.dump(obj, f)
     except OSError:
         pass

@@ -58,3 +58,26 @@ def assert_groups_equal(got, want):
 # differ by one f16 ulp (numpy's arccos is not correctly rounded); conftest prints the
 # total at the end of the run and writes it to gpurun_out/angle_mismatch.json
 ANGLE_TALLY = {'angles': 0, 'mismatch': 0}
+
+# on-the-fly / module-level angle changes (float32 or float64 arccos) compared against the
+# reference's in this session: ulp distance -> count; conftest prints the histogram and
+# writes gpurun_out/angle_change_ulps.json.  The bound is the observed maximum.
+CHANGE_TALLY = {}
+CHANGE_ULP_MAX = 2
+
+
+def check_changes(v, w, dtype, where):
+    """Angle changes ``v`` vs the reference's ``w``: NaN where it is NaN, elsewhere within
+    CHANGE_ULP_MAX ulps of ``dtype`` (the dtype arccos ran in), tallied by distance."""
+    v, w = np.asarray(v), np.asarray(w)
+    nan = np.isnan(w)
+    assert np.array_equal(np.isnan(v), nan), where
+    dt = np.dtype(dtype)
+    a, b = v[~nan].astype(dt), w[~nan].astype(dt)
+    assert np.all(b >= 0) and np.all(a >= 0), where          # arccos range: bits are monotone
+    it = np.int32 if dt.itemsize == 4 else np.int64
+    d = np.abs(a.view(it).astype(np.int64) - b.view(it).astype(np.int64))
+    for k, c in zip(*np.unique(d, return_counts=True)):
+        CHANGE_TALLY[int(k)] = CHANGE_TALLY.get(int(k), 0) + int(c)
+    assert d.max(initial=0) <= CHANGE_ULP_MAX, (where, int(d.max(initial=0)))
+

@@ -17,6 +17,8 @@ import os
 import tempfile
 
 import numpy as np
+
+from golden_util import check_changes
 import pytest
 import torch.multiprocessing as mp
 
@@ -124,11 +126,7 @@ def test_configs4_onthefly_rank_share_world1():
             assert np.array_equal(got[name + '_offsets'][:k + 1], o), name
             assert np.array_equal(got[name + '_IDs'][:o[-1]], want[name + '_IDs']), name
         w = want['angles']
-        v = got['angles'][:len(w)]
-        nan = np.isnan(w)
-        assert np.array_equal(np.isnan(v), nan)
-        ulp = np.spacing(np.abs(w[~nan]).astype(np.float32)).astype(np.float64)
-        assert np.all(np.abs(v[~nan].astype(np.float64) - w[~nan]) <= 2 * ulp)
+        check_changes(got['angles'][:len(w)], w, np.float32, 'configs[4] share')
         for a, b in zip(got['bulk_velocities'], want['bulk_velocities']):
             assert np.array_equal(a[:k], b), 'bulk velocities'
         # the single-GPU on-the-fly path on the same pair: the same file bit for bit
@@ -180,11 +178,59 @@ def _cfg3_worker(rank, world, port, contract, outdir):
         dist.destroy_process_group()
 
 
+def _oracle_pair(u, s, k, group, mode='pericentric'):
+    """The oracle's per-halo path (region_frame, compare_radial_velocities, calc_angles)
+    on the first k blocks of snapshot pair (s-1, s) of a universe whose snapshot 0 is the
+    frame-only one (angles 0), against a savefile group: per-halo offsets and apsis IDs
+    bit-exact, f16 angles within one ulp, at most ANGLE_MISMATCH_MAX of them off."""
+    from oracle import orbit_oracle as O
+    from orbitanalysis_amd.utils import hubble_parameter
+    from test_gpu_parity import mismatch_ok
+    from golden_util import ANGLE_TALLY
+    cos = u.gen.cosmology
+    H = hubble_parameter(cos['redshift'], cos['H0'], cos['Omega_m'], cos['Omega_L'])
+
+    def host(t):
+        d = u.host_blocks(t, k)
+        n = u.snaps[t]['ids'].numel()
+        d['redshift'] = u.snaps[t]['redshift']
+        off = np.append(u.snaps[t]['region_offsets'], n)[:k + 1]
+        return d, off
+    (prv, pb), (cur, cb) = host(s - 1), host(s)
+    cp, cc = u.cats[s - 1], u.cats[s]
+    ang = np.zeros(int(pb[-1]), np.float16)
+    ids, angs, lens = [], [], []
+    for j in range(k):
+        rp, vp, _ = O.region_frame(prv, (pb[j], pb[j + 1]), cp[0][j], cp[2][j], H)
+        rc, vc, _ = O.region_frame(cur, (cb[j], cb[j + 1]), cc[0][j], cc[2][j], H)
+        d = O.compare_radial_velocities(cur['ids'][cb[j]:cb[j + 1]], prv['ids'][pb[j]:pb[j + 1]],
+                                        vc, vp, rc, rp, mode)
+        _, aa = O.calc_angles(cb[j + 1] - cb[j], ang[pb[j]:pb[j + 1]], d)
+        ids.append(d['apsis_ids'])
+        angs.append(aa)
+        lens.append(len(d['apsis_ids']))
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    g_off = np.asarray(group['region_offsets'])
+    assert np.array_equal(g_off[:k + 1], offs), 'per-halo offsets'
+    tag = mode[:-3] + 'er_IDs'
+    assert np.array_equal(np.asarray(group[tag])[:offs[-1]], np.concatenate(ids)), 'apsis IDs'
+    a = np.asarray(group['angles'])[:offs[-1]].astype(np.float64)
+    b = np.concatenate(angs).astype(np.float64)
+    same = (a == b) | (np.isnan(a) & np.isnan(b))
+    ulp = np.spacing(np.maximum(np.abs(a), np.abs(b)).astype(np.float16)).astype(np.float64)
+    assert np.all(same | (np.abs(a - b) <= ulp)), 'apsis angle off by more than 1 f16 ulp'
+    assert mismatch_ok(int((~same).sum()), a.size), (int((~same).sum()), a.size)
+    ANGLE_TALLY['angles'] += int(a.size)
+    ANGLE_TALLY['mismatch'] += int((~same).sum())
+    return a.size
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize('contract', ['whole', 'presharded'])
 def test_configs3_sharded_engine_world2(contract):
     """configs[3]: 1e8 particles in total over two ranks (ID ranges), 1e4 halos, f32,
-    three snapshots; rank 0's savefile equals the single-process run's."""
+    three snapshots; rank 0's savefile equals the single-process run's (sha256 of every
+    dataset and the checkpoint), and that run's first 120 halos equal the oracle's."""
     import torch
     from orbitanalysis_amd.engine import OrbitEngine
     from orbitanalysis_amd.savefile import MemorySavefile
@@ -216,4 +262,6 @@ def test_configs3_sharded_engine_world2(contract):
         assert len(g['pericenter_IDs']) > 1e6
         check_apsis_in_prev_blocks(u.snaps[s - 1], u.n_halos, g['region_offsets'],
                                    g['pericenter_IDs'])
+    # oracle contact (the digests above tie the sharded run to this one)
+    assert _oracle_pair(u, 1, 120, want.groups['snapshot_001']) > 0
     torch.cuda.empty_cache()

@@ -18,7 +18,7 @@ BATCH = ['g1_config1', 'g2_overlap_birth_massarray', 'g3_apo_periodic',
 # fraction of f16 angles allowed to differ by 1 f16 ulp, rounded up to whole angles
 # (observed over the whole suite: 5 of 509,958, ~1e-5; profiles/r02/angle_mismatch_r02t.json)
 ANGLE_MISMATCH_MAX = 1e-4
-from golden_util import ANGLE_TALLY   # noqa: E402  (session total, printed by conftest)
+from golden_util import ANGLE_TALLY, check_changes   # noqa: E402  (tallies printed by conftest)
 
 
 def mismatch_ok(mismatch, total):
@@ -431,11 +431,8 @@ def test_onthefly_matches_reference_golden(name, mode):
         v = np.asarray(data[k])
         assert v.dtype == w.dtype and v.shape == w.shape, (k, v.dtype, w.dtype, v.shape, w.shape)
         if k == 'angles':
-            nan = np.isnan(w)
-            assert np.array_equal(np.isnan(v), nan), k
-            cd = np.dtype(meta['gen'].get('dtype', 'float64'))    # arccos computed in
-            ulp = np.spacing(np.abs(w[~nan]).astype(cd)).astype(np.float64)   # r̂'s dtype
-            assert np.all(np.abs(v[~nan].astype(np.float64) - w[~nan]) <= 2 * ulp), k
+            # arccos computed in r̂'s dtype (the coordinates')
+            check_changes(v, w, meta['gen'].get('dtype', 'float64'), (name, mode, k))
         elif w.dtype.kind == 'f':
             assert np.array_equal(v, w, equal_nan=True), k
         else:
@@ -476,10 +473,7 @@ def test_module_functions_match_reference_golden():
                 val = np.asarray(val)
                 if k == 'angle_changes':
                     assert val.dtype == w.dtype and val.shape == w.shape
-                    nan = np.isnan(w)
-                    assert np.array_equal(np.isnan(val), nan)
-                    ulp = np.spacing(np.abs(w[~nan])).astype(np.float64)
-                    assert np.all(np.abs(val[~nan].astype(np.float64) - w[~nan]) <= 2 * ulp), key
+                    check_changes(val, w, w.dtype, key)
                 else:
                     assert np.array_equal(val.astype(w.dtype), w), (key, k)
             # calc_angles on the reference's own compare output: exact (pure f16 rounding)
@@ -621,4 +615,45 @@ def test_direct_records_match_compaction(kw, hmax, mode, monkeypatch):
                                   np.asarray(w).view(np.uint8)), (g, k)
     rep = {}
     compare_groups(d.groups, _oracle_run(PlummerSnapshots(**kw), mode), rep)
+    assert rep['angles'] > 0
+
+
+@pytest.mark.parametrize('what', ['rhat', 'ids', 'uids'])
+def test_dtype_widened_between_snapshots(what):
+    """A loader whose snapshots switch to a wider dtype mid-run (float32 -> float64
+    coordinates and centres, or int32 / uint32 -> int64 IDs): the compare runs in the
+    promoted dtype as NumPy's does (the previous state is widened exactly), the apsis
+    IDs keep the previous snapshot's dtype, and every group equals the oracle's.
+    Large halos included (30000 particles: the partitioned path, whose bucket sets are
+    not inherited across the switch)."""
+    from orbitanalysis_amd.synthetic import PlummerSnapshots
+    kw = dict(n_halos=4, n_per_halo=[30000, 3000, 8000, 2000], n_snapshots=5, seed=71,
+              dtype=np.float32, centre_dtype=np.float32, box_size=120.0)
+    if what == 'ids':
+        kw['id_dtype'] = np.int32
+    elif what == 'uids':
+        kw['id_dtype'] = np.uint32
+        kw['id_offset'] = 2 ** 31 + 11
+    u = PlummerSnapshots(**kw)
+    orig_load, orig_regions = u.load_snapshot_data, u.regions
+
+    def load(s, pos, rad):
+        d = dict(orig_load(s, pos, rad))
+        if s >= 2:
+            if what == 'rhat':
+                for k in ('coordinates', 'velocities'):
+                    d[k] = np.asarray(d[k], dtype=np.float64)
+            else:
+                d['ids'] = np.asarray(d['ids']).astype(np.int64)
+        return d
+
+    def regions(s, hid):
+        c, r, b = orig_regions(s, hid)
+        if s >= 2 and what == 'rhat':
+            c = np.asarray(c, dtype=np.float64)
+        return c, r, b
+    u.load_snapshot_data, u.regions = load, regions
+    rep = {}
+    got = run_driver(u, dict(mode='pericentric', checkpoint=True))
+    compare_groups(got.groups, _oracle_run(u, 'pericentric'), rep)
     assert rep['angles'] > 0
