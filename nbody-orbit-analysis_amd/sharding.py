@@ -40,6 +40,8 @@ import hashlib
 from dataclasses import dataclass
 from typing import Optional
 
+from contextlib import nullcontext as _nullcontext
+
 import numpy as np
 import torch
 
@@ -238,6 +240,18 @@ class RowExchange:
         return out.to(dt).to(home)
 
 
+def _exchange_rows(t, group=None):
+    """Equal-split all-to-all of a (world, ...) tensor: rank d receives row d of every
+    rank, in rank order (on t's device)."""
+    import torch.distributed as dist
+    home = t.device
+    dev = _comm_device()
+    x = t.contiguous().to(dev)
+    out = torch.empty_like(x)
+    dist.all_to_all_single(out, x, group=group)
+    return out.to(home)
+
+
 def gather_rows(group, root, *tensors):
     """Gather the rows of each tensor (same row count) to ``root``, rank-ordered; the
     other ranks get empty tensors.  One count exchange + one collective per tensor."""
@@ -387,23 +401,36 @@ def stripe_shard(snapshot, starts, owner, group, device, bulk_fn=None, n=None):
         bulk = gather_bulk(rows, h0, nh, group) if world > 1 else \
             (np.asarray(rows) if rows is not None else np.zeros((0, 3)))
     owner.fit_group(st['ids'], group)
+    st_t = torch.from_numpy(starts).to(device)
+    nst = int(st['ids'].shape[0])
+    # every stripe row's block: the stripe holds blocks [h0, h1) (host layout)
+    sc = (np.append(starts[h0 + 1:h1], hi) - starts[h0:h1]) if h1 > h0 else np.zeros(0, np.int64)
+    sblock = torch.repeat_interleave(torch.arange(h0, h1, device=device),
+                                     torch.from_numpy(sc.astype(np.int64)).to(device),
+                                     output_size=nst) if nst else \
+        torch.zeros(0, dtype=torch.int64, device=device)
     if world > 1:
         dest = owner.ranks(st['ids'], world)
         dest, perm = torch.sort(dest, stable=True)
-        cnt = torch.bincount(dest, minlength=world).cpu().tolist()
-        rx = RowExchange(cnt, group)
+        # rows per (destination, block): one D2H; the row counts of the exchange and,
+        # after it, the shard's per-block counts follow from it and its exchange
+        hist = torch.bincount(dest * max(nh, 1) + sblock[perm], minlength=world * max(nh, 1))
+        hist = hist.view(world, max(nh, 1))
+        rx = RowExchange(hist.sum(1).cpu().tolist(), group)
         sel = rx.move(perm + lo)
         sh = {k: rx.move(v[perm]) for k, v in st.items()}
+        got = _exchange_rows(hist, group)       # row d of every sender: (world, nh)
+        counts = got.sum(0).cpu().numpy().astype(np.int64)[:nh] if nh else np.zeros(0, np.int64)
+        block = torch.repeat_interleave(torch.arange(nh, device=device),
+                                        torch.from_numpy(counts).to(device),
+                                        output_size=int(counts.sum())) if nh else sel
     else:
         sel = torch.arange(lo, hi, dtype=torch.int64, device=device)
         sh = st
-    st_t = torch.from_numpy(starts).to(device)
-    if nh:
-        block = torch.searchsorted(st_t, sel, right=True) - 1
-        counts = torch.bincount(block, minlength=nh).cpu().numpy().astype(np.int64)
-        gpos = sel - st_t[block]
-    else:
-        counts, gpos = np.zeros(0, np.int64), sel
+        counts = np.zeros(nh, np.int64)
+        counts[h0:h1] = sc
+        block = sblock
+    gpos = sel - st_t[block] if nh else sel
     shard = dict(snapshot)
     shard.update(sh)
     shard['region_offsets'] = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64) \
@@ -419,6 +446,27 @@ class ShardedResult:
     records: Optional[tuple] = None          # device (offsets, ids, f16 bits, prev-state row)
     gpos_prev: Optional[torch.Tensor] = None # previous shard row -> global block position
     bulk: Optional[np.ndarray] = None
+    lp: object = None                        # the local step (deferred: settled later)
+
+
+class ShardedFetch:
+    """A sharded step's records on their way to rank 0 and its host (fetch_async)."""
+
+    def __init__(self, done, n_slots, h_cnt, h_ids, h_ang, ids_dtype, root):
+        self.done, self.n_slots, self.root = done, n_slots, root
+        self.h_cnt, self.h_ids, self.h_ang, self.ids_dtype = h_cnt, h_ids, h_ang, ids_dtype
+
+    def wait(self):
+        dt = np.dtype(self.ids_dtype)
+        if not self.root:
+            return np.zeros(self.n_slots + 1, np.int64), np.zeros(0, dt), np.zeros(0, np.float16)
+        if self.done is not None:
+            self.done.synchronize()
+        cnt = self.h_cnt.numpy()
+        offsets = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+        h = self.h_ids.numpy()
+        ids_h = h.view(np.uint64).astype(dt) if dt.kind == 'u' else h.astype(dt)
+        return offsets, ids_h, self.h_ang.numpy().astype(np.uint16).view(np.float16)
 
 
 @dataclass
@@ -437,6 +485,7 @@ class ShardedPrep:
     lp: object = None
     layout: Optional[str] = None            # checkpoint row layout (presharded runs)
     h2d_bytes: int = 0
+    local_args: tuple = ()                  # the local engine's prepare arguments
 
 
 class _Plan:
@@ -476,8 +525,11 @@ class ShardedEngine:
         self.share_catalogue = bool(share_catalogue)
         self.device = getattr(local, 'device', torch.device('cpu'))
         self.prev: Optional[ShardedPrep] = None
+        self._pending: Optional[ShardedResult] = None   # a deferred step not yet settled
+        self._side = None                               # stream of the records' gathers
 
     def reset(self):
+        self.settle()
         self.prev = None
         self.owner.reset()
         self.local.reset()
@@ -502,21 +554,30 @@ class ShardedEngine:
         """Global block = the ranks' blocks concatenated in rank order: a shard row's
         position is the rows of lower ranks in its block + its own index.  Returns the
         block positions, the global snapshot rows, the global row count and the row
-        layout tag of a checkpoint written in this layout."""
-        cnt_all = allgather_v(torch.from_numpy(counts.astype(np.int64))[None, :], self.group)
-        before = cnt_all[:self.rank].sum(0).to(self.device) if self.rank else \
-            torch.zeros(len(counts), dtype=torch.int64, device=self.device)
-        tot = cnt_all.sum(0).to(self.device)
-        gstart = torch.cumsum(tot, 0) - tot
-        c = torch.from_numpy(counts).to(self.device)
-        block = torch.repeat_interleave(torch.arange(len(counts), device=self.device), c)
-        local = torch.arange(int(c.sum()), device=self.device) - \
-            torch.from_numpy(starts).to(self.device)[block]
-        gpos = before[block] + local
-        digest = hashlib.sha256(np.ascontiguousarray(cnt_all.cpu().numpy(), dtype='<i8')
-                                .tobytes()).hexdigest()[:16]
+        layout tag of a checkpoint written in this layout.  One all-gather of the ranks'
+        per-block counts (host arithmetic on them), then two device expansions with a
+        known output size: no other host round trip."""
+        import torch.distributed as dist
+        nh = len(counts)
+        dev = _comm_device()
+        mine = torch.from_numpy(np.ascontiguousarray(counts, dtype=np.int64)).to(dev)
+        allc = torch.empty(self.world * nh, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(allc, mine, group=self.group)
+        cnt_all = allc.cpu().numpy().reshape(self.world, nh)
+        before = cnt_all[:self.rank].sum(0)
+        tot = cnt_all.sum(0)
+        gstart = np.cumsum(tot) - tot
+        n = int(np.sum(counts))
+        c = torch.from_numpy(np.ascontiguousarray(counts, dtype=np.int64)).to(self.device)
+        row = torch.arange(n, dtype=torch.int64, device=self.device)
+        # gpos = before[block] + (row - starts[block]); sel = gstart[block] + gpos
+        b0 = torch.from_numpy(before - starts).to(self.device)
+        gpos = torch.repeat_interleave(b0, c, output_size=n) + row
+        sel = torch.repeat_interleave(torch.from_numpy(gstart).to(self.device), c,
+                                      output_size=n) + gpos
+        digest = hashlib.sha256(np.ascontiguousarray(cnt_all, dtype='<i8').tobytes()).hexdigest()[:16]
         layout = 'rank-major/world=%d/blocks=%s' % (self.world, digest)
-        return gpos, gstart[block] + gpos, int(tot.sum()), layout
+        return gpos, sel, int(tot.sum()), layout
 
     # ---------------------------------------------------------------- step
     def prepare(self, snapshot, centres, bulk_cat, H, z, exists, compare, angles_in=None,
@@ -571,20 +632,31 @@ class ShardedEngine:
                          rows=rows, bulk_out=None if bulk_cat is not None else bulk,
                          plan=_Plan(ids_dt, None if bulk is None else np.asarray(bulk).dtype),
                          layout=layout, h2d_bytes=h2d)
-        sp.lp = self.local.prepare(shard, centres, bulk, H, z, exists, compare, a_in,
-                                   None if (prev is None or p is None) else p.lp,
-                                   share=bulk_cat is not None)
+        sp.local_args = (shard, centres, bulk, H, z, exists, compare, a_in, bulk_cat is not None)
+        sp.lp = self._local_prepare(sp, None if (prev is None or p is None) else p.lp)
         return sp
 
-    def launch(self, sp, prev=None, step_events=None, check=True):
+    def _local_prepare(self, sp, prev_lp):
+        """The local engine's host half of a prepared step (no collective: a rank that
+        re-ran its previous step plans again on its own)."""
+        a = sp.local_args
+        return self.local.prepare(*a[:8], prev_lp, share=a[8])
+
+    def launch(self, sp, prev=None, step_events=None, check=True, defer=False):
         """Device half: the catalogue all-gather (written into the device halo table),
-        then the local step.  Records stay on the device (``fetch`` gathers them)."""
+        then the local step.  Records stay on the device (``fetch`` gathers them).
+        ``defer``: the local step's status is checked by ``settle`` (local engines that
+        support it), so the host can plan the next snapshot meanwhile."""
         p = prev if prev is not None else self.prev
         nh = len(sp.exists)
         if sp.rows is not None:
             self.local.set_catalogue(sp.lp, self._exchange(sp.rows, nh))
-        out = self.local.launch(sp.lp, None if prev is None else prev.lp, step_events, check)
-        res = ShardedResult(n_slots=0, has_prog=np.zeros(nh, dtype=bool), bulk=sp.bulk_out)
+        kw = {}
+        if defer and getattr(self.local, 'deferrable', False):
+            kw['defer'] = True
+        out = self.local.launch(sp.lp, None if p is None else p.lp, step_events, check, **kw)
+        res = ShardedResult(n_slots=0, has_prog=np.zeros(nh, dtype=bool), bulk=sp.bulk_out,
+                            lp=sp.lp)
         if sp.compare:
             has_prog = np.isin(sp.exists, p.exists)
             res.has_prog, res.n_slots = has_prog, int(has_prog.sum())
@@ -592,40 +664,100 @@ class ShardedEngine:
         return res
 
     def step(self, snapshot, centres, bulk_cat, H, z, exists, compare, angles_in=None,
-             angles_layout=None):
+             angles_layout=None, defer=False):
+        """One snapshot on every rank.  ``defer`` (track_orbits' pipelined driver): the
+        host half of this snapshot (shard, plan) runs while the previous step's kernels
+        run; that step is settled (re-run on an LDS overflow, locally) before this one
+        launches, and this one returns without waiting for its kernels."""
         if compare and self.prev is None:
             raise RuntimeError('compare step without a previous snapshot')
         sp = self.prepare(snapshot, centres, bulk_cat, H, z, exists, compare, angles_in,
                           angles_layout=angles_layout)
-        res = self.launch(sp)
+        if self._pending is not None and self.settle(self._pending) and compare:
+            # this rank's previous step was re-planned: plan this one again locally on
+            # its new layout (the shard and the collectives stand)
+            sp.lp = self._local_prepare(sp, self.prev.lp)
+        res = self.launch(sp, defer=defer)
+        if defer and compare and getattr(self.local, 'deferrable', False):
+            self._pending = res
         self.prev = sp
         return res
 
+    def settle(self, res=None):
+        """Wait for a deferred step (default: the pending one) and re-run it locally if
+        its kernels asked for a re-plan.  True when it was re-run."""
+        res = self._pending if res is None else res
+        if res is None or res.lp is None or not hasattr(res.lp, 'pending'):
+            if res is not None and res is self._pending:
+                self._pending = None
+            return False
+        if res is self._pending:
+            self._pending = None
+        out = self.local.settle(res.lp)
+        if out is None:
+            return False
+        res.records = out
+        return True
+
+    def step_ready(self, res):
+        f = getattr(self.local, 'ready', None)
+        return True if f is None or res.lp is None else f(res.lp)
+
     # ---------------------------------------------------------------- outputs
-    def fetch(self, res, ids_dtype):
-        """Gather every rank's records to rank 0 and put them in the reference's order:
-        key = halo slot << 32 | position in the global previous block.  Ranks other
-        than 0 (which write nothing) get zero offsets and no records."""
+    def fetch_async(self, res, ids_dtype):
+        """Start gathering a step's records to rank 0 (the only writer) and their D2H
+        there; ``wait()`` returns (offsets, IDs, f16 angles) in the reference's order:
+        key = halo slot << 32 | position in the global previous block (track_orbits.py:
+        199-227, 315-316).  The gather runs on a side stream behind the step's own
+        kernels only, so it overlaps whatever the compute stream runs next (the next
+        snapshot's step); the workspace holding the records is not reused before it.
+        Ranks other than 0 (which write nothing) get zero offsets and no records."""
+        self.settle(res)
         offs, a_ids, a_ang, a_pos = res.records
-        total = int(offs[-1])
-        slot = torch.repeat_interleave(torch.arange(res.n_slots, device=offs.device),
-                                       (offs[1:] - offs[:-1]).long())
-        g = res.gpos_prev[a_pos[:total].to(res.gpos_prev.device).long()]
-        rec = torch.stack([(slot.to(g.device) << 32) | g, _as_i64(a_ids[:total]).to(g.device),
-                           a_ang[:total].to(torch.int64).to(g.device)], dim=1)
-        rec, = gather_rows(self.group, self.ROOT, rec)
-        dt = np.dtype(ids_dtype)
-        if self.rank != self.ROOT:
-            return (np.zeros(res.n_slots + 1, np.int64), np.zeros(0, dt),
-                    np.zeros(0, np.float16))
-        order = torch.argsort(rec[:, 0])
-        rec = rec[order]
-        cnt = torch.bincount((rec[:, 0] >> 32).long(), minlength=res.n_slots)[:res.n_slots] \
-            if rec.shape[0] else torch.zeros(res.n_slots, dtype=torch.int64)
-        offsets = np.concatenate([[0], np.cumsum(cnt.cpu().numpy())]).astype(np.int64)
-        h = rec[:, 1:].cpu().numpy()
-        ids_h = h[:, 0].view(np.uint64).astype(dt) if dt.kind == 'u' else h[:, 0].astype(dt)
-        return offsets, ids_h, h[:, 1].astype(np.uint16).view(np.float16)
+        lp = res.lp
+        done = self.local.done_event(lp) if hasattr(self.local, 'done_event') else None
+        dev = offs.device
+        side = None
+        if dev.type == 'cuda':
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=dev)
+            side = self._side
+        ctx = torch.cuda.stream(side) if side is not None else _nullcontext()
+        with ctx:
+            if side is not None and done is not None:
+                side.wait_event(done)
+            total = self.local.total(lp) if hasattr(self.local, 'total') else int(offs[-1])
+            slot = torch.repeat_interleave(torch.arange(res.n_slots, device=dev),
+                                           (offs[1:] - offs[:-1]).long(), output_size=total)
+            g = res.gpos_prev[a_pos[:total].to(res.gpos_prev.device).long()]
+            rec = torch.stack([(slot.to(g.device) << 32) | g, _as_i64(a_ids[:total]).to(g.device),
+                               a_ang[:total].to(torch.int64).to(g.device)], dim=1)
+            rec, = gather_rows(self.group, self.ROOT, rec)
+            ev = None
+            h_cnt = h_ids = h_ang = None
+            if self.rank == self.ROOT:
+                order = torch.argsort(rec[:, 0])
+                rec = rec[order]
+                cnt = torch.bincount((rec[:, 0] >> 32).long(), minlength=res.n_slots)[:res.n_slots] \
+                    if rec.shape[0] else torch.zeros(res.n_slots, dtype=torch.int64, device=rec.device)
+                pin = rec.device.type == 'cuda'
+                h_cnt = torch.empty(cnt.shape, dtype=torch.int64, pin_memory=pin)
+                h_ids = torch.empty(rec.shape[0], dtype=torch.int64, pin_memory=pin)
+                h_ang = torch.empty(rec.shape[0], dtype=torch.int64, pin_memory=pin)
+                h_cnt.copy_(cnt, non_blocking=pin)
+                h_ids.copy_(rec[:, 1], non_blocking=pin)
+                h_ang.copy_(rec[:, 2], non_blocking=pin)
+            if side is not None:
+                ev = torch.cuda.Event()
+                ev.record(side)
+                if hasattr(self.local, 'records_consumed'):
+                    self.local.records_consumed(lp, ev)
+        return ShardedFetch(ev, res.n_slots, h_cnt, h_ids, h_ang, ids_dtype,
+                            self.rank == self.ROOT)
+
+    def fetch(self, res, ids_dtype):
+        """``fetch_async(...).wait()``: the records in the reference's order on rank 0."""
+        return self.fetch_async(res, ids_dtype).wait()
 
     def bulk_velocities(self, res, plan):
         return res.bulk
@@ -633,6 +765,7 @@ class ShardedEngine:
     def angles(self):
         """Global float16 angle state in current-snapshot order (checkpoint payload),
         gathered to rank 0; None on the other ranks."""
+        self.settle()
         p = self.prev
         loc = self.local.angles_tensor().to(torch.int64)
         rows = torch.stack([p.sel.to(loc.device), loc], dim=1) if loc.numel() else \
@@ -682,41 +815,116 @@ class EngineLocal:
         hi = 10 if lp.share_bulk else 7
         hv[:, 4:hi] = rows[:, :hi - 4].to(hv.device, non_blocking=True)
 
-    def launch(self, lp, prev_lp, step_events=None, check=True):
-        from .engine import SnapshotState, retry_plan
+    deferrable = True                  # launch(defer=True) + settle (ShardedEngine.step)
+
+    def _prev_state(self, lp, prev_lp):
+        from .engine import SnapshotState
+        if not (lp.compare and prev_lp is not None):
+            return None
+        return SnapshotState(ids=prev_lp.snap['ids'], rhat=prev_lp.rhat, meta=prev_lp.meta,
+                             starts=prev_lp.starts, counts=prev_lp.counts,
+                             exists=prev_lp.exists, plan=prev_lp.plan,
+                             buckets=prev_lp.buckets)
+
+    def _set_prev(self, lp):
+        from .engine import SnapshotState
+        self.engine.prev = SnapshotState(ids=lp.snap['ids'], rhat=lp.rhat, meta=lp.meta,
+                                         starts=lp.starts, counts=lp.counts, exists=lp.exists,
+                                         plan=lp.plan, buckets=lp.buckets)
+
+    def _replan(self, lp, st):
+        """The step re-planned after status ``st`` (smaller items / large halos on the
+        global-table path), in place; the exchanged catalogue rows are kept."""
+        from .engine import retry_plan
         eng = self.engine
+        eng.note_status(st)
+        entries, part = retry_plan(lp, st)
+        shard, centres, bulk, H, z, exists, compare, angles_in, layout = lp.src
+        hv = lp.halos.view(torch.float64).view(-1, 12)[:, 4:10].clone()
+        lp2 = eng.prepare(shard, centres, bulk, H, z, exists, compare, angles_in=angles_in,
+                          plan_src=shard, prev_layout=layout, entries=entries, part=part)
+        lp2.halos.view(torch.float64).view(-1, 12)[:, 4:10] = hv
+        lp2.exists, lp2.src, lp2.share_bulk = lp.exists, lp.src, lp.share_bulk
+        lp2.ws_idx = getattr(lp, 'ws_idx', eng._wsi)
+        lp.__dict__.update(lp2.__dict__)
+
+    def launch(self, lp, prev_lp, step_events=None, check=True, defer=False):
+        """The local step.  A compare step writes one of the engine's two workspaces
+        (alternating, so the previous step's records can still be on their way to rank
+        0); ``defer``: return without reading the status word -- it is copied to host
+        memory behind an event and ``settle`` checks it (and re-runs) before the next
+        launch.  Returns (offsets, IDs, f16 bits, previous-state rows) on the device."""
+        eng = self.engine
+        if lp.compare and not hasattr(lp, 'ws_idx'):
+            lp.ws_idx = eng._wsi
+            eng._wsi ^= 1
         for _ in range(10):
-            ws = eng.workspace(lp) if lp.compare else None
-            prev = None
-            if lp.compare and prev_lp is not None:
-                prev = SnapshotState(ids=prev_lp.snap['ids'], rhat=prev_lp.rhat, meta=prev_lp.meta,
-                                     starts=prev_lp.starts, counts=prev_lp.counts,
-                                     exists=prev_lp.exists, plan=prev_lp.plan,
-                                     buckets=prev_lp.buckets)
-            if check and ws is not None:
+            ws = eng.workspace(lp, lp.ws_idx) if lp.compare else None
+            if ws is not None:
+                if ws.copy_done is not None:
+                    # the last records of this workspace may still be gathered / copied
+                    torch.cuda.current_stream(eng.device).wait_event(ws.copy_done)
+                    ws.copy_done = None
                 ws.status.zero_()
-            res = eng.launch(lp, ws, prev=prev, step_events=step_events)
-            st = int(ws.status[0].item()) if (check and ws is not None) else 0
+            res = eng.launch(lp, ws, prev=self._prev_state(lp, prev_lp), step_events=step_events)
+            lp.res = res
+            if ws is not None:
+                ws.h_status.copy_(ws.status, non_blocking=True)
+                ws.h_total.copy_(ws.total, non_blocking=True)
+                res.done = torch.cuda.Event()
+                res.done.record(torch.cuda.current_stream(eng.device))
+            if ws is None or not check:
+                break
+            if defer:
+                lp.pending = prev_lp
+                break
+            res.done.synchronize()
+            st = int(ws.h_status[0])
             if not st:
                 break
-            # re-plan: smaller items / large halos on the global-table path
-            eng.note_status(st)
-            entries, part = retry_plan(lp, st)
-            shard, centres, bulk, H, z, exists, compare, angles_in, layout = lp.src
-            hv = lp.halos.view(torch.float64).view(-1, 12)[:, 4:10].clone()
-            lp2 = eng.prepare(shard, centres, bulk, H, z, exists, compare, angles_in=angles_in,
-                              plan_src=shard, prev_layout=layout, entries=entries, part=part)
-            lp2.halos.view(torch.float64).view(-1, 12)[:, 4:10] = hv
-            lp2.exists, lp2.src, lp2.share_bulk = lp.exists, lp.src, lp.share_bulk
-            lp.__dict__.update(lp2.__dict__)
+            self._replan(lp, st)
         else:
             raise RuntimeError('LDS hash tables kept overflowing')
-        eng.prev = SnapshotState(ids=lp.snap['ids'], rhat=lp.rhat, meta=lp.meta, starts=lp.starts,
-                                 counts=lp.counts, exists=lp.exists, plan=lp.plan,
-                                 buckets=lp.buckets)
+        self._set_prev(lp)
         if not lp.compare:
             return None
         return res.offsets, res.apsis_ids, res.apsis_ang, res.apsis_pos
+
+    def settle(self, lp):
+        """Wait for a deferred step; re-run it if its kernels asked for a re-plan.
+        Returns the new device records when it was re-run, else None."""
+        prev_lp = getattr(lp, 'pending', None)
+        if prev_lp is None and not hasattr(lp, 'pending'):
+            return None
+        del lp.pending
+        lp.res.done.synchronize()
+        st = int(lp.res.ws.h_status[0])
+        if not st:
+            return None
+        self._replan(lp, st)
+        return self.launch(lp, prev_lp, check=True)
+
+    def ready(self, lp):
+        """Without waiting: None while a deferred step runs, else whether its records
+        are final (False: it will be re-run)."""
+        if not hasattr(lp, 'pending'):
+            return True
+        if not lp.res.done.query():
+            return None
+        return not int(lp.res.ws.h_status[0])
+
+    def total(self, lp):
+        """The step's record count (host copy behind its event; settle first)."""
+        return int(lp.res.ws.h_total[0])
+
+    def done_event(self, lp):
+        return getattr(getattr(lp, 'res', None), 'done', None)
+
+    def records_consumed(self, lp, event):
+        """The records of ``lp``'s workspace are read once ``event`` completes."""
+        ws = getattr(getattr(lp, 'res', None), 'ws', None)
+        if ws is not None:
+            ws.copy_done = event
 
     def angles_tensor(self):
         """float16 bits of the current angle state (low half of the meta words)."""

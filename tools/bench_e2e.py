@@ -20,6 +20,15 @@ the status read, the D2H of the apsis CSR and the savefile write.  The per-phase
 host times are reported beside the wall time.
 
   python tools/bench_e2e.py [--particles 1e8] [--halos 10000] [--snapshots 6] [--device-loader]
+
+--sharded (under torch.distributed.run, one rank per GPU; --backend gloo rehearses
+several ranks on one GPU): the multi-GPU drop-in, track_orbits(..., engine=
+ShardedEngine(EngineLocal(OrbitEngine()))).  --contract presharded (default): each
+rank's loader returns its own ID range (--particles per rank, --scaling weak; or
+--particles in total, --scaling strong); --contract whole: every rank is handed the
+whole snapshot (device tensors) and the engine stripes + exchanges it.  Per-phase
+host times of the sharded engine (prepare = shard + plan, launch, settle, the records'
+gather to rank 0 and its wait) are reported per snapshot.
 """
 import argparse
 import json
@@ -49,16 +58,35 @@ def main():
     ap.add_argument('--mode', default='pericentric')
     ap.add_argument('--device-loader', action='store_true',
                     help='the loader returns device tensors (no H2D)')
+    ap.add_argument('--sharded', action='store_true', help='ShardedEngine over the ranks')
+    ap.add_argument('--contract', default='presharded', choices=['presharded', 'whole'])
+    ap.add_argument('--scaling', default='weak', choices=['weak', 'strong'])
+    ap.add_argument('--backend', default='nccl')
     args = ap.parse_args()
     import torch
     import orbitanalysis_amd  # noqa: F401
     from orbitanalysis_amd.synthetic_device import DevicePlummer
     from orbitanalysis_amd.track_orbits import track_orbits
     from orbitanalysis_amd.savefile import MemorySavefile
-    dev = torch.device('cuda', 0)
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0')) % max(torch.cuda.device_count(), 1)
+    dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
-    gen = DevicePlummer(n_halos=args.halos, n_particles=int(args.particles), seed=0,
-                        device=dev)
+    if args.sharded:
+        import torch.distributed as dist
+        if args.backend == 'gloo':
+            dist.init_process_group('gloo')
+        else:
+            dist.init_process_group('nccl', device_id=dev)
+        args.device_loader = True
+    per_rank = int(args.particles) if (args.scaling == 'weak' or not args.sharded) else \
+        int(args.particles) // world
+    if args.sharded and args.contract == 'presharded':
+        gen = DevicePlummer(n_halos=args.halos, n_particles=per_rank, seed=0, rank=rank,
+                            world=world, device=dev)
+    else:
+        gen = DevicePlummer(n_halos=args.halos, n_particles=per_rank, seed=0, device=dev)
     S = args.distinct
     host, cats = [], []
     t0 = time.perf_counter()
@@ -77,6 +105,9 @@ def main():
     from orbitanalysis_amd.engine import OrbitEngine
     phase = {'prepare': [], 'launch': [], 'settle': [], 'fetch': [], 'fetch_async': [],
              'wait': [], 'save': []}
+    if args.sharded:
+        phase.update({'shard_prepare': [], 'shard_settle': [], 'shard_fetch_async': [],
+                      'shard_wait': []})
 
     def timed(name, fn):
         def w(*a, **k):
@@ -104,6 +135,22 @@ def main():
     OrbitEngine.settle = settle
     E.PendingFetch.wait = timed('wait', E.PendingFetch.wait)
     TO.save_to_file = timed('save', TO.save_to_file)
+    engine = None
+    if args.sharded:
+        from orbitanalysis_amd import sharding as SH
+        SH.ShardedEngine.prepare = timed('shard_prepare', SH.ShardedEngine.prepare)
+        SH.ShardedEngine.fetch_async = timed('shard_fetch_async', SH.ShardedEngine.fetch_async)
+        SH.ShardedFetch.wait = timed('shard_wait', SH.ShardedFetch.wait)
+        _ssettle = SH.EngineLocal.settle
+
+        def ssettle(self, lp):
+            t = time.perf_counter()
+            out = _ssettle(self, lp)
+            phase['shard_settle'].append(time.perf_counter() - t)
+            return out
+        SH.EngineLocal.settle = ssettle
+        engine = SH.ShardedEngine(SH.EngineLocal(OrbitEngine(mode=args.mode, device=dev)),
+                                  presharded=args.contract == 'presharded')
     log('setup %.1f s: %d host snapshots of %s particles' % (
         time.perf_counter() - t0, S, [len(h['ids']) for h in host]))
 
@@ -129,8 +176,10 @@ def main():
     sink = CountingSink()
     branches = np.tile(np.arange(args.halos), (n, 1))
     t_start = time.perf_counter()
+    if args.sharded:
+        dist.barrier()
     track_orbits(np.arange(n), branches, regions, load_snapshot_data, sink, mode=args.mode,
-                 verbose=False)
+                 verbose=False, engine=engine)
     torch.cuda.synchronize()
     t_end = time.perf_counter()
     # timed: snapshots W .. n-1 (from the loader call of snapshot W to the end)
@@ -138,6 +187,16 @@ def main():
     timed = list(range(W, n))
     wall = t_end - stamps[W]
     units = sum(len(host[s % S]['ids']) for s in timed)
+    if args.sharded:
+        # whole-job rate: the slowest rank's wall, the units of every rank
+        t = torch.tensor([wall, float(units if args.contract == 'presharded' or rank == 0 else 0)],
+                         dtype=torch.float64, device=dev if args.backend != 'gloo' else 'cpu')
+        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        wall, units = float(t[0]), float(t[1])
+        if rank != 0:
+            dist.destroy_process_group()
+            return
     n_apsis = sum(g['pericenter_IDs' if args.mode == 'pericentric' else 'apocenter_IDs']
                   for g in sink.groups.values())
     per = [stamps[s + 1] - stamps[s] for s in range(W, n - 1)] + [t_end - stamps[n - 1]]
@@ -145,13 +204,16 @@ def main():
     res = {
         'metric': 'particle-snapshots/s (track_orbits end to end, %s loader)'
                   % ('device-tensor' if args.device_loader else 'host NumPy'),
-        'value': units / wall, 'unit': 'particle-snapshots/s', 'n_gpus': 1,
+        'value': units / wall, 'unit': 'particle-snapshots/s', 'n_gpus': world,
         'steps': len(timed), 'warmup': W, 'ms_per_step': wall / len(timed) * 1e3,
         'higher_is_better': True, 'dtype': 'f32', 'data': 'synthetic Plummer spheres, %s' % (
                     'device tensors' if args.device_loader else 'host NumPy'),
         'config': {'workload': 'BASELINE configs[2] shape: %d particles/snapshot, %d halos, f32, '
                                'public track_orbits, in-memory savefile' % (units // len(timed),
-                                                                          args.halos)},
+                                                                          args.halos),
+                   'engine': ('ShardedEngine x%d (%s loader, %s scaling, %s)'
+                              % (world, args.contract, args.scaling, args.backend))
+                   if args.sharded else 'OrbitEngine'},
         'ms_per_snapshot': [round(p * 1e3, 2) for p in per],
         'ms_per_snapshot_median': round(float(np.median(per)) * 1e3, 3),
         'h2d_bytes_per_snapshot': 0.0 if args.device_loader else b,
@@ -162,6 +224,8 @@ def main():
         'total_wall_s': t_end - t_start,
     }
     print(json.dumps(res), flush=True)
+    if args.sharded:
+        dist.destroy_process_group()
 
 
 if __name__ == '__main__':

@@ -13,6 +13,7 @@
 #   pmc       FETCH_SIZE / WRITE_SIZE passes over k_step -> pmc_k_step_$TAG.json
 #   big       configs[1] (1e7 f64, 100 large halos) bench + rocprof
 #   e2e       tools/bench_e2e.py with a device loader and with a host loader
+#   e2es      tools/bench_e2e.py --sharded, world 2 over gloo (presharded, whole)
 #   otf       tools/bench_onthefly.py $OTF_ARGS (configs[4] one-GPU share)
 #   post      tools/bench_post.py (+ rocprof)
 #   b2        bench.py --gpus 2 over gloo on this one GPU ($B2_SCALING, default strong)
@@ -67,6 +68,15 @@ e2e)
     timeout -k 10 400 python tools/bench_e2e.py --snapshots ${E2E_SNAPS:-14} $m \
       > "$O/e2e_$T${m:+_dev}.json" 2> "$O/e2e_$T${m:+_dev}.err"
     rc=$?; cat "$O/e2e_$T${m:+_dev}.json"; ok $rc "e2e $m"
+  done ;;
+e2es)
+  # the sharded driver end to end: world-2 gloo rehearsal on this one GPU
+  for c in presharded whole; do
+    timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+      --master-addr 127.0.0.1 --master-port ${E2E_PORT:-29521} tools/bench_e2e.py --sharded \
+      --backend gloo --contract $c --scaling ${E2E_SCALING:-strong} --snapshots ${E2E_SNAPS:-12} \
+      > "$O/e2es_${c}_$T.json" 2> "$O/e2es_${c}_$T.err"
+    rc=$?; grep -v Warning "$O/e2es_${c}_$T.err" | tail -2; cat "$O/e2es_${c}_$T.json"; ok $rc "e2es $c"
   done ;;
 otf)
   timeout -k 10 600 python tools/bench_onthefly.py ${OTF_ARGS:-} > "$O/otf_$T.json" 2> "$O/otf_$T.err"
