@@ -114,9 +114,13 @@ class IdRangeOwner:
         import torch.distributed as dist
         if self.lo is not None:
             return
+        if dist.get_world_size(group) == 1:
+            return                              # one rank owns every ID: nothing to fit
         t = ids_t.to(torch.int64)
-        mn = int(t.min()) if t.numel() else _I64_MAX
-        mx = int(t.max()) if t.numel() else _I64_MIN + 1
+        if t.numel():
+            mn, mx = (int(x) for x in torch.stack([t.min(), t.max()]).cpu())   # one D2H
+        else:
+            mn, mx = _I64_MAX, _I64_MIN + 1
         if dist.get_world_size(group) > 1:
             r = torch.tensor([mn, -mx], dtype=torch.int64, device=_comm_device())
             dist.all_reduce(r, op=dist.ReduceOp.MIN, group=group)

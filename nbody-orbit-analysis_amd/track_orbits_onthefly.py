@@ -325,7 +325,7 @@ def _by_unique_key(v, g, n):
     return out
 
 
-def merge_onthefly(parts, nh, prev_starts, p_has, ids_dtype, n_prev=None):
+def merge_onthefly(parts, nh, prev_starts, p_has, ids_dtype, n_prev=None, ordered=False):
     """Merge the ranks' on-the-fly records of one snapshot pair on the root rank
     (ShardedOnTheFly), on whatever device the tensors are on.
 
@@ -340,19 +340,22 @@ def merge_onthefly(parts, nh, prev_starts, p_has, ids_dtype, n_prev=None):
     IDs are per-halo sorted unique (setdiff1d, :145, :168), except the entered IDs of a
     halo without a progenitor block, which keep loader order (:178), i.e. global
     current-row order.  ``n_prev``: the previous snapshot's row count (bounds the
-    global previous rows).  Returns host arrays (IDs in ``ids_dtype``)."""
+    global previous rows).  ``ordered``: one rank contributed every row, in order
+    (world 1): apsis records and angle changes need no sort (``angle_g`` may then be
+    None).  Returns host arrays (IDs in ``ids_dtype``)."""
     ap = parts['apsis']
     dev = ap.device
     out = {}
-    order = torch.argsort(ap[:, 0])
-    ap = ap[order]
+    if not ordered:
+        ap = ap[torch.argsort(ap[:, 0])]
     st = torch.from_numpy(np.asarray(prev_starts, dtype=np.int64)).to(dev)
     halo = torch.searchsorted(st, ap[:, 0].contiguous(), right=True) - 1 if len(st) else ap[:, 0]
     cnt = torch.bincount(halo, minlength=nh)[:nh] if ap.shape[0] else \
         torch.zeros(nh, dtype=torch.int64, device=dev)
     out['apsis_offsets'] = np.concatenate([[0], np.cumsum(cnt.cpu().numpy())]).astype(np.int64)
     out['apsis_ids'] = ids_to_host(ap[:, 1], ids_dtype)
-    out['angles'] = _pinned_host(_by_unique_key(parts['angle_v'], parts['angle_g'], n_prev))
+    out['angles'] = _pinned_host(parts['angle_v'] if ordered or parts['angle_g'] is None else
+                                 _by_unique_key(parts['angle_v'], parts['angle_g'], n_prev))
 
     def grouped(h, ids, second, uniq):
         o = _sort_pairs(h, second)
@@ -481,8 +484,11 @@ class ShardedOnTheFly:
         total = int(res.offsets[-1]) if res.offsets is not None and res.offsets.numel() else 0
         a_ids = _i64(res.apsis_ids[:total])
         apsis = torch.stack([sel_p[res.apsis_pos[:total].long()], a_ids], dim=1)
-        mrow = torch.nonzero(d.matched_prev).squeeze(1)
-        angle_g, angle_v = sel_p[mrow], d.angle_out[mrow]
+        # angle changes: at world 1 the matched rows are already in global previous-row
+        # order (the shard is the snapshot), so they need no row key
+        angle_v = d.angle_out[d.matched_prev]
+        angle_g = sel_p[torch.nonzero(d.matched_prev).squeeze(1)] if self.world > 1 else \
+            torch.zeros(0, dtype=torch.int64, device=eng.device)
         drow = torch.nonzero(~d.matched_prev).squeeze(1)
         departed = torch.stack([_halo_of(drow, prev.starts, eng.device),
                                 _i64(prev.ids[drow])], dim=1)
@@ -490,7 +496,8 @@ class ShardedOnTheFly:
         entered = torch.stack([_halo_of(erow, pc.starts, eng.device),
                                _i64(pc.snap['ids'][erow]), sel_c[erow]], dim=1)
         apsis, = gather_rows(self.group, self.ROOT, apsis)
-        angle_g, angle_v = gather_rows(self.group, self.ROOT, angle_g, angle_v)
+        if self.world > 1:
+            angle_g, angle_v = gather_rows(self.group, self.ROOT, angle_g, angle_v)
         departed, = gather_rows(self.group, self.ROOT, departed)
         entered, = gather_rows(self.group, self.ROOT, entered)
         sl1 = np.asarray(slices[1], dtype=np.int64).reshape(-1, 2)
@@ -498,10 +505,10 @@ class ShardedOnTheFly:
         adt = _angles_dtype(pc.plan.coord, ids_dtype, p_has)
         if self.rank == self.ROOT:
             n_prev = int(np.max(sl1[:, 1])) if len(sl1) else 0
-            merged = merge_onthefly(dict(apsis=apsis, angle_g=angle_g, angle_v=angle_v,
-                                         departed=departed, entered=entered), nh,
-                                    _block_starts(sl1, max(n_prev, 0)), p_has, ids_dtype,
-                                    n_prev=max(n_prev, 0))
+            merged = merge_onthefly(dict(apsis=apsis, angle_g=angle_g if self.world > 1 else None,
+                                         angle_v=angle_v, departed=departed, entered=entered),
+                                    nh, _block_starts(sl1, max(n_prev, 0)), p_has, ids_dtype,
+                                    n_prev=max(n_prev, 0), ordered=self.world == 1)
             merged['angles'] = merged['angles'].astype(adt, copy=False)
         else:
             z = np.zeros(nh + 1, np.int64)

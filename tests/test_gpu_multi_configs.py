@@ -5,7 +5,8 @@
   share (1.25e8 f32 particles, 12,500 halos) through ``ShardedOnTheFly`` at world 1,
   three chained calls with the frame state carried, checked by size-independent
   properties, against the oracle on a halo sample, and bit for bit against the
-  single-GPU on-the-fly path.
+  single-GPU on-the-fly path; and the same share over two ranks handed whole
+  snapshots (stripes, the owner all-to-all and the root's merge at size).
 * configs[3] -- 1e8 particles in total sharded by ID range: two ranks run
   ``ShardedEngine`` over 1e4 halos, three snapshots, with the reference's whole-snapshot
   loader (stripes + all-to-all) and with a presharded loader; rank 0's savefile
@@ -142,6 +143,90 @@ def test_configs4_onthefly_rank_share_world1():
     finally:
         T.clear_carry()
         dist.destroy_process_group()
+
+
+def _otf_digests(out, calls):
+    return {'%d/%s' % (s, k): v for s in calls
+            for k, v in digest({'f': out.files[s][0]}).items()}
+
+
+def _otf_world2_worker(rank, world, port, outdir):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from orbitanalysis_amd import track_orbits_onthefly as T
+        from orbitanalysis_amd.engine import OrbitEngine
+        from orbitanalysis_amd.savefile import MemorySavefile
+        nh = 12500
+        # the reference's loader contract: every rank is handed the whole snapshot
+        u = DeviceUniverse(4, n_halos=nh, n_particles=125_000_000, seed=19, dtype='float32')
+        links = np.tile(np.arange(nh), (2, 1))
+        eng = T.ShardedOnTheFly(OrbitEngine(mode='apocentric'))
+        out = MemorySavefile()
+        for s in (1, 2, 3):
+            T.track_orbits(s, links, u.regions_otf, u.load_snapshot_data, out, verbose=False,
+                           engine=eng, mode='apocentric')
+        if rank == 0:
+            d = _otf_digests(out, (1, 2, 3))
+            d['loads'] = u.loads
+            with open(os.path.join(outdir, 'otf.json'), 'w') as f:
+                json.dump(d, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_configs4_onthefly_world2_whole_snapshots():
+    """configs[4]'s stream over two ranks (gloo, one GPU): 1.25e8 f32 particles in
+    12,500 halos handed whole to every rank (stripe upload + owner all-to-all at size),
+    apocentric, three chained calls with the carry on: the ranks' records meet in the
+    root's merge (counting placement of the angle changes, sorted departed / entered
+    IDs); every file equals the single-GPU on-the-fly path's bit for bit, and that path's
+    first 40 halos of the last pair equal the oracle's."""
+    from oracle import orbit_oracle as O
+    from orbitanalysis_amd import track_orbits_onthefly as T
+    from orbitanalysis_amd.engine import OrbitEngine
+    from orbitanalysis_amd.savefile import MemorySavefile
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_otf_world2_worker, args=(world, _free_port(), d), nprocs=world,
+                           join=True, start_method='spawn')
+        with open(os.path.join(d, 'otf.json')) as f:
+            got = json.load(f)
+    assert got.pop('loads') == [1, 0, 2, 3]             # s - 1 carried on every rank
+    nh = 12500
+    T.clear_carry()
+    try:
+        u = DeviceUniverse(4, n_halos=nh, n_particles=125_000_000, seed=19, dtype='float32')
+        links = np.tile(np.arange(nh), (2, 1))
+        single = MemorySavefile()
+        eng = OrbitEngine(mode='apocentric')
+        for s in (1, 2, 3):
+            T.track_orbits(s, links, u.regions_otf, u.load_snapshot_data, single, verbose=False,
+                           engine=eng, mode='apocentric')
+        want = _otf_digests(single, (1, 2, 3))
+        assert sorted(got) == sorted(want)
+        bad = [k for k in want if got[k] != want[k]]
+        assert not bad, bad
+        ref = single.files[3][0]
+        assert len(ref['apocentrer_IDs']) > 1e6 and len(ref['entered_IDs']) > 1e4
+        check_onthefly_properties(u.snaps[2], u.snaps[3], nh, ref, tag='apocentrer')
+        k = 40
+        hs = {s: u.host_blocks(s, k) for s in (2, 3)}
+        o = O.onthefly_track_orbits(3, np.tile(np.arange(k), (2, 1)),
+                                    lambda s, ids: (u.cats[s][0][ids], u.cats[s][1][ids]),
+                                    lambda s, p, r: hs[s], mode='apocentric')
+        for name in ('apocentrer', 'entered', 'departed'):
+            w = o[name + '_offsets']
+            assert np.array_equal(ref[name + '_offsets'][:k + 1], w), name
+            assert np.array_equal(ref[name + '_IDs'][:w[-1]], o[name + '_IDs']), name
+        check_changes(ref['angles'][:len(o['angles'])], o['angles'], np.float32,
+                      'configs[4] world 2')
+    finally:
+        T.clear_carry()
 
 
 def _universe(contract, rank, world):
