@@ -253,19 +253,47 @@ __global__ __launch_bounds__(1024) void k_collate_offsets(const oa_collate_args 
 // one work-group per halo: the halo's new unique keys and their "already present"
 // prefix in LDS (a.lds_keys slots); every old element goes to rank i + #new keys below
 // it not already present (adding the new count on a match), every new key absent
-// from the old list to rank lb + #such new keys before it
+// from the old list to rank lb + #such new keys before it.
+// An old list of <= a.lds_old keys takes that count from a shift table instead of a
+// binary search per element: a new key q absent from the old list is below old key i
+// exactly when its lower bound lb[q] <= i, so the count is the inclusive prefix over i
+// of the absent keys' lb histogram (one LDS read per old element); a found key adds its
+// count at old position lb[q].
 __global__ __launch_bounds__(CT) void k_collate_merge(const oa_collate_args a) {
     extern __shared__ __attribute__((aligned(16))) char cl_smem[];
     uint64_t *nk = reinterpret_cast<uint64_t *>(cl_smem);
     int *nfp = reinterpret_cast<int *>(nk + a.lds_keys);
+    int *shift = nfp + a.lds_keys + 1;                    // [lds_old + 1] (table path)
+    int *fadd = shift + a.lds_old + 1;                    // [lds_old]
+    __shared__ int wsum[CT / 64 + 1];
     const int j = blockIdx.x;
     const int u = a.w_ulen[j];
     const int64_t base = a.new_base[j];
     const int64_t ob = a.old_off[j], on = a.old_off[j + 1] - ob;
     const int64_t no = a.new_off[j];
+    const bool table = on <= a.lds_old;                   // uniform
     for (int q = threadIdx.x; q < u; q += CT) { nk[q] = a.w_keys[base + q]; nfp[q] = a.w_fp[base + q]; }
     if (threadIdx.x == 0) nfp[u] = a.w_found[j];
+    if (table)
+        for (int i = threadIdx.x; i <= on; i += CT) { shift[i] = 0; if (i < on) fadd[i] = 0; }
     __syncthreads();
+    if (table) {
+        for (int q = threadIdx.x; q < u; q += CT) {
+            const int lb = (int)a.w_lb[base + q];
+            if (nfp[q + 1] == nfp[q]) atomicAdd(&shift[lb], 1);      // absent from the old list
+            else fadd[lb] = (int)a.w_cnt[base + q];                // found at old position lb
+        }
+        __syncthreads();
+        // inclusive scan of shift[0 .. on] (thread t: the run [t c, t c + c))
+        const int n1 = (int)on + 1, c = (n1 + CT - 1) / CT;
+        const int r0 = min(n1, (int)threadIdx.x * c), r1 = min(n1, r0 + c);
+        int run = 0;
+        for (int i = r0; i < r1; ++i) run += shift[i];
+        int tot;
+        int acc = block_scan<CT, int>(run, wsum, tot);
+        for (int i = r0; i < r1; ++i) { acc += shift[i]; shift[i] = acc; }
+        __syncthreads();
+    }
     // old elements MU per thread per trip, every load issued before any store (the
     // stores may alias the old list for the compiler, which would otherwise hold each
     // trip's loads behind the previous trip's stores)
@@ -283,15 +311,22 @@ __global__ __launch_bounds__(CT) void k_collate_merge(const oa_collate_args a) {
         for (int e = 0; e < MU; ++e) {
             const int64_t i = i0 + (int64_t)e * CT;
             if (i >= on) break;
-            int L = 0, R = u;
-            while (L < R) {
-                const int mid = (L + R) >> 1;
-                if (nk[mid] < key[e]) L = mid + 1; else R = mid;
+            int64_t pos, add;
+            if (table) {
+                pos = no + i + shift[i];
+                add = fadd[i];
+            } else {
+                int L = 0, R = u;
+                while (L < R) {
+                    const int mid = (L + R) >> 1;
+                    if (nk[mid] < key[e]) L = mid + 1; else R = mid;
+                }
+                const bool eq = L < u && nk[L] == key[e];
+                pos = no + i + L - nfp[L];
+                add = eq ? a.w_cnt[base + L] : 0;
             }
-            const bool eq = L < u && nk[L] == key[e];
-            const int64_t pos = no + i + L - nfp[L];
             a.new_keys[pos] = key[e];
-            a.new_cnt[pos] = cnt[e] + (eq ? a.w_cnt[base + L] : 0);
+            a.new_cnt[pos] = cnt[e] + add;
         }
     }
     for (int q = threadIdx.x; q < u; q += CT) {
@@ -815,15 +850,6 @@ __device__ __forceinline__ int64_t mp_find(const MpSlot *tab, uint64_t cap, uint
 #ifndef OA_MP_U
 #define OA_MP_U 8
 #endif
-#ifndef OA_MP_NT
-#define OA_MP_NT 0          // non-temporal member loads (A/B)
-#endif
-#ifndef OA_MP_DIAG
-#define OA_MP_DIAG 0        // 1, 2: timing diagnostics with wrong results (variants only)
-#endif
-#ifndef OA_MP_QUEUE
-#define OA_MP_QUEUE 1       // 0: look candidates up in place (the previous kernel, A/B)
-#endif
 #ifndef OA_MP_SEG
 #define OA_MP_SEG 128       // queue entries per probe work-group (of 256 * MP_U members)
 #endif
@@ -844,33 +870,19 @@ __global__ __launch_bounds__(256) void k_mp_probe(const void *hp, int kind, int6
 #pragma unroll
     for (int u = 0; u < MP_U; ++u) {
         const int64_t p = p0 + u * stride;
-#if OA_MP_NT
-        v[u] = p < n ? (kind == OA_ID_I64 ? (uint64_t)__builtin_nontemporal_load(
-                            static_cast<const unsigned long long *>(hp) + p)
-                                          : load_val(hp, p, kind)) : 0ull;
-#else
         v[u] = p < n ? load_val(hp, p, kind) : 0ull;
-#endif
     }
 #pragma unroll
     for (int u = 0; u < MP_U; ++u) {
         const uint64_t h = mix64(v[u]);
         m[u] = filt_mask(h);
-#if OA_MP_DIAG == 2                        // timing only: stream, no filter / table
-        w[u] = 0u;
-#else
         w[u] = p0 + u * stride < n ? filt[filt_word(h, fbits)] : 0u;
-#endif
     }
 #pragma unroll
     for (int u = 0; u < MP_U; ++u) {
         const int64_t p = p0 + u * stride;
         if (p < n && v[u] == ~0ull) atomicMin(neg1, (uint32_t)p);
-        bool cand = p < n && (w[u] & m[u]) == m[u];
-#if OA_MP_DIAG == 1                        // timing only: filter, no table probe
-        cand = false;
-#endif
-#if OA_MP_QUEUE
+        const bool cand = p < n && (w[u] & m[u]) == m[u];
         const uint64_t bal = __ballot(cand);
         if (bal == 0ull) continue;                  // wave-uniform
         const int lane = __lane_id();
@@ -881,16 +893,11 @@ __global__ __launch_bounds__(256) void k_mp_probe(const void *hp, int kind, int6
         if (!cand) continue;
         const uint32_t slot = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
         if (slot < (uint32_t)MP_SEG) { seg[slot] = (uint32_t)p; continue; }
-#else
-        if (!cand) continue;
-#endif
         const int64_t s = mp_find(tab, cap, v[u]);
         if (s >= 0) atomicMin(&tab[s].hpos, (uint32_t)p);
     }
-#if OA_MP_QUEUE
     __syncthreads();
     if (threadIdx.x == 0) qcnt[blockIdx.x] = lcnt < (uint32_t)MP_SEG ? lcnt : (uint32_t)MP_SEG;
-#endif
 }
 
 // the queued candidates: table lookup, smallest member position per tracked key.  One
@@ -1021,7 +1028,7 @@ int oa_collate_step(const oa_collate_args *args, void *stream) {
     if (a.lds_keys < 64 || a.lds_keys > CH || (a.lds_keys & (a.lds_keys - 1)) || a.lds_old < 0)
         return fail(OA_E_ARG, "oa_collate_step: lds_keys must be a power of two in [64, CHUNK]");
     const int64_t lds1 = (int64_t)a.lds_keys * 12 + 4 + (int64_t)a.lds_old * 8;
-    const int64_t lds2 = (int64_t)a.lds_keys * 12 + 4;
+    const int64_t lds2 = (int64_t)a.lds_keys * 12 + 8 + (int64_t)a.lds_old * 8 + 4;
     if (lds1 > 150 * 1024) return fail(OA_E_ARG, "oa_collate_step: LDS request too large");
     if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_collate_new),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1) != hipSuccess ||
@@ -1133,11 +1140,9 @@ int oa_main_progenitors(const oa_mainprog_args *args, void *stream) {
             hipLaunchKernelGGL(k_mp_probe, dim3((unsigned)nseg), dim3(256), 0, st, a.halo_pids,
                                a.halo_kind, a.n_halo_pids, tab, ct, neg1, filt, fbits, q, qcnt);
             if (int rc = check_launch("k_mp_probe")) return rc;
-#if OA_MP_QUEUE
             hipLaunchKernelGGL(k_mp_resolve, dim3((unsigned)((nseg * MP_SEG + 255) / 256)), dim3(256), 0,
                                st, a.halo_pids, a.halo_kind, tab, ct, q, qcnt, (uint32_t)nseg);
             if (int rc = check_launch("k_mp_resolve")) return rc;
-#endif
         }
         hipLaunchKernelGGL(k_mp_lookup, dim3((unsigned)((a.n_tracked + 255) / 256)), dim3(256), 0,
                            st, a, tab, ct, neg1, hn);
