@@ -64,9 +64,12 @@ class _H5Store:
             for k, v in datasets.items():
                 grp.create_dataset(k, data=v)
 
-    def add_dataset(self, g, d, arr):
+    def add_datasets(self, items):
+        """(group, name, array) triples written in one 'r+' open, as the reference's
+        save_final_apsis_counts writes all of its datasets in one (postprocessing.py:200)."""
         with self._h5py.File(self.path, 'r+') as hf:
-            hf[g].create_dataset(d, data=arr)
+            for g, d, arr in items:
+                hf[g].create_dataset(d, data=arr)
 
 
 class _MemStore:
@@ -86,11 +89,12 @@ class _MemStore:
     def create_group(self, name, datasets):
         self.obj.write_group(name, datasets)
 
-    def add_dataset(self, g, d, arr):
-        grp = self.obj.groups[g]
-        if d in grp:
-            raise ValueError('dataset %s/%s exists' % (g, d))
-        grp[d] = np.asarray(arr)
+    def add_datasets(self, items):
+        for g, d, arr in items:
+            grp = self.obj.groups[g]
+            if d in grp:
+                raise ValueError('dataset %s/%s exists' % (g, d))
+            grp[d] = np.asarray(arr)
 
 
 def _store(f, mode='r'):
@@ -357,6 +361,7 @@ class Apsides:
         foff_d = _dev(offsets_final, dev)
         fcnt_d = _dev(counts_final, dev)
         stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        written = []
         for skey in skeys_:
             ids = st.read(skey, 'particle_IDs')
             if ids.dtype != ids_final.dtype:
@@ -378,6 +383,8 @@ class Apsides:
             if int(status.item()) & N.POST_MISSING:
                 raise ValueError('%s: particle IDs absent from the final snapshot\'s halo '
                                  '(shape mismatch in the reference)' % skey)
-            st.add_dataset(skey, '{}_counts_final'.format(tag), _host(out, n, np.float64))
-            if verbose:
+            written.append((skey, '{}_counts_final'.format(tag), _host(out, n, np.float64)))
+        st.add_datasets(written)
+        if verbose:
+            for skey in skeys_:
                 print('Final counts saved for {} {}'.format(*(skey.split('_'))))
