@@ -272,22 +272,40 @@ __device__ __forceinline__ uint64_t lb_poll(const uint64_t *w) {
     return __hip_atomic_load(const_cast<uint64_t *>(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One whole wave: publish `count` for item b, return the item's exclusive prefix (and
-// publish the inclusive one).  Lane l of a window reads item j0 - l.
-__device__ int64_t item_lookback(const oa_step_args &a, uint32_t b, uint32_t count) {
+// One whole wave: item b's exclusive prefix, summing the counts of the items before it
+// back to the nearest published inclusive prefix, LBW words per lane per poll (a window
+// of 64 * LBW items: the items of one dispatch round resolve in one round trip), and
+// publishes the inclusive one.  `publish_count`: also publish the count first.
+constexpr int LBW = 4;
+__device__ int64_t item_lookback(const oa_step_args &a, uint32_t b, uint32_t count,
+                                 bool publish_count = true) {
     const int lane = threadIdx.x & 63;
     const uint64_t tag = (uint64_t)(uint32_t)a.lb_epoch << 48;
-    if (lane == 0) lb_publish(&a.lookback[b], tag | LB_AGG | count);
+    if (publish_count && lane == 0) lb_publish(&a.lookback[b], tag | LB_AGG | count);
     int64_t excl = 0, j0 = (int64_t)b - 1;
     uint32_t spins = 0;
     while (j0 >= 0) {
-        const int64_t j = j0 - lane;
-        // before item 0: an inclusive prefix of 0
-        const uint64_t w = j >= 0 ? lb_poll(&a.lookback[j]) : (tag | LB_INC);
-        const bool ready = (w >> 48) == (tag >> 48) && (w & (3ull << 46)) != 0ull;
-        const uint64_t inc = __ballot(ready && (w & LB_INC) != 0ull);
+        uint64_t w[LBW];
+#pragma unroll
+        for (int q = 0; q < LBW; ++q) {
+            const int64_t j = j0 - (lane * LBW + q);
+            // before item 0: an inclusive prefix of 0
+            w[q] = j >= 0 ? lb_poll(&a.lookback[j]) : (tag | LB_INC);
+        }
+        // this lane's first inclusive word, and whether every word up to it is published
+        int qi = LBW;
+        bool ready = true;
+#pragma unroll
+        for (int q = 0; q < LBW; ++q) {
+            const bool r = (w[q] >> 48) == (tag >> 48) && (w[q] & (3ull << 46)) != 0ull;
+            if (qi == LBW) {
+                ready &= r;
+                if (r && (w[q] & LB_INC)) qi = q;
+            }
+        }
+        const uint64_t inc = __ballot(qi < LBW);
         const uint64_t notready = __ballot(!ready);
-        // lanes 0 .. the nearest inclusive word are needed, all of them published
+        // lanes 0 .. the nearest inclusive word's lane are needed
         const int f = inc ? __builtin_ctzll(inc) : 64;
         const uint64_t need = f == 64 ? ~0ull : ((2ull << f) - 1ull);
         if (notready & need) {
@@ -298,12 +316,15 @@ __device__ int64_t item_lookback(const oa_step_args &a, uint32_t b, uint32_t cou
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
-        int64_t v = lane <= f ? (int64_t)(w & LB_VAL) : 0;
+        int64_t v = 0;
+#pragma unroll
+        for (int q = 0; q < LBW; ++q)
+            if (lane < f || (lane == f && q <= qi)) v += (int64_t)(w[q] & LB_VAL);
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
         excl += v;
         if (f < 64) break;
-        j0 -= 64;
+        j0 -= 64 * LBW;
     }
     {   // uniform (every lane holds the same sum): keep it in SGPRs
         const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)excl);
@@ -1167,11 +1188,11 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             carry += (uint32_t)__shfl(incl, 63);
         }
         if (lane == 0) H.chunk_total = carry;
-        // direct records: the item's output prefix, while the other waves stage r̂
-        if (a.direct) {
-            const int64_t P = item_lookback(a, blockIdx.x, uni(carry));
-            if (lane == 0) H.prefix = P;
-        }
+        // direct records: the item's count is published now; its prefix is resolved
+        // after phase 2b, beside phase 3, and the records are stored after that
+        if (a.direct && lane == 0)
+            lb_publish(&a.lookback[blockIdx.x],
+                       ((uint64_t)(uint32_t)a.lb_epoch << 48) | LB_AGG | carry);
     }
     // the item's current r̂, from the registers phase 1 left it in
 #pragma unroll
@@ -1188,12 +1209,10 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     STAMP(5);
 
     const uint64_t lanemask_lt = (1ull << lane) - 1ull;
-    // records go to the item's scratch range, or (direct) straight to the output
+    // records go to the item's scratch range now, or (direct) from registers to the
+    // output once the item's prefix is known (after phase 3)
     const bool direct = a.direct != 0;
-    ID *scr_ids = reinterpret_cast<ID *>(direct ? a.out_ids : a.scratch_ids);
-    uint16_t *scr_ang = direct ? a.out_ang : a.scratch_ang;
-    int32_t *scr_pos = direct ? a.out_pos : a.scratch_pos;
-    const int64_t rec0 = direct ? uni64(H.prefix) : it.scratch_off;
+    ID *scr_ids = reinterpret_cast<ID *>(a.scratch_ids);
     uint32_t *rcw = reinterpret_cast<uint32_t *>(rcx);        // new angles over rc_x
     constexpr uint32_t RCW = sizeof(TD) / 4;
 #pragma unroll
@@ -1234,12 +1253,14 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         // item's records are contiguous and in order (k_gather_items copies them)
         const uint64_t mk = __ballot(flag);
         const uint32_t cnt = (uint32_t)__popcll(mk);
-        const int64_t sb = rec0 + uni(H.rowoff[r]);
-        if (flag) {
+        if (direct) {
+            if (p & PK_HIT) pk[k] = (p & 0xFFFFu) | ((uint32_t)a16 << 16);   // kept for later
+        } else if (flag) {
+            const int64_t sb = it.scratch_off + uni(H.rowoff[r]);
             const uint32_t q = (uint32_t)__popcll(mk & lanemask_lt);
             __builtin_nontemporal_store(pid[k], &scr_ids[sb + q]);
-            __builtin_nontemporal_store(a16, &scr_ang[sb + q]);
-            if (scr_pos) scr_pos[sb + q] = (int32_t)(kb + lane);
+            __builtin_nontemporal_store(a16, &a.scratch_ang[sb + q]);
+            if (a.scratch_pos) a.scratch_pos[sb + q] = (int32_t)(kb + lane);
         }
         if (lane == 0 && cnt) atomicAdd(&H.halo_cnt[hs], (int)cnt);
     }
@@ -1255,8 +1276,16 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // progenitor block: angle 0 (calc_angles :348-349).  Nothing in this launch reads
     // them again, so the stores are non-temporal.
     // (four consecutive positions per thread: one 16-byte store)
-    const uint32_t n4 = n_span & ~3u;
-    for (uint32_t l4 = (uint32_t)tid * 4u; l4 < n4; l4 += WG * 4u) {
+    // direct records: wave 0 resolves the item's prefix meanwhile (the look-back's
+    // round trips overlap the other waves' stores)
+    if (direct && wave == 0) {
+        const int64_t P = item_lookback(a, blockIdx.x, uni(H.chunk_total), false);
+        if (lane == 0) H.prefix = P;
+    }
+    const uint32_t t3 = direct ? (uint32_t)tid - 64u : (uint32_t)tid;
+    const uint32_t nt3 = direct ? (uint32_t)(WG - 64) : (uint32_t)WG;
+    const uint32_t n4 = (direct && wave == 0) ? 0u : n_span & ~3u;
+    for (uint32_t l4 = t3 * 4u; l4 < n4; l4 += nt3 * 4u) {
         const uint32_t s4 = *reinterpret_cast<const uint32_t *>(sgn8 + l4);
         i32x4 w;
 #pragma unroll
@@ -1267,12 +1296,34 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         }
         rbs_v4i32(w, r_mt, (int32_t)(l4 * 4u), 0, AUX_NT);
     }
-    for (uint32_t li = n4 + tid; li < n_span; li += WG) {
+    for (uint32_t li = (n_span & ~3u) + t3; li < n_span && !(direct && wave == 0); li += nt3) {
         const uint32_t s = sgn8[li];
         const uint32_t ang = (s & 4u) ? (rcw[RCW * li] & 0xFFFFu) : 0u;
         bst32<AUX_NT>(r_mt, li * 4u, ang | ((s & 3u) << 16));
     }
     if (direct) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();             // H.prefix
+        __builtin_amdgcn_sched_barrier(0);
+        const int64_t rec0 = uni64(H.prefix);
+        ID *out_ids = reinterpret_cast<ID *>(a.out_ids);
+#pragma unroll
+        for (int k = 0; k < KROWS; ++k) {
+            const uint32_t r = wave + NWAVE * k;
+            if (r >= nrow) continue;
+            uint32_t nv, hs;
+            int64_t kb;
+            row_of(r, nv, hs, kb);
+            const uint32_t p = pk[k];
+            const bool flag = (p & (PK_HIT | PK_FLAG)) == (PK_HIT | PK_FLAG);
+            const uint64_t mk = __ballot(flag);
+            if (flag) {
+                const int64_t sb = rec0 + uni(H.rowoff[r]) + __popcll(mk & lanemask_lt);
+                __builtin_nontemporal_store(pid[k], &out_ids[sb]);
+                __builtin_nontemporal_store((uint16_t)(p >> 16), &a.out_ang[sb]);
+                if (a.out_pos) a.out_pos[sb] = (int32_t)(kb + lane);
+            }
+        }
         if (wave == 0) direct_tail(rec0, uni(H.chunk_total));
     } else if (tid < nh) {
         const uint32_t os = H.hslot[tid] >> 1;
@@ -2341,7 +2392,11 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
                 mlds[hit[u] & 0x3FFFFFFFu] = (uint32_t)(flag ? 0u : acc) | (sc << 16);
                 rang[u] = acc;
                 // an inherited set's position words carry the sign in bits 30-31
+#ifdef OA_DIAG_NOREC
+                if (flag) rslot[u] = atomicAdd(nrec + 1, 1u) & (RCHUNK - 1);   // timing only
+#else
                 if (flag) rslot[u] = atomicAdd(&rcnt[(qpos[u] & 0x3FFFFFFFu) >> RCHUNK_LOG2], 1u);
+#endif
             }
             // the records: every slot claimed above first, then the stores
 #pragma unroll

@@ -54,6 +54,15 @@ big)
   prof "$O/prof_big_$T" 400 "$R/bench.py" --dtype float64 --particles 1e7 --halos 100 \
     --steps 10 --warmup 3 --no-cpu-baseline > "$O/big_$T.json" 2> "$O/big_$T.err"
   rc=$?; cat "$O/big_$T.json"; python3 tools/kstats.py "$O/prof_big_$T"; ok $rc big ;;
+envsweep)
+  # bench.py $BENCH_ARGS under environment settings ($ENVS: space-separated NAME=VALUE,NAME=VALUE)
+  for rep in ${REPS:-1 2}; do
+    for e in ${ENVS:-ORBIT_DIRECT=1}; do
+      env ${e//,/ } timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline \
+        ${BENCH_ARGS:-} > "$O/es_${T}_${e}_$rep.json" 2> "$O/es_${T}_${e}_$rep.err"
+      rc=$?; echo "$e rep$rep $(grep -o 'k_step [0-9.]* ms' "$O/es_${T}_${e}_$rep.err") $(grep -o '"ms_per_step": [0-9.]*' "$O/es_${T}_${e}_$rep.json")"; ok $rc "envsweep $e"
+    done
+  done ;;
 bigsweep)
   # configs[1] under environment settings ($BIG_ENVS: space-separated NAME=VALUE,NAME=VALUE)
   for rep in ${REPS:-1 2}; do
