@@ -2165,11 +2165,17 @@ __global__ __launch_bounds__(SCAT_WG) void k_part_scatter(const oa_step_args a, 
     SSTAMP(1);
 }
 
+// k_part_join's apsis records staged in LDS before their slots are claimed (16 B each:
+// ID, position in the halo's previous block, angle, rank in its chunk); a work-group
+// with more records claims the rest one global atomic each
+constexpr int PART_RB = 768;
+
 // LDS of one k_part_join work-group for a partition capacity of e entries, s slots:
-// the slots, then max(deferral list, the partition's state words), the stash, flags
+// the slots, then max(deferral list, the partition's state words), the stash, flags,
+// the staged records (two work-groups per CU at 4096 entries in 6144 slots)
 __host__ __device__ inline int64_t part_lds_bytes(int e, int sl) {
     const int64_t mid = (int64_t)e * 4 > (int64_t)(e / 4) * 8 ? (int64_t)e * 4 : (int64_t)(e / 4) * 8;
-    return (int64_t)sl * 8 + mid + (int64_t)STASH * 8 + 16 + 16;
+    return (int64_t)sl * 8 + mid + (int64_t)STASH * 8 + 16 + 16 + (int64_t)PART_RB * 16;
 }
 
 // The apsis records of a partitioned halo (k_part_join -> oa_compact): a record is
@@ -2199,6 +2205,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     uint64_t *stash = pend + (PE * 4 > (PE / 4) * 8 ? PE / 2 : PE / 4); // [STASH]
     uint32_t *flags = reinterpret_cast<uint32_t *>(stash + STASH);      // npend, nstash, overflow, nonuniform
     uint32_t *nrec = flags + 4;                                         // records of the work-group
+    uint64_t *rbuf = reinterpret_cast<uint64_t *>(flags + 8);           // [2 PART_RB] staged records
     const int tid = threadIdx.x;
     PSTAMP(0);
     const int32_t g = a.plist[2 * blockIdx.x], pp = a.plist[2 * blockIdx.x + 1];
@@ -2259,7 +2266,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     uint32_t nsl = 2u * nc + 64u;                      // load <= 1/2 where the LDS allows
     nsl = nsl < PS ? nsl : PS;
     for (uint32_t w = tid; w < nsl; w += PART_WG) slots[w] = 0ull;
-    if (tid < 5) flags[tid] = 0u;
+    if (tid < 8) flags[tid] = 0u;
     const uint32_t hi0 = (KB == 8 && nc) ? (uint32_t)((uint64_t)ck[0] >> 32) : 0u;
     __syncthreads();
     PSTAMP(1);
@@ -2336,7 +2343,6 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     uint32_t *rcnt = a.pcnt + gp[8];
     ID *scr_ids = static_cast<ID *>(a.scratch_ids);
     const uint64_t hiw = KB == 4 ? (uint64_t)a.part_hi << 32 : 0ull;
-    uint32_t mine = 0;                                  // records of this thread
     // previous entries, PU per thread: lookups, then the gathers of the matched current
     // r̂ (the partition's own bucket entries), then the angle and state-word arithmetic
     for (uint32_t q = 0; q < nq; ++q) {
@@ -2380,7 +2386,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
             uint32_t rslot[PU];
 #pragma unroll
             for (int u = 0; u < PU; ++u) {
-                rslot[u] = 0xFFFFFFFFu;
+                rslot[u] = 0xFFFFFFFFu;                 // staged (or none)
                 if (hit[u] == 0xFFFFFFFFu) continue;
                 const uint32_t sc = hit[u] >> 30, sp = qmeta[u] >> 16;
                 // strict sign test (:311-314), arccos of the r̂ dot product (:324-325),
@@ -2391,14 +2397,20 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
                 const uint16_t acc = angle_add((uint16_t)(qmeta[u] & 0xFFFFu), acos_td(dt));
                 mlds[hit[u] & 0x3FFFFFFFu] = (uint32_t)(flag ? 0u : acc) | (sc << 16);
                 rang[u] = acc;
-                // an inherited set's position words carry the sign in bits 30-31
-#ifdef OA_DIAG_NOREC
-                if (flag) rslot[u] = atomicAdd(nrec + 1, 1u) & (RCHUNK - 1);   // timing only
-#else
-                if (flag) rslot[u] = atomicAdd(&rcnt[(qpos[u] & 0x3FFFFFFFu) >> RCHUNK_LOG2], 1u);
-#endif
+                // an inherited set's position words carry the sign in bits 30-31; the
+                // record is staged in LDS (its slot is claimed per chunk below), or,
+                // past the stage's capacity, claims its slot with a global atomic
+                if (flag) {
+                    const uint32_t p = qpos[u] & 0x3FFFFFFFu;
+                    const uint32_t e = atomicAdd(nrec, 1u);
+                    if (e < (uint32_t)PART_RB) {
+                        rbuf[2 * e] = (uint64_t)qkey[u] | hiw;
+                        rbuf[2 * e + 1] = (uint64_t)p | ((uint64_t)acc << 32);
+                    } else {
+                        rslot[u] = atomicAdd(&rcnt[p >> RCHUNK_LOG2], 1u);
+                    }
+                }
             }
-            // the records: every slot claimed above first, then the stores
 #pragma unroll
             for (int u = 0; u < PU; ++u) {
                 if (rslot[u] == 0xFFFFFFFFu) continue;
@@ -2407,19 +2419,47 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
                 scr_ids[s] = (ID)((uint64_t)qkey[u] | hiw);
                 a.scratch_ang[s] = rang[u];
                 a.scratch_rk[s] = (uint16_t)(p & (RCHUNK - 1));
-                ++mine;
             }
             if (j0 == 0 && q == 0) PSTAMP(4);
         }
     }
-    // the work-group's record count: one pair of device atomics (halo and item counts)
-    uint32_t wc = mine;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) wc += __shfl_xor(wc, o);
-    if ((tid & 63) == 0 && wc) atomicAdd(nrec, wc);
     __syncthreads();
+    // the staged records: ranks within their chunks from LDS counters over the dead
+    // table, one global atomic per touched chunk for the chunk's slots, then the stores
+    // (a halo with more chunks than the counters claims per record)
+    const uint32_t nst = min(*nrec, (uint32_t)PART_RB);
+    const uint32_t nch = (uint32_t)((a.halos[it.h0].prev_cnt + RCHUNK - 1) >> RCHUNK_LOG2);
+    uint32_t *lc = reinterpret_cast<uint32_t *>(slots);
+    const bool lds_ranks = nch <= 2u * PS;
+    if (nst) {
+        if (lds_ranks)
+            for (uint32_t c = tid; c < nch; c += PART_WG) lc[c] = 0u;
+        __syncthreads();
+        for (uint32_t e = tid; e < nst; e += PART_WG) {
+            const uint32_t c = (uint32_t)rbuf[2 * e + 1] >> RCHUNK_LOG2;
+            const uint32_t r = lds_ranks ? atomicAdd(&lc[c], 1u) : atomicAdd(&rcnt[c], 1u);
+            rbuf[2 * e + 1] |= (uint64_t)r << 48;
+        }
+        __syncthreads();
+        if (lds_ranks)
+            for (uint32_t c = tid; c < nch; c += PART_WG) {
+                const uint32_t n = lc[c];
+                if (n) lc[c] = atomicAdd(&rcnt[c], n);
+            }
+        __syncthreads();
+        for (uint32_t e = tid; e < nst; e += PART_WG) {
+            const uint64_t w = rbuf[2 * e + 1];
+            const uint32_t p = (uint32_t)w, c = p >> RCHUNK_LOG2;
+            const uint32_t slot = (uint32_t)(w >> 48) + (lds_ranks ? lc[c] : 0u);
+            const int64_t s = it.scratch_off + (int64_t)c * RCHUNK + slot;
+            scr_ids[s] = (ID)rbuf[2 * e];
+            a.scratch_ang[s] = (uint16_t)(w >> 32);
+            a.scratch_rk[s] = (uint16_t)(p & (RCHUNK - 1));
+        }
+    }
     // the partition's state words leave as one coalesced run
     for (uint32_t i = tid; i < nc; i += PART_WG) cmeta[i] = mlds[i];
+    // the work-group's record count: one pair of device atomics (halo and item counts)
     if (tid == 0 && *nrec) {
         const oa_halo &h = a.halos[it.h0];
         atomicAdd(&a.halo_count[h.out_slot], (int32_t)*nrec);

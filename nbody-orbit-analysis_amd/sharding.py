@@ -448,7 +448,8 @@ class ShardedResult:
     n_slots: int
     has_prog: np.ndarray
     records: Optional[tuple] = None          # device (offsets, ids, f16 bits, prev-state row)
-    gpos_prev: Optional[torch.Tensor] = None # previous shard row -> global block position
+    prev_prep: object = None                 # the previous snapshot's ShardedPrep (its
+                                             # shard rows' global block positions: gpos)
     bulk: Optional[np.ndarray] = None
     lp: object = None                        # the local step (deferred: settled later)
 
@@ -476,20 +477,49 @@ class ShardedFetch:
 @dataclass
 class ShardedPrep:
     """One snapshot's host half (ShardedEngine.prepare): the shard, its rows' global
-    block positions and the local engine's prepared step."""
+    block positions and the local engine's prepared step.  With a presharded loader the
+    global positions come from an all-gather of the ranks' block counts that runs when
+    they are first needed (the records' gather, a checkpoint, a resume), not while the
+    snapshot is planned: every rank reaches those points in the same order."""
     n: int
     exists: np.ndarray
     compare: bool
-    gpos: torch.Tensor
-    sel: torch.Tensor                       # this rank's rows in the global snapshot
-    n_global: int
+    gpos_: Optional[torch.Tensor]
+    sel_: Optional[torch.Tensor]            # this rank's rows in the global snapshot
+    n_global_: Optional[int]
     rows: Optional[np.ndarray]              # catalogue rows (centre, bulk) to exchange
     bulk_out: Optional[np.ndarray]
     plan: object
     lp: object = None
-    layout: Optional[str] = None            # checkpoint row layout (presharded runs)
+    layout_: Optional[str] = None           # checkpoint row layout (presharded runs)
     h2d_bytes: int = 0
     local_args: tuple = ()                  # the local engine's prepare arguments
+    lazy: object = None                     # () -> (gpos, sel, n_global, layout)
+
+    def _resolve(self):
+        if self.lazy is not None:
+            self.gpos_, self.sel_, self.n_global_, self.layout_ = self.lazy()
+            self.lazy = None
+
+    @property
+    def gpos(self):
+        self._resolve()
+        return self.gpos_
+
+    @property
+    def sel(self):
+        self._resolve()
+        return self.sel_
+
+    @property
+    def n_global(self):
+        self._resolve()
+        return self.n_global_
+
+    @property
+    def layout(self):
+        self._resolve()
+        return self.layout_
 
 
 class _Plan:
@@ -610,7 +640,11 @@ class ShardedEngine:
             h2d = sum(int(np.asarray(snapshot[k]).nbytes) for k in ('ids', 'coordinates',
                                                                     'velocities')
                       if not isinstance(snapshot[k], torch.Tensor))
-            gpos, sel, n_global, layout = self._presharded_gpos(starts, counts)
+            lazy = (lambda st=starts, ct=counts: self._presharded_gpos(st, ct))
+            gpos = sel = n_global = layout = None
+            if angles_in is not None and not compare:      # a resume needs them now
+                gpos, sel, n_global, layout = lazy()
+                lazy = None
         else:
             sh = stripe_shard(snapshot, starts, self.owner, self.group, self.device,
                               bulk_fn=self.local.bulk if (bulk_cat is None and nh) else None)
@@ -631,11 +665,11 @@ class ShardedEngine:
                 rows[:, 3:] = np.asarray(bulk_cat, dtype=np.float64).reshape(nh, 3)
         p = prev if prev is not None else self.prev
         ids_dt = np.asarray(ids[:0].cpu() if isinstance(ids, torch.Tensor) else ids[:0]).dtype
-        sp = ShardedPrep(n=n, exists=exists, compare=bool(compare), gpos=gpos, sel=sel,
-                         n_global=n_global,
+        sp = ShardedPrep(n=n, exists=exists, compare=bool(compare), gpos_=gpos, sel_=sel,
+                         n_global_=n_global, lazy=lazy if self.presharded else None,
                          rows=rows, bulk_out=None if bulk_cat is not None else bulk,
                          plan=_Plan(ids_dt, None if bulk is None else np.asarray(bulk).dtype),
-                         layout=layout, h2d_bytes=h2d)
+                         layout_=layout, h2d_bytes=h2d)
         sp.local_args = (shard, centres, bulk, H, z, exists, compare, a_in, bulk_cat is not None)
         sp.lp = self._local_prepare(sp, None if (prev is None or p is None) else p.lp)
         return sp
@@ -664,7 +698,7 @@ class ShardedEngine:
         if sp.compare:
             has_prog = np.isin(sp.exists, p.exists)
             res.has_prog, res.n_slots = has_prog, int(has_prog.sum())
-            res.records, res.gpos_prev = out, p.gpos
+            res.records, res.prev_prep = out, p
         return res
 
     def step(self, snapshot, centres, bulk_cat, H, z, exists, compare, angles_in=None,
@@ -733,7 +767,8 @@ class ShardedEngine:
             total = self.local.total(lp) if hasattr(self.local, 'total') else int(offs[-1])
             slot = torch.repeat_interleave(torch.arange(res.n_slots, device=dev),
                                            (offs[1:] - offs[:-1]).long(), output_size=total)
-            g = res.gpos_prev[a_pos[:total].to(res.gpos_prev.device).long()]
+            gpos_prev = res.prev_prep.gpos
+            g = gpos_prev[a_pos[:total].to(gpos_prev.device).long()]
             rec = torch.stack([(slot.to(g.device) << 32) | g, _as_i64(a_ids[:total]).to(g.device),
                                a_ang[:total].to(torch.int64).to(g.device)], dim=1)
             rec, = gather_rows(self.group, self.ROOT, rec)
