@@ -234,15 +234,6 @@ typedef struct oa_step_args {
     const int64_t *gchunk3;     /* the previous chunks k_part_scatter reads: those of
                                    halos with a fresh previous set (NULL: gchunk2)    */
     int32_t n_gchunk3;
-    /* Halo groups of the partitioned path: with n_part_groups > 1 and no previous chunk
-     * to scatter (every previous set inherited), group g's scatter runs on `stream` and
-     * its join on a library-owned second stream as soon as that scatter is done, so a
-     * group's LDS-bound join overlaps the next group's streaming scatter; the joins
-     * are joined back into `stream` before oa_step returns.  part_groups is a HOST
-     * array of 2 * (n_part_groups + 1) int64: the first gchunk1 row and the first plist
-     * row of each group, then the totals.                                          */
-    int32_t n_part_groups;
-    const int64_t *part_groups;
     int32_t items_single;       /* 1: every packed item holds one halo (the launch takes
                                    k_step's one-halo specialisation); 0: any item plan */
     /* Direct records (replaces oa_compact for a compare step with packed items only,

@@ -56,7 +56,7 @@ class StepArgs(ctypes.Structure):
                 ('ikey', c_vp), ('ipos', c_vp), ('imeta', c_vp), ('irh', c_vp), ('icnt', c_vp),
                 ('pcnt', c_vp), ('n_pcnt', c_i64), ('scratch_rk', c_vp), ('part_key4', c_i32),
                 ('part_hi', ctypes.c_uint32), ('gchunk3', c_vp), ('n_gchunk3', c_i32),
-                ('n_part_groups', c_i32), ('part_groups', c_vp), ('items_single', c_i32), ('direct', c_i32), ('lookback', c_vp),
+                ('items_single', c_i32), ('direct', c_i32), ('lookback', c_vp),
                 ('lb_epoch', c_i32), ('n_slots', c_i32), ('offsets_out', c_vp), ('out_ids', c_vp),
                 ('out_ang', c_vp), ('out_pos', c_vp), ('total_out', c_vp)]
 

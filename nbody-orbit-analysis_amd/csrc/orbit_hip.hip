@@ -2490,76 +2490,8 @@ __global__ __launch_bounds__(256) void k_part_unbucket(const oa_unbucket_args a)
     }
 }
 
-// The library's second stream and events for the grouped scatter / join overlap (one
-// set per device, created on first use).
-struct SideStream {
-    int dev = -1;
-    hipStream_t s = nullptr;
-    hipEvent_t ev[66] = {};
-};
-SideStream g_side[16];
-
-SideStream *side_stream() {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
-    SideStream &x = g_side[dev];
-    if (x.s == nullptr) {
-        if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-        for (auto &e : x.ev)
-            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
-        x.dev = dev;
-    }
-    return &x;
-}
-
-template <typename TX, typename TV, typename TD, int IDB, int KB>
-int launch_part_grouped(const oa_step_args &a, hipStream_t st) {
-    SideStream *ss = side_stream();
-    if (!ss) return fail(OA_E_LAUNCH, "oa_step: side stream for the partition groups");
-    const int ng = a.n_part_groups;
-    const int64_t *gr = a.part_groups;
-    auto ks = k_part_scatter<TX, TV, TD, IDB, KB>;
-    auto kj = k_part_join<TD, IDB, KB>;
-    const int64_t lds_s = scat_lds_bytes(a.part_kmax, (int)sizeof(TD));
-    const int64_t lds_j = part_lds_bytes(a.part_e, a.part_slots);
-    if (int rc = set_lds(ks, lds_s)) return rc;
-    if (int rc = set_lds(kj, lds_j)) return rc;
-    // the side stream starts behind everything queued on `stream` (the counter reset)
-    if (hipEventRecord(ss->ev[0], st) != hipSuccess || hipStreamWaitEvent(ss->s, ss->ev[0], 0) != hipSuccess)
-        return fail(OA_E_LAUNCH, "oa_step: partition groups fork");
-    for (int g = 0; g < ng; ++g) {
-        const int64_t c0 = gr[2 * g], c1 = gr[2 * g + 2], p0 = gr[2 * g + 1], p1 = gr[2 * g + 3];
-        if (c1 > c0) {
-            oa_step_args ag = a;
-            ag.gchunk1 = a.gchunk1 + 3 * c0;
-            ag.n_gchunk1 = (int32_t)(c1 - c0);
-            ag.gchunk3 = a.gchunk1;                     // given and empty: no previous chunk
-            ag.n_gchunk3 = 0;
-            hipLaunchKernelGGL(ks, dim3((unsigned)(c1 - c0)), dim3(SCAT_WG), (size_t)lds_s, st, ag,
-                               make_frame_k(a));
-            if (int rc = check_launch("k_part_scatter")) return rc;
-        }
-        hipEvent_t e = ss->ev[1 + (g % 64)];
-        if (hipEventRecord(e, st) != hipSuccess || hipStreamWaitEvent(ss->s, e, 0) != hipSuccess)
-            return fail(OA_E_LAUNCH, "oa_step: partition group hand-off");
-        if (p1 > p0) {
-            oa_step_args aj = a;
-            aj.plist = a.plist + 2 * p0;
-            aj.n_parts = (int32_t)(p1 - p0);
-            hipLaunchKernelGGL(kj, dim3((unsigned)(p1 - p0)), dim3(PART_WG), (size_t)lds_j, ss->s, aj);
-            if (int rc = check_launch("k_part_join")) return rc;
-        }
-    }
-    if (hipEventRecord(ss->ev[65], ss->s) != hipSuccess || hipStreamWaitEvent(st, ss->ev[65], 0) != hipSuccess)
-        return fail(OA_E_LAUNCH, "oa_step: partition groups join");
-    return OA_OK;
-}
-
 template <typename TX, typename TV, typename TD, int IDB, int KB>
 int launch_part_k(const oa_step_args &a, hipStream_t st) {
-    // every previous set inherited: the groups' scatters and joins may overlap
-    if (a.n_part_groups > 1 && a.part_groups && a.gchunk3 && a.n_gchunk3 == 0)
-        return launch_part_grouped<TX, TV, TD, IDB, KB>(a, st);
     // previous chunks to scatter: those of halos without an inherited set (gchunk3)
     const int64_t n_scat = a.n_gchunk1 + (a.gchunk3 ? a.n_gchunk3 : a.n_gchunk2);
     if (n_scat > 0) {
@@ -2785,15 +2717,6 @@ int oa_step(const oa_step_args *args, void *stream) {
         return fail(OA_E_ARG, "bad large-halo partition arguments");
     if (a.onthefly && a.n_parts > 0)
         return fail(OA_E_ARG, "the partitioned large-halo path is not for on-the-fly steps");
-    if (part && a.n_part_groups > 1) {
-        const int64_t *g = a.part_groups;
-        bool ok = g && a.n_part_groups <= 64 && g[0] == 0 && g[1] == 0 &&
-                  g[2 * a.n_part_groups] == a.n_gchunk1 && g[2 * a.n_part_groups + 1] == a.n_parts;
-        for (int k = 0; ok && k < a.n_part_groups; ++k)
-            ok = g[2 * k + 2] >= g[2 * k] && g[2 * k + 3] >= g[2 * k + 1];
-        if (!ok) return fail(OA_E_ARG, "part_groups: <= 64 groups of non-decreasing gchunk1 / plist "
-                                        "rows from 0 to n_gchunk1 / n_parts");
-    }
     if (a.direct && (!a.compare || a.onthefly || a.n_global_items > 0 || !a.lookback ||
                      !a.offsets_out || !a.out_ids || !a.out_ang || !a.total_out ||
                      a.lb_epoch < 1 || a.lb_epoch > 0xFFFF || a.n_slots < 0))

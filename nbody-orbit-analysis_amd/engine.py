@@ -229,7 +229,7 @@ GPART_W = 16         # int64 per gpart row (orbit_hip.h)
 
 
 def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=None, n_xcd=8,
-              key4=False, td_f64=None, groups=1):
+              key4=False, td_f64=None):
     """Partition layout of the global items for the partitioned large-halo path
     (k_part_scatter / k_part_join), vectorised.
 
@@ -247,11 +247,8 @@ def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=No
     in contiguous runs (work-group b runs on XCD b % 8), so one halo's partitions share
     an L2.  The counters (pcnt) are the current set's, the fresh previous set's, then
     one record counter per previous-block chunk (gchunk2 row, GCHUNK positions; gpart[8]
-    is the item's first).  ``groups``: the global items are cut into up to that many
-    consecutive runs of about equal partition counts (oa_step_args.part_groups: a
-    group's join overlaps the next group's scatter); plist lists each group's
-    partitions contiguously, dealt to the XCDs within the group.  Returns None when no
-    halo needs the join or one needs more than ``kmax`` partitions."""
+    is the item's first).  Returns None when no halo needs the join or one needs more
+    than ``kmax`` partitions."""
     h = np.asarray(glob['h0'], dtype=np.int64)
     c = np.asarray(cur_cnt, dtype=np.int64)[h]
     p = np.maximum(np.asarray(prev_cnt, dtype=np.int64)[h], 0)
@@ -297,32 +294,16 @@ def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=No
     gpart[:, 8] = rc0 + np.cumsum(nrow) - nrow
     g = np.repeat(np.arange(ng), K)
     pp = np.arange(nk) - np.repeat(np.cumsum(K) - K, K)
-    # groups: consecutive items, cut where the running partition count crosses k / G
-    G = max(1, min(int(groups), int((K > 0).sum())))
-    cumk = np.cumsum(K)
-    cut = np.searchsorted(cumk, nk * np.arange(1, G) / G, side='left') + 1 if G > 1 else \
-        np.zeros(0, np.int64)
-    item_b = np.unique(np.concatenate([[0], np.minimum(cut, ng), [ng]]).astype(np.int64))
-    rows, plist_parts = [0], []
-    for i0, i1 in zip(item_b[:-1], item_b[1:]):
-        q0, q1 = int(cumk[i0] - K[i0]), int(cumk[i1 - 1])
-        n = q1 - q0
-        per = -(-n // n_xcd)
-        b = np.arange(per * n_xcd)
-        idx = (b % n_xcd) * per + b // n_xcd
-        okb = idx < n
-        pl = np.zeros((len(b), 2), dtype=np.int32)
-        pl[:, 0] = -1
-        pl[okb, 0], pl[okb, 1] = g[q0 + idx[okb]], pp[q0 + idx[okb]]
-        plist_parts.append(pl)
-        rows.append(rows[-1] + len(b))
-    plist = np.concatenate(plist_parts) if plist_parts else np.zeros((0, 2), np.int32)
-    # first gchunk1 row of each group (plan_global: GCHUNK chunks of every item, in order)
-    crow = np.concatenate([[0], np.cumsum(-(-c // GCHUNK))]).astype(np.int64)
-    part_groups = np.stack([crow[item_b], np.asarray(rows, np.int64)], axis=1).reshape(-1)
+    per = -(-nk // n_xcd)
+    b = np.arange(per * n_xcd)
+    idx = (b % n_xcd) * per + b // n_xcd
+    okb = idx < nk
+    plist = np.zeros((len(b), 2), dtype=np.int32)
+    plist[:, 0] = -1
+    plist[okb, 0], plist[okb, 1] = g[idx[okb]], pp[idx[okb]]
     return dict(gpart=gpart, plist=plist, n_cur=nk * int(part_e), n_prev=int(fsz.sum()),
                 n_pcnt=rc0 + int(nrow.sum()), rc0=rc0, kmax=int(K.max()), K=K, inherited=inh,
-                h=h, part_groups=part_groups.astype(np.int64), n_groups=len(item_b) - 1)
+                h=h)
 
 
 def retry_plan(pr, st):
@@ -677,8 +658,6 @@ class OrbitEngine:
         # 4-byte bucket keys (the IDs' low words) while every large-halo ID's high word
         # is 0; a step that meets another one re-runs and the engine keeps 8-byte keys
         self.part_key4 = env('ORBIT_PART_KEY4', '1') != '0'
-        # halo groups whose joins overlap the next group's scatter (oa_step_args.part_groups)
-        self.part_groups = max(1, int(env('ORBIT_PART_GROUPS', 4)))
         # packed-only compare steps write their records from k_step (direct records)
         self.direct = DIRECT
 
@@ -953,8 +932,7 @@ class OrbitEngine:
             if compare and part and self.part_large:
                 key4 = self.part_key4 or plan.ids.itemsize == 4
                 pl = plan_part(glob, counts, halos['prev_cnt'], self.part_e, self.part_kmax,
-                               prev_idx, prev_sets, key4=key4, td_f64=plan.dx == F64,
-                               groups=self.part_groups)
+                               prev_idx, prev_sets, key4=key4, td_f64=plan.dx == F64)
             if pl is not None:
                 pr.part = True
                 i32, i64 = torch.int32, torch.int64
@@ -974,8 +952,6 @@ class OrbitEngine:
                                             device=dev)
                 g['pcnt'] = torch.empty(pl['n_pcnt'], dtype=i32, device=dev)
                 g['rc0'] = pl['rc0']
-                g['part_groups'] = np.ascontiguousarray(pl['part_groups'])   # host array
-                g['n_groups'] = pl['n_groups']
                 g['n_parts'], g['kmax'] = len(pl['plist']), pl['kmax']
                 nh = len(halos)
                 K = np.zeros(nh, np.int64)
@@ -1045,8 +1021,6 @@ class OrbitEngine:
                                           _ptr(inh and inh.cnt))
                 a.pcnt, a.n_pcnt = g['pcnt'].data_ptr(), int(g['pcnt'].numel())
                 a.part_key4, a.part_hi = int(g['key4']), 0
-                a.n_part_groups = g['n_groups']
-                a.part_groups = g['part_groups'].ctypes.data
                 if 'n3' in g:
                     # a non-NULL pointer marks the list as given, even when empty
                     a.gchunk3 = g['ch3'].data_ptr() if g['ch3'] is not None else \

@@ -341,33 +341,3 @@ def test_plan_part_memory_scales_with_halo_size():
     assert retry_plan(pr, N.STATUS_LOOKBACK) == (6144, True)
     pr.entries = 256
     assert retry_plan(pr, N.STATUS_TABLE_OVERFLOW) == (0, False)
-
-
-def test_plan_part_groups():
-    """Halo groups of the partitioned path (oa_step_args.part_groups): consecutive items
-    of about equal partition counts; each group's partitions listed contiguously in
-    plist (every partition once), and its first gchunk1 row that of its first item."""
-    from orbitanalysis_amd.engine import plan_part, GCHUNK
-    cur = np.array([100000, 30000, 250000, 0, 90000, 60000, 120000])
-    prev = np.array([100000, 29000, 240000, 50, -1, 61000, 118000])
-    glob = {'h0': np.arange(len(cur))}
-    for G in (1, 2, 4, 16):
-        pl = plan_part(glob, cur, prev, 4096, 4096, groups=G)
-        K, gr = pl['K'], pl['part_groups'].reshape(-1, 2)
-        assert pl['n_groups'] == len(gr) - 1 <= max(1, min(G, int((K > 0).sum())))
-        assert gr[0].tolist() == [0, 0] and gr[-1, 1] == len(pl['plist'])
-        assert gr[-1, 0] == int(np.sum(-(-cur // GCHUNK)))
-        assert np.all(np.diff(gr, axis=0) >= 0)
-        seen, last = set(), -1
-        row = np.concatenate([[0], np.cumsum(-(-cur // GCHUNK))])
-        for k in range(len(gr) - 1):
-            rows = pl['plist'][gr[k, 1]:gr[k + 1, 1]]
-            rows = rows[rows[:, 0] >= 0]
-            items = set(rows[:, 0].tolist())
-            # groups hold increasing item runs; a group's chunk rows start after the
-            # previous group's items and at or before its own first item's
-            assert items and min(items) > last
-            assert row[last + 1] <= gr[k, 0] <= row[min(items)]
-            last = max(items)
-            seen |= {tuple(r) for r in rows.tolist()}
-        assert len(seen) == K.sum()

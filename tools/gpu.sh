@@ -63,6 +63,9 @@ envsweep)
       rc=$?; echo "$e rep$rep $(grep -o 'k_step [0-9.]* ms' "$O/es_${T}_${e}_$rep.err") $(grep -o '"ms_per_step": [0-9.]*' "$O/es_${T}_${e}_$rep.json")"; ok $rc "envsweep $e"
     done
   done ;;
+pmcbig)
+  TAG=$T bash tools/pmc_big.sh > "$O/pmcbig_$T.out" 2>&1
+  rc=$?; tail -8 "$O/pmcbig_$T.out"; ok $rc pmcbig ;;
 bigsweep)
   # configs[1] under environment settings ($BIG_ENVS: space-separated NAME=VALUE,NAME=VALUE)
   for rep in ${REPS:-1 2}; do
