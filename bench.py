@@ -296,7 +296,11 @@ def main():
                                'algorithm': 'reference join (setdiff1d + in1d + myin1d)'},
                'single_core_searchsorted': {'value': p1['rate'], 'seconds': p1['seconds'],
                                             'algorithm': 'oracle join (argsort + searchsorted)'},
-               'host_cpus': ncpu}
+               'host_cpus': ncpu,
+               'cores_note': ('P = min(16, os.cpu_count()): os.cpu_count() reports the whole '
+                              'host (%d CPUs) but the GPU box allots one GPU 16 host cores, so '
+                              'a pool of os.cpu_count() processes would time-share those 16 '
+                              '(--cpu-workers overrides)' % ncpu)}
         log('cpu baseline: %d procs %.3e/s, 1 core %.3e/s (searchsorted join %.3e/s), parity %s'
             % (workers, pc['rate'], r1['rate'], p1['rate'], cb['identical']))
 

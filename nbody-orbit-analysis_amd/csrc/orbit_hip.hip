@@ -229,6 +229,14 @@ __device__ __forceinline__ void id_split(typename IdT<IDB>::T id, uint32_t &lo, 
 }
 
 // ------------------------------------------------------------------ LDS layout
+// A work-group barrier that waits for this wave's LDS traffic only: global loads in
+// flight stay in flight across it (__syncthreads waits for them too)
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 struct ItemHdr {
     int64_t prefix;                 // direct records: the item's first output record
     uint32_t nonuniform, hi0, pad0, overflow;
@@ -1989,12 +1997,12 @@ __device__ __forceinline__ void block_scan_excl(uint32_t *v, uint32_t n, uint32_
         if (lane >= o) incl += y;
     }
     if (lane == 63) wtot[wave] = incl;
-    __syncthreads();
+    lds_barrier();
     uint32_t run = incl - s;
     for (int w = 0; w < wave; ++w) run += wtot[w];
     for (uint32_t i = 0; i < c; ++i)
         if (b + i < n) { const uint32_t x = v[b + i]; v[b + i] = run; run += x; }
-    __syncthreads();
+    lds_barrier();
 }
 
 // CUR: current chunks (gchunk1), else previous chunks (gchunk2).  A bucket entry holds
@@ -2054,7 +2062,7 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
         const int64_t n0 = min(start + cnt - s0, (int64_t)SCAT_NS);
         if (part) {
             for (uint32_t k = tid; k < K; k += SCAT_WG) lrun[k] = 0u;
-            __syncthreads();
+            lds_barrier();
         }
         uint64_t key[SCAT_PER];
         uint32_t pw[SCAT_PER], pr[SCAT_PER], pm[SCAT_PER];
@@ -2105,7 +2113,7 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
             pr[q] = (pp << 16) | atomicAdd(&lrun[pp], 1u);
         }
         if (!part) continue;                            // uniform
-        __syncthreads();
+        lds_barrier();
         // this sub-chunk's range of every bucket (one device atomic per partition hit),
         // then the runs' first staged indices
         for (uint32_t k = tid; k < K; k += SCAT_WG) {
@@ -2123,9 +2131,11 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
             smeta[e] = pm[q];
             spart[e] = (uint16_t)pp;
         }
-        __syncthreads();
+        lds_barrier();
         // copy-out: consecutive staged records of one partition go to consecutive bucket
         // entries, so a wave's stores are a few contiguous runs, not 64 scattered words
+        // (the work-group's barriers wait for LDS traffic only: these stores stay in
+        // flight into the next sub-chunk)
         for (int64_t s = tid; s < n0; s += SCAT_WG) {
             const uint32_t k = spart[s];
             const uint32_t e = gres[k] + (uint32_t)(s - lrun[k]);
@@ -2140,7 +2150,7 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
                 d[0] = srh[3 * s]; d[1] = srh[3 * s + 1]; d[2] = srh[3 * s + 2];
             }
         }
-        __syncthreads();
+        lds_barrier();
     }
     if (IDB == 8 && KB == 4 && __ballot(badhi) && (threadIdx.x & 63) == 0)
         atomicOr(a.status, OA_STATUS_PART_KEYS);
@@ -2268,7 +2278,9 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     for (uint32_t w = tid; w < nsl; w += PART_WG) slots[w] = 0ull;
     if (tid < 8) flags[tid] = 0u;
     const uint32_t hi0 = (KB == 8 && nc) ? (uint32_t)((uint64_t)ck[0] >> 32) : 0u;
-    __syncthreads();
+    // barriers on LDS traffic only up to the lookups: the previous entries' loads stay
+    // in flight behind the table build (each use waits for its own loads)
+    lds_barrier();
     PSTAMP(1);
     // current bucket -> LDS table: lo32(ID) | (sign << 16 | (entry + 1) << 18) << 32
     const uint32_t pend_cap = PE / 4;
@@ -2294,7 +2306,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
         const uint32_t e = atomicAdd(&flags[0], 1u);
         if (e < pend_cap) pend[e] = val; else flags[2] = 1u;
     }
-    __syncthreads();
+    lds_barrier();
     PSTAMP(2);
     {   // deferred eviction walks (as k_step's)
         const uint32_t npd = min(flags[0], pend_cap);
@@ -2321,7 +2333,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
             }
         }
     }
-    __syncthreads();
+    lds_barrier();
     PSTAMP(3);
     if (flags[2]) {
         if (tid == 0) atomicOr(a.status, OA_STATUS_PART_OVERFLOW);
@@ -2334,7 +2346,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
         const uint32_t i = (uint32_t)u * PART_WG + tid;
         if (i < nc) mlds[i] = (cpw[u] >> 30) << 16;
     }
-    __syncthreads();
+    lds_barrier();
     const bool nonuniform = KB == 8 && flags[3] != 0u;
     const uint32_t nstash = min(flags[1], (uint32_t)STASH);
     uint32_t *cmeta = a.pmeta_cur + cb;
@@ -2424,6 +2436,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
         }
     }
     __syncthreads();
+    PSTAMP(6);
     // the staged records: ranks within their chunks from LDS counters over the dead
     // table, one global atomic per touched chunk for the chunk's slots, then the stores
     // (a halo with more chunks than the counters claims per record)

@@ -66,6 +66,12 @@ envsweep)
 pmcbig)
   TAG=$T bash tools/pmc_big.sh > "$O/pmcbig_$T.out" 2>&1
   rc=$?; tail -8 "$O/pmcbig_$T.out"; ok $rc pmcbig ;;
+pstamps)
+  # per-work-group phases of the large-halo kernels (stamps build: tools/variants.sh with
+  # a "stamps -DOA_STAMPS=1" line)
+  ORBIT_HIP_LIB=$R/nbody-orbit-analysis_amd/variants/lib_stamps.so timeout -k 10 300 \
+    python tools/part_stamps.py > "$O/pstamps_$T.txt" 2>&1
+  rc=$?; tail -12 "$O/pstamps_$T.txt"; ok $rc pstamps ;;
 bigsweep)
   # configs[1] under environment settings ($BIG_ENVS: space-separated NAME=VALUE,NAME=VALUE)
   for rep in ${REPS:-1 2}; do

@@ -28,13 +28,14 @@ for which, name, k in ((1, 'k_part_scatter', 2), (0, 'k_part_join', 8)):
     t = buf.reshape(-1, k).astype(np.float64)
     t = t[t[:, 0] > 0]
     if which == 0:
-        t = t[t[:, 5] > 0]
+        t = t[(t[:, 5] > 0) & (t[:, 6] > 0)]
     t = (t - t[:, :1].min()) / 100.0                       # 100 MHz -> us
     print('%s: %d work-groups, span %.1f us, mean duration %.2f us' % (
         name, len(t), t[:, k - 1 if which else 5].max(), (t[:, 1 if which else 5] - t[:, 0]).mean()))
     if which == 0:
         for nm, a, b in (('loads+clear+bar', 0, 1), ('insert+bar', 1, 2), ('walks+bar', 2, 3),
-                         ('lookup chunk 0', 3, 4), ('rest', 4, 5)):
+                         ('lookup chunk 0', 3, 4), ('lookups rest', 4, 6),
+                         ('records+state words', 6, 5)):
             d = t[:, b] - t[:, a]
             print('  %-16s mean %6.2f p50 %6.2f p90 %6.2f us' % (nm, d.mean(), *np.percentile(d, [50, 90])))
     # concurrency: work-groups alive over time (start stamp 0 .. end stamp)
