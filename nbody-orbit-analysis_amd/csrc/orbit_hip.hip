@@ -1977,11 +1977,11 @@ __device__ __forceinline__ uint32_t part_of(uint64_t id, uint32_t K) {
 
 // LDS of one k_part_scatter work-group: per partition its sub-chunk count (scanned in
 // place into the run's first staged index) and reserved bucket index, then the staged
-// records {ID, r̂, position word, state word, partition} of one sub-chunk in partition
-// order, copied out as contiguous runs.
-__host__ __device__ inline int64_t scat_lds_bytes(int kmax, int td_bytes) {
+// records {r̂, key (kb bytes), position word, state word, partition} of one sub-chunk
+// in partition order, copied out as contiguous runs.
+__host__ __device__ inline int64_t scat_lds_bytes(int kmax, int td_bytes, int kb) {
     const int64_t k = ((int64_t)kmax * 8 + 15) & ~int64_t(15);
-    return 64 + k + (int64_t)SCAT_NS * (8 + 3 * td_bytes + 4 + 4 + 2);
+    return 64 + k + (int64_t)SCAT_NS * (3 * td_bytes + kb + 4 + 4 + 2);
 }
 
 // exclusive scan of v[0, n) in place (n <= PART_KMAX), SCAT_WG threads, wtot[>= 4]
@@ -2053,9 +2053,9 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
     uint32_t *lrun = wtot + 16;                         // [K] count -> first staged index
     uint32_t *gres = lrun + K;                          // [K] reserved bucket index
     char *stg = lds + 64 + (((int64_t)K * 8 + 15) & ~int64_t(15));
-    uint64_t *skey = reinterpret_cast<uint64_t *>(stg);
-    TD *srh = reinterpret_cast<TD *>(skey + SCAT_NS);
-    uint32_t *spw = reinterpret_cast<uint32_t *>(srh + 3 * SCAT_NS);
+    TD *srh = reinterpret_cast<TD *>(stg);
+    KEY *skey = reinterpret_cast<KEY *>(srh + 3 * SCAT_NS);
+    uint32_t *spw = reinterpret_cast<uint32_t *>(skey + SCAT_NS);
     uint32_t *smeta = spw + SCAT_NS;
     uint16_t *spart = reinterpret_cast<uint16_t *>(smeta + SCAT_NS);
     for (int64_t s0 = start; s0 < start + cnt; s0 += SCAT_NS) {
@@ -2067,20 +2067,33 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
         uint64_t key[SCAT_PER];
         uint32_t pw[SCAT_PER], pr[SCAT_PER], pm[SCAT_PER];
         V3<TD> rh[SCAT_PER];
-        // every load of the sub-chunk first (independent), then the arithmetic
+        V3<TX> xq[SCAT_PER];
+        V3<TV> vq[SCAT_PER];
+        // every load of the sub-chunk first, then the arithmetic: buffer loads, so lanes
+        // past the sub-chunk read 0 with no branch (a load under a lane test waits for
+        // its data before the next one issues)
+        const int64_t i0 = base + s0;
+        const Rsrc rid = make_rsrc(ids + i0, (uint32_t)n0 * IDB);
+        const Rsrc rx = make_rsrc(CUR ? (const void *)(xs + 3 * i0) : (const void *)(a.meta_prev + i0),
+                                  CUR ? (uint32_t)n0 * 3 * sizeof(TX) : (uint32_t)n0 * 4);
+        const Rsrc rv = make_rsrc(CUR ? (const void *)(vs + 3 * i0) : (const void *)(rhat_prev + 3 * i0),
+                                  (uint32_t)n0 * 3 * (CUR ? sizeof(TV) : sizeof(TD)));
 #pragma unroll
         for (int q = 0; q < SCAT_PER; ++q) {
-            const int64_t j = (int64_t)q * SCAT_WG + tid;
-            key[q] = 0ull;
-            pm[q] = 0u;
-            if (j >= n0) continue;
-            const int64_t i = base + s0 + j;
-            key[q] = (uint64_t)lds_nt(&ids[i]);
-            if (IDB == 8 && KB == 4 && part) badhi |= (uint32_t)(key[q] >> 32) != a.part_hi;
-            if (!CUR) {
-                pm[q] = lds_nt(&a.meta_prev[i]);
-                rh[q] = ld3_nt(rhat_prev, i);
+            const uint32_t j = (uint32_t)q * SCAT_WG + tid;
+            key[q] = (uint64_t)bld<ID, AUX_NT>(rid, j * IDB);
+            if (CUR) {
+                xq[q] = bld3<TX, AUX_NT>(rx, j * 3 * sizeof(TX));
+                vq[q] = bld3<TV, AUX_NT>(rv, j * 3 * sizeof(TV));
+            } else {
+                pm[q] = bld<uint32_t, AUX_NT>(rx, j * 4);
+                rh[q] = bld3<TD, AUX_NT>(rv, j * 3 * sizeof(TD));
             }
+        }
+        if (IDB == 8 && KB == 4 && part) {
+#pragma unroll
+            for (int q = 0; q < SCAT_PER; ++q)
+                badhi |= (int64_t)q * SCAT_WG + tid < n0 && (uint32_t)(key[q] >> 32) != a.part_hi;
         }
 #pragma unroll
         for (int q = 0; q < SCAT_PER; ++q) {
@@ -2091,8 +2104,8 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
             const int64_t p = s0 + j;                   // position in the halo's block
             const int64_t i = base + p;
             if (CUR) {
-                const V3<TX> x = ld3_nt(xs, i);
-                const V3<TV> v = ld3_nt(vs, i);
+                const V3<TX> x = xq[q];
+                const V3<TV> v = vq[q];
                 TD r[3];
                 const uint32_t sgn = frame<TX, TV, TD>(x, v, cb, cf, a, fk, r);
                 if (!part) {
@@ -2116,21 +2129,31 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
         lds_barrier();
         // this sub-chunk's range of every bucket (one device atomic per partition hit),
         // then the runs' first staged indices
-        for (uint32_t k = tid; k < K; k += SCAT_WG) {
-            const uint32_t c = lrun[k];
-            gres[k] = c ? atomicAdd(&ctr[k], c) : 0u;
+        // (up to SCAT_WG partitions the reservations stay in registers until the staging
+        // is done: the atomics' round trip overlaps the scan and the staging writes)
+        const bool kreg = K <= (uint32_t)SCAT_WG;
+        uint32_t res = 0u;
+        if (kreg) {
+            const uint32_t c = tid < (int)K ? lrun[tid] : 0u;
+            if (c) res = atomicAdd(&ctr[tid], c);
+        } else {
+            for (uint32_t k = tid; k < K; k += SCAT_WG) {
+                const uint32_t c = lrun[k];
+                gres[k] = c ? atomicAdd(&ctr[k], c) : 0u;
+            }
         }
         block_scan_excl(lrun, K, wtot);
 #pragma unroll
         for (int q = 0; q < SCAT_PER; ++q) {
             if (pr[q] == 0xFFFFFFFFu) continue;
             const uint32_t pp = pr[q] >> 16, e = lrun[pp] + (pr[q] & 0xFFFFu);
-            skey[e] = key[q];
+            skey[e] = (KEY)key[q];
             srh[3 * e] = rh[q].x; srh[3 * e + 1] = rh[q].y; srh[3 * e + 2] = rh[q].z;
             spw[e] = pw[q];
             smeta[e] = pm[q];
             spart[e] = (uint16_t)pp;
         }
+        if (kreg && tid < (int)K) gres[tid] = res;
         lds_barrier();
         // copy-out: consecutive staged records of one partition go to consecutive bucket
         // entries, so a wave's stores are a few contiguous runs, not 64 scattered words
@@ -2144,7 +2167,7 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
                 TD *d = brh + 3 * o;
                 // key, position and state words non-temporal; a current entry's state
                 // word is the join's (k_part_join stages them)
-                __builtin_nontemporal_store((KEY)skey[s], &bkey[o]);
+                __builtin_nontemporal_store(skey[s], &bkey[o]);
                 __builtin_nontemporal_store(spw[s], &bpos[o]);
                 if (!CUR) __builtin_nontemporal_store(smeta[s], &bmeta[o]);
                 d[0] = srh[3 * s]; d[1] = srh[3 * s + 1]; d[2] = srh[3 * s + 2];
@@ -2225,7 +2248,6 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     const int64_t *gp = a.gpart + GPART_W * (int64_t)g;
     const uint32_t K = (uint32_t)gp[1];
     const int64_t cb = gp[0] + (int64_t)pp * PE;
-    const uint32_t nc = a.pcnt[gp[2] + pp];
     const bool inh = gp[3] != 0;
     const uint32_t Kp = (uint32_t)gp[5], pcap = (uint32_t)gp[6];
     const uint32_t *qcnt = (inh ? a.icnt : a.pcnt) + gp[7];
@@ -2237,50 +2259,60 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     const bool filt = Kp < K;
     const uint32_t q0 = filt ? (uint32_t)pp / (K / Kp) : (uint32_t)pp * (Kp / K);
     const uint32_t nq = filt ? 1u : Kp / K;
-    bool over = nc > PE;
-    for (uint32_t q = 0; q < nq; ++q) over |= qcnt[q0 + q] > pcap;
-    if (over) {
-        if (tid == 0) atomicOr(a.status, OA_STATUS_PART_OVERFLOW);
-        return;
-    }
     const KEY *ck = static_cast<const KEY *>(a.pkey_cur) + cb;
     const uint32_t *cp = a.ppos_cur + cb;
     // Every load of the partition goes out first (both buckets are streamed once):
-    // their HBM latency hides behind the table clear, the inserts and the walks.
+    // their HBM latency hides behind the table clear, the inserts and the walks.  The
+    // loads are buffer loads bounded by the buckets' capacities, so they issue before
+    // the counts arrive and back to back (a load under a lane test waits for its data
+    // before the next one issues); entries past a count are masked where they are used.
     constexpr int CU = PART_E / PART_WG, PU = OA_PU;
     KEY ckey[CU];
     uint32_t cpw[CU];
+    {
+        const Rsrc rk = make_rsrc(ck, PE * KB), rp = make_rsrc(cp, PE * 4);
 #pragma unroll
-    for (int u = 0; u < CU; ++u) {
-        const uint32_t i = (uint32_t)u * PART_WG + tid;
-        ckey[u] = i < nc ? ck[i] : (KEY)0;
-        cpw[u] = i < nc ? cp[i] : 0u;
+        for (int u = 0; u < CU; ++u) {
+            const uint32_t i = (uint32_t)u * PART_WG + tid;
+            ckey[u] = bld<KEY, 0>(rk, i * KB);
+            cpw[u] = bld<uint32_t, 0>(rp, i * 4);
+        }
     }
     const TD *crh0 = static_cast<const TD *>(a.prh_cur) + 3 * cb;
     KEY qkey[PU];
     uint32_t qpos[PU], qmeta[PU];
     V3<TD> qrh[PU];
-    auto load_prev = [&](const KEY *qk, const uint32_t *qp, const uint32_t *qm, const TD *qr,
-                         uint32_t np, uint32_t j0) __attribute__((always_inline)) {
+    // entries [j0, j0 + PART_WG * PU) of previous partition q0 + q, lanes past np read 0
+    auto load_prev = [&](uint32_t q, uint32_t np, uint32_t j0) __attribute__((always_inline)) {
+        const int64_t qo = (int64_t)(q0 + q) * pcap;
+        const Rsrc rk = make_rsrc(qk0 + qo, np * KB), rp = make_rsrc(qp0 + qo, np * 4);
+        const Rsrc rm = make_rsrc(qm0 + qo, np * 4);
+        const Rsrc rr = make_rsrc(qr0 + 3 * qo, np * 3 * (uint32_t)sizeof(TD));
 #pragma unroll
         for (int u = 0; u < PU; ++u) {
             const uint32_t j = j0 + (uint32_t)u * PART_WG + tid;
-            qkey[u] = j < np ? qk[j] : (KEY)0;
-            qpos[u] = j < np ? qp[j] : 0u;
-            qmeta[u] = j < np ? qm[j] : 0u;
-            if (j < np) qrh[u] = ld3(qr, j);
+            qkey[u] = bld<KEY, 0>(rk, j * KB);
+            qpos[u] = bld<uint32_t, 0>(rp, j * 4);
+            qmeta[u] = bld<uint32_t, 0>(rm, j * 4);
+            qrh[u] = bld3<TD, 0>(rr, j * 3 * (uint32_t)sizeof(TD));
         }
     };
-    load_prev(qk0 + (int64_t)q0 * pcap, qp0 + (int64_t)q0 * pcap, qm0 + (int64_t)q0 * pcap,
-              qr0 + 3 * (int64_t)q0 * pcap, qcnt[q0], 0u);
+    load_prev(0u, pcap, 0u);                            // the capacity: the count is in flight
+    const uint32_t nc = a.pcnt[gp[2] + pp];
+    bool over = nc > PE;
+    for (uint32_t q = 0; q < nq; ++q) over |= qcnt[q0 + q] > pcap;
     uint32_t nsl = 2u * nc + 64u;                      // load <= 1/2 where the LDS allows
     nsl = nsl < PS ? nsl : PS;
     for (uint32_t w = tid; w < nsl; w += PART_WG) slots[w] = 0ull;
     if (tid < 8) flags[tid] = 0u;
-    const uint32_t hi0 = (KB == 8 && nc) ? (uint32_t)((uint64_t)ck[0] >> 32) : 0u;
+    const uint32_t hi0 = KB == 8 ? (uint32_t)((uint64_t)ck[0] >> 32) : 0u;
     // barriers on LDS traffic only up to the lookups: the previous entries' loads stay
     // in flight behind the table build (each use waits for its own loads)
     lds_barrier();
+    if (over) {                                         // uniform
+        if (tid == 0) atomicOr(a.status, OA_STATUS_PART_OVERFLOW);
+        return;
+    }
     PSTAMP(1);
     // current bucket -> LDS table: lo32(ID) | (sign << 16 | (entry + 1) << 18) << 32
     const uint32_t pend_cap = PE / 4;
@@ -2357,14 +2389,11 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     const uint64_t hiw = KB == 4 ? (uint64_t)a.part_hi << 32 : 0ull;
     // previous entries, PU per thread: lookups, then the gathers of the matched current
     // r̂ (the partition's own bucket entries), then the angle and state-word arithmetic
+    const Rsrc rcr = make_rsrc(crh0, PE * 3 * (uint32_t)sizeof(TD));
     for (uint32_t q = 0; q < nq; ++q) {
-        const int64_t qo = (int64_t)(q0 + q) * pcap;
-        const KEY *qk = qk0 + qo;
-        const uint32_t *qp = qp0 + qo, *qm = qm0 + qo;
-        const TD *qr = qr0 + 3 * qo;
         const uint32_t np = qcnt[q0 + q];
         for (uint32_t j0 = 0; j0 < np; j0 += (uint32_t)PART_WG * PU) {
-            if (j0 || q) load_prev(qk, qp, qm, qr, np, j0);
+            if (j0 || q) load_prev(q, np, j0);
             uint32_t hit[PU];
 #pragma unroll
             for (int u = 0; u < PU; ++u) {
@@ -2390,10 +2419,12 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
                 }
                 if (m) hit[u] = slot_pos(m) | ((slot_meta(m) >> 16) << 30);
             }
-            V3<TD> crh[PU];
+            V3<TD> crh[PU];                             // a miss reads past the buffer: 0
 #pragma unroll
             for (int u = 0; u < PU; ++u)
-                if (hit[u] != 0xFFFFFFFFu) crh[u] = ld3(crh0, hit[u] & 0x3FFFFFFFu);
+                crh[u] = bld3<TD, 0>(rcr, hit[u] != 0xFFFFFFFFu
+                                              ? (hit[u] & 0x3FFFFFFFu) * 3 * (uint32_t)sizeof(TD)
+                                              : 0x7FFFFFF0u);
             uint16_t rang[PU];
             uint32_t rslot[PU];
 #pragma unroll
@@ -2509,7 +2540,7 @@ int launch_part_k(const oa_step_args &a, hipStream_t st) {
     const int64_t n_scat = a.n_gchunk1 + (a.gchunk3 ? a.n_gchunk3 : a.n_gchunk2);
     if (n_scat > 0) {
         auto k = k_part_scatter<TX, TV, TD, IDB, KB>;
-        const int64_t lds = scat_lds_bytes(a.part_kmax, (int)sizeof(TD));
+        const int64_t lds = scat_lds_bytes(a.part_kmax, (int)sizeof(TD), KB);
         if (int rc = set_lds(k, lds)) return rc;
         hipLaunchKernelGGL(k, dim3((unsigned)n_scat), dim3(SCAT_WG), (size_t)lds,
                            st, a, make_frame_k(a));

@@ -855,7 +855,11 @@ __device__ __forceinline__ int64_t mp_find(const MpSlot *tab, uint64_t cap, uint
 #endif
 constexpr int MP_U = OA_MP_U;
 constexpr int MP_SEG = OA_MP_SEG;
-__global__ __launch_bounds__(256) void k_mp_probe(const void *hp, int kind, int64_t n,
+// KIND: the member ID kind, a template argument so the loads are plain and unconditional
+// (index clamped to the last member): a load under a lane test or a kind switch waits
+// for its data before the next one issues.
+template <int KIND>
+__global__ __launch_bounds__(256) void k_mp_probe(const void *hp, int64_t n,
                                                   MpSlot *tab, uint64_t cap, uint32_t *neg1,
                                                   const uint32_t *filt, uint64_t fbits,
                                                   uint32_t *q, uint32_t *qcnt) {
@@ -870,13 +874,13 @@ __global__ __launch_bounds__(256) void k_mp_probe(const void *hp, int kind, int6
 #pragma unroll
     for (int u = 0; u < MP_U; ++u) {
         const int64_t p = p0 + u * stride;
-        v[u] = p < n ? load_val(hp, p, kind) : 0ull;
+        v[u] = load_val(hp, p < n ? p : n - 1, KIND);
     }
 #pragma unroll
     for (int u = 0; u < MP_U; ++u) {
         const uint64_t h = mix64(v[u]);
         m[u] = filt_mask(h);
-        w[u] = p0 + u * stride < n ? filt[filt_word(h, fbits)] : 0u;
+        w[u] = filt[filt_word(h, fbits)];
     }
 #pragma unroll
     for (int u = 0; u < MP_U; ++u) {
@@ -1137,8 +1141,10 @@ int oa_main_progenitors(const oa_mainprog_args *args, void *stream) {
             // the queue segments after the filter, then their counts
             const uint64_t nseg = mp_segments((uint64_t)a.n_halo_pids);
             uint32_t *q = filt + fwords, *qcnt = q + nseg * MP_SEG;
-            hipLaunchKernelGGL(k_mp_probe, dim3((unsigned)nseg), dim3(256), 0, st, a.halo_pids,
-                               a.halo_kind, a.n_halo_pids, tab, ct, neg1, filt, fbits, q, qcnt);
+            auto probe = a.halo_kind == OA_ID_I64 ? k_mp_probe<OA_ID_I64>
+                       : a.halo_kind == OA_ID_I32 ? k_mp_probe<OA_ID_I32> : k_mp_probe<OA_ID_U32>;
+            hipLaunchKernelGGL(probe, dim3((unsigned)nseg), dim3(256), 0, st, a.halo_pids,
+                               a.n_halo_pids, tab, ct, neg1, filt, fbits, q, qcnt);
             if (int rc = check_launch("k_mp_probe")) return rc;
             hipLaunchKernelGGL(k_mp_resolve, dim3((unsigned)((nseg * MP_SEG + 255) / 256)), dim3(256), 0,
                                st, a.halo_pids, a.halo_kind, tab, ct, q, qcnt, (uint32_t)nseg);

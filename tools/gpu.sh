@@ -118,7 +118,7 @@ ab)
       ORBIT_HIP_LIB=$lib timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline \
         ${BENCH_ARGS:-} > "$O/ab_${T}_${v}_$rep.json" 2> "$O/ab_${T}_${v}_$rep.err"
       rc=$?; echo "$v rep$rep $(grep -o 'k_step [0-9.]* ms' "$O/ab_${T}_${v}_$rep.err") \
-$(grep -o '"ms_per_step": [0-9.]*' "$O/ab_${T}_${v}_$rep.json")"; ok $rc "ab $v"
+$(grep -o '"ms_per_step": [0-9.]*\|"kernel_ms": [0-9.]*' "$O/ab_${T}_${v}_$rep.json" | tr '\n' ' ')"; ok $rc "ab $v"
     done
   done ;;
 pab)
