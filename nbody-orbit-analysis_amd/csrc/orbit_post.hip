@@ -144,7 +144,11 @@ __device__ void bitonic_pairs(uint64_t *s, uint32_t *x, int P) {
 // Dynamic LDS sized by the host for this round: a.lds_keys sort slots (power of two,
 // >= every halo's kept count) and a.lds_old cached old keys (halos with more search
 // the old list in global memory), so several work-groups share a CU.
-constexpr int CT = 256;
+// KIND: the apsis ID kind (a template argument: the loads below are unconditional, index
+// clamped, so CL_U of them are in flight per thread; a load under a lane test or a kind
+// switch waits for its data before the next one issues)
+constexpr int CT = 256, CL_U = 4;
+template <int KIND>
 __global__ __launch_bounds__(CT) void k_collate_new(const oa_collate_args a) {
     extern __shared__ __attribute__((aligned(16))) char cl_smem[];
     uint64_t *sk = reinterpret_cast<uint64_t *>(cl_smem);
@@ -166,11 +170,39 @@ __global__ __launch_bounds__(CT) void k_collate_new(const oa_collate_args a) {
     if (threadIdx.x == 0) s_m = 0;
     __syncthreads();
     if (cached)
-        for (int i = threadIdx.x; i < on; i += CT) ok[i] = a.old_keys[ob + i];
-    for (int i = threadIdx.x; i < nraw; i += CT) {
-        if (a.keep_lut[a.angles[s0 + i]]) {
-            const int p = atomicAdd(&s_m, 1);
-            sk[p] = to_key(load_val(a.apsis_ids, s0 + i, a.in_kind), a.key_signed);
+        for (int i0 = 0; i0 < on; i0 += CL_U * CT) {
+            uint64_t t[CL_U];
+#pragma unroll
+            for (int u = 0; u < CL_U; ++u) {
+                const int64_t i = i0 + u * CT + threadIdx.x;
+                t[u] = a.old_keys[ob + (i < on ? i : on - 1)];
+            }
+#pragma unroll
+            for (int u = 0; u < CL_U; ++u) {
+                const int64_t i = i0 + u * CT + threadIdx.x;
+                if (i < on) ok[i] = t[u];
+            }
+        }
+    for (int i0 = 0; i0 < nraw; i0 += CL_U * CT) {
+        uint16_t an[CL_U];
+        uint64_t id[CL_U];
+#pragma unroll
+        for (int u = 0; u < CL_U; ++u) {
+            const int i = i0 + u * CT + (int)threadIdx.x;
+            const int64_t r = s0 + (i < nraw ? i : nraw - 1);
+            an[u] = a.angles[r];
+            id[u] = load_val(a.apsis_ids, r, KIND);
+        }
+        uint8_t kp[CL_U];
+#pragma unroll
+        for (int u = 0; u < CL_U; ++u) kp[u] = a.keep_lut[an[u]];
+#pragma unroll
+        for (int u = 0; u < CL_U; ++u) {
+            const int i = i0 + u * CT + (int)threadIdx.x;
+            if (i < nraw && kp[u]) {
+                const int p = atomicAdd(&s_m, 1);
+                sk[p] = to_key(id[u], a.key_signed);
+            }
         }
     }
     __syncthreads();
@@ -272,16 +304,42 @@ __global__ __launch_bounds__(CT) void k_collate_merge(const oa_collate_args a) {
     const int64_t ob = a.old_off[j], on = a.old_off[j + 1] - ob;
     const int64_t no = a.new_off[j];
     const bool table = on <= a.lds_old;                   // uniform
-    for (int q = threadIdx.x; q < u; q += CT) { nk[q] = a.w_keys[base + q]; nfp[q] = a.w_fp[base + q]; }
+    // (loads unconditional at clamped indices, CL_U per thread in flight)
+    for (int q0 = 0; q0 < u; q0 += CL_U * CT) {
+        uint64_t k[CL_U];
+        int f[CL_U];
+#pragma unroll
+        for (int e = 0; e < CL_U; ++e) {
+            const int q = q0 + e * CT + (int)threadIdx.x, qc = q < u ? q : u - 1;
+            k[e] = a.w_keys[base + qc];
+            f[e] = a.w_fp[base + qc];
+        }
+#pragma unroll
+        for (int e = 0; e < CL_U; ++e) {
+            const int q = q0 + e * CT + (int)threadIdx.x;
+            if (q < u) { nk[q] = k[e]; nfp[q] = f[e]; }
+        }
+    }
     if (threadIdx.x == 0) nfp[u] = a.w_found[j];
     if (table)
         for (int i = threadIdx.x; i <= on; i += CT) { shift[i] = 0; if (i < on) fadd[i] = 0; }
     __syncthreads();
     if (table) {
-        for (int q = threadIdx.x; q < u; q += CT) {
-            const int lb = (int)a.w_lb[base + q];
-            if (nfp[q + 1] == nfp[q]) atomicAdd(&shift[lb], 1);      // absent from the old list
-            else fadd[lb] = (int)a.w_cnt[base + q];                // found at old position lb
+        for (int q0 = 0; q0 < u; q0 += CL_U * CT) {
+            int lb[CL_U], c[CL_U];
+#pragma unroll
+            for (int e = 0; e < CL_U; ++e) {
+                const int q = q0 + e * CT + (int)threadIdx.x, qc = q < u ? q : u - 1;
+                lb[e] = (int)a.w_lb[base + qc];
+                c[e] = (int)a.w_cnt[base + qc];
+            }
+#pragma unroll
+            for (int e = 0; e < CL_U; ++e) {
+                const int q = q0 + e * CT + (int)threadIdx.x;
+                if (q >= u) continue;
+                if (nfp[q + 1] == nfp[q]) atomicAdd(&shift[lb[e]], 1);  // absent from the old list
+                else fadd[lb[e]] = c[e];                                // found at old position lb
+            }
         }
         __syncthreads();
         // inclusive scan of shift[0 .. on] (thread t: the run [t c, t c + c))
@@ -303,9 +361,9 @@ __global__ __launch_bounds__(CT) void k_collate_merge(const oa_collate_args a) {
         int64_t cnt[MU];
 #pragma unroll
         for (int e = 0; e < MU; ++e) {
-            const int64_t i = i0 + (int64_t)e * CT;
-            key[e] = i < on ? a.old_keys[ob + i] : 0ull;
-            cnt[e] = i < on ? a.old_cnt[ob + i] : 0;
+            const int64_t i = i0 + (int64_t)e * CT, ic = i < on ? i : on - 1;
+            key[e] = a.old_keys[ob + ic];
+            cnt[e] = a.old_cnt[ob + ic];
         }
 #pragma unroll
         for (int e = 0; e < MU; ++e) {
@@ -1034,12 +1092,15 @@ int oa_collate_step(const oa_collate_args *args, void *stream) {
     const int64_t lds1 = (int64_t)a.lds_keys * 12 + 4 + (int64_t)a.lds_old * 8;
     const int64_t lds2 = (int64_t)a.lds_keys * 12 + 8 + (int64_t)a.lds_old * 8 + 4;
     if (lds1 > 150 * 1024) return fail(OA_E_ARG, "oa_collate_step: LDS request too large");
-    if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_collate_new),
+    auto knew = a.in_kind == OA_ID_I64 ? k_collate_new<OA_ID_I64>
+              : a.in_kind == OA_ID_U64 ? k_collate_new<OA_ID_U64>
+              : a.in_kind == OA_ID_I32 ? k_collate_new<OA_ID_I32> : k_collate_new<OA_ID_U32>;
+    if (hipFuncSetAttribute(reinterpret_cast<const void *>(knew),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1) != hipSuccess ||
         hipFuncSetAttribute(reinterpret_cast<const void *>(k_collate_merge),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2) != hipSuccess)
         return fail(OA_E_LAUNCH, "oa_collate_step: hipFuncSetAttribute");
-    hipLaunchKernelGGL(k_collate_new, dim3(a.n_halos), dim3(CT), (size_t)lds1, st, a);
+    hipLaunchKernelGGL(knew, dim3(a.n_halos), dim3(CT), (size_t)lds1, st, a);
     if (int rc = check_launch("k_collate_new")) return rc;
     hipLaunchKernelGGL(k_collate_offsets, dim3(1), dim3(1024), 0, st, a);
     if (int rc = check_launch("k_collate_offsets")) return rc;
