@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OA_ABI_VERSION 14
+#define OA_ABI_VERSION 15
 
 #define OA_OK 0
 #define OA_E_ARG (-1)       /* invalid argument / unsupported dtype plan */
@@ -178,7 +178,7 @@ typedef struct oa_step_args {
      *                   (LDS-staged: each partition's entries leave as one run); the
      *                   previous chunks (gchunk2) of halos without an inherited set
      *                   into a fresh previous set, from the position-order state
-     *   k_part_join     one work-group per plist row (LDS: oa_part_lds_bytes): LDS table
+     *   k_part_join     one work-group per prow row (LDS: oa_part_lds_bytes): LDS table
      *                   of a current bucket, lookups of the previous bucket(s) holding
      *                   its IDs, the state word of every matched current entry; each
      *                   apsis record is appended to its previous-block chunk (gchunk2
@@ -187,13 +187,18 @@ typedef struct oa_step_args {
      *   oa_compact      ranks each chunk's records by position (k_gather_recs)
      * The position-order rhat_out / meta_out of these halos are NOT written
      * (oa_part_unbucket restores them from the set when a caller needs them).      */
-    int32_t n_parts;            /* rows of plist (padding rows included)              */
+    int32_t n_parts;            /* rows of prow (padding rows included)               */
     int32_t part_kmax;          /* largest K of any global item                       */
     int32_t part_e;             /* current bucket capacity = LDS table entries of one
                                    partition (multiple of 64, <= oa_build_info(4))    */
     int32_t part_slots;         /* its cuckoo slots (part_e < slots <= 1.5 build max) */
-    const int32_t *plist;       /* [n_parts] (global item g = item - n_items, partition)
-                                   pairs; g = -1: an idle padding row                */
+    const int64_t *prow;        /* [n_parts] join work-group descriptors, 16 int64:
+                                   [0..8] the gpart row of its global item g, [9] the
+                                   partition, [10] g (-1: an idle padding row), [11]
+                                   the item's scratch_off, [12] its record chunks
+                                   (ceil(previous block / oa_build_info(7))), [13] the
+                                   halo's out_slot (one row: a work-group's first
+                                   loads need no second, dependent one)              */
     const int64_t *gpart;       /* per global item, oa_build_info(6) = 16 int64:
                                    [0] current set base (entries; partition p at
                                    base + p * part_e), [1] K, [2] index of its first

@@ -13,7 +13,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.abspath(__file__))
 # ORBIT_HIP_LIB selects an alternative build (kernel variants for tuning sweeps)
 LIB_PATH = os.environ.get('ORBIT_HIP_LIB') or os.path.join(PKG, 'liborbit_hip.so')
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -50,7 +50,7 @@ class StepArgs(ctypes.Structure):
                 ('gchunk1', c_vp), ('gchunk2', c_vp), ('gtab', c_vp), ('gkeys', c_vp),
                 ('gvals', c_vp), ('gtab_total', c_i64), ('scratch_pos', c_vp),
                 ('n_parts', c_i32), ('part_kmax', c_i32), ('part_e', c_i32), ('part_slots', c_i32),
-                ('plist', c_vp), ('gpart', c_vp),
+                ('prow', c_vp), ('gpart', c_vp),
                 ('pkey_cur', c_vp), ('ppos_cur', c_vp), ('pmeta_cur', c_vp), ('prh_cur', c_vp),
                 ('pkey_prev', c_vp), ('ppos_prev', c_vp), ('pmeta_prev', c_vp), ('prh_prev', c_vp),
                 ('ikey', c_vp), ('ipos', c_vp), ('imeta', c_vp), ('irh', c_vp), ('icnt', c_vp),

@@ -111,15 +111,15 @@ __device__ uint64_t g_stamps[STAMP_MAX_WG * STAMP_N];
 // the last word: a diagnostic value of the work-group (table walks)
 #define DIAG(v) do { if (threadIdx.x == 0 && blockIdx.x < STAMP_MAX_WG) \
     g_stamps[blockIdx.x * STAMP_N + STAMP_N - 1] = (v); } while (0)
-// large-halo partition kernels: 8 stamps per work-group of k_part_join, then 2 per
-// work-group of k_part_scatter
+// large-halo partition kernels: 8 stamps per work-group of k_part_join, then 8 per
+// work-group of k_part_scatter (start, its first sub-chunk's phases, end)
 constexpr int PSTAMP_N = 8;
 __device__ uint64_t g_pstamps[STAMP_MAX_WG * PSTAMP_N];
-__device__ uint64_t g_sstamps[STAMP_MAX_WG * 2];
+__device__ uint64_t g_sstamps[STAMP_MAX_WG * PSTAMP_N];
 #define PSTAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < STAMP_MAX_WG) \
     g_pstamps[blockIdx.x * PSTAMP_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define SSTAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < STAMP_MAX_WG) \
-    g_sstamps[blockIdx.x * 2 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+    g_sstamps[blockIdx.x * PSTAMP_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define WSTAMP(k) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < STAMP_MAX_WG) \
     g_stamps[blockIdx.x * STAMP_N + STAMP_NP + 3 * (threadIdx.x >> 6) + (k)] = \
         __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -2126,7 +2126,9 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
             pr[q] = (pp << 16) | atomicAdd(&lrun[pp], 1u);
         }
         if (!part) continue;                            // uniform
+        if (s0 == start) SSTAMP(1);
         lds_barrier();
+        if (s0 == start) SSTAMP(2);
         // this sub-chunk's range of every bucket (one device atomic per partition hit),
         // then the runs' first staged indices
         // (up to SCAT_WG partitions the reservations stay in registers until the staging
@@ -2143,6 +2145,7 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
             }
         }
         block_scan_excl(lrun, K, wtot);
+        if (s0 == start) SSTAMP(3);
 #pragma unroll
         for (int q = 0; q < SCAT_PER; ++q) {
             if (pr[q] == 0xFFFFFFFFu) continue;
@@ -2155,6 +2158,7 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
         }
         if (kreg && tid < (int)K) gres[tid] = res;
         lds_barrier();
+        if (s0 == start) SSTAMP(4);
         // copy-out: consecutive staged records of one partition go to consecutive bucket
         // entries, so a wave's stores are a few contiguous runs, not 64 scattered words
         // (the work-group's barriers wait for LDS traffic only: these stores stay in
@@ -2174,6 +2178,7 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
             }
         }
         lds_barrier();
+        if (s0 == start) SSTAMP(5);
     }
     if (IDB == 8 && KB == 4 && __ballot(badhi) && (threadIdx.x & 63) == 0)
         atomicOr(a.status, OA_STATUS_PART_KEYS);
@@ -2182,8 +2187,13 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
 // Current and previous chunks interleaved in one grid (their latencies overlap):
 // even work-groups take current chunks, odd ones previous chunks, then the longer
 // list's remainder.
+#ifdef OA_SCAT_WPE
+#define SCAT_ATTR __attribute__((amdgpu_waves_per_eu(OA_SCAT_WPE)))
+#else
+#define SCAT_ATTR
+#endif
 template <typename TX, typename TV, typename TD, int IDB, int KB>
-__global__ __launch_bounds__(SCAT_WG) void k_part_scatter(const oa_step_args a, const FrameK fk) {
+__global__ __launch_bounds__(SCAT_WG) SCAT_ATTR void k_part_scatter(const oa_step_args a, const FrameK fk) {
     extern __shared__ __attribute__((aligned(16))) char slds[];
     const int64_t b = blockIdx.x, n1 = a.n_gchunk1,
                   n2 = a.gchunk3 ? a.n_gchunk3 : a.n_gchunk2;
@@ -2195,7 +2205,7 @@ __global__ __launch_bounds__(SCAT_WG) void k_part_scatter(const oa_step_args a, 
     SSTAMP(0);
     if (cur) part_scatter<TX, TV, TD, IDB, true, KB>(a, fk, slds, c);
     else part_scatter<TX, TV, TD, IDB, false, KB>(a, fk, slds, c);
-    SSTAMP(1);
+    SSTAMP(7);
 }
 
 // k_part_join's apsis records staged in LDS before their slots are claimed (16 B each:
@@ -2241,11 +2251,13 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     uint64_t *rbuf = reinterpret_cast<uint64_t *>(flags + 8);           // [2 PART_RB] staged records
     const int tid = threadIdx.x;
     PSTAMP(0);
-    const int32_t g = a.plist[2 * blockIdx.x], pp = a.plist[2 * blockIdx.x + 1];
+    // the work-group's descriptor row: its item's gpart row and the item and halo fields
+    // it needs, in one row (no dependent second load before the bucket loads)
+    const int64_t *gp = a.prow + GPART_W * (int64_t)blockIdx.x;
+    const int64_t g = gp[10];
     if (g < 0) return;                                  // padding row
+    const uint32_t pp = (uint32_t)gp[9];
     const int64_t gi = a.n_items + g;
-    const oa_item it = a.items[gi];
-    const int64_t *gp = a.gpart + GPART_W * (int64_t)g;
     const uint32_t K = (uint32_t)gp[1];
     const int64_t cb = gp[0] + (int64_t)pp * PE;
     const bool inh = gp[3] != 0;
@@ -2458,7 +2470,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
             for (int u = 0; u < PU; ++u) {
                 if (rslot[u] == 0xFFFFFFFFu) continue;
                 const uint32_t p = qpos[u] & 0x3FFFFFFFu;
-                const int64_t s = it.scratch_off + (int64_t)(p & ~(uint32_t)(RCHUNK - 1)) + rslot[u];
+                const int64_t s = gp[11] + (int64_t)(p & ~(uint32_t)(RCHUNK - 1)) + rslot[u];
                 scr_ids[s] = (ID)((uint64_t)qkey[u] | hiw);
                 a.scratch_ang[s] = rang[u];
                 a.scratch_rk[s] = (uint16_t)(p & (RCHUNK - 1));
@@ -2472,7 +2484,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     // table, one global atomic per touched chunk for the chunk's slots, then the stores
     // (a halo with more chunks than the counters claims per record)
     const uint32_t nst = min(*nrec, (uint32_t)PART_RB);
-    const uint32_t nch = (uint32_t)((a.halos[it.h0].prev_cnt + RCHUNK - 1) >> RCHUNK_LOG2);
+    const uint32_t nch = (uint32_t)gp[12];
     uint32_t *lc = reinterpret_cast<uint32_t *>(slots);
     const bool lds_ranks = nch <= 2u * PS;
     if (nst) {
@@ -2495,7 +2507,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
             const uint64_t w = rbuf[2 * e + 1];
             const uint32_t p = (uint32_t)w, c = p >> RCHUNK_LOG2;
             const uint32_t slot = (uint32_t)(w >> 48) + (lds_ranks ? lc[c] : 0u);
-            const int64_t s = it.scratch_off + (int64_t)c * RCHUNK + slot;
+            const int64_t s = gp[11] + (int64_t)c * RCHUNK + slot;
             scr_ids[s] = (ID)rbuf[2 * e];
             a.scratch_ang[s] = (uint16_t)(w >> 32);
             a.scratch_rk[s] = (uint16_t)(p & (RCHUNK - 1));
@@ -2505,8 +2517,7 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     for (uint32_t i = tid; i < nc; i += PART_WG) cmeta[i] = mlds[i];
     // the work-group's record count: one pair of device atomics (halo and item counts)
     if (tid == 0 && *nrec) {
-        const oa_halo &h = a.halos[it.h0];
-        atomicAdd(&a.halo_count[h.out_slot], (int32_t)*nrec);
+        atomicAdd(&a.halo_count[gp[13]], (int32_t)*nrec);
         atomicAdd(&a.item_count[gi], (int32_t)*nrec);
     }
     PSTAMP(5);
@@ -2698,7 +2709,7 @@ int64_t oa_debug_stamps(uint64_t *host, int64_t n) {
 // (which = 0: k_part_join, 8 per work-group; 1: k_part_scatter, 2 per work-group).
 int64_t oa_debug_part_stamps(int32_t which, uint64_t *host, int64_t n) {
 #if OA_STAMPS
-    const int64_t cap = (int64_t)STAMP_MAX_WG * (which ? 2 : PSTAMP_N);
+    const int64_t cap = (int64_t)STAMP_MAX_WG * PSTAMP_N;
     const int64_t m = n < cap ? n : cap;
     hipError_t e = which ? hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sstamps), m * sizeof(uint64_t))
                          : hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pstamps), m * sizeof(uint64_t));
@@ -2750,7 +2761,7 @@ int oa_step(const oa_step_args *args, void *stream) {
     if (a.compare && a.n_gchunk2 > 0 && !a.gchunk2)
         return fail(OA_E_ARG, "null large-halo chunk pointer");
     const bool part = a.compare && !a.onthefly && a.n_parts > 0;
-    if (part && (!a.plist || !a.gpart || !a.pkey_cur || !a.ppos_cur || !a.pmeta_cur ||
+    if (part && (!a.prow || !a.gpart || !a.pkey_cur || !a.ppos_cur || !a.pmeta_cur ||
                  !a.prh_cur || !a.pcnt || !a.scratch_rk || a.n_pcnt < 1 ||
                  (a.id_bytes == 4 && a.part_hi != 0) ||
                  (a.n_gchunk2 > 0 && (!a.pkey_prev || !a.ppos_prev || !a.pmeta_prev ||

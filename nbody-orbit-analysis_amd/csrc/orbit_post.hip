@@ -61,6 +61,15 @@ __device__ __forceinline__ uint64_t load_val(const void *p, int64_t i, int kind)
         default: return (uint64_t) static_cast<const uint32_t *>(p)[i];
     }
 }
+// streamed-once IDs (non-temporal: L2 stays with the tables and filters read at random)
+template <int KIND> __device__ __forceinline__ uint64_t load_val_nt(const void *p, int64_t i) {
+    if constexpr (KIND == OA_ID_I64 || KIND == OA_ID_U64)
+        return __builtin_nontemporal_load(static_cast<const uint64_t *>(p) + i);
+    else if constexpr (KIND == OA_ID_I32)
+        return (uint64_t)(int64_t)__builtin_nontemporal_load(static_cast<const int32_t *>(p) + i);
+    else
+        return (uint64_t)__builtin_nontemporal_load(static_cast<const uint32_t *>(p) + i);
+}
 __device__ __forceinline__ uint64_t to_key(uint64_t v, int key_signed) {
     return key_signed ? v ^ SIGN : v;
 }
@@ -932,7 +941,7 @@ __global__ __launch_bounds__(256) void k_mp_probe(const void *hp, int64_t n,
 #pragma unroll
     for (int u = 0; u < MP_U; ++u) {
         const int64_t p = p0 + u * stride;
-        v[u] = load_val(hp, p < n ? p : n - 1, KIND);
+        v[u] = load_val_nt<KIND>(hp, p < n ? p : n - 1);
     }
 #pragma unroll
     for (int u = 0; u < MP_U; ++u) {

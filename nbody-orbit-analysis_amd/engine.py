@@ -228,6 +228,14 @@ PART_SPREAD = int(_pow2_ceil(int(os.environ.get('ORBIT_PART_SPREAD', 32))))
 GPART_W = 16         # int64 per gpart row (orbit_hip.h)
 
 
+def _gfield(items, name, n):
+    """An item-table field as int64 (zeros when a test's stand-in table lacks it)."""
+    try:
+        return np.asarray(items[name], dtype=np.int64)
+    except (KeyError, ValueError):
+        return np.zeros(n, dtype=np.int64)
+
+
 def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=None, n_xcd=8,
               key4=False, td_f64=None):
     """Partition layout of the global items for the partitioned large-halo path
@@ -243,7 +251,7 @@ def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=No
     snapshot's halo number ``prev_idx``; any K: both are powers of two), else from a
     fresh previous set scattered from the position-order state (mean + 8 sqrt(mean) + 64
     entries per partition).  A previous set is inherited only when its keys have the
-    step's width (``key4``: 4-byte low words) and r̂ in the step's dtype (``td_f64``).  plist deals the partitions to the 8 XCDs
+    step's width (``key4``: 4-byte low words) and r̂ in the step's dtype (``td_f64``).  plist (and its descriptor rows, prow) deals the partitions to the 8 XCDs
     in contiguous runs (work-group b runs on XCD b % 8), so one halo's partitions share
     an L2.  The counters (pcnt) are the current set's, the fresh previous set's, then
     one record counter per previous-block chunk (gchunk2 row, GCHUNK positions; gpart[8]
@@ -301,7 +309,17 @@ def plan_part(glob, cur_cnt, prev_cnt, part_e, kmax, prev_idx=None, prev_sets=No
     plist = np.zeros((len(b), 2), dtype=np.int32)
     plist[:, 0] = -1
     plist[okb, 0], plist[okb, 1] = g[idx[okb]], pp[idx[okb]]
-    return dict(gpart=gpart, plist=plist, n_cur=nk * int(part_e), n_prev=int(fsz.sum()),
+    # the join's per-work-group descriptor rows (oa_step_args.prow): the item's gpart row,
+    # the partition, the item, its scratch base, record chunks and output slot
+    gg = g[idx[okb]]
+    prow = np.zeros((len(b), GPART_W), dtype=np.int64)
+    prow[:, 10] = -1
+    prow[okb, :9] = gpart[gg, :9]
+    prow[okb, 9], prow[okb, 10] = pp[idx[okb]], gg
+    prow[okb, 11] = _gfield(glob, 'scratch_off', ng)[gg]
+    prow[okb, 12] = -(-p[gg] // GCHUNK)
+    prow[okb, 13] = _gfield(glob, 'slot0', ng)[gg]
+    return dict(gpart=gpart, plist=plist, prow=prow, n_cur=nk * int(part_e), n_prev=int(fsz.sum()),
                 n_pcnt=rc0 + int(nrow.sum()), rc0=rc0, kmax=int(K.max()), K=K, inherited=inh,
                 h=h)
 
@@ -936,7 +954,7 @@ class OrbitEngine:
             if pl is not None:
                 pr.part = True
                 i32, i64 = torch.int32, torch.int64
-                g['plist'] = _up(pl['plist'].reshape(-1), dev)
+                g['prow'] = _up(pl['prow'].reshape(-1), dev)
                 g['gpart'] = _up(pl['gpart'].reshape(-1), dev)
                 # this step's current bucket set: the next step's previous state
                 kt = i32 if key4 else i64
@@ -1010,7 +1028,7 @@ class OrbitEngine:
             if pr.part:
                 a.n_parts, a.part_kmax = g['n_parts'], g['kmax']
                 a.part_e, a.part_slots = self.part_e, self.part_slots
-                a.plist, a.gpart = g['plist'].data_ptr(), g['gpart'].data_ptr()
+                a.prow, a.gpart = g['prow'].data_ptr(), g['gpart'].data_ptr()
                 a.pkey_cur, a.ppos_cur = g['pkey_cur'].data_ptr(), g['ppos_cur'].data_ptr()
                 a.pmeta_cur, a.prh_cur = g['pmeta_cur'].data_ptr(), g['prh_cur'].data_ptr()
                 a.pkey_prev, a.ppos_prev = g['pkey_prev'].data_ptr(), g['ppos_prev'].data_ptr()

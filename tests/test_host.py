@@ -317,6 +317,13 @@ def test_plan_part_bucket_sets():
     # every current partition listed once
     pl_ok = pl['plist'][pl['plist'][:, 0] >= 0]
     assert len(pl_ok) == K.sum() and len({tuple(r) for r in pl_ok}) == K.sum()
+    # the join's descriptor rows: the item's gpart row, partition, item, record chunks
+    pr = pl['prow']
+    assert pr.shape == (len(pl['plist']), 16)
+    assert np.array_equal(pr[:, 10], pl['plist'][:, 0]) and np.array_equal(pr[:, 9] * (pr[:, 10] >= 0), pl['plist'][:, 1] * (pl['plist'][:, 0] >= 0))
+    live = pr[:, 10] >= 0
+    assert np.array_equal(pr[live, :9], g[pr[live, 10], :9])
+    assert np.array_equal(pr[live, 12], rows[pr[live, 10]])
 
 
 def test_plan_part_memory_scales_with_halo_size():
