@@ -416,6 +416,18 @@ class ShardedOnTheFly:
         self.otf = OnTheFly(engine)
         self.carry = None
         self.h2d_bytes = 0
+        # per-phase wall times of run() (ms lists by phase) when set to a dict: each phase
+        # boundary synchronises the device, so only an instrumented pass sets it
+        self.timings = None
+        self._t0 = 0.0
+
+    def _mark(self, name):
+        if self.timings is None:
+            return
+        torch.cuda.synchronize(self.eng.device)
+        t = time.perf_counter()
+        self.timings.setdefault(name, []).append((t - self._t0) * 1e3)
+        self._t0 = t
 
     @property
     def rank(self):
@@ -456,6 +468,9 @@ class ShardedOnTheFly:
         shard of it, its device frame state and its bulk velocities are reused."""
         from .sharding import gather_rows
         eng = self.eng
+        if self.timings is not None:
+            torch.cuda.synchronize(eng.device)
+            self._t0 = time.perf_counter()
         if carried is None:
             self.owner.reset()                # a fresh pair: fit the ID ranges on it
         shards, lslices, sels, bulks = [], [], [], []
@@ -474,7 +489,9 @@ class ShardedOnTheFly:
             lslices.append(lsl)
             sels.append(sh.sel)
             bulks.append(sh.bulk)
+        self._mark('shard')
         d = self.otf.compare(shards, lslices, centres, carried=otf_carry, bulks=bulks)
+        self._mark('compare')
         self.carry = (self.otf.carry, sels[0])
         pc, prev, res = d.pc, d.prev, d.res
         nh = len(slices[0])
@@ -495,11 +512,13 @@ class ShardedOnTheFly:
         erow = torch.nonzero(~d.matched_cur).squeeze(1)
         entered = torch.stack([_halo_of(erow, pc.starts, eng.device),
                                _i64(pc.snap['ids'][erow]), sel_c[erow]], dim=1)
+        self._mark('records')
         apsis, = gather_rows(self.group, self.ROOT, apsis)
         if self.world > 1:
             angle_g, angle_v = gather_rows(self.group, self.ROOT, angle_g, angle_v)
         departed, = gather_rows(self.group, self.ROOT, departed)
         entered, = gather_rows(self.group, self.ROOT, entered)
+        self._mark('gather')
         sl1 = np.asarray(slices[1], dtype=np.int64).reshape(-1, 2)
         p_has = (sl1[:, 1] - sl1[:, 0]) > 0            # the reference's np.diff(sl_prev) > 0
         adt = _angles_dtype(pc.plan.coord, ids_dtype, p_has)
@@ -517,6 +536,7 @@ class ShardedOnTheFly:
                       'entered_ids': np.zeros(0, ids_dtype), 'departed_offsets': z,
                       'departed_ids': np.zeros(0, ids_dtype)}
         merged['bulk_velocities'] = [d.bulk_c, d.bulk_p]
+        self._mark('merge+d2h')
         return merged
 
 

@@ -192,6 +192,20 @@ def main():
             units += n_rows[k % S]
     torch.cuda.synchronize()
     wall = time.perf_counter() - t_start
+    phases = None
+    if args.sharded:
+        # an instrumented pass after the timed steps: per-phase wall times of the sharded
+        # run (each boundary synchronises the device)
+        otf.timings = {}
+        for k in range(total_steps + 1, total_steps + 3):
+            h2d(k)
+            torch.cuda.current_stream().wait_event(evs[k])
+            dk, slk = snap_dict(k)
+            _, slp = snap_dict(k - 1)
+            otf.run([dk, None], [slk, slp], [cats[k % S], cats[(k - 1) % S]], carried=otf.carry)
+        phases = {p: float(np.median(v)) for p, v in otf.timings.items()}
+        otf.timings = None
+        log('sharded phases (ms, median of 2): %s' % phases)
     if dist is not None:
         nccl = dist.get_backend() == 'nccl'
         t = torch.tensor([wall], dtype=torch.float64, device=dev if nccl else 'cpu')
@@ -239,6 +253,7 @@ def main():
                                'state carried between snapshots' % (units // args.steps, nh)},
         'compute_ms_per_step': float(np.mean(comp_ms)),
         'compute_only_rate': units / (sum(comp_ms) * 1e-3),
+        'sharded_phases_ms': phases,
         'apsis_last_step': n_apsis,
         'roofline': {'bound': 'pcie', 'achieved': h2d_bytes / h2d_s / 1e9, 'peak': PCIE_PEAK,
                      'unit': 'GB/s', 'frac': h2d_bytes / h2d_s / 1e9 / PCIE_PEAK,
