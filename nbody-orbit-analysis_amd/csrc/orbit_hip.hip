@@ -2252,8 +2252,19 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     const int tid = threadIdx.x;
     PSTAMP(0);
     // the work-group's descriptor row: its item's gpart row and the item and halo fields
-    // it needs, in one row (no dependent second load before the bucket loads)
-    const int64_t *gp = a.prow + GPART_W * (int64_t)blockIdx.x;
+    // it needs, in one row, read by one vector load (lane f: field f) and broadcast with
+    // readlane -- scalar loads of the row were split around the padding-row test and
+    // chained several round trips before the bucket loads
+    int64_t gp[GPART_W];
+    {
+        const Rsrc rrow = make_rsrc(a.prow + GPART_W * (int64_t)blockIdx.x, GPART_W * 8u);
+        const int64_t mine = bld<int64_t, 0>(rrow, (uint32_t)(tid & (GPART_W - 1)) * 8u);
+        const uint32_t lo = (uint32_t)mine, hi = (uint32_t)((uint64_t)mine >> 32);
+#pragma unroll
+        for (int f = 0; f < 14; ++f)
+            gp[f] = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, f) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)lo, f));
+    }
     const int64_t g = gp[10];
     if (g < 0) return;                                  // padding row
     const uint32_t pp = (uint32_t)gp[9];
@@ -2279,6 +2290,11 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     // the counts arrive and back to back (a load under a lane test waits for its data
     // before the next one issues); entries past a count are masked where they are used.
     constexpr int CU = PART_E / PART_WG, PU = OA_PU;
+    // the counts too, as uniform-address vector loads issued first: they are waited for
+    // after the table clear, beside the first bucket data, not on a scalar round trip
+    // before the clear (the table spans every slot, so its size needs no count)
+    const uint32_t nc_v = bld<uint32_t, 0>(make_rsrc(a.pcnt + gp[2] + pp, 4u), 0u);
+    const uint32_t np0_v = bld<uint32_t, 0>(make_rsrc(qcnt + q0, 4u), 0u);
     KEY ckey[CU];
     uint32_t cpw[CU];
     {
@@ -2310,17 +2326,16 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
         }
     };
     load_prev(0u, pcap, 0u);                            // the capacity: the count is in flight
-    const uint32_t nc = a.pcnt[gp[2] + pp];
-    bool over = nc > PE;
-    for (uint32_t q = 0; q < nq; ++q) over |= qcnt[q0 + q] > pcap;
-    uint32_t nsl = 2u * nc + 64u;                      // load <= 1/2 where the LDS allows
-    nsl = nsl < PS ? nsl : PS;
+    const uint32_t nsl = PS;                            // load <= 0.67 (4096 in 6144)
     for (uint32_t w = tid; w < nsl; w += PART_WG) slots[w] = 0ull;
     if (tid < 8) flags[tid] = 0u;
     const uint32_t hi0 = KB == 8 ? (uint32_t)((uint64_t)ck[0] >> 32) : 0u;
     // barriers on LDS traffic only up to the lookups: the previous entries' loads stay
     // in flight behind the table build (each use waits for its own loads)
     lds_barrier();
+    const uint32_t nc = uni(nc_v);
+    bool over = nc > PE || uni(np0_v) > pcap;
+    for (uint32_t q = 1; q < nq; ++q) over |= qcnt[q0 + q] > pcap;
     if (over) {                                         // uniform
         if (tid == 0) atomicOr(a.status, OA_STATUS_PART_OVERFLOW);
         return;

@@ -416,18 +416,37 @@ class ShardedOnTheFly:
         self.otf = OnTheFly(engine)
         self.carry = None
         self.h2d_bytes = 0
-        # per-phase wall times of run() (ms lists by phase) when set to a dict: each phase
-        # boundary synchronises the device, so only an instrumented pass sets it
+        # per-phase times of run() (ms lists by phase) when set to a dict: with
+        # timing_sync each phase boundary synchronises the device (wall time per phase);
+        # without, the host time between boundaries ('host:' phases) and the stream time
+        # between events recorded at them ('gpu:' phases) are kept, unperturbed
         self.timings = None
+        self.timing_sync = True
         self._t0 = 0.0
+        self._evs = []
 
     def _mark(self, name):
         if self.timings is None:
             return
-        torch.cuda.synchronize(self.eng.device)
+        if self.timing_sync:
+            torch.cuda.synchronize(self.eng.device)
         t = time.perf_counter()
-        self.timings.setdefault(name, []).append((t - self._t0) * 1e3)
+        self.timings.setdefault(('' if self.timing_sync else 'host:') + name, []).append(
+            (t - self._t0) * 1e3)
         self._t0 = t
+        if not self.timing_sync:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self._evs.append((name, ev))
+
+    def _close_marks(self):
+        """Stream times between this call's events (the call's last D2H has completed)."""
+        if self.timings is None or self.timing_sync or not self._evs:
+            return
+        self._evs[-1][1].synchronize()
+        for (_, a), (name, b) in zip(self._evs[:-1], self._evs[1:]):
+            self.timings.setdefault('gpu:' + name, []).append(a.elapsed_time(b))
+        self._evs = []
 
     @property
     def rank(self):
@@ -469,8 +488,11 @@ class ShardedOnTheFly:
         from .sharding import gather_rows
         eng = self.eng
         if self.timings is not None:
-            torch.cuda.synchronize(eng.device)
+            if self.timing_sync:
+                torch.cuda.synchronize(eng.device)
             self._t0 = time.perf_counter()
+            self._evs = []
+            self._mark('start')
         if carried is None:
             self.owner.reset()                # a fresh pair: fit the ID ranges on it
         shards, lslices, sels, bulks = [], [], [], []
@@ -537,6 +559,7 @@ class ShardedOnTheFly:
                       'departed_ids': np.zeros(0, ids_dtype)}
         merged['bulk_velocities'] = [d.bulk_c, d.bulk_p]
         self._mark('merge+d2h')
+        self._close_marks()
         return merged
 
 

@@ -164,6 +164,8 @@ def main():
                                  starts=pp.starts, counts=pp.counts, exists=np.arange(nh),
                                  plan=pp.plan), bulk0)
     total_steps = 1 + args.steps              # 1 warm-up step
+    if args.sharded:                          # unperturbed per-phase host / stream times
+        otf.timings, otf.timing_sync = {}, False
     comp_ms, units, outs = [], 0, None
     t_start = None
     for k in range(1, total_steps + 1):
@@ -194,16 +196,17 @@ def main():
     wall = time.perf_counter() - t_start
     phases = None
     if args.sharded:
-        # an instrumented pass after the timed steps: per-phase wall times of the sharded
-        # run (each boundary synchronises the device)
-        otf.timings = {}
+        # the timed steps' host and stream time per phase (medians), then an instrumented
+        # pass: per-phase wall times of the sharded run (each boundary synchronises)
+        phases = {p: float(np.median(v[1:])) for p, v in otf.timings.items() if len(v) > 1}
+        otf.timings, otf.timing_sync = {}, True
         for k in range(total_steps + 1, total_steps + 3):
             h2d(k)
             torch.cuda.current_stream().wait_event(evs[k])
             dk, slk = snap_dict(k)
             _, slp = snap_dict(k - 1)
             otf.run([dk, None], [slk, slp], [cats[k % S], cats[(k - 1) % S]], carried=otf.carry)
-        phases = {p: float(np.median(v)) for p, v in otf.timings.items()}
+        phases.update({p: float(np.median(v)) for p, v in otf.timings.items()})
         otf.timings = None
         log('sharded phases (ms, median of 2): %s' % phases)
     if dist is not None:
