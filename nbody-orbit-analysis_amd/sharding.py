@@ -122,7 +122,7 @@ class IdRangeOwner:
         else:
             mn, mx = _I64_MAX, _I64_MIN + 1
         if dist.get_world_size(group) > 1:
-            r = torch.tensor([mn, -mx], dtype=torch.int64, device=_comm_device())
+            r = _h2d(np.asarray([mn, -mx], dtype=np.int64), _comm_device())
             dist.all_reduce(r, op=dist.ReduceOp.MIN, group=group)
             mn, mx = int(r[0]), -int(r[1])
         self.lo, self.hi = (mn, mx + 1) if mn <= mx else (0, 1)
@@ -194,6 +194,19 @@ def stripe_rows(starts, n, hb, r):
     return row(int(hb[r])), row(int(hb[r + 1]))
 
 
+def _h2d(a, device):
+    """A small host array -> tensor on ``device`` through a page-locked staging block
+    (``engine._up``: asynchronous on the current stream).  A pageable ``.to(device)`` is
+    a synchronous copy that waits behind whatever DMA is in flight -- a double-buffered
+    snapshot H2D on a copy stream held each sharded on-the-fly step's host ~70 ms
+    (bench_onthefly --sharded, r04q)."""
+    a = np.ascontiguousarray(a)
+    if torch.device(device).type != 'cuda':
+        return torch.from_numpy(a)
+    from .engine import _up
+    return _up(a, device)
+
+
 # ------------------------------------------------------------------ collectives
 def _comm_device():
     import torch.distributed as dist
@@ -221,7 +234,7 @@ class RowExchange:
             self.recv = list(self.send)
             return
         self.dev = _comm_device()
-        s = torch.tensor(self.send, dtype=torch.int64, device=self.dev)
+        s = _h2d(np.asarray(self.send, dtype=np.int64), self.dev)
         r = torch.empty_like(s)
         dist.all_to_all_single(r, s, group=group)
         self.recv = [int(x) for x in r.cpu()]
@@ -297,7 +310,7 @@ def all_true(flag, group=None):
     import torch.distributed as dist
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return bool(flag)
-    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=_comm_device())
+    t = _h2d(np.asarray([1 if flag else 0], dtype=np.int32), _comm_device())
     dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
     return bool(int(t.item()))
 
@@ -405,12 +418,12 @@ def stripe_shard(snapshot, starts, owner, group, device, bulk_fn=None, n=None):
         bulk = gather_bulk(rows, h0, nh, group) if world > 1 else \
             (np.asarray(rows) if rows is not None else np.zeros((0, 3)))
     owner.fit_group(st['ids'], group)
-    st_t = torch.from_numpy(starts).to(device)
+    st_t = _h2d(starts, device)
     nst = int(st['ids'].shape[0])
     # every stripe row's block: the stripe holds blocks [h0, h1) (host layout)
     sc = (np.append(starts[h0 + 1:h1], hi) - starts[h0:h1]) if h1 > h0 else np.zeros(0, np.int64)
     sblock = torch.repeat_interleave(torch.arange(h0, h1, device=device),
-                                     torch.from_numpy(sc.astype(np.int64)).to(device),
+                                     _h2d(sc.astype(np.int64), device),
                                      output_size=nst) if nst else \
         torch.zeros(0, dtype=torch.int64, device=device)
     if world > 1:
@@ -426,7 +439,7 @@ def stripe_shard(snapshot, starts, owner, group, device, bulk_fn=None, n=None):
         got = _exchange_rows(hist, group)       # row d of every sender: (world, nh)
         counts = got.sum(0).cpu().numpy().astype(np.int64)[:nh] if nh else np.zeros(0, np.int64)
         block = torch.repeat_interleave(torch.arange(nh, device=device),
-                                        torch.from_numpy(counts).to(device),
+                                        _h2d(counts, device),
                                         output_size=int(counts.sum())) if nh else sel
     else:
         sel = torch.arange(lo, hi, dtype=torch.int64, device=device)
@@ -580,7 +593,7 @@ class ShardedEngine:
             mine[:hi - lo] = rows[lo:hi]
         dev = _comm_device()
         out = torch.empty((nl * self.world, 6), dtype=torch.float64, device=dev)
-        dist.all_gather_into_tensor(out, torch.from_numpy(mine).to(dev), group=self.group)
+        dist.all_gather_into_tensor(out, _h2d(mine, dev), group=self.group)
         return out[:nh]
 
     # ---------------------------------------------------------------- shard
@@ -594,7 +607,7 @@ class ShardedEngine:
         import torch.distributed as dist
         nh = len(counts)
         dev = _comm_device()
-        mine = torch.from_numpy(np.ascontiguousarray(counts, dtype=np.int64)).to(dev)
+        mine = _h2d(np.ascontiguousarray(counts, dtype=np.int64), dev)
         allc = torch.empty(self.world * nh, dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(allc, mine, group=self.group)
         cnt_all = allc.cpu().numpy().reshape(self.world, nh)
@@ -602,12 +615,12 @@ class ShardedEngine:
         tot = cnt_all.sum(0)
         gstart = np.cumsum(tot) - tot
         n = int(np.sum(counts))
-        c = torch.from_numpy(np.ascontiguousarray(counts, dtype=np.int64)).to(self.device)
+        c = _h2d(np.ascontiguousarray(counts, dtype=np.int64), self.device)
         row = torch.arange(n, dtype=torch.int64, device=self.device)
         # gpos = before[block] + (row - starts[block]); sel = gstart[block] + gpos
-        b0 = torch.from_numpy(before - starts).to(self.device)
+        b0 = _h2d(before - starts, self.device)
         gpos = torch.repeat_interleave(b0, c, output_size=n) + row
-        sel = torch.repeat_interleave(torch.from_numpy(gstart).to(self.device), c,
+        sel = torch.repeat_interleave(_h2d(gstart, self.device), c,
                                       output_size=n) + gpos
         digest = hashlib.sha256(np.ascontiguousarray(cnt_all, dtype='<i8').tobytes()).hexdigest()[:16]
         layout = 'rank-major/world=%d/blocks=%s' % (self.world, digest)

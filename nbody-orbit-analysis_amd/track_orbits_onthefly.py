@@ -26,6 +26,7 @@ import torch
 
 from . import _native as N
 from .engine import OrbitEngine, SnapshotState, to_device, F64, np_dtype, is_array
+from .sharding import _h2d
 
 _TORCH = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64}
 
@@ -213,7 +214,7 @@ class OnTheFly:
 
         def halo_of(pos, starts):
             # block of each selected position (blocks tile [0, n) in halo order)
-            st = torch.from_numpy(np.asarray(starts, dtype=np.int64)).to(eng.device)
+            st = _h2d(np.asarray(starts, dtype=np.int64), eng.device)
             return torch.searchsorted(st, pos, right=True) - 1
         # departed: setdiff1d(previous, current) per halo (:145), i.e. the sorted unique
         # IDs of the unmatched previous rows (which already sit in halo order)
@@ -231,7 +232,7 @@ class OnTheFly:
         eh = halo_of(esel, pc.starts)
         esel, eh = esel[eh >= 0], eh[eh >= 0]
         e_ids = pc.snap['ids'][esel]
-        sorted_h = torch.from_numpy(p_has).to(eng.device)[eh]
+        sorted_h = _h2d(p_has, eng.device)[eh]
         srt, s_off = _sorted_unique_per_halo(
             eng.lib, eng.device, e_ids[sorted_h],
             torch.bincount(eh[sorted_h], minlength=nh).cpu().numpy(), ids_dtype)
@@ -348,7 +349,7 @@ def merge_onthefly(parts, nh, prev_starts, p_has, ids_dtype, n_prev=None, ordere
     out = {}
     if not ordered:
         ap = ap[torch.argsort(ap[:, 0])]
-    st = torch.from_numpy(np.asarray(prev_starts, dtype=np.int64)).to(dev)
+    st = _h2d(np.asarray(prev_starts, dtype=np.int64), dev)
     halo = torch.searchsorted(st, ap[:, 0].contiguous(), right=True) - 1 if len(st) else ap[:, 0]
     cnt = torch.bincount(halo, minlength=nh)[:nh] if ap.shape[0] else \
         torch.zeros(nh, dtype=torch.int64, device=dev)
@@ -374,7 +375,7 @@ def merge_onthefly(parts, nh, prev_starts, p_has, ids_dtype, n_prev=None, ordere
         dp[:, 0], dp[:, 1], id_order_key(dp[:, 1], ids_dtype),
         torch.ones(dp.shape[0], dtype=torch.bool, device=dev))
     en = parts['entered']
-    ph = torch.from_numpy(np.asarray(p_has, dtype=bool)).to(dev)
+    ph = _h2d(np.asarray(p_has, dtype=bool), dev)
     srt = ph[en[:, 0]] if en.shape[0] else torch.zeros(0, dtype=torch.bool, device=dev)
     second = torch.where(srt, id_order_key(en[:, 1], ids_dtype), en[:, 2])
     out['entered_ids'], out['entered_offsets'] = grouped(en[:, 0], en[:, 1], second, srt)
@@ -569,7 +570,7 @@ def _i64(t):
 
 def _halo_of(rows, starts, device):
     """Block of each row (blocks tile their snapshot in halo order)."""
-    st = torch.from_numpy(np.asarray(starts, dtype=np.int64)).to(device)
+    st = _h2d(np.asarray(starts, dtype=np.int64), device)
     if not len(st):
         return rows
     return torch.searchsorted(st, rows, right=True) - 1
