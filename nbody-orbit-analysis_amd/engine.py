@@ -1228,7 +1228,10 @@ class OrbitEngine:
         halos = np.zeros(len(halo_idx), dtype=N.HALO_DTYPE)
         halos['cur_off'] = starts[halo_idx]
         halos['cur_cnt'] = counts[halo_idx]
-        d_h = torch.from_numpy(halos.view(np.uint8)).to(dev)
+        # pinned staging both ways: a pageable copy is synchronous and waits behind any
+        # DMA in flight (a double-buffered snapshot H2D held the sharded on-the-fly
+        # step's stripe bulk ~70 ms)
+        d_h = _up(halos.view(np.uint8), dev)
         lst = torch.arange(len(halo_idx), dtype=torch.int32, device=dev)
         st = torch.cuda.current_stream(dev).cuda_stream
         if len(halo_idx):
@@ -1236,7 +1239,10 @@ class OrbitEngine:
                                               int(plan.mass == F64), d_h.data_ptr(),
                                               lst.data_ptr(), len(halo_idx), st),
                     'oa_bulk_velocity')
-        out = d_h.cpu().numpy().view(N.HALO_DTYPE)['bulk']
+        h = _pinned(d_h.numel(), torch.uint8)
+        h.copy_(d_h, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        out = h.numpy().view(N.HALO_DTYPE)['bulk']
         return out.astype(plan.bulk)
 
     def bulk_velocities(self, res, plan):

@@ -326,7 +326,20 @@ def _by_unique_key(v, g, n):
     return out
 
 
-def merge_onthefly(parts, nh, prev_starts, p_has, ids_dtype, n_prev=None, ordered=False):
+def _to_loader_width(ids64, ids_dtype):
+    """int64 ID values -> a device tensor of the loader's width (bit patterns kept)."""
+    return ids64 if np.dtype(ids_dtype).itemsize == 8 else ids64.to(torch.int32)
+
+
+def _ids_to_host_pinned(ids64, ids_dtype):
+    """ids_to_host through a page-locked block (one DMA, no pageable staging)."""
+    dt = np.dtype(ids_dtype)
+    h = _pinned_host(ids64)
+    return h.view(dt) if dt.itemsize == 8 else h.astype(dt)
+
+
+def merge_onthefly(parts, nh, prev_starts, p_has, ids_dtype, n_prev=None, ordered=False,
+                   lib=None):
     """Merge the ranks' on-the-fly records of one snapshot pair on the root rank
     (ShardedOnTheFly), on whatever device the tensors are on.
 
@@ -343,7 +356,11 @@ def merge_onthefly(parts, nh, prev_starts, p_has, ids_dtype, n_prev=None, ordere
     current-row order.  ``n_prev``: the previous snapshot's row count (bounds the
     global previous rows).  ``ordered``: one rank contributed every row, in order
     (world 1): apsis records and angle changes need no sort (``angle_g`` may then be
-    None).  Returns host arrays (IDs in ``ids_dtype``)."""
+    None), and departed / entered rows already come in halo order.  ``lib`` (device
+    tensors): the per-halo sorted-unique IDs come from the collation kernels (per-halo
+    LDS sort, as the single-GPU ``OnTheFly``) after at most one stable sort by halo, and
+    the IDs come back through pinned memory; without it, two stable torch sorts per
+    list (any device).  Returns host arrays (IDs in ``ids_dtype``)."""
     ap = parts['apsis']
     dev = ap.device
     out = {}
@@ -354,7 +371,9 @@ def merge_onthefly(parts, nh, prev_starts, p_has, ids_dtype, n_prev=None, ordere
     cnt = torch.bincount(halo, minlength=nh)[:nh] if ap.shape[0] else \
         torch.zeros(nh, dtype=torch.int64, device=dev)
     out['apsis_offsets'] = np.concatenate([[0], np.cumsum(cnt.cpu().numpy())]).astype(np.int64)
-    out['apsis_ids'] = ids_to_host(ap[:, 1], ids_dtype)
+    kern = lib is not None and dev.type == 'cuda'
+    out['apsis_ids'] = _ids_to_host_pinned(ap[:, 1].contiguous(), ids_dtype) if kern else \
+        ids_to_host(ap[:, 1], ids_dtype)
     out['angles'] = _pinned_host(parts['angle_v'] if ordered or parts['angle_g'] is None else
                                  _by_unique_key(parts['angle_v'], parts['angle_g'], n_prev))
 
@@ -370,6 +389,9 @@ def merge_onthefly(parts, nh, prev_starts, p_has, ids_dtype, n_prev=None, ordere
         return ids_to_host(ids, ids_dtype), \
             np.concatenate([[0], np.cumsum(c.cpu().numpy())]).astype(np.int64)
 
+    if kern:
+        _merge_lists_kernels(out, parts, nh, p_has, ids_dtype, ordered, lib, dev)
+        return out
     dp = parts['departed']
     out['departed_ids'], out['departed_offsets'] = grouped(
         dp[:, 0], dp[:, 1], id_order_key(dp[:, 1], ids_dtype),
@@ -380,6 +402,45 @@ def merge_onthefly(parts, nh, prev_starts, p_has, ids_dtype, n_prev=None, ordere
     second = torch.where(srt, id_order_key(en[:, 1], ids_dtype), en[:, 2])
     out['entered_ids'], out['entered_offsets'] = grouped(en[:, 0], en[:, 1], second, srt)
     return out
+
+
+def _merge_lists_kernels(out, parts, nh, p_has, ids_dtype, ordered, lib, dev):
+    """merge_onthefly's departed / entered lists with the collation kernels: rows put in
+    halo order by one stable sort (none when ``ordered``), then each halo's sorted
+    unique IDs (setdiff1d, :145, :168) by ``_sorted_unique_per_halo``; the entered IDs
+    of a halo without a progenitor block keep global current-row order (:178)."""
+    def by_halo(h, *cols):
+        keep = h >= 0                          # rows before the first block: no halo
+        h = h[keep]
+        cols = [c[keep] for c in cols]
+        if not ordered and h.numel() > 1:
+            o = torch.sort(h, stable=True)[1]
+            h = h[o]
+            cols = [c[o] for c in cols]
+        return h, cols
+
+    def counts(h):
+        return torch.bincount(h, minlength=nh)[:nh].cpu().numpy() if h.numel() else \
+            np.zeros(nh, np.int64)
+    dp = parts['departed']
+    h, (ids,) = by_halo(dp[:, 0], dp[:, 1])
+    out['departed_ids'], out['departed_offsets'] = _sorted_unique_per_halo(
+        lib, dev, _to_loader_width(ids, ids_dtype), counts(h), ids_dtype)
+    en = parts['entered']
+    ph = _h2d(np.asarray(p_has, dtype=bool), dev)
+    h, (ids, row) = by_halo(en[:, 0], en[:, 1], en[:, 2])
+    srt = ph[h] if h.numel() else torch.zeros(0, dtype=torch.bool, device=dev)
+    s_ids, s_off = _sorted_unique_per_halo(lib, dev, _to_loader_width(ids[srt], ids_dtype),
+                                           counts(h[srt]), ids_dtype)
+    hr, ir, rr = h[~srt], ids[~srt], row[~srt]
+    if not ordered and hr.numel() > 1:         # loader order: the global current row
+        o = _sort_pairs(hr, rr)
+        hr, ir = hr[o], ir[o]
+    raw = _ids_to_host_pinned(ir.contiguous(), ids_dtype) if ir.numel() else \
+        np.zeros(0, np.dtype(ids_dtype))
+    r_off = np.concatenate([[0], np.cumsum(counts(hr))]).astype(np.int64)
+    out['entered_ids'], out['entered_offsets'] = _interleave_halos(
+        np.asarray(p_has, dtype=bool), s_ids, s_off, raw, r_off)
 
 
 class ShardedOnTheFly:
@@ -550,7 +611,8 @@ class ShardedOnTheFly:
             merged = merge_onthefly(dict(apsis=apsis, angle_g=angle_g if self.world > 1 else None,
                                          angle_v=angle_v, departed=departed, entered=entered),
                                     nh, _block_starts(sl1, max(n_prev, 0)), p_has, ids_dtype,
-                                    n_prev=max(n_prev, 0), ordered=self.world == 1)
+                                    n_prev=max(n_prev, 0), ordered=self.world == 1,
+                                    lib=eng.lib)
             merged['angles'] = merged['angles'].astype(adt, copy=False)
         else:
             z = np.zeros(nh + 1, np.int64)

@@ -106,7 +106,12 @@ def main():
     nmax = max(int(h['ids'].numel()) for h in host)
     slots = [{k: torch.empty((nmax,) + tuple(host[0][k].shape[1:]), dtype=host[0][k].dtype,
                              device=dev) for k in host[0]} for _ in range(3)]
-    cs = torch.cuda.Stream(device=dev)
+    # the copy stream at high priority: HIP maps a process's streams onto
+    # GPU_MAX_HW_QUEUES hardware queues (4 on the box) by priority, and with RCCL's
+    # streams beside the compute stream a normal-priority copy stream shared the compute
+    # stream's queue, so every sharded step waited behind the next snapshot's 70-ms H2D
+    # (r04t: 127 ms per step; GPU_MAX_HW_QUEUES=8: 86 ms, r04v)
+    cs = torch.cuda.Stream(device=dev, priority=-1)
     evs = {}
 
     def h2d(k):
