@@ -1154,7 +1154,10 @@ class OrbitEngine:
         res.check_fresh()
         dev = self.device
         if getattr(self, '_copy_stream', None) is None:
-            self._copy_stream = torch.cuda.Stream(device=dev)
+            # high priority: a normal-priority stream may share the compute stream's
+            # hardware queue (GPU_MAX_HW_QUEUES) and hold the next snapshot's kernels
+            # behind this copy (deployment note)
+            self._copy_stream = torch.cuda.Stream(device=dev, priority=-1)
         cs = self._copy_stream
         n = res.n_slots + 1
         if res.done is None:                # a result of launch() itself, not of step()

@@ -771,7 +771,8 @@ class ShardedEngine:
         side = None
         if dev.type == 'cuda':
             if self._side is None:
-                self._side = torch.cuda.Stream(device=dev)
+                # high priority: its own hardware queue (engine.fetch_async)
+                self._side = torch.cuda.Stream(device=dev, priority=-1)
             side = self._side
         ctx = torch.cuda.stream(side) if side is not None else _nullcontext()
         with ctx:
