@@ -262,8 +262,10 @@ def main():
         % (elapsed, args.steps, kern_ms, achieved, n_apsis))
 
     traffic = None
-    pmc = os.path.join(ROOT, 'profiles', 'pmc_k_step.json')
-    if os.path.exists(pmc):
+    for name in ('pmc_k_step.json', 'pmc_part.json'):
+        pmc = os.path.join(ROOT, 'profiles', name)
+        if traffic is not None or not os.path.exists(pmc):
+            continue
         with open(pmc) as f:
             pj = json.load(f)
         # only for the workload the counters were collected on
