@@ -2187,13 +2187,8 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
 // Current and previous chunks interleaved in one grid (their latencies overlap):
 // even work-groups take current chunks, odd ones previous chunks, then the longer
 // list's remainder.
-#ifdef OA_SCAT_WPE
-#define SCAT_ATTR __attribute__((amdgpu_waves_per_eu(OA_SCAT_WPE)))
-#else
-#define SCAT_ATTR
-#endif
 template <typename TX, typename TV, typename TD, int IDB, int KB>
-__global__ __launch_bounds__(SCAT_WG) SCAT_ATTR void k_part_scatter(const oa_step_args a, const FrameK fk) {
+__global__ __launch_bounds__(SCAT_WG) void k_part_scatter(const oa_step_args a, const FrameK fk) {
     extern __shared__ __attribute__((aligned(16))) char slds[];
     const int64_t b = blockIdx.x, n1 = a.n_gchunk1,
                   n2 = a.gchunk3 ? a.n_gchunk3 : a.n_gchunk2;
