@@ -2488,8 +2488,12 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
             if (j0 == 0 && q == 0) PSTAMP(4);
         }
     }
-    __syncthreads();
+    // barriers on LDS traffic only from here: the state words' stores go out first and
+    // stay in flight through the record claims (a full __syncthreads would wait for them)
+    lds_barrier();
     PSTAMP(6);
+    // the partition's state words leave as one coalesced run
+    for (uint32_t i = tid; i < nc; i += PART_WG) cmeta[i] = mlds[i];
     // the staged records: ranks within their chunks from LDS counters over the dead
     // table, one global atomic per touched chunk for the chunk's slots, then the stores
     // (a halo with more chunks than the counters claims per record)
@@ -2500,19 +2504,19 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
     if (nst) {
         if (lds_ranks)
             for (uint32_t c = tid; c < nch; c += PART_WG) lc[c] = 0u;
-        __syncthreads();
+        lds_barrier();
         for (uint32_t e = tid; e < nst; e += PART_WG) {
             const uint32_t c = (uint32_t)rbuf[2 * e + 1] >> RCHUNK_LOG2;
             const uint32_t r = lds_ranks ? atomicAdd(&lc[c], 1u) : atomicAdd(&rcnt[c], 1u);
             rbuf[2 * e + 1] |= (uint64_t)r << 48;
         }
-        __syncthreads();
+        lds_barrier();
         if (lds_ranks)
             for (uint32_t c = tid; c < nch; c += PART_WG) {
                 const uint32_t n = lc[c];
                 if (n) lc[c] = atomicAdd(&rcnt[c], n);
             }
-        __syncthreads();
+        lds_barrier();
         for (uint32_t e = tid; e < nst; e += PART_WG) {
             const uint64_t w = rbuf[2 * e + 1];
             const uint32_t p = (uint32_t)w, c = p >> RCHUNK_LOG2;
@@ -2523,8 +2527,6 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
             a.scratch_rk[s] = (uint16_t)(p & (RCHUNK - 1));
         }
     }
-    // the partition's state words leave as one coalesced run
-    for (uint32_t i = tid; i < nc; i += PART_WG) cmeta[i] = mlds[i];
     // the work-group's record count: one pair of device atomics (halo and item counts)
     if (tid == 0 && *nrec) {
         atomicAdd(&a.halo_count[gp[13]], (int32_t)*nrec);
