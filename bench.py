@@ -150,7 +150,7 @@ def main():
 
     import orbitanalysis_amd  # noqa: F401
     from orbitanalysis_amd import _native
-    from orbitanalysis_amd.engine import OrbitEngine, SnapshotState, meta_angles
+    from orbitanalysis_amd.engine import OrbitEngine, SnapshotState, layout_of, meta_angles
     from orbitanalysis_amd.synthetic_device import DevicePlummer
     from orbitanalysis_amd.utils import hubble_parameter
 
@@ -182,7 +182,7 @@ def main():
         prep0 = eng.prepare(snaps[0], cats[0][0], cats[0][2], H, z, exists, False)
         eng.launch(prep0, None)
         chain = [(prep0, 0)]
-        layout = (prep0.starts, prep0.counts, exists, prep0.plan, prep0.n, prep0.buckets)
+        layout = layout_of(prep0, exists)
         for t in range(1, args.warmup + args.steps + 1):
             tp = time.perf_counter()
             pr = eng.prepare(snaps[t], cats[t][0], cats[t][2], H, z, exists, True,
@@ -190,7 +190,7 @@ def main():
             prep_s.append(time.perf_counter() - tp)
             chain.append((pr, t))
             # large halos: this step's bucket set is the next step's previous state
-            layout = (pr.starts, pr.counts, exists, pr.plan, pr.n, pr.buckets)
+            layout = layout_of(pr, exists)
         preps = [c[0] for c in chain[1:]]
     else:
         # the product's multi-GPU path: ShardedEngine over this rank's ID range (the
@@ -222,9 +222,7 @@ def main():
         if world > 1:
             seng.launch(pr, prev=prev_pr, step_events=events, check=False)
         else:
-            eng.launch(pr, ws, SnapshotState(snaps[ps]['ids'], prev_pr.rhat, prev_pr.meta,
-                                             prev_pr.starts, prev_pr.counts, exists,
-                                             prev_pr.plan, prev_pr.buckets),
+            eng.launch(pr, ws, SnapshotState.of(prev_pr, exists, ids=snaps[ps]['ids']),
                        step_events=events)
 
     for k in range(args.warmup):

@@ -1,8 +1,11 @@
 """Build liborbit_hip.so (hipcc, gfx950) in-tree.  Used by __graft_entry__.build().
 
-Two translation units: ``orbit_hip.hip`` (the per-snapshot path) and
-``orbit_post.hip``; each is compiled to an object only
-when it (or a header) changed, then both are linked into one shared library."""
+Two source files: ``orbit_hip.hip`` (the per-snapshot path) and ``orbit_post.hip``
+(SURVEY §8(f) rows f3/f4).  ``orbit_hip.hip`` is compiled as four units in parallel
+(OA_TU = -1: the C ABI and the helper kernels; 1, 2, 3: the step kernels of one dtype
+plan each -- their template instantiations are most of the device compile time).  Each
+object is rebuilt only when its source (or a header) changed, then all are linked into
+one shared library."""
 import os
 import subprocess
 from concurrent.futures import ThreadPoolExecutor
@@ -20,10 +23,12 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC',
          # used: the atomic optimizer's wave-reduction rewrite would wait on them at once
          '-mllvm', '-amdgpu-atomic-optimizer-strategy=None',
          '-I' + os.path.join(ROOT, 'include')]
+UNITS = (-1, 1, 2, 3)           # OA_TU units of orbit_hip.hip
 
 
-def _obj(src):
-    return os.path.join(PKG, 'csrc', os.path.basename(src) + '.o')
+def _obj(src, tu=None):
+    tag = '' if tu is None else '.tu%s' % str(tu).replace('-', 'm')
+    return os.path.join(PKG, 'csrc', os.path.basename(src) + tag + '.o')
 
 
 def _newer(path, deps):
@@ -41,19 +46,22 @@ def build(force=False, verbose=True):
     if not force and not stale():
         return LIB
 
-    def compile_one(src):
-        obj = _obj(src)
+    def compile_one(job):
+        src, tu = job
+        obj = _obj(src, tu)
         hdrs = HDRS if src.endswith('orbit_post.hip') else HDRS[:1]
         if force or _newer(obj, [src] + hdrs + [__file__]):
-            cmd = [HIPCC] + FLAGS + ['-c', '-o', obj + '.tmp', src]
+            extra = [] if tu is None else ['-DOA_TU=%d' % tu]
+            cmd = [HIPCC] + FLAGS + extra + ['-c', '-o', obj + '.tmp', src]
             if verbose:
                 print(' '.join(cmd), flush=True)
             subprocess.run(cmd, check=True)
             os.replace(obj + '.tmp', obj)
-        return _obj(src)
+        return obj
 
-    with ThreadPoolExecutor(len(SRCS)) as ex:
-        objs = list(ex.map(compile_one, SRCS))
+    jobs = [(SRCS[0], tu) for tu in UNITS] + [(SRCS[1], None)]
+    with ThreadPoolExecutor(len(jobs)) as ex:
+        objs = list(ex.map(compile_one, jobs))
     cmd = [HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', LIB + '.tmp'] + objs
     if verbose:
         print(' '.join(cmd), flush=True)

@@ -37,6 +37,15 @@
 
 #include "orbit_hip.h"
 
+// Units of the library built from this file (OA_TU): 0 = everything in one unit; the
+// split build (_build.py, units compiled in parallel) = -1 (the C ABI and every kernel
+// but the step launchers) + 1, 2, 3 (the step launchers of one dtype plan each: float32
+// coordinates and r̂, float32 coordinates with float64 r̂, float64).
+#ifndef OA_TU
+#define OA_TU 0
+#endif
+void oa_internal_error(const char *msg);   // the oa_last_error() buffer (unit 0 / -1)
+
 namespace {
 
 #ifndef OA_WG
@@ -75,14 +84,22 @@ constexpr int MAX_EVICT = OA_MAXEV; // eviction-chain length before an entry is 
 constexpr int NCAND = 3;            // cuckoo candidate slots per key
 static_assert(WG % 64 == 0 && WG <= 1024, "work-group must be whole waves");
 static_assert(HMAX < WG, "halo table is staged by one thread per halo");
+// direct records: wave 0 writes one halo offset per lane (direct_tail) and resolves the
+// look-back while waves 1.. write the state words (phase 3)
+static_assert(HMAX <= 64, "an item's halos are one lane each of wave 0");
+static_assert(WG > 64, "phase 3 of a direct-records step needs waves beside wave 0");
 
+#if OA_TU <= 0
 thread_local char g_err[512] = "";
+#endif
 
 int fail(int code, const char *fmt, ...) {
+    char buf[512];
     va_list ap;
     va_start(ap, fmt);
-    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
     va_end(ap);
+    oa_internal_error(buf);
     return code;
 }
 
@@ -258,6 +275,7 @@ struct ItemHdr {
     int64_t seg_prev_off[HMAX];
     double cb[HMAX][6];             // centre[3], bulk[3]
     float cf[HMAX][6];              // the same, rounded to float32
+    double cbp[HMAX][3];            // RC: the progenitor's previous centre (prev_centre)
 };
 constexpr int64_t HDR_BYTES = (sizeof(ItemHdr) + 255) & ~int64_t(255);
 
@@ -292,6 +310,7 @@ __device__ int64_t item_lookback(const oa_step_args &a, uint32_t b, uint32_t cou
     if (publish_count && lane == 0) lb_publish(&a.lookback[b], tag | LB_AGG | count);
     int64_t excl = 0, j0 = (int64_t)b - 1;
     uint32_t spins = 0;
+    const uint32_t spin_max = a.lb_spin_max ? a.lb_spin_max : LB_SPIN_MAX;
     while (j0 >= 0) {
         uint64_t w[LBW];
 #pragma unroll
@@ -317,7 +336,7 @@ __device__ int64_t item_lookback(const oa_step_args &a, uint32_t b, uint32_t cou
         const int f = inc ? __builtin_ctzll(inc) : 64;
         const uint64_t need = f == 64 ? ~0ull : ((2ull << f) - 1ull);
         if (notready & need) {
-            if (++spins > LB_SPIN_MAX) {
+            if (++spins > spin_max) {
                 if (lane == 0) atomicOr(a.status, OA_STATUS_LOOKBACK);
                 break;
             }
@@ -365,39 +384,74 @@ __device__ __forceinline__ uint32_t upper_find(const uint32_t *starts, uint32_t 
 }
 
 // ------------------------------------------------------------------ frame
+// One snapshot's periodic box as recenter_coordinates (utils.py:24-33) applies it,
+// derived on the host (make_wrap): the current snapshot's for the frame, the previous
+// snapshot's for a previous r̂ recomputed from its coordinates (oa_step_args.coords_prev).
+struct WrapK {
+    double box[3];         // L per dimension (float64 values)
+    float hi[3];           // smallest float32 with  dx >  L/2  (float32 dx plans)
+    float lo[3];           // largest  float32 with  dx < -L/2
+    float ab[3];           // min(hi, -lo): |dx| below it never wraps
+    int32_t n_dims;        // 0: no periodic wrap
+    int32_t f64;           // recenter arithmetic in float64 (wrap_f64)
+};
 // Per-launch constants derived on the host from oa_step_args (oa_step()).
 struct FrameK {
     float h_f;             // RN32(H / (1 + z)): Hubble factor of the f32 sign filter
-    float wrap_hi[3];      // smallest float32 with  dx >  L/2  (float32 dx plans)
-    float wrap_lo[3];      // largest  float32 with  dx < -L/2
-    float wrap_abs[3];     // min(wrap_hi, -wrap_lo): |dx| below it never wraps
+    WrapK w;               // the current snapshot's box
 };
 
 template <typename TD> struct WrapT;
 template <> struct WrapT<float> {
-    static __device__ __forceinline__ bool hi(float dx, const oa_step_args &a, const FrameK &k, int d) {
-        return dx >= k.wrap_hi[d];
-    }
-    static __device__ __forceinline__ bool lo(float dx, const oa_step_args &a, const FrameK &k, int d) {
-        return dx <= k.wrap_lo[d];
-    }
+    static __device__ __forceinline__ bool hi(float dx, const WrapK &w, int d) { return dx >= w.hi[d]; }
+    static __device__ __forceinline__ bool lo(float dx, const WrapK &w, int d) { return dx <= w.lo[d]; }
 };
 template <> struct WrapT<double> {
-    static __device__ __forceinline__ bool hi(double dx, const oa_step_args &a, const FrameK &, int d) {
-        return dx > a.box[d] / 2;
-    }
-    static __device__ __forceinline__ bool lo(double dx, const oa_step_args &a, const FrameK &, int d) {
-        return dx < -(a.box[d] / 2);
-    }
+    static __device__ __forceinline__ bool hi(double dx, const WrapK &w, int d) { return dx > w.box[d] / 2; }
+    static __device__ __forceinline__ bool lo(double dx, const WrapK &w, int d) { return dx < -(w.box[d] / 2); }
 };
 
 template <typename TD>
-__device__ __forceinline__ TD wrap_sub(TD dx, const oa_step_args &a, int d) {
-    return a.wrap_f64 ? (TD)((double)dx - a.box[d]) : (TD)((float)dx - (float)a.box[d]);
+__device__ __forceinline__ TD wrap_sub(TD dx, const WrapK &w, int d) {
+    return w.f64 ? (TD)((double)dx - w.box[d]) : (TD)((float)dx - (float)w.box[d]);
 }
 template <typename TD>
-__device__ __forceinline__ TD wrap_add(TD dx, const oa_step_args &a, int d) {
-    return a.wrap_f64 ? (TD)((double)dx + a.box[d]) : (TD)((float)dx + (float)a.box[d]);
+__device__ __forceinline__ TD wrap_add(TD dx, const WrapK &w, int d) {
+    return w.f64 ? (TD)((double)dx + w.box[d]) : (TD)((float)dx + (float)w.box[d]);
+}
+
+// dx = recenter_coordinates(x - centre) (track_orbits.py:256-259, utils.py:24-33): one
+// strict wrap per dimension, in the promoted dtype of (dx, box); the float64 arithmetic
+// runs only in waves where some particle crosses the box edge.  cf = the centre rounded
+// to float32 (exact for a float32 dx plan).
+template <typename TX, typename TD>
+__device__ __forceinline__ void centre_dx(const V3<TX> &x, const double *cb, const float *cf,
+                                          const WrapK &w, TD dx[3]) {
+    if constexpr (sizeof(TD) == 4) {
+        dx[0] = (float)x.x - cf[0]; dx[1] = (float)x.y - cf[1]; dx[2] = (float)x.z - cf[2];
+    } else {
+        dx[0] = (TD)x.x - cb[0]; dx[1] = (TD)x.y - cb[1]; dx[2] = (TD)x.z - cb[2];
+    }
+    if (w.n_dims > 0) {
+        // one wave-level test for the common case (no particle beyond half a box)
+        bool m = false;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            if (d < w.n_dims) {
+                if constexpr (sizeof(TD) == 4) m = m | (fabsf(dx[d]) >= w.ab[d]);
+                else m = m | WrapT<TD>::hi(dx[d], w, d) | WrapT<TD>::lo(dx[d], w, d);
+            }
+        }
+        if (__any(m)) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                if (d < w.n_dims) {
+                    if (WrapT<TD>::hi(dx[d], w, d)) dx[d] = wrap_sub(dx[d], w, d);
+                    if (WrapT<TD>::lo(dx[d], w, d)) dx[d] = wrap_add(dx[d], w, d);
+                }
+            }
+        }
+    }
 }
 
 // rads = sqrt(dot(dx, dx)); r̂ = dx / rads, correctly rounded in TD.
@@ -466,34 +520,7 @@ __device__ __forceinline__ uint32_t frame(const V3<TX> &x, const V3<TV> &v, cons
                                           const float *cf, const oa_step_args &a,
                                           const FrameK &k, TD r[3], double *vr_full = nullptr) {
     TD dx[3];
-    if constexpr (sizeof(TD) == 4) {
-        dx[0] = (float)x.x - cf[0]; dx[1] = (float)x.y - cf[1]; dx[2] = (float)x.z - cf[2];
-    } else {
-        dx[0] = (TD)x.x - cb[0]; dx[1] = (TD)x.y - cb[1]; dx[2] = (TD)x.z - cb[2];
-    }
-    // recenter_coordinates (utils.py:24-33): one strict wrap per dimension, in the
-    // promoted dtype of (dx, box); the float64 arithmetic runs only in waves where
-    // some particle crosses the box edge
-    if (a.n_box_dims > 0) {
-        // one wave-level test for the common case (no particle beyond half a box)
-        bool w = false;
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            if (d < a.n_box_dims) {
-                if constexpr (sizeof(TD) == 4) w = w | (fabsf(dx[d]) >= k.wrap_abs[d]);
-                else w = w | WrapT<TD>::hi(dx[d], a, k, d) | WrapT<TD>::lo(dx[d], a, k, d);
-            }
-        }
-        if (__any(w)) {
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                if (d < a.n_box_dims) {
-                    if (WrapT<TD>::hi(dx[d], a, k, d)) dx[d] = wrap_sub(dx[d], a, d);
-                    if (WrapT<TD>::lo(dx[d], a, k, d)) dx[d] = wrap_add(dx[d], a, d);
-                }
-            }
-        }
-    }
+    centre_dx<TX, TD>(x, cb, cf, k.w, dx);
     // rads = sqrt(dot(dx, dx)); rhats = dx / rads   (:286-287), exact in dx's dtype
     unit_vector(dx, r);
     // sign filter: w = (v - bulk) + (H * dx) / (1 + z), v_r = dot(w, r̂)   (:275-288)
@@ -539,16 +566,16 @@ __device__ __forceinline__ uint32_t frame_otf(const V3<TX> &x, const V3<TV> &v, 
     for (int d = 0; d < 3; ++d) {
         if (a.dx_f64) {
             double t = (double)xs[d] - cb[d];
-            if (d < a.n_box_dims) {
-                if (t > a.box[d] / 2) t = t - a.box[d];
-                if (t < -(a.box[d] / 2)) t = t + a.box[d];
+            if (d < k.w.n_dims) {
+                if (t > k.w.box[d] / 2) t = t - k.w.box[d];
+                if (t < -(k.w.box[d] / 2)) t = t + k.w.box[d];
             }
             dx[d] = (TD)t;
         } else {
             float t = (float)xs[d] - (float)cb[d];
-            if (d < a.n_box_dims) {
-                if (t >= k.wrap_hi[d]) t = wrap_sub(t, a, d);
-                if (t <= k.wrap_lo[d]) t = wrap_add(t, a, d);
+            if (d < k.w.n_dims) {
+                if (t >= k.w.hi[d]) t = wrap_sub(t, k.w, d);
+                if (t <= k.w.lo[d]) t = wrap_add(t, k.w, d);
             }
             dx[d] = (TD)t;
         }
@@ -684,9 +711,14 @@ __device__ __forceinline__ int64_t uni64(int64_t x) {
 constexpr uint32_t PK_HIT = 1u << 14, PK_FLAG = 1u << 15;
 
 // SINGLE: every item holds one halo (oa_step_args.items_single): the packed-item paths
-// (per-row halo and segment lookups) are compiled out
-template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF, bool SINGLE = false>
-__global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK fk) {
+// (per-row halo and segment lookups) are compiled out.
+// RC: the previous r̂ is recomputed from the previous snapshot's coordinates
+// (oa_step_args.coords_prev, the previous centre and box wp) instead of read from
+// rhat_prev: the same 3 values per previous particle come from HBM, and the step that
+// produced the previous state never had to write them.
+template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF, bool SINGLE = false,
+          bool RC = false>
+__global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK fk, const WrapK wp) {
     typedef typename IdT<IDB>::T ID;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     ItemHdr &H = *reinterpret_cast<ItemHdr *>(smem);
@@ -732,8 +764,12 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     const Rsrc r_id = make_rsrc(ids + base, n_span * IDB);
     const Rsrc r_x = make_rsrc(reinterpret_cast<const TX *>(a.coords) + 3 * base, n_span * SX);
     const Rsrc r_v = make_rsrc(reinterpret_cast<const TV *>(a.vels) + 3 * base, n_span * SV);
-    const Rsrc r_rh = make_rsrc(rhat_out + 3 * base, n_span * SD);
-    const Rsrc r_mt = make_rsrc(a.meta_out + base, n_span * 4u);
+    // rhat_out == NULL: no r̂ is written (its successor recomputes it, RC); meta_out ==
+    // NULL: a frame-only launch that materialises r̂ alone (its stores fall outside a
+    // 0-byte resource and are dropped)
+    const bool wr_rh = rhat_out != nullptr;
+    const Rsrc r_rh = make_rsrc(rhat_out + 3 * base, wr_rh ? n_span * SD : 0u);
+    const Rsrc r_mt = make_rsrc(a.meta_out + base, a.meta_out ? n_span * 4u : 0u);
     // Phase-1 rows go in trips of U1 consecutive rows; a wave takes at most NTRIP trips
     // (<= SU rows) and keeps each row's r̂ in registers (rr) until phase 2b writes it
     // into the LDS the table held -- no read-back of the rows it stored.
@@ -795,6 +831,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             H.halo_cnt[lane] = 0;
             for (int d = 0; d < 3; ++d) { H.cb[lane][d] = hrow.centre[d]; H.cb[lane][3 + d] = hrow.bulk[d]; }
             for (int d = 0; d < 3; ++d) { H.cf[lane][d] = (float)hrow.centre[d]; H.cf[lane][3 + d] = (float)hrow.bulk[d]; }
+            if (RC)
+                for (int d = 0; d < 3; ++d) H.cbp[lane][d] = hrow.prev_centre[d];
             if (hp) {
                 const uint32_t sg = si - 1u;
                 H.seg_halo[sg] = lane; H.seg_prev_off[sg] = hrow.prev_off;
@@ -869,7 +907,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
             // compare steps store r̂ from registers in phase 2b (RDEFER): phase 1 then
             // issues loads only and ends without waiting on stores
-            if (!RD) bst3<TD>(r_rh, li * SD, r);
+            if (!RD && wr_rh) bst3<TD>(r_rh, li * SD, r);
             rr[kp * U1 + u] = V3<TD>{r[0], r[1], r[2]};
             if constexpr (!COMPARE) {
                 uint32_t ang = 0;
@@ -970,7 +1008,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         }
     };
     if (n_pv == 0) {                                 // nothing to join: state words only
-        if (RD) store_rhat();
+        if (RD && wr_rh) store_rhat();
         __syncthreads();
         for (uint32_t li = tid; li < n_span; li += WG)
             bst32<AUX_NT>(r_mt, li * 4u, (uint32_t)(sgn8[li] & 3u) << 16);
@@ -1001,7 +1039,11 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // up to 2 * KROWS loads in flight per wave hide the HBM latency behind them.
     ID pid[KROWS];
     uint32_t pk[KROWS];
-    V3<TD> prh[KROWS];
+    // phase 2b: each row's previous r̂, or (RC) its previous coordinates
+    typedef typename std::conditional<RC, TX, TD>::type TP;
+    constexpr uint32_t SP = 3 * sizeof(TP);
+    const TP *prev3 = RC ? static_cast<const TP *>(a.coords_prev) : reinterpret_cast<const TP *>(rhat_prev);
+    V3<TP> prh[KROWS];
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < KROWS; ++k) {
@@ -1174,7 +1216,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         uint32_t nv, hs;
         int64_t kb;
         row_of(wave + NWAVE * k, nv, hs, kb);
-        prh[k] = bld3<TD, AUX_NT>(make_rsrc(rhat_prev + 3 * kb, nv * SD), lane * SD);
+        prh[k] = bld3<TP, AUX_NT>(make_rsrc(prev3 + 3 * kb, nv * SP), lane * SP);
     }
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1210,7 +1252,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                                 : (uint32_t)(wave + NWAVE * k) * 64 + lane;
         if (li < n_span) { rcx[li] = rr[k].x; rcy[li] = rr[k].y; rcz[li] = rr[k].z; }
     }
-    if (RD) store_rhat();
+    if (RD && wr_rh) store_rhat();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -1229,7 +1271,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             uint32_t nv, hs;
             int64_t kb;
             row_of(wave + NWAVE * (k + PF2), nv, hs, kb);
-            prh[k + PF2] = bld3<TD, AUX_NT>(make_rsrc(rhat_prev + 3 * kb, nv * SD), lane * SD);
+            prh[k + PF2] = bld3<TP, AUX_NT>(make_rsrc(prev3 + 3 * kb, nv * SP), lane * SP);
         }
         const uint32_t r = wave + NWAVE * k;
         if (r >= nrow) continue;
@@ -1241,8 +1283,20 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         uint16_t a16 = 0;
         if (p & PK_HIT) {
             const uint32_t c = p & (PK_HIT - 1u);
+            TD rp[3];
+            if constexpr (RC) {
+                // the previous r̂ exactly as the previous step's frame computed it
+                // (track_orbits.py:256-287 in the previous snapshot's frame)
+                const double *cb = H.cbp[hs];
+                const float cf[3] = {(float)cb[0], (float)cb[1], (float)cb[2]};
+                TD dx[3];
+                centre_dx<TX, TD>(prh[k], cb, cf, wp, dx);
+                unit_vector(dx, rp);
+            } else {
+                rp[0] = prh[k].x; rp[1] = prh[k].y; rp[2] = prh[k].z;
+            }
             // angle change = arccos(dot(r̂_prev, r̂_match)), no clamp (:324-325)
-            const TD dt = dot3(prh[k].x, prh[k].y, prh[k].z, rcx[c], rcy[c], rcz[c]);
+            const TD dt = dot3(rp[0], rp[1], rp[2], rcx[c], rcy[c], rcz[c]);
             const TD change = acos_change<OTF>(dt);
             // calc_angles (:342-349): f16 + change, rounded once; reset at an apsis
             const uint16_t acc = angle_add((uint16_t)(p >> 16), change);
@@ -1640,19 +1694,28 @@ __global__ __launch_bounds__(64) void k_bulk(const TV *vels, const TM *masses, o
     if (lane < 3) h.bulk[lane] = (double)res;
 }
 
+WrapK make_wrap(const double box[3], int32_t n_dims, int32_t f64) {
+    WrapK w;
+    w.n_dims = n_dims;
+    w.f64 = f64;
+    for (int d = 0; d < 3; ++d) {
+        w.box[d] = box[d];
+        // exact float32 thresholds of the strict tests dx > L/2 and dx < -L/2, where
+        // L/2 is float64 (wrap_f64) or float32 arithmetic
+        const double half = f64 ? box[d] / 2 : (double)((float)box[d] / 2.0f);
+        float f = (float)half;
+        w.hi[d] = (double)f > half ? f : nextafterf(f, INFINITY);
+        float g = (float)(-half);
+        w.lo[d] = (double)g < -half ? g : nextafterf(g, -INFINITY);
+        w.ab[d] = fminf(w.hi[d], -w.lo[d]);
+    }
+    return w;
+}
+
 FrameK make_frame_k(const oa_step_args &a) {
     FrameK k;
     k.h_f = (float)(a.H / a.one_plus_z);
-    for (int d = 0; d < 3; ++d) {
-        // exact float32 thresholds of the strict tests dx > L/2 and dx < -L/2, where
-        // L/2 is float64 (wrap_f64) or float32 arithmetic
-        const double half = a.wrap_f64 ? a.box[d] / 2 : (double)((float)a.box[d] / 2.0f);
-        float f = (float)half;
-        k.wrap_hi[d] = (double)f > half ? f : nextafterf(f, INFINITY);
-        float g = (float)(-half);
-        k.wrap_lo[d] = (double)g < -half ? g : nextafterf(g, -INFINITY);
-        k.wrap_abs[d] = fminf(k.wrap_hi[d], -k.wrap_lo[d]);
-    }
+    k.w = make_wrap(a.box, a.n_box_dims, a.wrap_f64);
     return k;
 }
 
@@ -1680,10 +1743,15 @@ int launch_step_c(const oa_step_args &a, hipStream_t st) {
         // a frame-only launch needs no table: several work-groups share a CU
         const int64_t lds = COMPARE ? step_lds_bytes(a.lds_entries, a.lds_slots, (int)sizeof(TD))
                                     : HDR_BYTES;
-        auto k = (COMPARE && !OTF && a.items_single) ? k_step<TX, TV, TD, IDB, COMPARE, OTF, true>
-                                                     : k_step<TX, TV, TD, IDB, COMPARE, OTF, false>;
-        if (int rc = set_lds(k, lds)) return rc;
-        hipLaunchKernelGGL(k, dim3(a.n_items), dim3(WG), (size_t)lds, st, a, make_frame_k(a));
+        const bool rc = COMPARE && !OTF && a.coords_prev;
+        auto k = !(COMPARE && !OTF) ? k_step<TX, TV, TD, IDB, COMPARE, OTF, false, false>
+                 : a.items_single ? (rc ? k_step<TX, TV, TD, IDB, COMPARE, OTF, true, true>
+                                        : k_step<TX, TV, TD, IDB, COMPARE, OTF, true, false>)
+                                  : (rc ? k_step<TX, TV, TD, IDB, COMPARE, OTF, false, true>
+                                        : k_step<TX, TV, TD, IDB, COMPARE, OTF, false, false>);
+        if (int rc2 = set_lds(k, lds)) return rc2;
+        hipLaunchKernelGGL(k, dim3(a.n_items), dim3(WG), (size_t)lds, st, a, make_frame_k(a),
+                           make_wrap(a.box_prev, a.n_box_dims_prev, a.wrap_f64_prev));
         if (int rc = check_launch("k_step")) return rc;
     }
     return launch_big<TX, TV, TD, IDB, COMPARE, OTF>(a, st);
@@ -2608,10 +2676,26 @@ int launch_big(const oa_step_args &a, hipStream_t st) {
 
 }  // namespace
 
-// Error channel shared with the second translation unit (orbit_post.hip):
+// The step launchers of the three dtype plans (oa_step), one unit each in the split build.
+int oa_step_plan_f32(const oa_step_args &a, hipStream_t st);    // float32 coordinates, r̂
+int oa_step_plan_f32d(const oa_step_args &a, hipStream_t st);   // float32 coordinates, f64 r̂
+int oa_step_plan_f64(const oa_step_args &a, hipStream_t st);    // float64 coordinates, r̂
+#if OA_TU == 0 || OA_TU == 1
+int oa_step_plan_f32(const oa_step_args &a, hipStream_t st) { return launch_step_v<float, float>(a, st); }
+#endif
+#if OA_TU == 0 || OA_TU == 2
+int oa_step_plan_f32d(const oa_step_args &a, hipStream_t st) { return launch_step_v<float, double>(a, st); }
+#endif
+#if OA_TU == 0 || OA_TU == 3
+int oa_step_plan_f64(const oa_step_args &a, hipStream_t st) { return launch_step_v<double, double>(a, st); }
+#endif
+
+#if OA_TU <= 0
+// Error channel shared with the other units (orbit_post.hip, the step-plan units):
 // nullptr clears the message, anything else becomes oa_last_error().
 void oa_internal_error(const char *msg) {
-    if (msg) fail(OA_E_ARG, "%s", msg); else g_err[0] = 0;
+    if (!msg) { g_err[0] = 0; return; }
+    snprintf(g_err, sizeof(g_err), "%s", msg);
 }
 
 extern "C" {
@@ -2756,10 +2840,20 @@ int oa_step(const oa_step_args *args, void *stream) {
                           a.lds_slots <= a.lds_entries))
         return fail(OA_E_ARG, "bad lds_entries/lds_slots (entries <= %d (r̂ dtype) < slots)",
                     (a.dx_f64 ? STAGE_F64 : STAGE_F32) * WG);
+    // packed items only (k_step) may skip the r̂ output, recompute the previous r̂ (RC) or,
+    // frame-only, skip the state words (ABI 16: oa_step_args.coords_prev)
+    const bool packed_only = a.n_global_items == 0 && !a.onthefly;
     if (a.n_items + a.n_global_items > 0 &&
-        (!a.halos || !a.ids || !a.coords || !a.vels || !a.rhat_out || !a.meta_out))
+        (!a.halos || !a.ids || !a.coords || !a.vels || (!a.rhat_out && !packed_only) ||
+         (!a.meta_out && !(packed_only && !a.compare && !a.vr_out))))
         return fail(OA_E_ARG, "null input/output pointer");
-    if (a.compare && (!a.ids_prev || !a.rhat_prev || !a.meta_prev || !a.halo_count || !a.status ||
+    if (a.coords_prev && (!packed_only || !a.compare))
+        return fail(OA_E_ARG, "coords_prev: compare steps of packed items only");
+    if (a.coords_prev && (a.n_box_dims_prev < 0 || a.n_box_dims_prev > 3 ||
+                          (a.wrap_f64_prev == 0 && a.dx_f64)))
+        return fail(OA_E_ARG, "coords_prev: bad previous box");
+    if (a.compare && (!a.ids_prev || (!a.rhat_prev && !a.coords_prev) || !a.meta_prev ||
+                      !a.halo_count || !a.status ||
                       (a.n_items > 0 && (!a.scratch_ids || !a.scratch_ang || !a.item_count ||
                                          !a.seg_count))))
         return fail(OA_E_ARG, "null previous-state / scratch pointer");
@@ -2801,13 +2895,9 @@ int oa_step(const oa_step_args *args, void *stream) {
             hipMemsetAsync(a.item_count + a.n_items, 0, (size_t)a.n_global_items * 4, st) != hipSuccess)
             return fail(OA_E_LAUNCH, "oa_step: large-halo table reset");
     }
-    if (a.onthefly)
-        return a.coord_f64 ? launch_step_v<double, double>(a, st) : launch_step_v<float, float>(a, st);
-    if (a.dx_f64) {
-        return a.coord_f64 ? launch_step_v<double, double>(a, st)
-                           : launch_step_v<float, double>(a, st);
-    }
-    return launch_step_v<float, float>(a, st);
+    if (a.onthefly) return a.coord_f64 ? oa_step_plan_f64(a, st) : oa_step_plan_f32(a, st);
+    if (a.dx_f64) return a.coord_f64 ? oa_step_plan_f64(a, st) : oa_step_plan_f32d(a, st);
+    return oa_step_plan_f32(a, st);
 }
 
 int oa_part_unbucket(const oa_unbucket_args *args, void *stream) {
@@ -2958,3 +3048,4 @@ int oa_angle_add(const uint16_t *angles_prev, const void *change, int64_t n, int
 }
 
 }  // extern "C"
+#endif  // OA_TU <= 0

@@ -18,6 +18,8 @@ no CPU fallback: without the library or a device these calls raise.
 import ctypes
 import time
 
+import contextlib
+
 import numpy as np
 
 from . import _native as N
@@ -64,12 +66,30 @@ class _H5Store:
             for k, v in datasets.items():
                 grp.create_dataset(k, data=v)
 
-    def add_datasets(self, items):
-        """(group, name, array) triples written in one 'r+' open, as the reference's
-        save_final_apsis_counts writes all of its datasets in one (postprocessing.py:200)."""
+    @contextlib.contextmanager
+    def session(self):
+        """One 'r+' open held across a run of reads and dataset writes, as the
+        reference's save_final_apsis_counts holds one (postprocessing.py:196-240): each
+        dataset is in the file as soon as it is computed, so an error part-way leaves the
+        earlier snapshots' datasets written, as the reference's does."""
         with self._h5py.File(self.path, 'r+') as hf:
-            for g, d, arr in items:
-                hf[g].create_dataset(d, data=arr)
+            yield _H5Session(hf)
+
+
+class _H5Session:
+    """Reads and dataset writes through one open h5py file (_H5Store.session)."""
+
+    def __init__(self, hf):
+        self.hf = hf
+
+    def group_names(self):
+        return list(self.hf.keys())
+
+    def read(self, g, d):
+        return self.hf[g][d][:]
+
+    def add_dataset(self, g, d, arr):
+        self.hf[g].create_dataset(d, data=arr)
 
 
 class _MemStore:
@@ -89,12 +109,15 @@ class _MemStore:
     def create_group(self, name, datasets):
         self.obj.write_group(name, datasets)
 
-    def add_datasets(self, items):
-        for g, d, arr in items:
-            grp = self.obj.groups[g]
-            if d in grp:
-                raise ValueError('dataset %s/%s exists' % (g, d))
-            grp[d] = np.asarray(arr)
+    @contextlib.contextmanager
+    def session(self):
+        yield self
+
+    def add_dataset(self, g, d, arr):
+        grp = self.obj.groups[g]
+        if d in grp:
+            raise ValueError('dataset %s/%s exists' % (g, d))
+        grp[d] = np.asarray(arr)
 
 
 def _store(f, mode='r'):
@@ -344,7 +367,12 @@ class Apsides:
         lib = N.load(require_device=True)
         dev = self._dev()
         torch = _torch()
-        st = _store(collated_file, 'r+')
+        with _store(collated_file, 'r+').session() as st:
+            self._final_counts(st, lib, dev, torch, snapshot_numbers, verbose)
+
+    def _final_counts(self, st, lib, dev, torch, snapshot_numbers, verbose):
+        """save_final_apsis_counts inside one open store session: each snapshot's
+        counts are computed on the device and written before the next one's."""
         tag = '{}er'.format(self.mode[:-3])
         skeys = np.array(st.group_names())
         ids_final = st.read(skeys[-1], 'particle_IDs')
@@ -361,7 +389,6 @@ class Apsides:
         foff_d = _dev(offsets_final, dev)
         fcnt_d = _dev(counts_final, dev)
         stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        written = []
         for skey in skeys_:
             ids = st.read(skey, 'particle_IDs')
             if ids.dtype != ids_final.dtype:
@@ -383,8 +410,6 @@ class Apsides:
             if int(status.item()) & N.POST_MISSING:
                 raise ValueError('%s: particle IDs absent from the final snapshot\'s halo '
                                  '(shape mismatch in the reference)' % skey)
-            written.append((skey, '{}_counts_final'.format(tag), _host(out, n, np.float64)))
-        st.add_datasets(written)
-        if verbose:
-            for skey in skeys_:
+            st.add_dataset(skey, '{}_counts_final'.format(tag), _host(out, n, np.float64))
+            if verbose:
                 print('Final counts saved for {} {}'.format(*(skey.split('_'))))

@@ -701,7 +701,8 @@ class ShardedEngine:
         p = prev if prev is not None else self.prev
         nh = len(sp.exists)
         if sp.rows is not None:
-            self.local.set_catalogue(sp.lp, self._exchange(sp.rows, nh))
+            self.local.set_catalogue(sp.lp, self._exchange(sp.rows, nh),
+                                     None if p is None else p.lp)
         kw = {}
         if defer and getattr(self.local, 'deferrable', False):
             kw['defer'] = True
@@ -853,20 +854,34 @@ class EngineLocal:
         layout = None
         if compare and prev_lp is not None:
             layout = (prev_lp.starts, prev_lp.counts, prev_lp.exists, prev_lp.plan, prev_lp.n,
-                      prev_lp.buckets)
+                      prev_lp.buckets, prev_lp.centres)
         lp = eng.prepare(shard, centres, bulk, H, z, exists, compare, angles_in=angles_in,
                          plan_src=shard, prev_layout=layout)
         lp.exists = np.asarray(exists)
         lp.src = (shard, centres, bulk, H, z, exists, compare, angles_in, layout)
+        # halos with a progenitor and its row in the previous step's table (set_catalogue)
+        pidx = eng.last_prev_idx
+        hp = np.flatnonzero(pidx >= 0)
+        from .engine import _up
+        lp.prev_sel = (_up(hp.astype(np.int64), eng.device),
+                       _up(pidx[hp].astype(np.int64), eng.device)) if compare else None
         lp.share_bulk = bool(share)
         return lp
 
-    def set_catalogue(self, lp, rows):
+    def set_catalogue(self, lp, rows, prev_lp=None):
         """The exchanged catalogue rows into the device halo table (centre, and the
-        bulk velocity when it comes from the catalogue)."""
-        hv = lp.halos.view(torch.float64).view(-1, 12)
+        bulk velocity when it comes from the catalogue); a compare step's halos also get
+        their progenitors' previous centres from the previous step's device table (the
+        centres that step's frame used: the recomputed previous r̂ needs exactly those)."""
+        from . import _native as N
+        w = N.HALO_DTYPE.itemsize // 8
+        hv = lp.halos.view(torch.float64).view(-1, w)
         hi = 10 if lp.share_bulk else 7
         hv[:, 4:hi] = rows[:, :hi - 4].to(hv.device, non_blocking=True)
+        sel = getattr(lp, 'prev_sel', None)
+        if lp.compare and prev_lp is not None and sel is not None and len(sel[0]):
+            pv = prev_lp.halos.view(torch.float64).view(-1, w)
+            hv[sel[0], 12:15] = pv[sel[1], 4:7]
 
     deferrable = True                  # launch(defer=True) + settle (ShardedEngine.step)
 
@@ -874,16 +889,11 @@ class EngineLocal:
         from .engine import SnapshotState
         if not (lp.compare and prev_lp is not None):
             return None
-        return SnapshotState(ids=prev_lp.snap['ids'], rhat=prev_lp.rhat, meta=prev_lp.meta,
-                             starts=prev_lp.starts, counts=prev_lp.counts,
-                             exists=prev_lp.exists, plan=prev_lp.plan,
-                             buckets=prev_lp.buckets)
+        return SnapshotState.of(prev_lp, prev_lp.exists)
 
     def _set_prev(self, lp):
         from .engine import SnapshotState
-        self.engine.prev = SnapshotState(ids=lp.snap['ids'], rhat=lp.rhat, meta=lp.meta,
-                                         starts=lp.starts, counts=lp.counts, exists=lp.exists,
-                                         plan=lp.plan, buckets=lp.buckets)
+        self.engine.prev = SnapshotState.of(lp, lp.exists)
 
     def _replan(self, lp, st):
         """The step re-planned after status ``st`` (smaller items / large halos on the
@@ -893,10 +903,14 @@ class EngineLocal:
         eng.note_status(st)
         entries, part = retry_plan(lp, st)
         shard, centres, bulk, H, z, exists, compare, angles_in, layout = lp.src
-        hv = lp.halos.view(torch.float64).view(-1, 12)[:, 4:10].clone()
+        from . import _native as N
+        w = N.HALO_DTYPE.itemsize // 8
+        hv = lp.halos.view(torch.float64).view(-1, w)
+        cat, pc = hv[:, 4:10].clone(), hv[:, 12:15].clone()     # centre + bulk, prev centre
         lp2 = eng.prepare(shard, centres, bulk, H, z, exists, compare, angles_in=angles_in,
                           plan_src=shard, prev_layout=layout, entries=entries, part=part)
-        lp2.halos.view(torch.float64).view(-1, 12)[:, 4:10] = hv
+        hv2 = lp2.halos.view(torch.float64).view(-1, w)
+        hv2[:, 4:10], hv2[:, 12:15] = cat, pc
         lp2.exists, lp2.src, lp2.share_bulk = lp.exists, lp.src, lp.share_bulk
         lp2.ws_idx = getattr(lp, 'ws_idx', eng._wsi)
         lp.__dict__.update(lp2.__dict__)

@@ -183,12 +183,18 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
                     flush()
 
             progen_exists = halo_exists
-    except Exception:
+    except BaseException as e:
         # the reference had written every group before the failing snapshot: write
         # those whose records are available without re-running anything (a step that
         # asks for a re-plan, a device that does not answer within a few seconds, or a
-        # failing query ends this); KeyboardInterrupt / SystemExit touch nothing
-        _salvage(groups, eng, out)
+        # failing query ends this).  No new record fetch is started when fetching is a
+        # collective (a sharded engine: the other ranks may already be in the next
+        # step's collectives, and an unmatched gather would hang them) or after a
+        # KeyboardInterrupt / SystemExit (only fetches already complete are written).
+        collective = getattr(eng, 'world', 1) > 1
+        interrupted = not isinstance(e, Exception)
+        _salvage(groups, eng, out, new_fetches=not (collective or interrupted),
+                 timeout=0.0 if interrupted else 10.0)
         raise
     flush()
 
@@ -205,14 +211,17 @@ def _poll(ready, t_end):
     return True
 
 
-def _salvage(groups, eng, out, timeout=10.0):
+def _salvage(groups, eng, out, timeout=10.0, new_fetches=True):
     """Error path of track_orbits: write pending groups oldest first while each one's
-    records can be had without a re-run or an unbounded wait."""
+    records can be had without a re-run or an unbounded wait (``new_fetches`` False:
+    only groups whose fetch was already issued)."""
     t_end = time.time() + timeout
     try:
         while groups:
             g = groups[0]
             if g[2] is None:
+                if not new_fetches:
+                    return
                 ready = getattr(eng, 'step_ready', None)
                 if ready is None or not _poll(lambda: ready(g[0]) is not None, t_end) or \
                         not ready(g[0]):

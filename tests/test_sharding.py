@@ -261,3 +261,104 @@ def test_stripes_partition_rows_at_block_bounds(world):
     assert all(rows[r][1] == rows[r + 1][0] for r in range(world - 1))
     for lo, hi in rows:                              # balanced to within one block
         assert abs((hi - lo) - (n - 7) / world) <= cnt.max()
+
+
+class _Boom(RuntimeError):
+    pass
+
+
+def _fail_worker(rank, world, port, outdir):
+    """Rank 0's loader raises at the fifth snapshot (the other rank is then already in
+    that step's collectives); every rank must end."""
+    import datetime
+    import time
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))
+    t_err = None
+    status = 'ok'
+    try:
+        from orbitanalysis_amd.sharding import ShardedEngine
+        from orbitanalysis_amd.savefile import MemorySavefile
+        from orbitanalysis_amd.track_orbits import track_orbits
+        from oracle_local import OracleLocal
+        from orbitanalysis_amd.synthetic import PlummerSnapshots
+        u = PlummerSnapshots(n_halos=3, n_per_halo=[300, 200, 150], n_snapshots=7, seed=9)
+        bad = u.snapshot_numbers[4]
+
+        def load(s, pos, rad):
+            nonlocal t_err
+            if rank == 0 and s == bad:
+                t_err = time.time()
+                raise _Boom('loader failed')
+            return u.load_snapshot_data(s, pos, rad)
+        out = MemorySavefile()
+        try:
+            track_orbits(u.snapshot_numbers, u.main_branches(), u.regions, load, out,
+                         verbose=False, engine=ShardedEngine(OracleLocal('pericentric')))
+        except _Boom:
+            status = 'boom %.2f %d' % (time.time() - t_err, len(out.groups))
+        except Exception as e:          # a peer that left mid-collective: also an exit
+            status = 'peer %s' % type(e).__name__
+    finally:
+        with open(os.path.join(outdir, 'rank%d' % rank), 'w') as f:
+            f.write(status)
+        try:
+            dist.destroy_process_group()
+        except Exception:
+            pass
+
+
+def test_sharded_error_on_root_ends_every_rank():
+    """an error on rank 0 alone while the ranks are pipelined must not start
+    a collective record fetch in the error path (the other rank is already in the next
+    step's collectives, and an unmatched gather would hang or mix them): rank 0 writes
+    the groups whose records it already has, re-raises at once, and every rank ends."""
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.start_processes(_fail_worker, args=(2, _free_port(), d), nprocs=2,
+                                 join=False, start_method='spawn')
+        import time
+        t_end = time.time() + 150
+        while not ctx.join(timeout=5):
+            assert time.time() < t_end, 'a rank hung after the root failed'
+        st = {r: open(os.path.join(d, 'rank%d' % r)).read() for r in range(2)}
+    assert st[0].startswith('boom'), st
+    _, dt, n = st[0].split()
+    assert float(dt) < 5.0, st                        # no wait on an unmatched collective
+    assert int(n) == 2, st                            # groups 1-2 of 3 computed before it
+
+
+def test_salvage_starts_no_collective_fetch():
+    """The error path writes only groups whose records' fetch was already issued when
+    fetching is a collective (ShardedEngine) or after an interrupt."""
+    from orbitanalysis_amd import track_orbits as T
+    from orbitanalysis_amd.savefile import MemorySavefile
+
+    class Eng:
+        world = 2
+
+        def step_ready(self, res):
+            return True
+
+        def fetch_async(self, *a):
+            raise AssertionError('collective fetch started in the error path')
+
+    class Done:
+        def query(self):
+            return True
+
+    class Fetched:
+        done = Done()
+
+        def wait(self):
+            return np.array([0, 1]), np.array([7]), np.array([0.5], np.float16)
+
+    out = MemorySavefile()
+    out.initialize('pericentric', None)
+    ga = (np.zeros((1, 3)), np.ones(1), np.zeros((1, 3)), np.array([3]), None, 4,
+          'pericentric', False, None, False)
+    gb = ga[:5] + (5,) + ga[6:]
+    groups = [[None, np.int64, Fetched(), ga, {}], [None, np.int64, None, gb, {}]]
+    T._salvage(groups, Eng(), out, new_fetches=False)
+    assert sorted(out.groups) == ['snapshot_004'] and len(groups) == 1

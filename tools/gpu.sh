@@ -72,6 +72,11 @@ pstamps)
   ORBIT_HIP_LIB=$R/nbody-orbit-analysis_amd/variants/lib_stamps.so timeout -k 10 300 \
     python tools/part_stamps.py > "$O/pstamps_$T.txt" 2>&1
   rc=$?; tail -12 "$O/pstamps_$T.txt"; ok $rc pstamps ;;
+stamps)
+  # per-work-group phases of k_step (stamps build: tools/variants.sh "stamps -DOA_STAMPS=1")
+  ORBIT_HIP_LIB=$R/nbody-orbit-analysis_amd/variants/lib_${STAMPS_LIB:-stamps}.so timeout -k 10 300 \
+    python tools/stamps.py > "$O/stamps_$T.txt" 2>&1
+  rc=$?; tail -22 "$O/stamps_$T.txt"; ok $rc stamps ;;
 bigsweep)
   # configs[1] under environment settings ($BIG_ENVS: space-separated NAME=VALUE,NAME=VALUE)
   for rep in ${REPS:-1 2}; do

@@ -11,7 +11,6 @@ from orbitanalysis_amd import _native as N
 from orbitanalysis_amd.engine import OrbitEngine
 from orbitanalysis_amd.synthetic_device import DevicePlummer
 from orbitanalysis_amd.utils import hubble_parameter
-from collections import namedtuple
 
 n = float(os.environ.get('NPART', 1e8)); nh = int(os.environ.get('NHALO', 10000))
 gen = DevicePlummer(n_halos=nh, n_particles=int(n))
@@ -24,12 +23,12 @@ ex = np.arange(nh)
 eng = OrbitEngine()
 p0 = eng.prepare(s0, c0[0], c0[2], H, z, ex, False)
 eng.launch(p0, None)
-p1 = eng.prepare(s1, c1[0], c1[2], H, z, ex, True,
-                 prev_layout=(p0.starts, p0.counts, ex, p0.plan, p0.n))
+from orbitanalysis_amd.engine import SnapshotState, layout_of
+p1 = eng.prepare(s1, c1[0], c1[2], H, z, ex, True, prev_layout=layout_of(p0, ex))
 ws = eng.workspace(p1)
-St = namedtuple('St', 'ids rhat meta')
+st0 = SnapshotState.of(p0, ex)
 for rep in range(3):
-    eng.launch(p1, ws, St(s0['ids'], p0.rhat, p0.meta))
+    eng.launch(p1, ws, st0)
 torch.cuda.synchronize()
 ni = len(p1.items)
 nw = eng.lib.oa_build_info(0) // 64
