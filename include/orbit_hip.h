@@ -56,7 +56,7 @@ extern "C" {
 #define OA_MODE_PERICENTRIC 0
 #define OA_MODE_APOCENTRIC 1
 
-/* One current-snapshot halo (region block).  128 bytes, device array. */
+/* One current-snapshot halo (region block).  96 bytes, device array. */
 typedef struct oa_halo {
     int64_t cur_off, cur_cnt;   /* block [cur_off, cur_off+cur_cnt) of the current arrays
                                    (region_offsets, track_orbits.py:129-132)            */
@@ -68,10 +68,6 @@ typedef struct oa_halo {
     int64_t out_slot;           /* index among halos with a progenitor (apsis offsets),
                                    -1 if none                                            */
     int64_t reserved;
-    double prev_centre[3];      /* the progenitor's centre in the previous snapshot (its
-                                   region_positions row, track_orbits.py:155): the frame
-                                   a previous r̂ is recomputed in (coords_prev)          */
-    int64_t reserved2;
 } oa_halo;
 
 /* One work-group's share of a snapshot.  48 bytes, device array, built on the host by
@@ -264,22 +260,6 @@ typedef struct oa_step_args {
     int32_t *out_pos;           /* optional: each record's previous-state row (the
                                    oa_compact_args.out_pos of a scratch_pos step)     */
     int64_t *total_out;         /* device scalar: number of records                    */
-    /* Previous r̂ recomputed, not stored (ABI 16).  The reference carries rhats between
-     * snapshots (track_orbits.py:234-240); r̂ is a pure function of a particle's
-     * coordinates, its halo's centre and the box (region_frame :256-287), so a compare
-     * step can recompute the previous r̂ from the previous snapshot's coordinates
-     * instead of reading a stored copy, and a step whose successor does so need not
-     * write one.  coords_prev != NULL (packed items only: n_global_items = 0, not
-     * on-the-fly): k_step reads coords_prev + halos[].prev_centre + the previous box
-     * below instead of rhat_prev (which may be NULL); the previous snapshot's
-     * coordinate and r̂ dtypes must equal this one's (coord_f64, dx_f64).
-     * rhat_out may be NULL for packed items only (n_global_items = 0, not on-the-fly):
-     * no r̂ is written.  meta_out may be NULL for a frame-only launch of packed items:
-     * only r̂ is written (the previous snapshot's r̂ materialised on demand). */
-    const void *coords_prev;    /* (n_prev,3) the previous snapshot's coordinates       */
-    double box_prev[3];         /* the previous snapshot's box (as box / n_box_dims /  */
-    int32_t n_box_dims_prev;    /*   wrap_f64 of its own step)                         */
-    int32_t wrap_f64_prev;
     uint32_t lb_spin_max;       /* direct records: polls of an unpublished look-back word
                                    before OA_STATUS_LOOKBACK (0: the default, 2^20; a
                                    test sets 1 to exercise the re-run without direct)  */

@@ -20,8 +20,7 @@ c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, cty
 # numpy mirrors of the device tables (little-endian, C layout)
 HALO_DTYPE = np.dtype([('cur_off', '<i8'), ('cur_cnt', '<i8'), ('prev_off', '<i8'),
                        ('prev_cnt', '<i8'), ('centre', '<f8', (3,)), ('bulk', '<f8', (3,)),
-                       ('out_slot', '<i8'), ('reserved', '<i8'), ('prev_centre', '<f8', (3,)),
-                       ('reserved2', '<i8')])
+                       ('out_slot', '<i8'), ('reserved', '<i8')])
 ITEM_DTYPE = np.dtype([('h0', '<i4'), ('h1', '<i4'), ('slot0', '<i4'), ('n_span', '<i4'),
                        ('scratch_off', '<i8'), ('n_pv', '<i8'), ('cur_off', '<i8'),
                        ('n_slots', '<i4'), ('reserved', '<i4')])
@@ -60,8 +59,7 @@ class StepArgs(ctypes.Structure):
                 ('items_single', c_i32), ('direct', c_i32), ('lookback', c_vp),
                 ('lb_epoch', c_i32), ('n_slots', c_i32), ('offsets_out', c_vp), ('out_ids', c_vp),
                 ('out_ang', c_vp), ('out_pos', c_vp), ('total_out', c_vp),
-                ('coords_prev', c_vp), ('box_prev', c_dbl * 3), ('n_box_dims_prev', c_i32),
-                ('wrap_f64_prev', c_i32), ('lb_spin_max', ctypes.c_uint32),
+                ('lb_spin_max', ctypes.c_uint32),
                 ('reserved_abi16', c_i32)]
 
 

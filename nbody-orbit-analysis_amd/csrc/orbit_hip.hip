@@ -275,7 +275,6 @@ struct ItemHdr {
     int64_t seg_prev_off[HMAX];
     double cb[HMAX][6];             // centre[3], bulk[3]
     float cf[HMAX][6];              // the same, rounded to float32
-    double cbp[HMAX][3];            // RC: the progenitor's previous centre (prev_centre)
 };
 constexpr int64_t HDR_BYTES = (sizeof(ItemHdr) + 255) & ~int64_t(255);
 
@@ -385,8 +384,7 @@ __device__ __forceinline__ uint32_t upper_find(const uint32_t *starts, uint32_t 
 
 // ------------------------------------------------------------------ frame
 // One snapshot's periodic box as recenter_coordinates (utils.py:24-33) applies it,
-// derived on the host (make_wrap): the current snapshot's for the frame, the previous
-// snapshot's for a previous r̂ recomputed from its coordinates (oa_step_args.coords_prev).
+// derived on the host (make_wrap).
 struct WrapK {
     double box[3];         // L per dimension (float64 values)
     float hi[3];           // smallest float32 with  dx >  L/2  (float32 dx plans)
@@ -711,14 +709,9 @@ __device__ __forceinline__ int64_t uni64(int64_t x) {
 constexpr uint32_t PK_HIT = 1u << 14, PK_FLAG = 1u << 15;
 
 // SINGLE: every item holds one halo (oa_step_args.items_single): the packed-item paths
-// (per-row halo and segment lookups) are compiled out.
-// RC: the previous r̂ is recomputed from the previous snapshot's coordinates
-// (oa_step_args.coords_prev, the previous centre and box wp) instead of read from
-// rhat_prev: the same 3 values per previous particle come from HBM, and the step that
-// produced the previous state never had to write them.
-template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF, bool SINGLE = false,
-          bool RC = false>
-__global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK fk, const WrapK wp) {
+// (per-row halo and segment lookups) are compiled out
+template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF, bool SINGLE = false>
+__global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK fk) {
     typedef typename IdT<IDB>::T ID;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     ItemHdr &H = *reinterpret_cast<ItemHdr *>(smem);
@@ -764,12 +757,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     const Rsrc r_id = make_rsrc(ids + base, n_span * IDB);
     const Rsrc r_x = make_rsrc(reinterpret_cast<const TX *>(a.coords) + 3 * base, n_span * SX);
     const Rsrc r_v = make_rsrc(reinterpret_cast<const TV *>(a.vels) + 3 * base, n_span * SV);
-    // rhat_out == NULL: no r̂ is written (its successor recomputes it, RC); meta_out ==
-    // NULL: a frame-only launch that materialises r̂ alone (its stores fall outside a
-    // 0-byte resource and are dropped)
-    const bool wr_rh = rhat_out != nullptr;
-    const Rsrc r_rh = make_rsrc(rhat_out + 3 * base, wr_rh ? n_span * SD : 0u);
-    const Rsrc r_mt = make_rsrc(a.meta_out + base, a.meta_out ? n_span * 4u : 0u);
+    const Rsrc r_rh = make_rsrc(rhat_out + 3 * base, n_span * SD);
+    const Rsrc r_mt = make_rsrc(a.meta_out + base, n_span * 4u);
     // Phase-1 rows go in trips of U1 consecutive rows; a wave takes at most NTRIP trips
     // (<= SU rows) and keeps each row's r̂ in registers (rr) until phase 2b writes it
     // into the LDS the table held -- no read-back of the rows it stored.
@@ -831,8 +820,6 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             H.halo_cnt[lane] = 0;
             for (int d = 0; d < 3; ++d) { H.cb[lane][d] = hrow.centre[d]; H.cb[lane][3 + d] = hrow.bulk[d]; }
             for (int d = 0; d < 3; ++d) { H.cf[lane][d] = (float)hrow.centre[d]; H.cf[lane][3 + d] = (float)hrow.bulk[d]; }
-            if (RC)
-                for (int d = 0; d < 3; ++d) H.cbp[lane][d] = hrow.prev_centre[d];
             if (hp) {
                 const uint32_t sg = si - 1u;
                 H.seg_halo[sg] = lane; H.seg_prev_off[sg] = hrow.prev_off;
@@ -907,7 +894,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             }
             // compare steps store r̂ from registers in phase 2b (RDEFER): phase 1 then
             // issues loads only and ends without waiting on stores
-            if (!RD && wr_rh) bst3<TD>(r_rh, li * SD, r);
+            if (!RD) bst3<TD>(r_rh, li * SD, r);
             rr[kp * U1 + u] = V3<TD>{r[0], r[1], r[2]};
             if constexpr (!COMPARE) {
                 uint32_t ang = 0;
@@ -1008,7 +995,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         }
     };
     if (n_pv == 0) {                                 // nothing to join: state words only
-        if (RD && wr_rh) store_rhat();
+        if (RD) store_rhat();
         __syncthreads();
         for (uint32_t li = tid; li < n_span; li += WG)
             bst32<AUX_NT>(r_mt, li * 4u, (uint32_t)(sgn8[li] & 3u) << 16);
@@ -1039,11 +1026,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // up to 2 * KROWS loads in flight per wave hide the HBM latency behind them.
     ID pid[KROWS];
     uint32_t pk[KROWS];
-    // phase 2b: each row's previous r̂, or (RC) its previous coordinates
-    typedef typename std::conditional<RC, TX, TD>::type TP;
-    constexpr uint32_t SP = 3 * sizeof(TP);
-    const TP *prev3 = RC ? static_cast<const TP *>(a.coords_prev) : reinterpret_cast<const TP *>(rhat_prev);
-    V3<TP> prh[KROWS];
+    V3<TD> prh[KROWS];
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < KROWS; ++k) {
@@ -1216,7 +1199,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         uint32_t nv, hs;
         int64_t kb;
         row_of(wave + NWAVE * k, nv, hs, kb);
-        prh[k] = bld3<TP, AUX_NT>(make_rsrc(prev3 + 3 * kb, nv * SP), lane * SP);
+        prh[k] = bld3<TD, AUX_NT>(make_rsrc(rhat_prev + 3 * kb, nv * SD), lane * SD);
     }
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1252,7 +1235,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
                                 : (uint32_t)(wave + NWAVE * k) * 64 + lane;
         if (li < n_span) { rcx[li] = rr[k].x; rcy[li] = rr[k].y; rcz[li] = rr[k].z; }
     }
-    if (RD && wr_rh) store_rhat();
+    if (RD) store_rhat();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -1271,7 +1254,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
             uint32_t nv, hs;
             int64_t kb;
             row_of(wave + NWAVE * (k + PF2), nv, hs, kb);
-            prh[k + PF2] = bld3<TP, AUX_NT>(make_rsrc(prev3 + 3 * kb, nv * SP), lane * SP);
+            prh[k + PF2] = bld3<TD, AUX_NT>(make_rsrc(rhat_prev + 3 * kb, nv * SD), lane * SD);
         }
         const uint32_t r = wave + NWAVE * k;
         if (r >= nrow) continue;
@@ -1283,20 +1266,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         uint16_t a16 = 0;
         if (p & PK_HIT) {
             const uint32_t c = p & (PK_HIT - 1u);
-            TD rp[3];
-            if constexpr (RC) {
-                // the previous r̂ exactly as the previous step's frame computed it
-                // (track_orbits.py:256-287 in the previous snapshot's frame)
-                const double *cb = H.cbp[hs];
-                const float cf[3] = {(float)cb[0], (float)cb[1], (float)cb[2]};
-                TD dx[3];
-                centre_dx<TX, TD>(prh[k], cb, cf, wp, dx);
-                unit_vector(dx, rp);
-            } else {
-                rp[0] = prh[k].x; rp[1] = prh[k].y; rp[2] = prh[k].z;
-            }
             // angle change = arccos(dot(r̂_prev, r̂_match)), no clamp (:324-325)
-            const TD dt = dot3(rp[0], rp[1], rp[2], rcx[c], rcy[c], rcz[c]);
+            const TD dt = dot3(prh[k].x, prh[k].y, prh[k].z, rcx[c], rcy[c], rcz[c]);
             const TD change = acos_change<OTF>(dt);
             // calc_angles (:342-349): f16 + change, rounded once; reset at an apsis
             const uint16_t acc = angle_add((uint16_t)(p >> 16), change);
@@ -1743,15 +1714,10 @@ int launch_step_c(const oa_step_args &a, hipStream_t st) {
         // a frame-only launch needs no table: several work-groups share a CU
         const int64_t lds = COMPARE ? step_lds_bytes(a.lds_entries, a.lds_slots, (int)sizeof(TD))
                                     : HDR_BYTES;
-        const bool rc = COMPARE && !OTF && a.coords_prev;
-        auto k = !(COMPARE && !OTF) ? k_step<TX, TV, TD, IDB, COMPARE, OTF, false, false>
-                 : a.items_single ? (rc ? k_step<TX, TV, TD, IDB, COMPARE, OTF, true, true>
-                                        : k_step<TX, TV, TD, IDB, COMPARE, OTF, true, false>)
-                                  : (rc ? k_step<TX, TV, TD, IDB, COMPARE, OTF, false, true>
-                                        : k_step<TX, TV, TD, IDB, COMPARE, OTF, false, false>);
-        if (int rc2 = set_lds(k, lds)) return rc2;
-        hipLaunchKernelGGL(k, dim3(a.n_items), dim3(WG), (size_t)lds, st, a, make_frame_k(a),
-                           make_wrap(a.box_prev, a.n_box_dims_prev, a.wrap_f64_prev));
+        auto k = (COMPARE && !OTF && a.items_single) ? k_step<TX, TV, TD, IDB, COMPARE, OTF, true>
+                                                     : k_step<TX, TV, TD, IDB, COMPARE, OTF, false>;
+        if (int rc = set_lds(k, lds)) return rc;
+        hipLaunchKernelGGL(k, dim3(a.n_items), dim3(WG), (size_t)lds, st, a, make_frame_k(a));
         if (int rc = check_launch("k_step")) return rc;
     }
     return launch_big<TX, TV, TD, IDB, COMPARE, OTF>(a, st);
@@ -2840,20 +2806,10 @@ int oa_step(const oa_step_args *args, void *stream) {
                           a.lds_slots <= a.lds_entries))
         return fail(OA_E_ARG, "bad lds_entries/lds_slots (entries <= %d (r̂ dtype) < slots)",
                     (a.dx_f64 ? STAGE_F64 : STAGE_F32) * WG);
-    // packed items only (k_step) may skip the r̂ output, recompute the previous r̂ (RC) or,
-    // frame-only, skip the state words (ABI 16: oa_step_args.coords_prev)
-    const bool packed_only = a.n_global_items == 0 && !a.onthefly;
     if (a.n_items + a.n_global_items > 0 &&
-        (!a.halos || !a.ids || !a.coords || !a.vels || (!a.rhat_out && !packed_only) ||
-         (!a.meta_out && !(packed_only && !a.compare && !a.vr_out))))
+        (!a.halos || !a.ids || !a.coords || !a.vels || !a.rhat_out || !a.meta_out))
         return fail(OA_E_ARG, "null input/output pointer");
-    if (a.coords_prev && (!packed_only || !a.compare))
-        return fail(OA_E_ARG, "coords_prev: compare steps of packed items only");
-    if (a.coords_prev && (a.n_box_dims_prev < 0 || a.n_box_dims_prev > 3 ||
-                          (a.wrap_f64_prev == 0 && a.dx_f64)))
-        return fail(OA_E_ARG, "coords_prev: bad previous box");
-    if (a.compare && (!a.ids_prev || (!a.rhat_prev && !a.coords_prev) || !a.meta_prev ||
-                      !a.halo_count || !a.status ||
+    if (a.compare && (!a.ids_prev || !a.rhat_prev || !a.meta_prev || !a.halo_count || !a.status ||
                       (a.n_items > 0 && (!a.scratch_ids || !a.scratch_ang || !a.item_count ||
                                          !a.seg_count))))
         return fail(OA_E_ARG, "null previous-state / scratch pointer");

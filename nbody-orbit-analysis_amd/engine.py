@@ -208,10 +208,6 @@ def plan_global(glob, cur_cnt, prev_cnt, first_index, compare):
 # from k_step (oa_step_args.direct: decoupled look-back over items), so the step needs
 # no oa_compact; ORBIT_DIRECT=0 keeps scratch + oa_compact
 DIRECT = os.environ.get('ORBIT_DIRECT', '1') != '0'
-# compare steps of packed items recompute the previous r̂ from the previous snapshot's
-# coordinates (oa_step_args.coords_prev), and steps of packed items write no r̂ (it is
-# materialised on demand: OrbitEngine.rhat_of); ORBIT_RC=0 stores and reads r̂
-RC = os.environ.get('ORBIT_RC', '1') != '0'
 
 PART_FILL = 0.9      # mean fill of a large-halo partition's LDS table at most (k_part_join)
 
@@ -488,45 +484,31 @@ class BucketSet:
 
 @dataclass
 class SnapshotState:
-    """Device state a snapshot leaves for the next one (track_orbits.py:234-240).
-
-    ``rhat`` is None when the step wrote no r̂ (packed items, ``engine.RC``): the next
-    step recomputes it from ``coords`` (the snapshot's coordinates, retained like the
-    reference retains ``ids_prev``, :237) and ``centres``; ``OrbitEngine.rhat_of``
-    materialises it from ``src`` (the step that produced the state) when a caller
-    needs the stored form."""
+    """Device state a snapshot leaves for the next one (track_orbits.py:234-240)."""
     ids: torch.Tensor
-    rhat: Optional[torch.Tensor]
+    rhat: torch.Tensor
     meta: torch.Tensor
     starts: np.ndarray
     counts: np.ndarray
     exists: np.ndarray
     plan: DtypePlan
     buckets: Optional[BucketSet] = None
-    coords: Optional[torch.Tensor] = None      # the snapshot's device coordinates
-    centres: Optional[np.ndarray] = None       # (n_halos, 3) float64 frame centres
-    src: Optional['PreparedStep'] = None       # for rhat_of (when rhat is None)
-    coords_version: int = -1                   # coords._version when retained
 
     @classmethod
     def of(cls, pr, exists, ids=None):
         """The state a prepared (and launched) step leaves for the next one."""
-        coords = pr.snap.get('coordinates') if pr.snap else None
         return cls(ids=pr.snap['ids'] if ids is None else ids, rhat=pr.rhat, meta=pr.meta,
                    starts=pr.starts, counts=pr.counts, exists=np.asarray(exists), plan=pr.plan,
-                   buckets=pr.buckets, coords=coords, centres=pr.centres,
-                   src=pr if pr.rhat is None else None,
-                   coords_version=-1 if coords is None else coords._version)
+                   buckets=pr.buckets)
 
     def layout(self):
         """The ``prev_layout`` of the next step's ``prepare``."""
-        return (self.starts, self.counts, self.exists, self.plan, self.ids.numel(), self.buckets,
-                self.centres)
+        return (self.starts, self.counts, self.exists, self.plan, self.ids.numel(), self.buckets)
 
 
 def layout_of(pr, exists):
     """``prev_layout`` for the step after the prepared step ``pr`` (bench / tools)."""
-    return (pr.starts, pr.counts, np.asarray(exists), pr.plan, pr.n, pr.buckets, pr.centres)
+    return (pr.starts, pr.counts, np.asarray(exists), pr.plan, pr.n, pr.buckets)
 
 
 @dataclass
@@ -580,7 +562,6 @@ class PreparedStep:
     bulk_computed: bool = False
     buckets: Optional['BucketSet'] = None          # this step's current bucket set
     unbucket_prev: Optional[np.ndarray] = None     # previous halos to restore first
-    centres: Optional[np.ndarray] = None           # (n_halos, 3) float64 frame centres
     snap: dict = field(default_factory=dict)
     args: N.StepArgs = field(default_factory=N.StepArgs)
     cargs: N.CompactArgs = field(default_factory=N.CompactArgs)
@@ -713,8 +694,6 @@ class OrbitEngine:
         self.part_key4 = env('ORBIT_PART_KEY4', '1') != '0'
         # packed-only compare steps write their records from k_step (direct records)
         self.direct = DIRECT
-        # packed items: previous r̂ recomputed, none stored (engine.RC)
-        self.rc = RC
         # direct records' look-back poll bound (0: the library default); tests set 1 to
         # force OA_STATUS_LOOKBACK and the re-run through oa_compact
         self.lb_spin_max = 0
@@ -795,16 +774,11 @@ class OrbitEngine:
             has_prog = (p < len(pe)) & (pe[pc] == exists) if len(pe) else has_prog
             halos['prev_off'][has_prog] = p_starts[p[has_prog]]
             halos['prev_cnt'][has_prog] = p_counts[p[has_prog]]
-            p_centres = prev_layout[6] if len(prev_layout) > 6 else None
-            if p_centres is not None and len(p_centres):
-                halos['prev_centre'][has_prog] = np.asarray(p_centres)[p[has_prog]]
             halos['out_slot'][has_prog] = np.arange(int(has_prog.sum()))
             prev_idx[has_prog] = p[has_prog]
         buf, k, n_it, scratch = _plan(counts, halos['prev_cnt'], entries, self.hmax,
                                       halos['out_slot'], self.max_pv, slots, starts)
         self._prev_idx = prev_idx
-        self.last_prev_idx = prev_idx
-        self._prev_centres = compare and len(prev_layout) > 6 and prev_layout[6] is not None
         return halos, buf[:n_it], k, scratch, starts, counts, has_prog
 
     # ------------------------------------------------------------------ step
@@ -935,16 +909,14 @@ class OrbitEngine:
         return True
 
     def prepare(self, snap, centres, bulk_cat, H, z, exists, compare, angles_in=None,
-                plan_src=None, prev_layout=None, entries=None, part=True, keep_rhat=None):
+                plan_src=None, prev_layout=None, entries=None, part=True):
         """Host half of a step: dtype plan, halo/item tables, device uploads.
 
         ``snap`` holds device tensors for ids/coordinates/velocities(/masses);
         ``prev_layout`` (starts, counts, exists, plan) defaults to the engine state.
         ``entries`` overrides the per-item particle budget of the plan (0: every halo
         on the large-halo path); ``part`` = False keeps large halos on the global-table
-        path (k_big_*) instead of the partitioned one (k_part_*).  ``keep_rhat``: write
-        the r̂ state (default: only when the step has large halos or ``rc`` is off; a step
-        of packed items leaves it to be recomputed, ``rhat_of``)."""
+        path (k_big_*) instead of the partitioned one (k_part_*)."""
         dev = self.device
         exists = np.asarray(exists)
         plan = plan_dtypes(plan_src if plan_src is not None else snap,
@@ -978,8 +950,7 @@ class OrbitEngine:
         pr = PreparedStep(plan=plan, n=n, starts=starts, counts=counts, has_prog=has_prog,
                           items=all_items, n_small=n_small, scratch=scratch,
                           compare=bool(compare), n_prev=prev_layout[4] if compare else 0,
-                          entries=plan_e, centres=np.array(halos['centre']))
-        pr.prev_centres = bool(self._prev_centres)
+                          entries=plan_e)
         pr.halos = _upload(halos.view(np.uint8), dev)
         pr.d_items = _upload(all_items.view(np.uint8), dev)
         if len(glob):
@@ -1046,9 +1017,7 @@ class OrbitEngine:
                 done[prev_idx[hh]] = True
                 need &= ~done
             pr.unbucket_prev = np.flatnonzero(need & (prev_sets.K > 0))
-        if keep_rhat is None:
-            keep_rhat = len(glob) > 0 or not self.rc
-        pr.rhat = torch.empty(n * 3, dtype=plan.torch_dx, device=dev) if keep_rhat else None
+        pr.rhat = torch.empty(n * 3, dtype=plan.torch_dx, device=dev)
         pr.meta = torch.empty(n, dtype=torch.int32, device=dev)
         pr.snap = snap
         pr.bulk_computed = bulk_cat is None and len(halos) > 0
@@ -1059,7 +1028,7 @@ class OrbitEngine:
         a = pr.args
         a.ids, a.coords, a.vels, a.n_cur = (snap['ids'].data_ptr(), snap['coordinates'].data_ptr(),
                                             snap['velocities'].data_ptr(), n)
-        a.rhat_out, a.meta_out = _ptr(pr.rhat), pr.meta.data_ptr()
+        a.rhat_out, a.meta_out = pr.rhat.data_ptr(), pr.meta.data_ptr()
         a.angles_in = _ptr(pr.angles_in)
         a.halos, a.n_halos = pr.halos.data_ptr(), len(halos)
         a.items, a.n_items = pr.d_items.data_ptr(), len(items)
@@ -1121,29 +1090,16 @@ class OrbitEngine:
                 # progenitor blocks this step reads in position order (packed items, the
                 # global tables) from the previous step's bucket set
                 self.unbucket(p.buckets, pr.unbucket_prev, p.starts, p.rhat, p.meta, st)
-            # packed items recompute the previous r̂ from the previous coordinates when both
-            # snapshots share the coordinate and r̂ dtypes; anything else reads it stored
-            rc = self.can_recompute(pr, p)
-            a.coords_prev = p.coords.data_ptr() if rc else None
-            if rc:
-                self._check_coords(p)
-                box = tuple(p.plan.box)
-                a.n_box_dims_prev, a.wrap_f64_prev = len(box), int(p.plan.wrap_f64)
-                for d in range(3):
-                    a.box_prev[d] = box[d] if d < len(box) else 0.0
-                p_rhat = None
-            else:
-                p_rhat = self.rhat_of(p, st)
-                if p.plan.dx != pr.plan.dx:              # float32 -> float64 r̂: exact
-                    p_rhat = p_rhat.to(pr.plan.torch_dx)
-            p_ids = p.ids
+            p_ids, p_rhat = p.ids, p.rhat
+            if p.plan.dx != pr.plan.dx:                  # float32 -> float64 r̂: exact
+                p_rhat = p.rhat.to(pr.plan.torch_dx)
             if p.plan.ids.itemsize != pr.plan.ids.itemsize:
                 # 4-byte -> 8-byte IDs (unsigned ones zero-extended)
                 p_ids = p.ids.to(torch.int64)
                 if p.plan.ids.kind == 'u':
                     p_ids &= 0xFFFFFFFF
             res.extra['prev_widened'] = (p_ids, p_rhat)   # alive until the step is done
-            a.ids_prev, a.rhat_prev, a.meta_prev = (p_ids.data_ptr(), _ptr(p_rhat),
+            a.ids_prev, a.rhat_prev, a.meta_prev = (p_ids.data_ptr(), p_rhat.data_ptr(),
                                                     p.meta.data_ptr())
             a.n_prev = pr.n_prev
             # packed items only: k_step writes the records, offsets and total itself
@@ -1201,48 +1157,6 @@ class OrbitEngine:
         res.apsis_ids, res.apsis_ang, res.total = ws.out_ids, ws.out_ang, ws.total
         res.apsis_pos = ws.out_pos
         return res
-
-    # ------------------------------------------------------------------ r̂ state
-    def can_recompute(self, pr, p):
-        """Whether compare step ``pr`` recomputes the previous r̂ (oa_step_args.coords_prev):
-        packed items only (k_step), not on-the-fly, both snapshots in one coordinate and
-        r̂ dtype, and the previous coordinates and centres at hand."""
-        return bool(self.rc and pr.n_global == 0 and not pr.args.onthefly and
-                    p.coords is not None and p.centres is not None and
-                    getattr(pr, 'prev_centres', False) and
-                    p.plan.coord == pr.plan.coord and p.plan.dx == pr.plan.dx and
-                    p.coords.numel() == 3 * p.ids.numel())
-
-    @staticmethod
-    def _check_coords(p):
-        """The previous coordinates are read again by the next step (as the reference
-        reads ids_prev, track_orbits.py:237): a loader must not overwrite a device array
-        it handed over before the next snapshot's step has run."""
-        if p.coords_version >= 0 and p.coords._version != p.coords_version:
-            raise RuntimeError('the previous snapshot\'s coordinate tensor was modified in place '
-                               'before the next step read it (a loader must hand each snapshot '
-                               'its own arrays)')
-
-    def rhat_of(self, p, stream=None):
-        """The stored r̂ of state ``p`` (position order, its r̂ dtype), materialised on the
-        device when its step wrote none: a frame-only launch of that step's own packed
-        items over its own arrays, writing r̂ alone (oa_step_args.meta_out = NULL)."""
-        if p.rhat is not None:
-            return p.rhat
-        src = p.src
-        if src is None:
-            raise RuntimeError('snapshot state without r̂ and without the step that made it')
-        self._check_coords(p)
-        st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
-        rh = torch.empty(max(3 * src.n, 3), dtype=src.plan.torch_dx, device=self.device)
-        a = N.StepArgs.from_buffer_copy(src.args)
-        a.compare, a.direct, a.onthefly = 0, 0, 0
-        a.rhat_out, a.meta_out, a.angles_in, a.vr_out = rh.data_ptr(), None, None, None
-        a.coords_prev, a.n_global_items = None, 0
-        N.check(self.lib.oa_step(a, st), 'oa_step (r̂ materialised)')
-        p.rhat = rh
-        p.src = None
-        return rh
 
     # ------------------------------------------------------------------ host views
     def fetch_async(self, res, ids_dtype):

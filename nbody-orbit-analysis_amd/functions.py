@@ -58,7 +58,7 @@ def region_frame(snapshot, region_slice, region_position, region_bulk_vel, H):
     centres = np.asarray([region_position])
     bulk_cat = None if region_bulk_vel is None else np.asarray([region_bulk_vel])
     pr = eng.prepare(dsub, centres, bulk_cat, H, snapshot['redshift'], np.zeros(1, np.int64),
-                     False, plan_src=sub, keep_rhat=True)
+                     False, plan_src=sub)
     vr = torch.empty(max(n, 1), dtype=torch.float64, device=eng.device)
     pr.args.vr_out = vr.data_ptr()
     eng.launch(pr, None)

@@ -319,9 +319,14 @@ def _f64_bits(x):
     return np.ascontiguousarray(x, dtype=np.float64).view(np.int64)
 
 
-def _as_i64(t):
-    """IDs of any 32/64-bit integer dtype as int64 values (bit pattern kept for 64-bit)."""
-    return t if t.dtype == torch.int64 else t.to(torch.int64)
+def _sync_time(on):
+    """A synchronised timestamp (profiling only; 0 when off)."""
+    if not on:
+        return 0.0
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    import time
+    return time.perf_counter()
 
 
 def _to_tensor(x, device):
@@ -470,21 +475,46 @@ class ShardedResult:
 class ShardedFetch:
     """A sharded step's records on their way to rank 0 and its host (fetch_async)."""
 
-    def __init__(self, done, n_slots, h_cnt, h_ids, h_ang, ids_dtype, root):
+    def __init__(self, done, n_slots, h_off, h_ids, h_ang, ids_dtype, root):
         self.done, self.n_slots, self.root = done, n_slots, root
-        self.h_cnt, self.h_ids, self.h_ang, self.ids_dtype = h_cnt, h_ids, h_ang, ids_dtype
+        self.h_off, self.h_ids, self.h_ang, self.ids_dtype = h_off, h_ids, h_ang, ids_dtype
 
     def wait(self):
+        from .engine import ids_as
         dt = np.dtype(self.ids_dtype)
         if not self.root:
             return np.zeros(self.n_slots + 1, np.int64), np.zeros(0, dt), np.zeros(0, np.float16)
         if self.done is not None:
             self.done.synchronize()
-        cnt = self.h_cnt.numpy()
-        offsets = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
-        h = self.h_ids.numpy()
-        ids_h = h.view(np.uint64).astype(dt) if dt.kind == 'u' else h.astype(dt)
-        return offsets, ids_h, self.h_ang.numpy().astype(np.uint16).view(np.float16)
+        return (self.h_off.numpy().astype(np.int64), ids_as(self.h_ids.numpy(), dt),
+                self.h_ang.numpy().view(np.float16))
+
+
+def place_presharded(C, off, n):
+    """Output positions of the records gathered from the ranks of a presharded run.
+    ``C`` (W, S): rank r's records per halo slot, received rank-major and slot-major
+    within a rank; ``off`` (S + 1): the merged offsets.  A halo's global previous block
+    is the rank-major concatenation of the ranks' blocks, so its records from rank r
+    follow those from ranks < r, each rank's in its own (previous-block) order: a
+    per-(rank, slot) count scan places them, no sort."""
+    W, S = C.shape
+    flat = C.reshape(-1)
+    seg0 = torch.cumsum(flat, 0) - flat                         # (r, h) run start, received
+    before = torch.cumsum(C, 0) - C                             # ranks < r in slot h
+    D = (off[:S].unsqueeze(0) + before).reshape(-1) - seg0
+    return torch.arange(n, dtype=torch.int64, device=C.device) + \
+        torch.repeat_interleave(D, flat, output_size=n)
+
+
+def place_by_row(rows, n_rows):
+    """Output positions of records keyed by their global previous-snapshot row (the
+    stripe layout: a halo's records from different ranks interleave).  The reference's
+    order is increasing previous row (slots follow the previous blocks' order, and each
+    slot's records its block's order), so a record's position is the number of keyed rows
+    before it: a counting pass over the previous snapshot's rows (O(rows), no sort)."""
+    flags = torch.zeros(max(int(n_rows), 1), dtype=torch.int8, device=rows.device)
+    flags[rows.long()] = 1
+    return (torch.cumsum(flags, 0, dtype=torch.int32)[rows.long()] - 1).long()
 
 
 @dataclass
@@ -574,6 +604,9 @@ class ShardedEngine:
         self.prev: Optional[ShardedPrep] = None
         self._pending: Optional[ShardedResult] = None   # a deferred step not yet settled
         self._side = None                               # stream of the records' gathers
+        # rank 0's record placement timed (synchronised) into fetch_stats (rehearsals)
+        self.profile_fetch = False
+        self.fetch_stats = None
 
     def reset(self):
         self.settle()
@@ -701,8 +734,7 @@ class ShardedEngine:
         p = prev if prev is not None else self.prev
         nh = len(sp.exists)
         if sp.rows is not None:
-            self.local.set_catalogue(sp.lp, self._exchange(sp.rows, nh),
-                                     None if p is None else p.lp)
+            self.local.set_catalogue(sp.lp, self._exchange(sp.rows, nh))
         kw = {}
         if defer and getattr(self.local, 'deferrable', False):
             kw['defer'] = True
@@ -758,12 +790,15 @@ class ShardedEngine:
     # ---------------------------------------------------------------- outputs
     def fetch_async(self, res, ids_dtype):
         """Start gathering a step's records to rank 0 (the only writer) and their D2H
-        there; ``wait()`` returns (offsets, IDs, f16 angles) in the reference's order:
-        key = halo slot << 32 | position in the global previous block (track_orbits.py:
-        199-227, 315-316).  The gather runs on a side stream behind the step's own
-        kernels only, so it overlaps whatever the compute stream runs next (the next
-        snapshot's step); the workspace holding the records is not reused before it.
-        Ranks other than 0 (which write nothing) get zero offsets and no records."""
+        there; ``wait()`` returns (offsets, IDs, f16 angles) in the reference's order
+        (track_orbits.py:199-227, 315-316).  A record travels as its ID and f16 angle
+        (10 B with int64 IDs) plus, in the stripe layout, its 4-byte global previous row;
+        rank 0 places the rank-ordered runs by a per-(rank, slot) count scan (presharded)
+        or a counting pass over the previous rows (stripes), never a sort.  The gather
+        runs on a side stream behind the step's own kernels only, so it overlaps whatever
+        the compute stream runs next (the next snapshot's step); the workspace holding
+        the records is not reused before it.  Ranks other than 0 (which write nothing)
+        get zero offsets and no records."""
         self.settle(res)
         offs, a_ids, a_ang, a_pos = res.records
         lp = res.lp
@@ -776,38 +811,60 @@ class ShardedEngine:
                 self._side = torch.cuda.Stream(device=dev, priority=-1)
             side = self._side
         ctx = torch.cuda.stream(side) if side is not None else _nullcontext()
+        S = res.n_slots
+        root = self.rank == self.ROOT
+        prof = self.profile_fetch
         with ctx:
             if side is not None and done is not None:
                 side.wait_event(done)
             total = self.local.total(lp) if hasattr(self.local, 'total') else int(offs[-1])
-            slot = torch.repeat_interleave(torch.arange(res.n_slots, device=dev),
-                                           (offs[1:] - offs[:-1]).long(), output_size=total)
-            gpos_prev = res.prev_prep.gpos
-            g = gpos_prev[a_pos[:total].to(gpos_prev.device).long()]
-            rec = torch.stack([(slot.to(g.device) << 32) | g, _as_i64(a_ids[:total]).to(g.device),
-                               a_ang[:total].to(torch.int64).to(g.device)], dim=1)
-            rec, = gather_rows(self.group, self.ROOT, rec)
+            cnt = (offs[1:S + 1] - offs[:S]).to(torch.int64).reshape(1, S)
+            send = [a_ids[:total], a_ang[:total].to(torch.int16)]
+            rows = None
+            if not self.presharded:
+                pp = res.prev_prep
+                rows = pp.sel[a_pos[:total].to(pp.sel.device).long()]
+                n_rows = int(pp.n_global)
+                send.append(rows.to(torch.int32 if n_rows < 2 ** 31 else torch.int64).to(dev))
+            C, = gather_rows(self.group, self.ROOT, cnt)
+            got = gather_rows(self.group, self.ROOT, *send)
             ev = None
-            h_cnt = h_ids = h_ang = None
-            if self.rank == self.ROOT:
-                order = torch.argsort(rec[:, 0])
-                rec = rec[order]
-                cnt = torch.bincount((rec[:, 0] >> 32).long(), minlength=res.n_slots)[:res.n_slots] \
-                    if rec.shape[0] else torch.zeros(res.n_slots, dtype=torch.int64, device=rec.device)
-                pin = rec.device.type == 'cuda'
-                h_cnt = torch.empty(cnt.shape, dtype=torch.int64, pin_memory=pin)
-                h_ids = torch.empty(rec.shape[0], dtype=torch.int64, pin_memory=pin)
-                h_ang = torch.empty(rec.shape[0], dtype=torch.int64, pin_memory=pin)
-                h_cnt.copy_(cnt, non_blocking=pin)
-                h_ids.copy_(rec[:, 1], non_blocking=pin)
-                h_ang.copy_(rec[:, 2], non_blocking=pin)
+            h_off = h_ids = h_ang = None
+            if root:
+                t0 = _sync_time(prof)
+                ids_r, ang_r = got[0], got[1]
+                n = int(ids_r.shape[0])
+                C = C.to(ids_r.device)
+                off = torch.zeros(S + 1, dtype=torch.int64, device=ids_r.device)
+                off[1:] = torch.cumsum(C.sum(0), 0)
+                if n:
+                    dst = place_presharded(C, off, n) if self.presharded else \
+                        place_by_row(got[2], n_rows)
+                    out_ids = torch.empty_like(ids_r)
+                    out_ang = torch.empty_like(ang_r)
+                    out_ids[dst] = ids_r
+                    out_ang[dst] = ang_r
+                else:
+                    out_ids, out_ang = ids_r, ang_r
+                t1 = _sync_time(prof)
+                pin = out_ids.device.type == 'cuda'
+                h_off = torch.empty(S + 1, dtype=torch.int64, pin_memory=pin)
+                h_ids = torch.empty(n, dtype=out_ids.dtype, pin_memory=pin)
+                h_ang = torch.empty(n, dtype=torch.int16, pin_memory=pin)
+                h_off.copy_(off, non_blocking=pin)
+                h_ids.copy_(out_ids, non_blocking=pin)
+                h_ang.copy_(out_ang, non_blocking=pin)
+                if prof:
+                    self.fetch_stats = dict(
+                        records=n, merge_ms=(t1 - t0) * 1e3,
+                        bytes_per_record=sum(t.element_size() for t in send),
+                        layout='presharded' if self.presharded else 'stripes')
             if side is not None:
                 ev = torch.cuda.Event()
                 ev.record(side)
                 if hasattr(self.local, 'records_consumed'):
                     self.local.records_consumed(lp, ev)
-        return ShardedFetch(ev, res.n_slots, h_cnt, h_ids, h_ang, ids_dtype,
-                            self.rank == self.ROOT)
+        return ShardedFetch(ev, S, h_off, h_ids, h_ang, ids_dtype, root)
 
     def fetch(self, res, ids_dtype):
         """``fetch_async(...).wait()``: the records in the reference's order on rank 0."""
@@ -854,34 +911,21 @@ class EngineLocal:
         layout = None
         if compare and prev_lp is not None:
             layout = (prev_lp.starts, prev_lp.counts, prev_lp.exists, prev_lp.plan, prev_lp.n,
-                      prev_lp.buckets, prev_lp.centres)
+                      prev_lp.buckets)
         lp = eng.prepare(shard, centres, bulk, H, z, exists, compare, angles_in=angles_in,
                          plan_src=shard, prev_layout=layout)
         lp.exists = np.asarray(exists)
         lp.src = (shard, centres, bulk, H, z, exists, compare, angles_in, layout)
-        # halos with a progenitor and its row in the previous step's table (set_catalogue)
-        pidx = eng.last_prev_idx
-        hp = np.flatnonzero(pidx >= 0)
-        from .engine import _up
-        lp.prev_sel = (_up(hp.astype(np.int64), eng.device),
-                       _up(pidx[hp].astype(np.int64), eng.device)) if compare else None
         lp.share_bulk = bool(share)
         return lp
 
-    def set_catalogue(self, lp, rows, prev_lp=None):
+    def set_catalogue(self, lp, rows):
         """The exchanged catalogue rows into the device halo table (centre, and the
-        bulk velocity when it comes from the catalogue); a compare step's halos also get
-        their progenitors' previous centres from the previous step's device table (the
-        centres that step's frame used: the recomputed previous r̂ needs exactly those)."""
+        bulk velocity when it comes from the catalogue)."""
         from . import _native as N
-        w = N.HALO_DTYPE.itemsize // 8
-        hv = lp.halos.view(torch.float64).view(-1, w)
+        hv = lp.halos.view(torch.float64).view(-1, N.HALO_DTYPE.itemsize // 8)
         hi = 10 if lp.share_bulk else 7
         hv[:, 4:hi] = rows[:, :hi - 4].to(hv.device, non_blocking=True)
-        sel = getattr(lp, 'prev_sel', None)
-        if lp.compare and prev_lp is not None and sel is not None and len(sel[0]):
-            pv = prev_lp.halos.view(torch.float64).view(-1, w)
-            hv[sel[0], 12:15] = pv[sel[1], 4:7]
 
     deferrable = True                  # launch(defer=True) + settle (ShardedEngine.step)
 
@@ -905,12 +949,10 @@ class EngineLocal:
         shard, centres, bulk, H, z, exists, compare, angles_in, layout = lp.src
         from . import _native as N
         w = N.HALO_DTYPE.itemsize // 8
-        hv = lp.halos.view(torch.float64).view(-1, w)
-        cat, pc = hv[:, 4:10].clone(), hv[:, 12:15].clone()     # centre + bulk, prev centre
+        cat = lp.halos.view(torch.float64).view(-1, w)[:, 4:10].clone()    # centre + bulk
         lp2 = eng.prepare(shard, centres, bulk, H, z, exists, compare, angles_in=angles_in,
                           plan_src=shard, prev_layout=layout, entries=entries, part=part)
-        hv2 = lp2.halos.view(torch.float64).view(-1, w)
-        hv2[:, 4:10], hv2[:, 12:15] = cat, pc
+        lp2.halos.view(torch.float64).view(-1, w)[:, 4:10] = cat
         lp2.exists, lp2.src, lp2.share_bulk = lp.exists, lp.src, lp.share_bulk
         lp2.ws_idx = getattr(lp, 'ws_idx', eng._wsi)
         lp.__dict__.update(lp2.__dict__)

@@ -70,7 +70,7 @@ class OracleLocal:
         return {'args': [shard, np.asarray(centres), bulk, H, z, exists, compare, angles_in],
                 'share': share}
 
-    def set_catalogue(self, lp, rows, prev_lp=None):
+    def set_catalogue(self, lp, rows):
         r = rows.cpu().numpy()
         c = lp['args'][1]
         lp['args'][1] = r[:, :3].astype(c.dtype).reshape(c.shape)

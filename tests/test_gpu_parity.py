@@ -393,8 +393,7 @@ def test_frame_state_bits_match_oracle(dtype, centre_dtype):
     H = np.float64(0.07)                   # hubble_parameter returns np.float64
     eng = OrbitEngine(mode='pericentric')
     eng.step(snap, centres, bulk, H, snap['redshift'], np.arange(nh), False)
-    # a step of packed items stores no r̂ (engine.RC): materialised from the snapshot
-    rh = eng.rhat_of(eng.prev).cpu().numpy().reshape(-1, 3)
+    rh = eng.prev.rhat.cpu().numpy().reshape(-1, 3)
     meta = eng.prev.meta.cpu().numpy().view(np.uint32)
     sgn = (meta >> 16) & 3
     for j in range(nh):
@@ -658,130 +657,6 @@ def test_dtype_widened_between_snapshots(what):
     got = run_driver(u, dict(mode='pericentric', checkpoint=True))
     compare_groups(got.groups, _oracle_run(u, 'pericentric'), rep)
     assert rep['angles'] > 0
-
-
-RC_STEPS = []          # recomputing compare steps per case (test_recomputed_... below)
-
-
-def _rc_spy(eng):
-    """Record, per compare launch, whether the previous r̂ was recomputed (coords_prev)
-    and whether the step wrote an r̂ state."""
-    seen = []
-    orig = eng.launch
-
-    def launch(pr, ws, *a, **k):
-        r = orig(pr, ws, *a, **k)
-        if pr.compare:
-            seen.append(dict(rc=bool(pr.args.coords_prev), wrote=pr.rhat is not None,
-                             glob=pr.n_global))
-        return r
-    eng.launch = launch
-    return seen
-
-
-@pytest.mark.parametrize('name', ['g1_config1', 'g2_overlap_birth_massarray', 'g3_apo_periodic',
-                                  'g4_hubble_catalogue', 'g5_fp32_centre32', 'g5_fp32_centre64',
-                                  'g8_many_small_halos', 'g11_edges'])
-def test_recomputed_previous_rhat_matches_stored(name):
-    """Compare steps of packed items recompute the previous r̂ from the previous
-    snapshot's coordinates, centre and box (oa_step_args.coords_prev) and store none
-    (engine.RC): the savefile and checkpoint equal the stored-r̂ path's bit for bit
-    (ORBIT_RC=0, the round-4 dataflow), and the reference's."""
-    from orbitanalysis_amd.engine import OrbitEngine
-    fix = load(name)
-    u, meta = universe(fix)
-    outs, spies = [], []
-    for rc in (True, False):
-        eng = OrbitEngine(mode=meta['run']['mode'])
-        eng.rc = rc
-        spies.append(_rc_spy(eng))
-        outs.append(run_driver(u, dict(meta['run'], checkpoint=True), engine=eng))
-    # packed-only steps recompute and store nothing; steps with large halos keep r̂
-    assert spies[0] and all(s['rc'] == (s['glob'] == 0) and s['wrote'] == (s['glob'] > 0)
-                            for s in spies[0]), spies[0]
-    assert all(not s['rc'] and s['wrote'] for s in spies[1]), spies[1]
-    RC_STEPS.append(sum(s['rc'] for s in spies[0]))
-    r, s = outs
-    assert sorted(r.groups) == sorted(s.groups)
-    for g in s.groups:
-        for k, w in s.groups[g].items():
-            assert np.array_equal(np.asarray(r.groups[g][k]).view(np.uint8),
-                                  np.asarray(w).view(np.uint8)), (g, k)
-    assert np.array_equal(r.checkpoint.view(np.uint16), s.checkpoint.view(np.uint16))
-    compare_groups(r.groups, groups(fix), {})
-
-
-def test_recomputed_previous_rhat_cases_ran():
-    """The cases above include recomputing steps (g1's single halo is a large one)."""
-    assert len(RC_STEPS) >= 8 and sum(RC_STEPS) >= 20, RC_STEPS
-
-
-@pytest.mark.parametrize('mode', ['pericentric', 'apocentric'])
-def test_lazy_rhat_materialised_for_large_halos(mode):
-    """A step of packed items leaves no r̂; when the next step turns a halo large (the
-    partitioned path scatters its progenitor block from position-order state, or the
-    global tables read it), the previous r̂ is materialised first (OrbitEngine.rhat_of:
-    a frame-only launch writing r̂ alone).  Steps alternate packed-only / mixed; output
-    and checkpoint against the oracle."""
-    from orbitanalysis_amd.engine import OrbitEngine
-    from orbitanalysis_amd.synthetic import PlummerSnapshots
-    from oracle import orbit_oracle as O
-    u = PlummerSnapshots(n_halos=4, n_per_halo=[9000, 5000, 7000, 3000], n_snapshots=8,
-                         seed=47, box_size=140.0, dtype=np.float32, centre_dtype=np.float32)
-    rec = O.MemoryRecord()
-    want = O.track_orbits(u.snapshot_numbers, u.main_branches(), u.regions, u.load_snapshot_data,
-                          rec, mode=mode, checkpoint=True)
-    for part in (True, False):
-        eng = OrbitEngine(mode=mode)
-        eng.part_large = part
-        plan = iter([None, None, 6000, None, 6000, 6000, None, None])
-        orig = eng.prepare
-
-        def prepare(*a, **k):
-            eng.entries_cfg = next(plan, None)
-            return orig(*a, **k)
-        eng.prepare = prepare
-        seen = _rc_spy(eng)
-        mats = []
-        orig_rhat = eng.rhat_of
-
-        def rhat_of(p, *a, **k):
-            mats.append(p.rhat is None)
-            return orig_rhat(p, *a, **k)
-        eng.rhat_of = rhat_of
-        rep = {}
-        out = run_driver(u, dict(mode=mode, checkpoint=True), engine=eng)
-        compare_groups(out.groups, want.groups, rep)
-        c, w = out.checkpoint, np.asarray(rec.checkpoint)
-        bad = int(np.sum((c != w) & ~(np.isnan(c) & np.isnan(w))))
-        assert c.shape == w.shape and mismatch_ok(bad, c.size), (bad, c.size)
-        assert any(s['rc'] for s in seen) and any(s['glob'] for s in seen), seen
-        assert any(mats), (part, mats, seen)                # packed-only -> mixed
-
-
-def test_modified_previous_coordinates_raise():
-    """The previous snapshot's coordinates are read again by the next step (as the
-    reference reads ids_prev, track_orbits.py:237): a device loader that overwrites the
-    tensor it handed over is caught instead of silently changing the angles."""
-    import torch
-    from orbitanalysis_amd.engine import OrbitEngine
-    from orbitanalysis_amd.synthetic import PlummerSnapshots
-    u = PlummerSnapshots(n_halos=2, n_per_halo=[2000, 1500], n_snapshots=3, seed=5)
-    held = {}
-
-    def load(s, pos, rad):
-        d = dict(u.load_snapshot_data(s, pos, rad))
-        x = torch.as_tensor(np.asarray(d['coordinates'])).cuda()
-        if 'x' in held:
-            held['x'].add_(1.0)                  # the previous snapshot's tensor, in place
-        held['x'] = x
-        d['coordinates'] = x
-        return d
-    from orbitanalysis_amd.track_orbits import track_orbits
-    from orbitanalysis_amd.savefile import MemorySavefile
-    with pytest.raises(RuntimeError, match='modified in place'):
-        track_orbits(u.snapshot_numbers, u.main_branches(), u.regions, load, MemorySavefile(),
-                     verbose=False, engine=OrbitEngine())
 
 
 @pytest.mark.parametrize('mode', ['pericentric', 'apocentric'])

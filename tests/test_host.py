@@ -23,7 +23,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(raw, name), name
     assert declared == set(N.SYMBOLS), declared ^ set(N.SYMBOLS)
     assert lib.oa_abi_version() == N.ABI_VERSION
-    assert lib.oa_struct_size(0) == 128 and lib.oa_struct_size(1) == 48
+    assert lib.oa_struct_size(0) == 96 and lib.oa_struct_size(1) == 48
     from orbitanalysis_amd import engine as E
     for f64 in (False, True):
         assert lib.oa_step_lds_bytes(E.DEFAULT_ENTRIES[f64], E.DEFAULT_SLOTS[f64], int(f64)) \
