@@ -220,10 +220,9 @@ def main():
         pr, s = chain[k + 1]
         prev_pr, ps = chain[k]
         if world > 1:
-            seng.launch(pr, prev=prev_pr, step_events=events, check=False)
-        else:
-            eng.launch(pr, ws, SnapshotState.of(prev_pr, exists, ids=snaps[ps]['ids']),
-                       step_events=events)
+            return seng.launch(pr, prev=prev_pr, step_events=events, check=False)
+        return eng.launch(pr, ws, SnapshotState.of(prev_pr, exists, ids=snaps[ps]['ids']),
+                          step_events=events)
 
     for k in range(args.warmup):
         run(k)
@@ -233,7 +232,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        run(args.warmup + i, evs[i])
+        last_res = run(args.warmup + i, evs[i])
     torch.cuda.synchronize()
     if dist:
         barrier()
@@ -253,8 +252,38 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     last = preps[-1]
     n_apsis = int(ws.total.item())
+
+    # the records' gather to rank 0 and D2H of the last timed step (outside the timed
+    # region, as the driver overlaps it with the next snapshot's step): ms per fetch,
+    # the max over ranks, over 3 repetitions
+    fetch = []
+    fdt = snaps[0]['ids'].cpu().numpy().dtype
+    for _ in range(3):
+        if dist:
+            barrier()
+        torch.cuda.synchronize()
+        tf = time.perf_counter()
+        (seng if world > 1 else eng).fetch_async(last_res, fdt).wait()
+        if dist:
+            barrier()
+        fetch.append(time.perf_counter() - tf)
+    fetch_ms = float(np.median(fetch)) * 1e3
+    if dist:
+        t = torch.tensor([fetch_ms], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        fetch_ms = float(t.item())
+
+    # each timed step's own apsis count (its records' bytes): the steps are re-run
+    # once, untimed, in order (each reads the state its predecessor wrote)
+    n_aps = []
+    if world == 1:
+        for i in range(args.steps):
+            run(args.warmup + i)
+            n_aps.append(int(ws.total.item()))
+    else:
+        n_aps = [n_apsis] * args.steps
     bytes_launch = float(np.mean([step_bytes(preps[args.warmup + i], preps[args.warmup + i].n_prev,
-                                             n_apsis) for i in range(args.steps)]))
+                                             n_aps[i]) for i in range(args.steps)]))
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     log('elapsed %.4f s for %d steps; k_step %.3f ms; %.1f GB/s; apsis %d'
         % (elapsed, args.steps, kern_ms, achieved, n_apsis))
@@ -333,7 +362,12 @@ def main():
                                        'HBM; the host planning of each step (prepare: halo '
                                        'table, item plan, partition plan) runs before the '
                                        'timed region and is excluded, see host_prepare_ms',
-                       'host_prepare_ms': float(np.median(prep_s)) * 1e3},
+                       'host_prepare_ms': float(np.median(prep_s)) * 1e3,
+                       'fetch_ms': fetch_ms,
+                       'fetch_note': 'records of one step gathered to rank 0 (ShardedEngine: '
+                                     '10-B records, count-scan placement) and copied to '
+                                     'host, outside the timed region (the driver overlaps '
+                                     'it with the next step); max over ranks'},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
                          'traffic': traffic, 'kernel': kernel_label(last), 'kernel_ms': kern_ms,

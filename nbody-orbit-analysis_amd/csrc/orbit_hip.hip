@@ -1702,10 +1702,15 @@ template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF
 int launch_big(const oa_step_args &a, hipStream_t st);
 
 int cu_count() {
+    // cached per device (the attribute query is per launch otherwise)
+    static int cache[64] = {0};
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 1;
+    if (dev >= 0 && dev < 64 && cache[dev] > 0) return cache[dev];
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1;
-    return n > 0 ? n : 1;
+    if (n <= 0) n = 1;
+    if (dev >= 0 && dev < 64) cache[dev] = n;
+    return n;
 }
 
 template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF>

@@ -23,7 +23,16 @@ def pytest_terminal_summary(terminalreporter):
         n = sum(ch.values())
         terminalreporter.write_line('angle changes vs reference: %d compared, ulp distance histogram %s'
                                     % (n, dict(sorted(ch.items()))))
-        _dump('angle_change_ulps.json', {str(k): v for k, v in sorted(ch.items())})
+        per = getattr(gu, 'CHANGE_TALLY_DT', {})
+        rel = getattr(gu, 'CHANGE_REL_MAX', {})
+        for dt, h in sorted(per.items()):
+            terminalreporter.write_line('  %s: %d compared, ulp histogram %s, max relative error %.3g'
+                                        % (dt, sum(h.values()), dict(sorted(h.items())),
+                                           rel.get(dt, 0.0)))
+        _dump('angle_change_ulps.json', dict(
+            {str(k): v for k, v in sorted(ch.items())},
+            by_dtype={dt: {str(k): v for k, v in sorted(h.items())} for dt, h in per.items()},
+            max_rel_error=rel))
     t = getattr(gu, 'ANGLE_TALLY', None)
     if not t or not t['angles']:
         return

@@ -64,6 +64,10 @@ ANGLE_TALLY = {'angles': 0, 'mismatch': 0}
 # writes gpurun_out/angle_change_ulps.json.  The bound is the observed maximum.
 CHANGE_TALLY = {}
 CHANGE_ULP_MAX = 2
+# the same split by the dtype arccos ran in ({'float32': {ulps: count}, ...}), and per
+# dtype the largest relative error |v - w| / |w| (north_star: 1e-10 for float64)
+CHANGE_TALLY_DT = {}
+CHANGE_REL_MAX = {}
 
 
 def check_changes(v, w, dtype, where):
@@ -77,7 +81,17 @@ def check_changes(v, w, dtype, where):
     assert np.all(b >= 0) and np.all(a >= 0), where          # arccos range: bits are monotone
     it = np.int32 if dt.itemsize == 4 else np.int64
     d = np.abs(a.view(it).astype(np.int64) - b.view(it).astype(np.int64))
+    per = CHANGE_TALLY_DT.setdefault(dt.name, {})
     for k, c in zip(*np.unique(d, return_counts=True)):
         CHANGE_TALLY[int(k)] = CHANGE_TALLY.get(int(k), 0) + int(c)
+        per[int(k)] = per.get(int(k), 0) + int(c)
+    nz = b != 0
+    if nz.any():
+        rel = float(np.max(np.abs(a[nz].astype(np.float64) - b[nz].astype(np.float64)) /
+                           np.abs(b[nz].astype(np.float64))))
+        CHANGE_REL_MAX[dt.name] = max(CHANGE_REL_MAX.get(dt.name, 0.0), rel)
     assert d.max(initial=0) <= CHANGE_ULP_MAX, (where, int(d.max(initial=0)))
+    if dt == np.float64:
+        # north_star: float64 values within 1e-10 relative of the reference's
+        assert not nz.any() or CHANGE_REL_MAX[dt.name] <= 1e-10, (where, CHANGE_REL_MAX)
 
