@@ -697,6 +697,9 @@ class OrbitEngine:
         # direct records' look-back poll bound (0: the library default); tests set 1 to
         # force OA_STATUS_LOOKBACK and the re-run through oa_compact
         self.lb_spin_max = 0
+        # diagnostics (tools/bench_e2e.py --timeline): a list collecting (start, end) timing
+        # events of each fetch_async's copies on the copy stream; None: off
+        self.copy_events = None
 
     def note_status(self, st):
         """Run-wide switches a step's status word turns off before its re-run."""
@@ -1185,6 +1188,10 @@ class OrbitEngine:
             total = int(res.ws.h_total[0]) if res.n_slots else 0
         with torch.cuda.stream(cs):
             cs.wait_event(res.done)
+            tev = None
+            if self.copy_events is not None:
+                tev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                tev[0].record(cs)
             h_off = _pinned(n, torch.int64)
             h_off.copy_(res.offsets[:n], non_blocking=True)
             h_ids = h_ang = None
@@ -1193,6 +1200,9 @@ class OrbitEngine:
                 h_ang = _pinned(total, torch.int16)
                 h_ids.copy_(res.apsis_ids[:total], non_blocking=True)
                 h_ang.copy_(res.apsis_ang[:total], non_blocking=True)
+            if tev is not None:
+                tev[1].record(cs)
+                self.copy_events.append(tev + (total,))
             done = torch.cuda.Event()
             done.record(cs)
         res.ws.copy_done = done             # the workspace's next launch waits for it

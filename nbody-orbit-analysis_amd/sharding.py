@@ -360,7 +360,7 @@ class Shard:
     """This rank's rows of one snapshot (device tensors in block order)."""
     snap: dict                         # ids / coordinates / velocities (/ masses) + region_offsets
     sel: torch.Tensor                  # global snapshot row of every shard row (int64)
-    gpos: torch.Tensor                 # position of every shard row in its global block
+    gpos: Optional[torch.Tensor]       # position in its global block (presharded only)
     counts: np.ndarray                 # shard rows per halo
     bulk: Optional[np.ndarray] = None  # (nh, 3) bulk velocities of the whole blocks
     h2d_bytes: int = 0                 # loader bytes this rank moved to its device
@@ -423,15 +423,14 @@ def stripe_shard(snapshot, starts, owner, group, device, bulk_fn=None, n=None):
         bulk = gather_bulk(rows, h0, nh, group) if world > 1 else \
             (np.asarray(rows) if rows is not None else np.zeros((0, 3)))
     owner.fit_group(st['ids'], group)
-    st_t = _h2d(starts, device)
     nst = int(st['ids'].shape[0])
-    # every stripe row's block: the stripe holds blocks [h0, h1) (host layout)
     sc = (np.append(starts[h0 + 1:h1], hi) - starts[h0:h1]) if h1 > h0 else np.zeros(0, np.int64)
-    sblock = torch.repeat_interleave(torch.arange(h0, h1, device=device),
-                                     _h2d(sc.astype(np.int64), device),
-                                     output_size=nst) if nst else \
-        torch.zeros(0, dtype=torch.int64, device=device)
     if world > 1:
+        # every stripe row's block: the stripe holds blocks [h0, h1) (host layout)
+        sblock = torch.repeat_interleave(torch.arange(h0, h1, device=device),
+                                         _h2d(sc.astype(np.int64), device),
+                                         output_size=nst) if nst else \
+            torch.zeros(0, dtype=torch.int64, device=device)
         dest = owner.ranks(st['ids'], world)
         dest, perm = torch.sort(dest, stable=True)
         # rows per (destination, block): one D2H; the row counts of the exchange and,
@@ -443,21 +442,19 @@ def stripe_shard(snapshot, starts, owner, group, device, bulk_fn=None, n=None):
         sh = {k: rx.move(v[perm]) for k, v in st.items()}
         got = _exchange_rows(hist, group)       # row d of every sender: (world, nh)
         counts = got.sum(0).cpu().numpy().astype(np.int64)[:nh] if nh else np.zeros(0, np.int64)
-        block = torch.repeat_interleave(torch.arange(nh, device=device),
-                                        _h2d(counts, device),
-                                        output_size=int(counts.sum())) if nh else sel
     else:
+        # one rank: the stripe is the snapshot, in its own row order
         sel = torch.arange(lo, hi, dtype=torch.int64, device=device)
         sh = st
         counts = np.zeros(nh, np.int64)
         counts[h0:h1] = sc
-        block = sblock
-    gpos = sel - st_t[block] if nh else sel
     shard = dict(snapshot)
     shard.update(sh)
     shard['region_offsets'] = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64) \
         if nh else counts
-    return Shard(snap=shard, sel=sel, gpos=gpos, counts=counts, bulk=bulk, h2d_bytes=h2d)
+    # (a row's block position is its global row minus its block's start: the record
+    # merges key on the global row itself, so it is not materialised)
+    return Shard(snap=shard, sel=sel, gpos=None, counts=counts, bulk=bulk, h2d_bytes=h2d)
 
 
 # ------------------------------------------------------------------ engine facade

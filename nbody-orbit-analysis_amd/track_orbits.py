@@ -170,7 +170,13 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
                 if region_bulk_vels is None:
                     bulk = eng.bulk_velocities(res, eng.prev.plan)
                 else:
-                    bulk = np.array([region_bulk_vels[j] for j in range(len(halo_exists))])
+                    # the reference's per-halo bulk_vels rows stacked (track_orbits.py:155,
+                    # :199-203): one slice copy for an array (7 ms of Python per 1e4
+                    # halos as a loop), the loop for any other sequence
+                    nb = len(halo_exists)
+                    bulk = np.array(region_bulk_vels[:nb]) if isinstance(
+                        region_bulk_vels, np.ndarray) else \
+                        np.array([region_bulk_vels[j] for j in range(nb)])
                 halo_ids_final = main_branches[-1][progen_exists] if \
                     snapshot_number != snapshot_numbers[-1] else None
                 # checkpoint angles now: the next step replaces the engine's state

@@ -536,8 +536,11 @@ class ShardedOnTheFly:
         n = int(snap['n_rows']) if STRIPE in snap else \
             (int(ids.numel()) if isinstance(ids, torch.Tensor) else len(ids))
         eng = self.eng
+        # bulk velocities: of the stripe's whole blocks before the exchange splits them,
+        # all-gathered (world > 1); at world 1 the shard is the snapshot and the step
+        # computes them itself, as OnTheFly does (no host round trip)
         sh = stripe_shard(snap, _block_starts(sl, n), self.owner, self.group, eng.device,
-                          bulk_fn=eng.block_bulk, n=n)
+                          bulk_fn=eng.block_bulk if self.world > 1 else None, n=n)
         st = np.concatenate([[0], np.cumsum(sh.counts)[:-1]]).astype(np.int64)
         lsl = np.where(sl[:, :1] >= 0, np.stack([st, st + sh.counts], axis=1), -1)
         self.h2d_bytes += sh.h2d_bytes

@@ -145,6 +145,63 @@ def test_configs4_onthefly_rank_share_world1():
         dist.destroy_process_group()
 
 
+def test_configs4_pinned_ring_stream_world1():
+    """configs[4]'s double-buffered H2D under test: one GPU's share
+    (1.25e8 f32 particles, 12,500 halos) streamed from page-locked host memory by
+    ``streaming.PinnedRing`` -- the copy of snapshot s + 1 runs on a high-priority copy
+    stream into one of three device slots while s is compared -- through
+    ``ShardedOnTheFly`` at world 1 (RCCL is not needed at world 1: gloo), three chained
+    calls with the carry on.  Every file equals the device-tensor loader's bit for bit,
+    and the oracle's on 40 halos of the last pair."""
+    import torch
+    import torch.distributed as dist
+    from oracle import orbit_oracle as O
+    from orbitanalysis_amd import track_orbits_onthefly as T
+    from orbitanalysis_amd.engine import OrbitEngine
+    from orbitanalysis_amd.savefile import MemorySavefile
+    from orbitanalysis_amd.streaming import PinnedRing, pin_snapshot
+    dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d' % _free_port(),
+                            rank=0, world_size=1)
+    try:
+        nh = 12500
+        u = DeviceUniverse(4, n_halos=nh, n_particles=125_000_000, seed=29, dtype='float32')
+        links = np.tile(np.arange(nh), (2, 1))
+        ring = PinnedRing({s: pin_snapshot(u.snaps[s]) for s in range(4)})
+        outs = []
+        for loader in (ring.loader, u.load_snapshot_data):
+            T.clear_carry()
+            eng = T.ShardedOnTheFly(OrbitEngine(mode='pericentric'))
+            out = MemorySavefile()
+            for s in (1, 2, 3):
+                T.track_orbits(s, links, u.regions_otf, loader, out, verbose=False, engine=eng)
+            outs.append(out)
+        # every snapshot crossed PCIe once (32 B per particle), s - 1 carried, not reloaded
+        assert ring.h2d_bytes == 32 * sum(int(u.snaps[s]['ids'].numel()) for s in range(4))
+        for s in (1, 2, 3):
+            a, b = outs[0].files[s][0], outs[1].files[s][0]
+            assert sorted(a) == sorted(b)
+            for key in a:
+                x, y = np.asarray(a[key]), np.asarray(b[key])
+                assert x.dtype == y.dtype and x.shape == y.shape, (s, key)
+                assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), (s, key)
+        check_onthefly_properties(u.snaps[2], u.snaps[3], nh, outs[0].files[3][0])
+        got = outs[0].files[3][0]
+        k = 40
+        hs = {s: u.host_blocks(s, k) for s in (2, 3)}
+        want = O.onthefly_track_orbits(3, np.tile(np.arange(k), (2, 1)),
+                                       lambda s, ids: (u.cats[s][0][ids], u.cats[s][1][ids]),
+                                       lambda s, p, r: hs[s], mode='pericentric')
+        for name in ('pericenter', 'entered', 'departed'):
+            o = want[name + '_offsets']
+            assert np.array_equal(got[name + '_offsets'][:k + 1], o), name
+            assert np.array_equal(got[name + '_IDs'][:o[-1]], want[name + '_IDs']), name
+        check_changes(got['angles'][:len(want['angles'])], want['angles'], np.float32,
+                      'configs[4] pinned ring')
+    finally:
+        T.clear_carry()
+        dist.destroy_process_group()
+
+
 def _otf_digests(out, calls):
     return {'%d/%s' % (s, k): v for s in calls
             for k, v in digest({'f': out.files[s][0]}).items()}

@@ -62,6 +62,9 @@ def main():
     ap.add_argument('--contract', default='presharded', choices=['presharded', 'whole'])
     ap.add_argument('--scaling', default='weak', choices=['weak', 'strong'])
     ap.add_argument('--backend', default='nccl')
+    ap.add_argument('--timeline', action='store_true',
+                    help='GPU timeline per snapshot: k_step start/end and the records\' D2H '
+                         '(timing events; the events themselves cost a few us)')
     args = ap.parse_args()
     import torch
     import orbitanalysis_amd  # noqa: F401
@@ -117,6 +120,20 @@ def main():
             return r
         return w
     OrbitEngine.prepare = timed('prepare', OrbitEngine.prepare)
+    kern_ev, host_launch = [], []
+    if args.timeline:
+        _launch = OrbitEngine.launch
+
+        def launch_tl(self, pr, ws, prev=None, stream=None, step_events=None):
+            if self.copy_events is None:
+                self.copy_events = []
+            if pr.compare and step_events is None:
+                step_events = (torch.cuda.Event(enable_timing=True),
+                               torch.cuda.Event(enable_timing=True))
+                kern_ev.append(step_events)
+                host_launch.append(time.perf_counter())
+            return _launch(self, pr, ws, prev, stream, step_events)
+        OrbitEngine.launch = launch_tl
     OrbitEngine.launch = timed('launch', OrbitEngine.launch)
     OrbitEngine.fetch = timed('fetch', OrbitEngine.fetch)
     OrbitEngine.fetch_async = timed('fetch_async', OrbitEngine.fetch_async)
@@ -151,6 +168,8 @@ def main():
         SH.EngineLocal.settle = ssettle
         engine = SH.ShardedEngine(SH.EngineLocal(OrbitEngine(mode=args.mode, device=dev)),
                                   presharded=args.contract == 'presharded')
+    if engine is None:
+        engine = OrbitEngine(mode=args.mode, device=dev)
     log('setup %.1f s: %d host snapshots of %s particles' % (
         time.perf_counter() - t0, S, [len(h['ids']) for h in host]))
 
@@ -223,6 +242,23 @@ def main():
         'apsis_records': n_apsis,
         'total_wall_s': t_end - t_start,
     }
+    if args.timeline and kern_ev:
+        # GPU timeline relative to the first timed compare step's start: each step's
+        # kernel window, the gap before it, and each records D2H window and its rate
+        eng_obj = engine.local.engine if args.sharded else engine
+        cev = eng_obj.copy_events or []
+        t0e = kern_ev[0][0]
+        ks = [(t0e.elapsed_time(a), t0e.elapsed_time(b)) for a, b in kern_ev]
+        cs = [(t0e.elapsed_time(a), t0e.elapsed_time(b), n) for a, b, n in cev]
+        res['timeline'] = {
+            'kernel_ms': [round(b - a, 3) for a, b in ks],
+            'gap_before_kernel_ms': [None] + [round(ks[i][0] - ks[i - 1][1], 3)
+                                             for i in range(1, len(ks))],
+            'd2h_ms': [round(b - a, 3) for a, b, _ in cs],
+            'd2h_gbs': [round(n * 10 / max(b - a, 1e-6) / 1e6, 1) for a, b, n in cs],
+            'd2h_start_after_kernel_end_ms': [round(cs[i][0] - ks[i][1], 3)
+                                             for i in range(min(len(cs), len(ks)))],
+        }
     print(json.dumps(res), flush=True)
     if args.sharded:
         dist.destroy_process_group()
