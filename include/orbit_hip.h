@@ -380,6 +380,16 @@ int64_t oa_plan_items(const int64_t *cur_off, const int64_t *cur_cnt, const int6
                       int64_t hmax, int64_t max_pv, oa_item *items, int64_t cap,
                       int64_t *n_small, int64_t *scratch);
 
+/* HOST function (no device needed): the halo table of one snapshot (oa_halo rows) from
+ * its columns -- block starts and sizes (region_offsets, track_orbits.py:129-132), the
+ * progenitor blocks (prev_off / prev_cnt, -1: none, :162-165), output slots, centres
+ * (region_positions) and catalogue bulk velocities (NULL: zero, computed later by
+ * oa_bulk_velocity).  All arrays are host arrays of n rows; centre / bulk are (n, 3)
+ * float64.  Returns 0 or OA_E_ARG. */
+int oa_build_halos(const int64_t *cur_off, const int64_t *cur_cnt, const int64_t *prev_off,
+                   const int64_t *prev_cnt, const int64_t *out_slot, const double *centre,
+                   const double *bulk, int64_t n, oa_halo *halos);
+
 /* Diagnostic builds only (-DOA_STAMPS=1): copy the per-work-group phase timestamps
  * (s_memrealtime, 100 MHz; 6 per work-group) of the last oa_step to host memory.
  * Returns the number of values copied, -1 in normal builds. */

@@ -125,6 +125,7 @@ SYMBOLS = {
     'oa_plan_items': (c_i64, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp,
                               c_i64, c_vp, c_vp]),
     'oa_max_lds_bytes': (c_i64, []),
+    'oa_build_halos': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     'oa_debug_stamps': (c_i64, [c_vp, c_i64]),
     'oa_debug_part_stamps': (c_i64, [c_i32, c_vp, c_i64]),
     'oa_debug_central_stamps': (c_i64, [c_vp, c_i64]),

@@ -2758,6 +2758,29 @@ int64_t oa_plan_items(const int64_t *cur_off, const int64_t *cur_cnt, const int6
     return n;
 }
 
+int oa_build_halos(const int64_t *cur_off, const int64_t *cur_cnt, const int64_t *prev_off,
+                   const int64_t *prev_cnt, const int64_t *out_slot, const double *centre,
+                   const double *bulk, int64_t n, oa_halo *halos) {
+    g_err[0] = 0;
+    if (n < 0 || (n > 0 && (!cur_off || !cur_cnt || !prev_off || !prev_cnt || !out_slot ||
+                            !centre || !halos)))
+        return fail(OA_E_ARG, "oa_build_halos: bad arguments");
+    for (int64_t j = 0; j < n; ++j) {
+        oa_halo &h = halos[j];
+        h.cur_off = cur_off[j];
+        h.cur_cnt = cur_cnt[j];
+        h.prev_off = prev_off[j];
+        h.prev_cnt = prev_cnt[j];
+        for (int d = 0; d < 3; ++d) {
+            h.centre[d] = centre[3 * j + d];
+            h.bulk[d] = bulk ? bulk[3 * j + d] : 0.0;
+        }
+        h.out_slot = out_slot[j];
+        h.reserved = 0;
+    }
+    return OA_OK;
+}
+
 // Diagnostic builds (-DOA_STAMPS=1): copy the per-work-group phase stamps of the last
 // oa_step launch (s_memrealtime, 100 MHz) to host memory; returns count or -1.
 int64_t oa_debug_stamps(uint64_t *host, int64_t n) {

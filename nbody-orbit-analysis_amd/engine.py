@@ -753,7 +753,7 @@ class OrbitEngine:
                      entries=None, slots=None):
         n = int(snapshot['ids'].numel()) if isinstance(snapshot['ids'], torch.Tensor) \
             else len(snapshot['ids'])
-        starts = np.asarray(snapshot['region_offsets'], dtype=np.int64).reshape(-1)
+        starts = np.ascontiguousarray(np.asarray(snapshot["region_offsets"], dtype=np.int64).reshape(-1))
         ends = np.append(starts[1:], n)
         counts = ends - starts
         nh = len(starts)
@@ -761,26 +761,40 @@ class OrbitEngine:
             raise ValueError('region_offsets has %d blocks for %d halos' % (nh, len(exists)))
         if nh and (np.any(counts < 0) or starts[0] < 0 or ends[-1] > n):
             raise ValueError('region_offsets must be non-decreasing block starts within [0, N]')
-        halos = np.zeros(nh, dtype=N.HALO_DTYPE)
-        halos['cur_off'], halos['cur_cnt'] = starts, counts
-        halos['centre'] = np.asarray(centres, dtype=np.float64).reshape(nh, 3)
-        if bulk_cat is not None:
-            halos['bulk'] = np.asarray(bulk_cat, dtype=np.float64).reshape(nh, 3)
-        halos['prev_cnt'] = -1
-        halos['out_slot'] = -1
+        # columns first (contiguous), then the 96-byte rows in one host pass (C++)
+        prev_off = np.zeros(nh, dtype=np.int64)
+        prev_cnt = np.full(nh, -1, dtype=np.int64)
+        out_slot = np.full(nh, -1, dtype=np.int64)
         has_prog = np.zeros(nh, dtype=bool)
         prev_idx = np.full(nh, -1, dtype=np.int64)     # the progenitor's previous halo number
         if compare:
             p_starts, p_counts, pe = prev_layout[0], prev_layout[1], np.asarray(prev_layout[2])
-            p = np.searchsorted(pe, exists)
-            pc = np.minimum(p, max(len(pe) - 1, 0))
-            has_prog = (p < len(pe)) & (pe[pc] == exists) if len(pe) else has_prog
-            halos['prev_off'][has_prog] = p_starts[p[has_prog]]
-            halos['prev_cnt'][has_prog] = p_counts[p[has_prog]]
-            halos['out_slot'][has_prog] = np.arange(int(has_prog.sum()))
-            prev_idx[has_prog] = p[has_prog]
-        buf, k, n_it, scratch = _plan(counts, halos['prev_cnt'], entries, self.hmax,
-                                      halos['out_slot'], self.max_pv, slots, starts)
+            if len(pe) == nh and np.array_equal(pe, exists):
+                # the same halos as the previous snapshot (the usual case): no search
+                prev_off[:] = p_starts
+                prev_cnt[:] = p_counts
+                out_slot[:] = prev_idx[:] = np.arange(nh)
+                has_prog[:] = True
+            elif len(pe):
+                p = np.searchsorted(pe, exists)
+                pc = np.minimum(p, len(pe) - 1)
+                has_prog = (p < len(pe)) & (pe[pc] == exists)
+                prev_off[has_prog] = p_starts[p[has_prog]]
+                prev_cnt[has_prog] = p_counts[p[has_prog]]
+                out_slot[has_prog] = np.arange(int(has_prog.sum()))
+                prev_idx[has_prog] = p[has_prog]
+        cen = np.ascontiguousarray(centres, dtype=np.float64).reshape(nh, 3)
+        blk = None if bulk_cat is None else \
+            np.ascontiguousarray(bulk_cat, dtype=np.float64).reshape(nh, 3)
+        halos = np.empty(nh, dtype=N.HALO_DTYPE)
+        if nh:
+            N.check(self.lib.oa_build_halos(starts.ctypes.data, counts.ctypes.data,
+                                            prev_off.ctypes.data, prev_cnt.ctypes.data,
+                                            out_slot.ctypes.data, cen.ctypes.data,
+                                            None if blk is None else blk.ctypes.data, nh,
+                                            halos.ctypes.data), 'oa_build_halos')
+        buf, k, n_it, scratch = _plan(counts, prev_cnt, entries, self.hmax, out_slot,
+                                      self.max_pv, slots, starts)
         self._prev_idx = prev_idx
         return halos, buf[:n_it], k, scratch, starts, counts, has_prog
 

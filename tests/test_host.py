@@ -348,3 +348,31 @@ def test_plan_part_memory_scales_with_halo_size():
     assert retry_plan(pr, N.STATUS_LOOKBACK) == (6144, True)
     pr.entries = 256
     assert retry_plan(pr, N.STATUS_TABLE_OVERFLOW) == (0, False)
+
+
+def test_build_halos_matches_structured_fill():
+    """oa_build_halos (host C++) writes the same oa_halo rows as field-by-field NumPy
+    assignment into HALO_DTYPE (the table OrbitEngine.build_tables uploads)."""
+    import numpy as np
+    from orbitanalysis_amd import _native as N
+    lib = N.load()
+    rng = np.random.default_rng(4)
+    n = 257
+    cols = {k: rng.integers(-5, 1 << 40, n).astype(np.int64)
+            for k in ('cur_off', 'cur_cnt', 'prev_off', 'prev_cnt', 'out_slot')}
+    cen, blk = rng.normal(size=(n, 3)), rng.normal(size=(n, 3))
+    for bulk in (blk, None):
+        want = np.zeros(n, dtype=N.HALO_DTYPE)
+        for k, v in cols.items():
+            want[k] = v
+        want['centre'] = cen
+        if bulk is not None:
+            want['bulk'] = bulk
+        got = np.empty(n, dtype=N.HALO_DTYPE)
+        rc = lib.oa_build_halos(*(cols[k].ctypes.data for k in ('cur_off', 'cur_cnt', 'prev_off',
+                                                                 'prev_cnt', 'out_slot')),
+                                cen.ctypes.data, None if bulk is None else bulk.ctypes.data, n,
+                                got.ctypes.data)
+        assert rc == 0
+        assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+    assert lib.oa_build_halos(None, None, None, None, None, None, None, 3, None) < 0

@@ -168,6 +168,18 @@ def main():
         SH.EngineLocal.settle = ssettle
         engine = SH.ShardedEngine(SH.EngineLocal(OrbitEngine(mode=args.mode, device=dev)),
                                   presharded=args.contract == 'presharded')
+        # rank 0's record placement timed (synchronised) per fetch: bytes per record
+        # and merge ms in the output line
+        engine.profile_fetch = True
+        fstats = []
+        _fa = SH.ShardedEngine.fetch_async
+
+        def fa(self, res, ids_dtype):
+            f = _fa(self, res, ids_dtype)
+            if self.fetch_stats is not None:
+                fstats.append(dict(self.fetch_stats))
+            return f
+        SH.ShardedEngine.fetch_async = fa
     if engine is None:
         engine = OrbitEngine(mode=args.mode, device=dev)
     log('setup %.1f s: %d host snapshots of %s particles' % (
@@ -242,6 +254,17 @@ def main():
         'apsis_records': n_apsis,
         'total_wall_s': t_end - t_start,
     }
+    if args.sharded and fstats:
+        res['records_gather'] = {
+            'layout': fstats[-1]['layout'],
+            'bytes_per_record': fstats[-1]['bytes_per_record'],
+            'records_per_snapshot_median': float(np.median([f['records'] for f in fstats[W:]]
+                                                           or [f['records'] for f in fstats])),
+            'root_merge_ms_median': float(np.median([f['merge_ms'] for f in fstats[W:]]
+                                                    or [f['merge_ms'] for f in fstats])),
+            'note': 'rank 0 places the gathered records by a per-(rank, slot) count scan '
+                    '(presharded) or a counting pass over previous rows (stripes); '
+                    'synchronised timing of the placement alone'}
     if args.timeline and kern_ev:
         # GPU timeline relative to the first timed compare step's start: each step's
         # kernel window, the gap before it, and each records D2H window and its rate
