@@ -62,6 +62,8 @@ def main():
     ap.add_argument('--contract', default='presharded', choices=['presharded', 'whole'])
     ap.add_argument('--scaling', default='weak', choices=['weak', 'strong'])
     ap.add_argument('--backend', default='nccl')
+    ap.add_argument('--profile-host', action='store_true',
+                    help='cProfile of the driver (host functions by own time, to stderr)')
     ap.add_argument('--timeline', action='store_true',
                     help='GPU timeline per snapshot: k_step start/end and the records\' D2H '
                          '(timing events; the events themselves cost a few us)')
@@ -209,9 +211,21 @@ def main():
     t_start = time.perf_counter()
     if args.sharded:
         dist.barrier()
+    prof = None
+    if args.profile_host:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     track_orbits(np.arange(n), branches, regions, load_snapshot_data, sink, mode=args.mode,
                  verbose=False, engine=engine)
     torch.cuda.synchronize()
+    if prof is not None:
+        prof.disable()
+        import io
+        import pstats
+        buf = io.StringIO()
+        pstats.Stats(prof, stream=buf).sort_stats('tottime').print_stats(30)
+        log('host profile (whole run, %d snapshots):\n%s' % (n, buf.getvalue()))
     t_end = time.perf_counter()
     # timed: snapshots W .. n-1 (from the loader call of snapshot W to the end)
     W = args.warmup
