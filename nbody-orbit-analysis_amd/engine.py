@@ -414,15 +414,17 @@ def _up(a, device):
 
 
 _PIN_GRAIN = 1 << 22
+N_WS = 3                       # compare-step workspaces in rotation (OrbitEngine)
 
 
 def _pinned(n, dtype):
     """A page-locked host tensor of n elements from torch's caching host allocator, the
-    block rounded up to 4 MiB: snapshots' record counts differ a little, and a block
-    that fits the next request is reused instead of page-locking a new one (that, not
-    the DMA, is what held the D2H of the records to ~20 GB/s)."""
+    block rounded up to a power of two (>= 4 MiB): snapshots' record counts differ, and
+    a block that fits the next request is reused instead of page-locking a new one
+    (that, not the DMA, is what held the D2H of the records to ~20 GB/s; a 4-MiB grain
+    still page-locked a new block whenever the count crossed one, ~3-7 ms each)."""
     itemsize = torch.empty(0, dtype=dtype).element_size()
-    nb = max(-(-int(n) * itemsize // _PIN_GRAIN) * _PIN_GRAIN, _PIN_GRAIN)
+    nb = max(1 << max(int(n) * itemsize - 1, 1).bit_length(), _PIN_GRAIN)
     return torch.empty(nb // itemsize, dtype=dtype, pin_memory=True)[:n]
 
 
@@ -513,8 +515,8 @@ def layout_of(pr, exists):
 
 @dataclass
 class StepResult:
-    """A compare step's records.  They live in one of the engine's two workspaces and
-    are valid until the step after next reuses it: ``fetch`` / ``fetch_async`` of an
+    """A compare step's records.  They live in one of the engine's N_WS workspaces and
+    are valid until the step N_WS later reuses it: ``fetch`` / ``fetch_async`` of an
     older result raise instead of returning another snapshot's records."""
     n_slots: int
     has_prog: np.ndarray                       # bool per current halo
@@ -529,12 +531,12 @@ class StepResult:
     gen: int = 0                               # its launch count when they were written
     done: object = None                        # event after its kernels (compare steps)
     pending: object = None                     # (ctx, prep) until OrbitEngine.settle
-    ws_idx: int = 0                            # which of the engine's two workspaces
+    ws_idx: int = 0                            # which of the engine's workspaces
 
     def check_fresh(self):
         if self.ws is not None and self.ws.gen != self.gen:
             raise RuntimeError('StepResult is stale: its workspace was reused by a later '
-                               'step (fetch a result before the step after next)')
+                               'step (fetch a result before N_WS later steps ran)')
 
 
 @dataclass
@@ -670,10 +672,12 @@ class OrbitEngine:
         for f64 in (False, True):
             self.table_sizes(f64)                   # validates the LDS budget
         self.prev: Optional[SnapshotState] = None
-        # two compare-step workspaces, alternating between snapshots (step): a snapshot's
+        # N_WS compare-step workspaces, in rotation between snapshots (step): a snapshot's
         # records can still be on their way to the host (fetch_async) while the next
-        # snapshot's kernels write the other one
-        self._wss = [None, None]
+        # snapshots' kernels write the others; with three, the D2H of step s - 1 has two
+        # steps' time before step s + 2 reuses its workspace (a copy slower than one
+        # step no longer holds the next kernel back)
+        self._wss = [None] * N_WS
         self._wsi = 0
         self._pending = None                # a deferred step not yet settled (step)
         # apsis records also carry their previous-state row (ShardedEngine's merge)
@@ -700,6 +704,12 @@ class OrbitEngine:
         # diagnostics (tools/bench_e2e.py --timeline): a list collecting (start, end) timing
         # events of each fetch_async's copies on the copy stream; None: off
         self.copy_events = None
+
+    def _advance_ws(self):
+        """The current workspace index, then rotate to the next one."""
+        i = self._wsi
+        self._wsi = (self._wsi + 1) % len(self._wss)
+        return i
 
     def note_status(self, st):
         """Run-wide switches a step's status word turns off before its re-run."""
@@ -840,7 +850,7 @@ class OrbitEngine:
             res, prep = self._run_ctx(ctx, prep)
         self._set_prev(ctx, prep)
         if compare:
-            self._wsi ^= 1                  # the next snapshot writes the other workspace
+            self._advance_ws()              # the next snapshot writes the next workspace
         return res
 
     def _prepare_ctx(self, ctx, entries, part):
@@ -1180,7 +1190,7 @@ class OrbitEngine:
         """Start the D2H of a compare step's records on the engine's copy stream and
         return a ``PendingFetch`` whose ``wait()`` gives (offsets, ids, angles) as
         ``fetch`` does.  The copies overlap whatever the compute stream runs next (the
-        next snapshot's kernels write the other workspace), so the records' transfer is
+        next snapshots' kernels write the other workspaces), so the records' transfer is
         off the per-snapshot critical path.  The result's workspace must not be reused
         before ``wait()``: ``step`` alternates two."""
         self.settle(res)

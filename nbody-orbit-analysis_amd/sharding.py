@@ -955,15 +955,14 @@ class EngineLocal:
         lp.__dict__.update(lp2.__dict__)
 
     def launch(self, lp, prev_lp, step_events=None, check=True, defer=False):
-        """The local step.  A compare step writes one of the engine's two workspaces
+        """The local step.  A compare step writes one of the engine's workspaces
         (alternating, so the previous step's records can still be on their way to rank
         0); ``defer``: return without reading the status word -- it is copied to host
         memory behind an event and ``settle`` checks it (and re-runs) before the next
         launch.  Returns (offsets, IDs, f16 bits, previous-state rows) on the device."""
         eng = self.engine
         if lp.compare and not hasattr(lp, 'ws_idx'):
-            lp.ws_idx = eng._wsi
-            eng._wsi ^= 1
+            lp.ws_idx = eng._advance_ws()
         for _ in range(10):
             ws = eng.workspace(lp, lp.ws_idx) if lp.compare else None
             if ws is not None:

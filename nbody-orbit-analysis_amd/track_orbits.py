@@ -143,13 +143,14 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
             res = eng.step(snapshot, region_positions, region_bulk_vels, H, snapshot['redshift'],
                            halo_exists, compare, angles_in=angles_in, **step_kw)
             if defer:
-                # the group before the previous one is written (its records crossed PCIe
-                # during the previous step's kernels; its host blocks are then free for
-                # reuse), and the previous step, settled now, starts its own D2H, which
-                # runs during this step's kernels
-                flush(keep=1)
+                # the previous step, settled now, starts its D2H (queued on the copy
+                # stream behind the older group's, so the copy engine does not idle while
+                # the host writes), which runs during this step's kernels; then the group
+                # before it is written (its records crossed PCIe during the previous
+                # step's kernels; its host blocks are then free for reuse)
                 if groups and groups[-1][2] is None:
                     groups[-1][2] = eng.fetch_async(groups[-1][0], groups[-1][1])
+                flush(keep=1)
             else:
                 flush()
             if compare and res.n_slots == 0:
