@@ -45,10 +45,31 @@ def _block_starts(slices, n):
     """Repacked (start, end) rows (-1, -1 = absent) -> non-decreasing block starts that
     tile [0, n) (an absent halo gets an empty block)."""
     slices = np.asarray(slices, dtype=np.int64).reshape(-1, 2)
+    present = slices[:, 0] >= 0
+    if not present.any():
+        return np.zeros(len(slices), dtype=np.int64)
+    a, b = slices[:, 0], slices[:, 1]
+    if np.any(present & (b < a)):
+        return _block_starts_loop(slices)
+    # an absent halo starts where the last present block before it ends (before the
+    # first present one: where that one starts; rows before it are in no block), and
+    # a present block may not start before that end: the running maximum of the present
+    # blocks' ends (vectorised; 12,500 halos took 5.6 ms as a loop per call)
+    first = int(a[present][0])
+    run = np.maximum.accumulate(np.where(present, b, np.iinfo(np.int64).min))
+    prev = np.empty_like(run)
+    prev[0] = first
+    prev[1:] = np.maximum(run[:-1], first)
+    if np.any(present & (a < prev)):
+        raise ValueError('region blocks must follow halo order')
+    return np.where(present, a, prev)
+
+
+def _block_starts_loop(slices):
+    """_block_starts for rows with negative-size blocks (end < start): the running end
+    then steps back, as the row-by-row rule does."""
     starts = np.empty(len(slices), dtype=np.int64)
     present = slices[:, 0] >= 0
-    # an absent halo before the first present one starts where that one starts (rows
-    # before the first block are in no block)
     pos = int(slices[present, 0][0]) if present.any() else 0
     for j, (a, b) in enumerate(slices):
         if a >= 0:

@@ -376,3 +376,30 @@ def test_build_halos_matches_structured_fill():
         assert rc == 0
         assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
     assert lib.oa_build_halos(None, None, None, None, None, None, None, 3, None) < 0
+
+
+def test_block_starts_vectorised_matches_rule():
+    """track_orbits_onthefly._block_starts (vectorised) equals the row-by-row rule on
+    random repacked slices: absent halos, gaps, empty blocks, and out-of-order blocks
+    (ValueError in both)."""
+    import numpy as np
+    from orbitanalysis_amd.track_orbits_onthefly import _block_starts, _block_starts_loop
+    rng = np.random.default_rng(0)
+    for _ in range(2000):
+        nh = int(rng.integers(1, 30))
+        sizes, gaps = rng.integers(0, 5, nh), rng.integers(0, 3, nh)
+        st = np.cumsum(gaps + np.concatenate([[0], sizes[:-1]]))
+        sl = np.stack([st, st + sizes], 1)
+        sl[rng.uniform(size=nh) < 0.3] = -1
+        if rng.uniform() < 0.2:
+            i = int(rng.integers(0, nh))
+            if sl[i, 0] >= 0:
+                sl[i, 0] = max(sl[i, 0] - 3, 0)
+        outs = []
+        for f in (_block_starts_loop, lambda s: _block_starts(s, 100)):
+            try:
+                outs.append(f(sl))
+            except ValueError:
+                outs.append(None)
+        assert (outs[0] is None) == (outs[1] is None)
+        assert outs[0] is None or np.array_equal(outs[0], outs[1])

@@ -56,6 +56,8 @@ def main():
     ap.add_argument('--mode', default='pericentric')
     ap.add_argument('--sharded', action='store_true')
     ap.add_argument('--backend', default='nccl')
+    ap.add_argument('--profile-host', action='store_true',
+                    help='cProfile of the timed steps (host functions by own time, stderr)')
     args = ap.parse_args()
     import torch
     import orbitanalysis_amd  # noqa: F401
@@ -173,7 +175,12 @@ def main():
         otf.timings, otf.timing_sync = {}, False
     comp_ms, units, outs = [], 0, None
     t_start = None
+    prof = None
     for k in range(1, total_steps + 1):
+        if k == 2 and args.profile_host:
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         if k == 2:
             torch.cuda.synchronize()
             if dist is not None:
@@ -199,6 +206,13 @@ def main():
             units += n_rows[k % S]
     torch.cuda.synchronize()
     wall = time.perf_counter() - t_start
+    if prof is not None:
+        prof.disable()
+        import io
+        import pstats
+        buf = io.StringIO()
+        pstats.Stats(prof, stream=buf).sort_stats('tottime').print_stats(30)
+        log('host profile (%d timed steps):\n%s' % (total_steps - 1, buf.getvalue()))
     phases = None
     if args.sharded:
         # the timed steps' host and stream time per phase (medians), then an instrumented
