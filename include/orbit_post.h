@@ -58,8 +58,7 @@ typedef struct oa_collate_args {
     int32_t chunk_start;        /* round r: records [r*CHUNK, (r+1)*CHUNK) of each slice   */
     int32_t lds_keys;           /* sort slots: power of two in [64, CHUNK], >= every halo's
                                    record count this round                                */
-    int32_t lds_old;            /* old keys cached in LDS per halo (<= 12288); halos with
-                                   more are searched in global memory                     */
+    int32_t reserved;
     const void *apsis_ids;      /* this snapshot's {peri|apo}center_IDs                    */
     const uint16_t *angles;     /* this snapshot's angles (float16 bits)                   */
     const uint8_t *keep_lut;    /* [65536]: 1 if (float16 value > angle_cut) in NumPy      */
@@ -68,15 +67,15 @@ typedef struct oa_collate_args {
     const int64_t *new_base;    /* [n_halos] exclusive prefix of this round's chunk sizes  */
     const uint64_t *old_keys;   /* cumulative state in: sorted unique keys per halo, CSR   */
     const int64_t *old_cnt;
-    const int64_t *old_off;     /* [n_halos + 1]                                          */
+    const int64_t *old_off;     /* [n_halos + 1]; every halo's list < 2^31 elements        */
     int64_t n_old;              /* old_off[n_halos]                                        */
     int64_t n_new_cap;          /* sum of this round's chunk sizes                         */
     uint64_t *w_keys;           /* workspace [n_new_cap]: sorted unique new keys per halo  */
-    int64_t *w_cnt;             /* [n_new_cap] their multiplicities                        */
-    int64_t *w_lb;              /* [n_new_cap] lower bound in the halo's old keys          */
-    int32_t *w_fp;              /* [n_new_cap] exclusive prefix of "already in old"       */
+    int32_t *w_cnt;             /* [n_new_cap] their multiplicities                        */
+    int32_t *w_lb;              /* [n_new_cap] old keys below each                         */
+    int32_t *w_fp;              /* [n_new_cap] new keys below each already in the old list */
     int32_t *w_ulen;            /* [n_halos] unique new keys                               */
-    int32_t *w_found;           /* [n_halos] of which already in old                       */
+    int32_t *w_found;           /* [n_halos] of which already in the old list              */
     int64_t *new_off;           /* out [n_halos + 1] merged state offsets                  */
     uint64_t *new_keys;         /* out [n_old + n_new_cap] merged state (prefix used)      */
     int64_t *new_cnt;

@@ -13,7 +13,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.abspath(__file__))
 # ORBIT_HIP_LIB selects an alternative build (kernel variants for tuning sweeps)
 LIB_PATH = os.environ.get('ORBIT_HIP_LIB') or os.path.join(PKG, 'liborbit_hip.so')
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -82,12 +82,12 @@ class CompactArgs(ctypes.Structure):
 
 class CollateArgs(ctypes.Structure):
     _fields_ = [('n_halos', c_i32), ('in_kind', c_i32), ('key_signed', c_i32),
-                ('chunk_start', c_i32), ('lds_keys', c_i32), ('lds_old', c_i32), ('apsis_ids', c_vp), ('angles', c_vp),
-                ('keep_lut', c_vp), ('src_off', c_vp), ('src_cnt', c_vp), ('new_base', c_vp),
-                ('old_keys', c_vp), ('old_cnt', c_vp), ('old_off', c_vp), ('n_old', c_i64),
-                ('n_new_cap', c_i64), ('w_keys', c_vp), ('w_cnt', c_vp), ('w_lb', c_vp),
-                ('w_fp', c_vp), ('w_ulen', c_vp), ('w_found', c_vp), ('new_off', c_vp),
-                ('new_keys', c_vp), ('new_cnt', c_vp)]
+                ('chunk_start', c_i32), ('lds_keys', c_i32), ('reserved', c_i32),
+                ('apsis_ids', c_vp), ('angles', c_vp), ('keep_lut', c_vp), ('src_off', c_vp),
+                ('src_cnt', c_vp), ('new_base', c_vp), ('old_keys', c_vp), ('old_cnt', c_vp),
+                ('old_off', c_vp), ('n_old', c_i64), ('n_new_cap', c_i64), ('w_keys', c_vp),
+                ('w_cnt', c_vp), ('w_lb', c_vp), ('w_fp', c_vp), ('w_ulen', c_vp),
+                ('w_found', c_vp), ('new_off', c_vp), ('new_keys', c_vp), ('new_cnt', c_vp)]
 
 
 class CentralArgs(ctypes.Structure):

@@ -3,8 +3,8 @@
 // of include/orbit_post.h (second translation unit of liborbit_hip.so).
 //
 // Reference (paths under /root/reference/orbitanalysis/):
-//   Apsides.collate_apsides        postprocessing.py:118-142 -> k_collate_new,
-//                                  k_collate_offsets, k_collate_merge
+//   Apsides.collate_apsides        postprocessing.py:118-142 -> k_collate_rank,
+//                                  k_collate_offsets, k_collate_place
 //   Apsides.save_final_apsis_counts postprocessing.py:215-236 -> k_retro_counts
 //   get_central_particle_ids       progenitors.py:38-56       -> k_central
 //   find_main_progenitors          progenitors.py:82-117      -> k_mp_insert,
@@ -13,9 +13,10 @@
 // Design: no global sort anywhere.
 //  * collate keeps, per collated halo, the cumulative sorted-unique (ID, count) list
 //    the reference rebuilds with np.unique every snapshot; a snapshot's kept apsis IDs
-//    are sorted per halo in LDS (bitonic, <= OA_COLLATE_CHUNK keys), run-length
-//    encoded and located in the halo's old list (LDS-cached up to 12288 keys) by
-//    binary search; a second per-halo pass writes every element at its merge rank;
+//    are sorted per halo in LDS (bitonic, <= OA_COLLATE_CHUNK keys) and run-length
+//    encoded, the old list streams past them (binary search in LDS) to count the
+//    merged length; after a scan of the lengths a second per-halo pass writes every
+//    element at its merge rank;
 //  * central IDs: per region block, an MSB-first radix select of the n-th smallest
 //    radius (common high bits skipped, early exit when a bin is taken whole; keys
 //    cached in LDS for blocks <= 12288) and an LDS bitonic sort of the <= n
@@ -51,6 +52,28 @@ int check_launch(const char *what) {
 constexpr uint64_t SIGN = 0x8000000000000000ull;
 constexpr int CH = OA_COLLATE_CHUNK;
 constexpr int SC = OA_CENTRAL_MAX_N;     // k_central: survivors sorted in LDS
+
+#ifndef OA_STAMPS
+#define OA_STAMPS 0
+#endif
+#if OA_STAMPS
+// diagnostic builds: per-block s_memrealtime at the phase boundaries of k_central
+// (OA_STAMPS=1) or k_collate_rank (OA_STAMPS=2)
+constexpr int CST_N = 8, CST_MAX = 1 << 16;
+__device__ uint64_t g_cstamps[CST_MAX * CST_N];
+#define STAMP_AT(k) do { if (threadIdx.x == 0 && blockIdx.x < CST_MAX) \
+    g_cstamps[blockIdx.x * CST_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#endif
+#if OA_STAMPS == 1
+#define CSTAMP(k) STAMP_AT(k)
+#else
+#define CSTAMP(k) do { } while (0)
+#endif
+#if OA_STAMPS == 2
+#define RSTAMP(k) STAMP_AT(k)
+#else
+#define RSTAMP(k) do { } while (0)
+#endif
 
 // value of element i as 64-bit two's complement (signed kinds sign-extend)
 __device__ __forceinline__ uint64_t load_val(const void *p, int64_t i, int kind) {
@@ -147,74 +170,150 @@ __device__ void bitonic_pairs(uint64_t *s, uint32_t *x, int P) {
 }
 
 // ------------------------------------------------------------------ f3: collate
-// One 256-thread work-group per collated halo: this round's kept apsis IDs (angle > cut
-// via the NumPy-evaluated LUT, postprocessing.py:127-128), sorted, run-length encoded
-// (np.unique(return_counts), :135), each unique key located in the halo's old list.
-// Dynamic LDS sized by the host for this round: a.lds_keys sort slots (power of two,
-// >= every halo's kept count) and a.lds_old cached old keys (halos with more search
-// the old list in global memory), so several work-groups share a CU.
+// Apsides.collate_apsides (postprocessing.py:118-142) as three launches per round:
+//   k_collate_rank   one 256-thread work-group per halo: this round's kept apsis IDs
+//                    (angle > cut via the NumPy-evaluated LUT, :127-128) sorted in LDS
+//                    and run-length encoded (np.unique(return_counts), :135) into u unique
+//                    new keys; the halo's old keys stream past them once (binary search
+//                    in LDS), giving per new key q: F(q) = #new keys below q already in the
+//                    old list, H(q) = #old keys below q; and the merged length
+//                    on + u - F(u)  (np.append + np.unique, :130-136);
+//   k_collate_offsets  the merged lengths -> offsets (one work-group);
+//   k_collate_place  one work-group per halo: old element i (rank L among the new keys)
+//                    goes to i + L - F(L), adding the new count when it is new key L;
+//                    absent new key q goes to H(q) + q - F(q).
+// No cross-work-group waits (a single-pass variant placing halos behind a decoupled
+// look-back waited on its slowest predecessors: profiles/r05/ab_collate_lookback_r05su.txt).
+constexpr int CT = 256, CL_U = 4;
+
+__device__ __forceinline__ int lower_rank(const uint64_t *nk, int u, uint64_t key) {
+    int L = 0, R = u;
+    while (L < R) {
+        const int mid = (L + R) >> 1;
+        if (nk[mid] < key) L = mid + 1; else R = mid;
+    }
+    return L;
+}
+
 // KIND: the apsis ID kind (a template argument: the loads below are unconditional, index
 // clamped, so CL_U of them are in flight per thread; a load under a lane test or a kind
 // switch waits for its data before the next one issues)
-constexpr int CT = 256, CL_U = 4;
-template <int KIND>
-__global__ __launch_bounds__(CT) void k_collate_new(const oa_collate_args a) {
+constexpr int CTILE = 2 * CT;          // old keys per LDS tile of k_collate_rank
+
+// ascending bitonic sort of the first P (a power of two) keys, held K per thread
+// (thread t: keys K t .. K t + K - 1; the threads past P / K idle): a stage whose partner
+// is in the same thread swaps registers, one in another lane of the wave exchanges
+// through a lane shuffle, one in another wave (j >= 64 K: P > 512 only) through LDS
+// (lds: P keys).
+template <int K>
+__device__ void bitonic_regs(uint64_t (&v)[K], int P, uint64_t *lds) {
+    const int t = threadIdx.x;
+    const bool active = K * (t & ~63) < P;                   // uniform per wave
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j >= K; j >>= 1) {
+            if (j >= 64 * K) {
+                if (active)
+#pragma unroll
+                    for (int r = 0; r < K; ++r) lds[K * t + r] = v[r];
+                __syncthreads();
+                if (active)
+#pragma unroll
+                    for (int r = 0; r < K; ++r) {
+                        const int i = K * t + r;
+                        const uint64_t w = lds[i ^ j];
+                        const bool up = (i & k) == 0, lower = (i & j) == 0;
+                        v[r] = (up == lower) ? (v[r] < w ? v[r] : w) : (v[r] < w ? w : v[r]);
+                    }
+                __syncthreads();
+            } else if (active) {
+                const int mk = j / K;
+                const bool lower = (t & mk) == 0;
+#pragma unroll
+                for (int r = 0; r < K; ++r) {
+                    const uint64_t w = __shfl_xor((unsigned long long)v[r], mk);
+                    const bool up = ((K * t + r) & k) == 0;
+                    v[r] = (up == lower) ? (v[r] < w ? v[r] : w) : (v[r] < w ? w : v[r]);
+                }
+            }
+        }
+        if (active)
+#pragma unroll
+            for (int jj = K / 2; jj > 0; jj >>= 1) {
+                if (jj >= k) continue;
+#pragma unroll
+                for (int r = 0; r < K; ++r) {
+                    if (r & jj) continue;
+                    const bool up = ((K * t + r) & k) == 0;
+                    const uint64_t x = v[r], y = v[r | jj];
+                    if ((x > y) == up) { v[r] = y; v[r | jj] = x; }
+                }
+            }
+    }
+}
+
+// K: sort keys per thread (lds_keys / CT, at least 2)
+// LDS (a.lds_keys = S): [S] u64 sort slots, then the unique new keys in place;
+// [max(S + 1, 2 * CTILE)] int run heads, then old-key tiles of CTILE; [S + 1] int flags.
+template <int KIND, int K>
+__global__ __launch_bounds__(CT) void k_collate_rank(const oa_collate_args a) {
     extern __shared__ __attribute__((aligned(16))) char cl_smem[];
-    uint64_t *sk = reinterpret_cast<uint64_t *>(cl_smem);
-    uint64_t *ok = sk + a.lds_keys;                       // the halo's old keys, when they fit
-    int *hp = reinterpret_cast<int *>(ok + a.lds_old);
+    const int S = a.lds_keys;
+    const int hs = S + 1 > 2 * CTILE ? S + 1 : 2 * CTILE;
+    uint64_t *sk = reinterpret_cast<uint64_t *>(cl_smem);   // sort slots -> unique new keys
+    int *hp = reinterpret_cast<int *>(sk + S);               // run heads -> old-key tiles
+    uint64_t *tile = reinterpret_cast<uint64_t *>(hp);
+    int *fp = hp + hs;                                       // bit 0: found in the old list,
+                                                             // bit 1: lower bound written
     __shared__ int wsum[CT / 64 + 1];
     __shared__ int s_m;
     const int j = blockIdx.x;
+    RSTAMP(0);
+    const int64_t ob = a.old_off[j], on = a.old_off[j + 1] - ob;
     const int64_t rem = a.src_cnt[j] - a.chunk_start;
-    if (rem <= 0) {
+    const int nraw = rem <= 0 ? 0 : (rem < CH ? (int)rem : CH);
+    if (nraw == 0) {                                         // nothing new: the list is kept
         if (threadIdx.x == 0) { a.w_ulen[j] = 0; a.w_found[j] = 0; }
         return;
     }
-    const int nraw = rem < CH ? (int)rem : CH;
-    const int64_t s0 = a.src_off[j] + a.chunk_start;
-    const int64_t base = a.new_base[j];
-    const int64_t ob = a.old_off[j], on = a.old_off[j + 1] - ob;
-    const bool cached = on <= a.lds_old;
+    // the first old-key tile: loads issued now, staged after the sort
+    uint64_t okey[CTILE / CT];
+    if (on > 0)
+#pragma unroll
+        for (int e = 0; e < CTILE / CT; ++e) {
+            const int64_t i = e * CT + threadIdx.x, ic = i < on ? i : on - 1;
+            okey[e] = __builtin_nontemporal_load(a.old_keys + ob + ic);
+        }
     if (threadIdx.x == 0) s_m = 0;
     __syncthreads();
-    if (cached)
-        for (int i0 = 0; i0 < on; i0 += CL_U * CT) {
-            uint64_t t[CL_U];
-#pragma unroll
-            for (int u = 0; u < CL_U; ++u) {
-                const int64_t i = i0 + u * CT + threadIdx.x;
-                t[u] = a.old_keys[ob + (i < on ? i : on - 1)];
-            }
-#pragma unroll
-            for (int u = 0; u < CL_U; ++u) {
-                const int64_t i = i0 + u * CT + threadIdx.x;
-                if (i < on) ok[i] = t[u];
-            }
-        }
+    const int64_t s0 = a.src_off[j] + a.chunk_start;
     for (int i0 = 0; i0 < nraw; i0 += CL_U * CT) {
         uint16_t an[CL_U];
         uint64_t id[CL_U];
 #pragma unroll
-        for (int u = 0; u < CL_U; ++u) {
-            const int i = i0 + u * CT + (int)threadIdx.x;
+        for (int e = 0; e < CL_U; ++e) {
+            const int i = i0 + e * CT + (int)threadIdx.x;
             const int64_t r = s0 + (i < nraw ? i : nraw - 1);
-            an[u] = a.angles[r];
-            id[u] = load_val(a.apsis_ids, r, KIND);
+            an[e] = a.angles[r];
+            id[e] = load_val_nt<KIND>(a.apsis_ids, r);
         }
         uint8_t kp[CL_U];
 #pragma unroll
-        for (int u = 0; u < CL_U; ++u) kp[u] = a.keep_lut[an[u]];
+        for (int e = 0; e < CL_U; ++e) kp[e] = a.keep_lut[an[e]];
 #pragma unroll
-        for (int u = 0; u < CL_U; ++u) {
-            const int i = i0 + u * CT + (int)threadIdx.x;
-            if (i < nraw && kp[u]) {
-                const int p = atomicAdd(&s_m, 1);
-                sk[p] = to_key(id[u], a.key_signed);
-            }
+        for (int e = 0; e < CL_U; ++e) {
+            const int i = i0 + e * CT + (int)threadIdx.x;
+            // compaction: one LDS atomic per wave, lanes placed by their ballot rank
+            const bool keep = i < nraw && kp[e];
+            const uint64_t bal = __ballot(keep);
+            const int lane = threadIdx.x & 63;
+            int wb = 0;
+            if (lane == 0 && bal) wb = atomicAdd(&s_m, __popcll(bal));
+            wb = __shfl(wb, 0);
+            if (keep) sk[wb + __popcll(bal & ((1ull << lane) - 1))] = to_key(id[e], a.key_signed);
         }
     }
     __syncthreads();
+    RSTAMP(1);
     const int m = s_m;
     if (m == 0) {
         if (threadIdx.x == 0) { a.w_ulen[j] = 0; a.w_found[j] = 0; }
@@ -222,57 +321,104 @@ __global__ __launch_bounds__(CT) void k_collate_new(const oa_collate_args a) {
     }
     int P = 1;
     while (P < m) P <<= 1;
-    for (int i = m + threadIdx.x; i < P; i += CT) sk[i] = ~0ull;   // ties with a real ~0 key are harmless
-    __syncthreads();
-    bitonic_keys<CT>(sk, P);
-    // run heads: thread t owns positions [t*E, t*E + E)
-    const int E = (m + CT - 1) / CT;
-    const int lo = threadIdx.x * E, hi = min(lo + E, m);
-    int nh = 0;
-    for (int i = lo; i < hi; ++i) nh += (i == 0 || sk[i] != sk[i - 1]);
-    int u;
-    int q = block_scan<CT, int>(nh, wsum, u);
-    for (int i = lo; i < hi; ++i)
-        if (i == 0 || sk[i] != sk[i - 1]) hp[q++] = i;
-    if (threadIdx.x == 0) hp[u] = m;
-    __syncthreads();
-    int carry = 0;
-    for (int q0 = 0; q0 < u; q0 += CT) {
-        const int qq = q0 + threadIdx.x;
-        int f = 0;
-        uint64_t key = 0;
-        int64_t lb = 0;
-        int c = 0;
-        if (qq < u) {
-            key = sk[hp[qq]];
-            c = hp[qq + 1] - hp[qq];
-            int64_t L = 0, R = on;
-            if (cached) {
-                while (L < R) {
-                    const int64_t mid = (L + R) >> 1;
-                    if (ok[mid] < key) L = mid + 1; else R = mid;
-                }
-                f = (L < on && ok[L] == key) ? 1 : 0;
-            } else {
-                while (L < R) {
-                    const int64_t mid = (L + R) >> 1;
-                    if (a.old_keys[ob + mid] < key) L = mid + 1; else R = mid;
-                }
-                f = (L < on && a.old_keys[ob + L] == key) ? 1 : 0;
-            }
-            lb = L;
+    {   // sort in registers: thread t holds keys [K t, K t + K), padded with ~0 (ties with a
+        // real ~0 key are harmless)
+        uint64_t v[K];
+        const bool mine = K * (int)threadIdx.x < P;
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+            const int i = K * (int)threadIdx.x + r;
+            v[r] = i < m ? sk[i] : ~0ull;
         }
-        int tf;
-        const int ex = block_scan<CT, int>(f, wsum, tf);
-        if (qq < u) {
-            a.w_keys[base + qq] = key;
-            a.w_cnt[base + qq] = c;
-            a.w_lb[base + qq] = lb;
-            a.w_fp[base + qq] = carry + ex;
-        }
-        carry += tf;
+        __syncthreads();
+        bitonic_regs<K>(v, P, sk);
+        if (mine)
+#pragma unroll
+            for (int r = 0; r < K; ++r) sk[K * threadIdx.x + r] = v[r];
+        __syncthreads();
     }
-    if (threadIdx.x == 0) { a.w_ulen[j] = u; a.w_found[j] = carry; }
+    RSTAMP(2);
+    int u;
+    const int64_t base = a.new_base[j];
+    {   // run heads: thread t owns positions [t*E, t*E + E)
+        const int E = (m + CT - 1) / CT;
+        const int lo = threadIdx.x * E, hi = min(lo + E, m);
+        int nh = 0;
+        for (int i = lo; i < hi; ++i) nh += (i == 0 || sk[i] != sk[i - 1]);
+        int q = block_scan<CT, int>(nh, wsum, u);
+        for (int i = lo; i < hi; ++i)
+            if (i == 0 || sk[i] != sk[i - 1]) hp[q++] = i;
+        if (threadIdx.x == 0) hp[u] = m;
+        __syncthreads();
+        // the unique keys move down in place (all read before any is written); their
+        // multiplicities go out now, which frees the run heads for the tiles
+        uint64_t kq[K];
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+            const int qq = r * CT + (int)threadIdx.x;
+            if (qq < u) {
+                kq[r] = sk[hp[qq]];
+                a.w_cnt[base + qq] = hp[qq + 1] - hp[qq];
+                fp[qq] = 0;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+            const int qq = r * CT + (int)threadIdx.x;
+            if (qq < u) sk[qq] = kq[r];
+        }
+    }
+    __syncthreads();
+    RSTAMP(3);
+    const uint64_t *nk = sk;
+    // lower bound of every new key in the old list: the old keys pass through LDS one
+    // tile at a time (the next tile's loads in flight); a key is searched in the tile
+    // whose key range holds it
+    uint64_t prev_last = 0;
+    for (int64_t t0 = 0; t0 < on; t0 += CTILE) {
+        const int nt = on - t0 < CTILE ? (int)(on - t0) : CTILE;
+#pragma unroll
+        for (int e = 0; e < CTILE / CT; ++e) {
+            const int i = e * CT + (int)threadIdx.x;
+            if (i < nt) tile[i] = okey[e];
+        }
+        if (t0 + CTILE < on)
+#pragma unroll
+            for (int e = 0; e < CTILE / CT; ++e) {
+                const int64_t i = t0 + CTILE + e * CT + threadIdx.x, ic = i < on ? i : on - 1;
+                okey[e] = __builtin_nontemporal_load(a.old_keys + ob + ic);
+            }
+        __syncthreads();
+        const uint64_t last = tile[nt - 1];
+        for (int q = threadIdx.x; q < u; q += CT) {
+            const uint64_t key = nk[q];
+            if (key <= last && (t0 == 0 || key > prev_last)) {
+                const int L = lower_rank(tile, nt, key);
+                a.w_lb[base + q] = (int)(t0 + L);
+                fp[q] = 2 | (tile[L] == key ? 1 : 0);
+            }
+        }
+        prev_last = last;
+        __syncthreads();
+    }
+    RSTAMP(4);
+    // F: exclusive prefix of the found flags (thread t: the run [t c, t c + c))
+    const int c = (u + CT - 1) / CT;
+    const int r0 = min(u, (int)threadIdx.x * c), r1 = min(u, r0 + c);
+    int run = 0;
+    for (int i = r0; i < r1; ++i) run += fp[i] & 1;
+    int tot;
+    int acc = block_scan<CT, int>(run, wsum, tot);
+    for (int i = r0; i < r1; ++i) {
+        const int f = fp[i];
+        a.w_keys[base + i] = nk[i];
+        a.w_fp[base + i] = acc;
+        if (!(f & 2)) a.w_lb[base + i] = (int)on;            // above every old key
+        acc += f & 1;
+    }
+    if (threadIdx.x == 0) { a.w_ulen[j] = u; a.w_found[j] = tot; }
+    RSTAMP(5);
 }
 
 // merged lengths -> offsets (one work-group; n_halos is a catalogue size)
@@ -291,79 +437,38 @@ __global__ __launch_bounds__(1024) void k_collate_offsets(const oa_collate_args 
     if (threadIdx.x == 0) a.new_off[a.n_halos] = carry;
 }
 
-// one work-group per halo: the halo's new unique keys and their "already present"
-// prefix in LDS (a.lds_keys slots); every old element goes to rank i + #new keys below
-// it not already present (adding the new count on a match), every new key absent
-// from the old list to rank lb + #such new keys before it.
-// An old list of <= a.lds_old keys takes that count from a shift table instead of a
-// binary search per element: a new key q absent from the old list is below old key i
-// exactly when its lower bound lb[q] <= i, so the count is the inclusive prefix over i
-// of the absent keys' lb histogram (one LDS read per old element); a found key adds its
-// count at old position lb[q].
-__global__ __launch_bounds__(CT) void k_collate_merge(const oa_collate_args a) {
+// one work-group per halo: the new keys, their F and counts in LDS (a.lds_keys slots);
+// the old list streams through once, MU elements per thread per trip, every load of a
+// trip issued before any store (the stores may alias the old list for the compiler,
+// which would otherwise hold each trip's loads behind the previous trip's stores)
+__global__ __launch_bounds__(CT) void k_collate_place(const oa_collate_args a) {
     extern __shared__ __attribute__((aligned(16))) char cl_smem[];
-    uint64_t *nk = reinterpret_cast<uint64_t *>(cl_smem);
-    int *nfp = reinterpret_cast<int *>(nk + a.lds_keys);
-    int *shift = nfp + a.lds_keys + 1;                    // [lds_old + 1] (table path)
-    int *fadd = shift + a.lds_old + 1;                    // [lds_old]
-    __shared__ int wsum[CT / 64 + 1];
+    uint64_t *nk = reinterpret_cast<uint64_t *>(cl_smem);   // [lds_keys]
+    int *fp = reinterpret_cast<int *>(nk + a.lds_keys);      // [lds_keys + 1]
+    int *nc = fp + a.lds_keys + 1;                           // [lds_keys]
     const int j = blockIdx.x;
     const int u = a.w_ulen[j];
     const int64_t base = a.new_base[j];
     const int64_t ob = a.old_off[j], on = a.old_off[j + 1] - ob;
     const int64_t no = a.new_off[j];
-    const bool table = on <= a.lds_old;                   // uniform
-    // (loads unconditional at clamped indices, CL_U per thread in flight)
     for (int q0 = 0; q0 < u; q0 += CL_U * CT) {
         uint64_t k[CL_U];
-        int f[CL_U];
+        int f[CL_U], c[CL_U];
 #pragma unroll
         for (int e = 0; e < CL_U; ++e) {
             const int q = q0 + e * CT + (int)threadIdx.x, qc = q < u ? q : u - 1;
             k[e] = a.w_keys[base + qc];
             f[e] = a.w_fp[base + qc];
+            c[e] = a.w_cnt[base + qc];
         }
 #pragma unroll
         for (int e = 0; e < CL_U; ++e) {
             const int q = q0 + e * CT + (int)threadIdx.x;
-            if (q < u) { nk[q] = k[e]; nfp[q] = f[e]; }
+            if (q < u) { nk[q] = k[e]; fp[q] = f[e]; nc[q] = c[e]; }
         }
     }
-    if (threadIdx.x == 0) nfp[u] = a.w_found[j];
-    if (table)
-        for (int i = threadIdx.x; i <= on; i += CT) { shift[i] = 0; if (i < on) fadd[i] = 0; }
+    if (threadIdx.x == 0) fp[u] = a.w_found[j];
     __syncthreads();
-    if (table) {
-        for (int q0 = 0; q0 < u; q0 += CL_U * CT) {
-            int lb[CL_U], c[CL_U];
-#pragma unroll
-            for (int e = 0; e < CL_U; ++e) {
-                const int q = q0 + e * CT + (int)threadIdx.x, qc = q < u ? q : u - 1;
-                lb[e] = (int)a.w_lb[base + qc];
-                c[e] = (int)a.w_cnt[base + qc];
-            }
-#pragma unroll
-            for (int e = 0; e < CL_U; ++e) {
-                const int q = q0 + e * CT + (int)threadIdx.x;
-                if (q >= u) continue;
-                if (nfp[q + 1] == nfp[q]) atomicAdd(&shift[lb[e]], 1);  // absent from the old list
-                else fadd[lb[e]] = c[e];                                // found at old position lb
-            }
-        }
-        __syncthreads();
-        // inclusive scan of shift[0 .. on] (thread t: the run [t c, t c + c))
-        const int n1 = (int)on + 1, c = (n1 + CT - 1) / CT;
-        const int r0 = min(n1, (int)threadIdx.x * c), r1 = min(n1, r0 + c);
-        int run = 0;
-        for (int i = r0; i < r1; ++i) run += shift[i];
-        int tot;
-        int acc = block_scan<CT, int>(run, wsum, tot);
-        for (int i = r0; i < r1; ++i) { acc += shift[i]; shift[i] = acc; }
-        __syncthreads();
-    }
-    // old elements MU per thread per trip, every load issued before any store (the
-    // stores may alias the old list for the compiler, which would otherwise hold each
-    // trip's loads behind the previous trip's stores)
     constexpr int MU = 8;
     for (int64_t i0 = threadIdx.x; i0 < on; i0 += (int64_t)CT * MU) {
         uint64_t key[MU];
@@ -371,37 +476,36 @@ __global__ __launch_bounds__(CT) void k_collate_merge(const oa_collate_args a) {
 #pragma unroll
         for (int e = 0; e < MU; ++e) {
             const int64_t i = i0 + (int64_t)e * CT, ic = i < on ? i : on - 1;
-            key[e] = a.old_keys[ob + ic];
-            cnt[e] = a.old_cnt[ob + ic];
+            key[e] = __builtin_nontemporal_load(a.old_keys + ob + ic);
+            cnt[e] = __builtin_nontemporal_load(a.old_cnt + ob + ic);
         }
 #pragma unroll
         for (int e = 0; e < MU; ++e) {
             const int64_t i = i0 + (int64_t)e * CT;
             if (i >= on) break;
-            int64_t pos, add;
-            if (table) {
-                pos = no + i + shift[i];
-                add = fadd[i];
-            } else {
-                int L = 0, R = u;
-                while (L < R) {
-                    const int mid = (L + R) >> 1;
-                    if (nk[mid] < key[e]) L = mid + 1; else R = mid;
-                }
-                const bool eq = L < u && nk[L] == key[e];
-                pos = no + i + L - nfp[L];
-                add = eq ? a.w_cnt[base + L] : 0;
-            }
+            const int L = lower_rank(nk, u, key[e]);
+            const bool eq = L < u && nk[L] == key[e];
+            const int64_t pos = no + i + L - fp[L];
+            // plain stores: the positions shift by one at every inserted key, so a wave's
+            // stores straddle lines, which L2 merges (non-temporal: 1.6x the time)
             a.new_keys[pos] = key[e];
-            a.new_cnt[pos] = cnt[e] + add;
+            a.new_cnt[pos] = cnt[e] + (eq ? (int64_t)nc[L] : 0);
         }
     }
     for (int q = threadIdx.x; q < u; q += CT) {
-        if (nfp[q + 1] != nfp[q]) continue;               // already in the old list
-        const int64_t pos = no + a.w_lb[base + q] + (q - nfp[q]);
+        if (fp[q + 1] != fp[q]) continue;                    // already in the old list
+        const int64_t pos = no + a.w_lb[base + q] + (q - fp[q]);
         a.new_keys[pos] = nk[q];
-        a.new_cnt[pos] = a.w_cnt[base + q];
+        a.new_cnt[pos] = nc[q];
     }
+}
+
+template <int KIND>
+void (*collate_rank_kernel(int lds_keys))(oa_collate_args) {
+    static_assert(16 * CT >= CH, "k_collate_rank sorts at most 16 keys per thread");
+    return lds_keys <= 2 * CT ? k_collate_rank<KIND, 2>
+         : lds_keys <= 4 * CT ? k_collate_rank<KIND, 4>
+         : lds_keys <= 8 * CT ? k_collate_rank<KIND, 8> : k_collate_rank<KIND, 16>;
 }
 
 __global__ __launch_bounds__(256) void k_keys_to_ids(const uint64_t *keys, int64_t n, int key_signed,
@@ -473,18 +577,6 @@ __device__ __forceinline__ uint64_t r_of(uint64_t k2) {
     return (uint64_t)__double_as_longlong(sqrt(__longlong_as_double((long long)k2)));
 }
 
-#ifndef OA_STAMPS
-#define OA_STAMPS 0
-#endif
-#if OA_STAMPS
-// diagnostic builds: per-block s_memrealtime at k_central's phase boundaries
-constexpr int CST_N = 8, CST_MAX = 1 << 16;
-__device__ uint64_t g_cstamps[CST_MAX * CST_N];
-#define CSTAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < CST_MAX) \
-    g_cstamps[blockIdx.x * CST_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define CSTAMP(k) do { } while (0)
-#endif
 // Raw buffer loads (resource: 48-bit base, byte size; lanes past the size read 0), so a
 // block's coordinates are addressed by one 32-bit lane offset plus a scalar offset per
 // particle instead of a 64-bit address per load.
@@ -1060,8 +1152,9 @@ uint64_t mp_filter_bits(uint64_t n_tracked) {
 
 extern "C" {
 
-// Diagnostic builds (-DOA_STAMPS=1): k_central's per-block phase stamps of its last
-// launch (8 per block, s_memrealtime at 100 MHz); returns the count copied or -1.
+// Diagnostic builds (-DOA_STAMPS=1 / 2): k_central's / k_collate_rank's per-block phase
+// stamps of its last launch (8 per block, s_memrealtime at 100 MHz); returns the count
+// copied or -1.
 int64_t oa_debug_central_stamps(uint64_t *host, int64_t n) {
 #if OA_STAMPS
     const int64_t m = n < (int64_t)CST_MAX * CST_N ? n : (int64_t)CST_MAX * CST_N;
@@ -1095,27 +1188,29 @@ int oa_collate_step(const oa_collate_args *args, void *stream) {
         (a.n_old > 0 && (!a.old_keys || !a.old_cnt)) ||
         (a.n_old + a.n_new_cap > 0 && (!a.new_keys || !a.new_cnt)))
         return fail(OA_E_ARG, "oa_collate_step: null pointer");
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (a.lds_keys < 64 || a.lds_keys > CH || (a.lds_keys & (a.lds_keys - 1)) || a.lds_old < 0)
+    if (a.lds_keys < 64 || a.lds_keys > CH || (a.lds_keys & (a.lds_keys - 1)))
         return fail(OA_E_ARG, "oa_collate_step: lds_keys must be a power of two in [64, CHUNK]");
-    const int64_t lds1 = (int64_t)a.lds_keys * 12 + 4 + (int64_t)a.lds_old * 8;
-    const int64_t lds2 = (int64_t)a.lds_keys * 12 + 8 + (int64_t)a.lds_old * 8 + 4;
-    if (lds1 > 150 * 1024) return fail(OA_E_ARG, "oa_collate_step: LDS request too large");
-    auto knew = a.in_kind == OA_ID_I64 ? k_collate_new<OA_ID_I64>
-              : a.in_kind == OA_ID_U64 ? k_collate_new<OA_ID_U64>
-              : a.in_kind == OA_ID_I32 ? k_collate_new<OA_ID_I32> : k_collate_new<OA_ID_U32>;
-    if (hipFuncSetAttribute(reinterpret_cast<const void *>(knew),
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int64_t lds1 = (int64_t)a.lds_keys * 8 +
+                         (int64_t)(a.lds_keys + 1 > 2 * CTILE ? a.lds_keys + 1 : 2 * CTILE) * 4 +
+                         ((int64_t)a.lds_keys + 1) * 4;
+    const int64_t lds3 = (int64_t)a.lds_keys * 12 + ((int64_t)a.lds_keys + 1) * 4;
+    auto krank = a.in_kind == OA_ID_I64 ? collate_rank_kernel<OA_ID_I64>(a.lds_keys)
+               : a.in_kind == OA_ID_U64 ? collate_rank_kernel<OA_ID_U64>(a.lds_keys)
+               : a.in_kind == OA_ID_I32 ? collate_rank_kernel<OA_ID_I32>(a.lds_keys)
+                                        : collate_rank_kernel<OA_ID_U32>(a.lds_keys);
+    if (hipFuncSetAttribute(reinterpret_cast<const void *>(krank),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void *>(k_collate_merge),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2) != hipSuccess)
+        hipFuncSetAttribute(reinterpret_cast<const void *>(k_collate_place),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds3) != hipSuccess)
         return fail(OA_E_LAUNCH, "oa_collate_step: hipFuncSetAttribute");
-    hipLaunchKernelGGL(knew, dim3(a.n_halos), dim3(CT), (size_t)lds1, st, a);
-    if (int rc = check_launch("k_collate_new")) return rc;
+    hipLaunchKernelGGL(krank, dim3(a.n_halos), dim3(CT), (size_t)lds1, st, a);
+    if (int rc = check_launch("k_collate_rank")) return rc;
     hipLaunchKernelGGL(k_collate_offsets, dim3(1), dim3(1024), 0, st, a);
     if (int rc = check_launch("k_collate_offsets")) return rc;
     if (a.n_old + a.n_new_cap > 0) {
-        hipLaunchKernelGGL(k_collate_merge, dim3(a.n_halos), dim3(CT), (size_t)lds2, st, a);
-        if (int rc = check_launch("k_collate_merge")) return rc;
+        hipLaunchKernelGGL(k_collate_place, dim3(a.n_halos), dim3(CT), (size_t)lds3, st, a);
+        if (int rc = check_launch("k_collate_place")) return rc;
     }
     return OA_OK;
 }

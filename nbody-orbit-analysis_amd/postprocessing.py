@@ -169,9 +169,6 @@ def _id_kind(dt, what):
     return N.ID_KIND[dt]
 
 
-OLD_CACHE = 12288        # old keys per halo cached in LDS by k_collate_new (a.lds_old cap)
-
-
 class _CollateState:
     """Cumulative per-halo sorted-unique (key, count) lists in HBM (CSR)."""
 
@@ -189,8 +186,8 @@ class _CollateState:
     def merge(self, lib, ids_d, in_kind, key_signed, angles_d, lut_d, src_off, src_cnt,
               events=None):
         """Merge one snapshot's kept apsis IDs into the state (rounds of at most
-        COLLATE_CHUNK records per halo).  ``events``: optional list that receives a
-        (start, end) HIP-event pair around every oa_collate_step launch."""
+        COLLATE_CHUNK records per halo, one oa_collate_step each).  ``events``: optional
+        list that receives a (start, end) HIP-event pair around every oa_collate_step."""
         torch = self.torch
         dev = self.device
         ch = N.COLLATE_CHUNK
@@ -200,34 +197,31 @@ class _CollateState:
         st = torch.cuda.current_stream(dev).cuda_stream
         for r in range(rounds):
             chunk = np.clip(src_cnt - r * ch, 0, ch).astype(np.int64)
-            # LDS sized to this round: sort slots for the largest chunk, old keys for the
-            # largest cached list (several work-groups then share a CU)
+            # LDS sized to this round's largest chunk (several work-groups share a CU)
             lds_keys = 64
             while lds_keys < int(chunk.max(initial=0)):
                 lds_keys <<= 1
-            lds_old = int(min(np.diff(self.off_h).max(initial=0), OLD_CACHE))
+            if int(np.diff(self.off_h).max(initial=0)) + ch >= 2 ** 31:
+                raise NotImplementedError('a collated halo of 2^31 or more particle IDs')
             base = np.concatenate([[0], np.cumsum(chunk)[:-1]]).astype(np.int64)
             cap = int(chunk.sum())
-            i64 = dict(dtype=torch.int64, device=dev)
-            w_keys = torch.empty(max(cap, 1), **i64)
-            w_cnt = torch.empty(max(cap, 1), **i64)
-            w_lb = torch.empty(max(cap, 1), **i64)
-            w_fp = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
-            w_ulen = torch.empty(self.n, dtype=torch.int32, device=dev)
-            w_found = torch.empty(self.n, dtype=torch.int32, device=dev)
-            new_off = torch.empty(self.n + 1, **i64)
-            new_keys = torch.empty(max(self.total + cap, 1), **i64)
-            new_cnt = torch.empty(max(self.total + cap, 1), **i64)
+            i32 = dict(dtype=torch.int32, device=dev)
+            w_keys = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+            w_cnt, w_lb, w_fp = (torch.empty(max(cap, 1), **i32) for _ in range(3))
+            w_ulen, w_found = (torch.empty(self.n, **i32) for _ in range(2))
+            new_off = torch.empty(self.n + 1, dtype=torch.int64, device=dev)
+            new_keys = torch.empty(max(self.total + cap, 1), dtype=torch.int64, device=dev)
+            new_cnt = torch.empty(max(self.total + cap, 1), dtype=torch.int64, device=dev)
             base_d = _dev(base, dev)
             a = N.CollateArgs(
                 n_halos=self.n, in_kind=in_kind, key_signed=key_signed, chunk_start=r * ch,
-                lds_keys=lds_keys, lds_old=lds_old,
-                apsis_ids=_ptr(ids_d), angles=_ptr(angles_d), keep_lut=_ptr(lut_d),
-                src_off=_ptr(src_off_d), src_cnt=_ptr(src_cnt_d), new_base=_ptr(base_d),
-                old_keys=_ptr(self.keys), old_cnt=_ptr(self.cnt), old_off=_ptr(self.off),
-                n_old=self.total, n_new_cap=cap, w_keys=_ptr(w_keys), w_cnt=_ptr(w_cnt),
-                w_lb=_ptr(w_lb), w_fp=_ptr(w_fp), w_ulen=_ptr(w_ulen), w_found=_ptr(w_found),
-                new_off=_ptr(new_off), new_keys=_ptr(new_keys), new_cnt=_ptr(new_cnt))
+                lds_keys=lds_keys, apsis_ids=_ptr(ids_d), angles=_ptr(angles_d),
+                keep_lut=_ptr(lut_d), src_off=_ptr(src_off_d), src_cnt=_ptr(src_cnt_d),
+                new_base=_ptr(base_d), old_keys=_ptr(self.keys), old_cnt=_ptr(self.cnt),
+                old_off=_ptr(self.off), n_old=self.total, n_new_cap=cap, w_keys=_ptr(w_keys),
+                w_cnt=_ptr(w_cnt), w_lb=_ptr(w_lb), w_fp=_ptr(w_fp), w_ulen=_ptr(w_ulen),
+                w_found=_ptr(w_found), new_off=_ptr(new_off), new_keys=_ptr(new_keys),
+                new_cnt=_ptr(new_cnt))
             if events is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()

@@ -99,6 +99,19 @@ def test_collate_random_vs_oracle(id_dtype, id_hi, per_halo):
                 assert_same(got[g][d], want[g][d], '%s/%s' % (g, d))
 
 
+def test_collate_many_halos_lookback():
+    """k_collate places every halo's merged list behind a look-back over the halos
+    before it: 3000 halos (47 windows of 64) over 5 snapshots, all outputs vs the oracle."""
+    rng = np.random.default_rng(11)
+    groups, attrs = _random_track_file(rng, 3000, 5, 60, np.int64, 2 ** 40)
+    want = PO.collate_apsides(groups, attrs)
+    got = _collate(groups, attrs, {'save_final_counts': False}, None)
+    assert sorted(got) == sorted(want)
+    for g in want:
+        for d in want[g]:
+            assert_same(got[g][d], want[g][d], '%s/%s' % (g, d))
+
+
 def test_retro_counts_missing_id_raises():
     from orbitanalysis_amd.postprocessing import Apsides
     rng = np.random.default_rng(3)

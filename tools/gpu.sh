@@ -19,6 +19,7 @@
 #   b2        bench.py --gpus 2 over gloo on this one GPU ($B2_SCALING, default strong)
 #   ab        alternating bench runs of library variants ($VARS, tools/variants.sh)
 #   pab       the same for tools/bench_post.py ($PAB_WHICH, default mainprog)
+#   pprof     rocprofv3 kernel stats of tools/bench_post.py per variant in $VARS
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; O=$R/gpurun_out; mkdir -p "$O"; T=${TAG:-x}
 ok() { local rc=$1; echo "[$2] rc=$rc"; [ "$rc" = 0 ] || exit "$rc"; }
@@ -136,6 +137,15 @@ pab)
       rc=$?; echo "$v rep$rep $(grep -o '"ms_per_[a-z]*": [0-9.]*\|identical to the GPU: [A-Za-z]*' "$O/pab_${T}_${v}_$rep.jsonl" | tr '\n' ' ')"
       ok $rc "pab $v"
     done
+  done ;;
+pprof)   # per-kernel stats of tools/bench_post.py for each library variant in $VARS
+  D=$R/nbody-orbit-analysis_amd/variants
+  for v in ${VARS:-base}; do
+    lib=""; [ "$v" != base ] && lib="$D/lib_$v.so"
+    ORBIT_HIP_LIB=$lib prof "$O/pprof_${T}_$v" 300 "$R/tools/bench_post.py" --which ${PAB_WHICH:-collate} \
+      > "$O/pprof_${T}_$v.jsonl" 2> "$O/pprof_${T}_$v.err"
+    rc=$?; echo "== $v $(grep -o '"ms_per_[a-z]*": [0-9.]*' "$O/pprof_${T}_$v.jsonl")"
+    python3 tools/kstats.py "$O/pprof_${T}_$v" | head -6; ok $rc "pprof $v"
   done ;;
 *) echo "unknown step $step"; exit 2 ;;
 esac
