@@ -417,10 +417,6 @@ _PIN_GRAIN = 1 << 22
 N_WS = 3                       # compare-step workspaces in rotation (OrbitEngine)
 
 
-_PIN_WARM = set()          # block sizes whose first request pre-locked _PIN_SETS blocks
-_PIN_SETS = N_WS + 2       # records of the workspaces in flight, plus the two being written
-
-
 def _pinned(n, dtype):
     """A page-locked host tensor of n elements from torch's caching host allocator, the
     block rounded up to a power of two (>= 4 MiB): snapshots' record counts differ, and
@@ -429,13 +425,6 @@ def _pinned(n, dtype):
     still page-locked a new block whenever the count crossed one, ~3-7 ms each)."""
     itemsize = torch.empty(0, dtype=dtype).element_size()
     nb = max(1 << max(int(n) * itemsize - 1, 1).bit_length(), _PIN_GRAIN)
-    if nb not in _PIN_WARM:
-        # the first request of a block size page-locks the blocks that the workspaces in
-        # flight will hold at once, and hands them back to the cache: later steps reuse
-        # them instead of page-locking one mid-stream (a 5-20 ms stall each)
-        _PIN_WARM.add(nb)
-        warm = [torch.empty(nb, dtype=torch.uint8, pin_memory=True) for _ in range(_PIN_SETS)]
-        del warm
     return torch.empty(nb // itemsize, dtype=dtype, pin_memory=True)[:n]
 
 
