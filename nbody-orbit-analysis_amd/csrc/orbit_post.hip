@@ -185,6 +185,9 @@ __device__ void bitonic_pairs(uint64_t *s, uint32_t *x, int P) {
 // No cross-work-group waits (a single-pass variant placing halos behind a decoupled
 // look-back waited on its slowest predecessors: profiles/r05/ab_collate_lookback_r05su.txt).
 constexpr int CT = 256, CL_U = 4;
+#ifndef OA_PLACE_MU
+#define OA_PLACE_MU 16         // k_collate_place: old elements per thread per trip
+#endif
 
 __device__ __forceinline__ int lower_rank(const uint64_t *nk, int u, uint64_t key) {
     int L = 0, R = u;
@@ -469,7 +472,7 @@ __global__ __launch_bounds__(CT) void k_collate_place(const oa_collate_args a) {
     }
     if (threadIdx.x == 0) fp[u] = a.w_found[j];
     __syncthreads();
-    constexpr int MU = 8;
+    constexpr int MU = OA_PLACE_MU;
     for (int64_t i0 = threadIdx.x; i0 < on; i0 += (int64_t)CT * MU) {
         uint64_t key[MU];
         int64_t cnt[MU];
