@@ -201,7 +201,10 @@ __device__ __forceinline__ int lower_rank(const uint64_t *nk, int u, uint64_t ke
 // KIND: the apsis ID kind (a template argument: the loads below are unconditional, index
 // clamped, so CL_U of them are in flight per thread; a load under a lane test or a kind
 // switch waits for its data before the next one issues)
-constexpr int CTILE = 2 * CT;          // old keys per LDS tile of k_collate_rank
+#ifndef OA_CTILE_WAVES
+#define OA_CTILE_WAVES 2        // k_collate_rank: old keys per LDS tile, in units of CT
+#endif
+constexpr int CTILE = OA_CTILE_WAVES * CT;
 
 // ascending bitonic sort of the first P (a power of two) keys, held K per thread
 // (thread t: keys K t .. K t + K - 1; the threads past P / K idle): a stage whose partner
