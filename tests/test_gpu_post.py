@@ -112,6 +112,32 @@ def test_collate_many_halos_lookback():
             assert_same(got[g][d], want[g][d], '%s/%s' % (g, d))
 
 
+@pytest.mark.parametrize('id_dtype', [np.int64, np.uint64])
+def test_collate_extreme_ids_vs_oracle(id_dtype):
+    """IDs at the ends of the key range: the largest one's order key is all ones, the
+    value k_collate_rank pads its sort with; the smallest is key 0."""
+    rng = np.random.default_rng(17)
+    groups, attrs = _random_track_file(rng, 6, 4, 300, np.int64, 10 ** 6)
+    info = np.iinfo(id_dtype)
+    for s, g in enumerate(sorted(groups)):
+        ids = g_ids = groups[g]['pericenter_IDs'].astype(id_dtype)
+        off = groups[g]['region_offsets']
+        for h in range(len(off) - 1):
+            if off[h + 1] - off[h] >= 3:            # extremes in several halos, repeated
+                g_ids[off[h]] = info.max
+                g_ids[off[h] + 1] = info.min
+                if s % 2:
+                    g_ids[off[h] + 2] = info.max - 1
+        groups[g]['pericenter_IDs'] = ids
+        groups[g]['angles'] = np.full(len(ids), 2.0, dtype=np.float16)
+    want = PO.collate_apsides(groups, attrs)
+    got = _collate(groups, attrs, {'save_final_counts': False}, None)
+    assert sorted(got) == sorted(want)
+    for g in want:
+        for d in want[g]:
+            assert_same(got[g][d], want[g][d], '%s/%s' % (g, d))
+
+
 def test_retro_counts_missing_id_raises():
     from orbitanalysis_amd.postprocessing import Apsides
     rng = np.random.default_rng(3)
