@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OA_ABI_VERSION 17
+#define OA_ABI_VERSION 18
 
 #define OA_OK 0
 #define OA_E_ARG (-1)       /* invalid argument / unsupported dtype plan */
@@ -410,6 +410,29 @@ int oa_part_unbucket(const oa_unbucket_args *args, void *stream);
 
 /* Scan the per-halo / per-item apsis counts and gather the records in output order. */
 int oa_compact(const oa_compact_args *args, void *stream);
+
+/* ---- multi-GPU output stage (sharding.ShardedEngine.fetch_async) ----------------
+ * Replaces the single writer's gather of every per-halo result (track_orbits.py:199-227,
+ * save_to_file :366-397): each rank stores its own apsis records at their final
+ * positions in one page-locked host buffer that every rank maps, over its own PCIe
+ * link, so rank 0 only waits and writes the file. */
+
+/* Page-lock `bytes` of host memory at `host` (e.g. a shared-memory mapping) and return
+ * the device-visible address of its first byte in *device_ptr. */
+int oa_host_register(void *host, int64_t bytes, void **device_ptr);
+int oa_host_unregister(void *host);
+
+/* When the work queued on `stream` so far has completed, store `value` to the host
+ * word `*host_addr` (a HIP host callback, release order): a rank tells the writing rank
+ * that its records are in place without its host waiting for them. */
+int oa_stream_set_flag(void *stream, int64_t *host_addr, int64_t value);
+
+/* out_ids[dst[i]] = ids[i] (id_bytes 4 or 8 each), out_ang[dst[i]] = ang[i] for
+ * i < n; dst values must lie in [0, cap) (a record outside is dropped and counted in
+ * *status).  The outputs may be host memory from oa_host_register (zero-copy stores). */
+int oa_place_records(const void *ids, const uint16_t *ang, const int64_t *dst, int64_t n,
+                     int32_t id_bytes, void *out_ids, uint16_t *out_ang, int64_t cap,
+                     int32_t *status, void *stream);
 
 /* ---- block helpers: the module-level functions on arbitrary arrays ---------------- */
 

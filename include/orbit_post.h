@@ -48,6 +48,8 @@ extern "C" {
 #define OA_POST_MISSING 1u      /* oa_retro_counts: an ID absent from the final slice  */
 #define OA_POST_SENTINEL 2u     /* oa_main_progenitors: an ID equals INT64_MIN           */
 #define OA_POST_OVERFLOW 4u     /* oa_main_progenitors: a block's halo tally overflowed  */
+#define OA_POST_BOUNDS 8u       /* oa_collate_step: a computed position fell outside its
+                                   halo's range (inconsistent workspace); nothing stored  */
 
 /* One round of collate_apsides for one snapshot: merge the kept apsis IDs of every
  * collated halo into its cumulative sorted-unique (key, count) state. */
@@ -58,7 +60,9 @@ typedef struct oa_collate_args {
     int32_t chunk_start;        /* round r: records [r*CHUNK, (r+1)*CHUNK) of each slice   */
     int32_t lds_keys;           /* sort slots: power of two in [64, CHUNK], >= every halo's
                                    record count this round                                */
-    int32_t reserved;
+    int32_t phases;             /* 0 or 3: the whole round; 1: k_collate_rank only (fills
+                                   the w_* workspace); 2: k_collate_offsets + k_collate_place
+                                   only, from the workspace a phases = 1 call filled        */
     const void *apsis_ids;      /* this snapshot's {peri|apo}center_IDs                    */
     const uint16_t *angles;     /* this snapshot's angles (float16 bits)                   */
     const uint8_t *keep_lut;    /* [65536]: 1 if (float16 value > angle_cut) in NumPy      */
@@ -79,6 +83,11 @@ typedef struct oa_collate_args {
     int64_t *new_off;           /* out [n_halos + 1] merged state offsets                  */
     uint64_t *new_keys;         /* out [n_old + n_new_cap] merged state (prefix used)      */
     int64_t *new_cnt;
+    int32_t *status;            /* OR-ed OA_POST_BOUNDS (NULL: not reported).  Every store
+                                   is checked against its halo's range first: a workspace
+                                   row outside [new_base, n_new_cap), or a merged position
+                                   outside [new_off[j], new_off[j + 1]), raises the bit and
+                                   is dropped instead of faulting                          */
 } oa_collate_args;
 
 int oa_collate_step(const oa_collate_args *args, void *stream);

@@ -13,7 +13,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.abspath(__file__))
 # ORBIT_HIP_LIB selects an alternative build (kernel variants for tuning sweeps)
 LIB_PATH = os.environ.get('ORBIT_HIP_LIB') or os.path.join(PKG, 'liborbit_hip.so')
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -82,12 +82,13 @@ class CompactArgs(ctypes.Structure):
 
 class CollateArgs(ctypes.Structure):
     _fields_ = [('n_halos', c_i32), ('in_kind', c_i32), ('key_signed', c_i32),
-                ('chunk_start', c_i32), ('lds_keys', c_i32), ('reserved', c_i32),
+                ('chunk_start', c_i32), ('lds_keys', c_i32), ('phases', c_i32),
                 ('apsis_ids', c_vp), ('angles', c_vp), ('keep_lut', c_vp), ('src_off', c_vp),
                 ('src_cnt', c_vp), ('new_base', c_vp), ('old_keys', c_vp), ('old_cnt', c_vp),
                 ('old_off', c_vp), ('n_old', c_i64), ('n_new_cap', c_i64), ('w_keys', c_vp),
                 ('w_cnt', c_vp), ('w_lb', c_vp), ('w_fp', c_vp), ('w_ulen', c_vp),
-                ('w_found', c_vp), ('new_off', c_vp), ('new_keys', c_vp), ('new_cnt', c_vp)]
+                ('w_found', c_vp), ('new_off', c_vp), ('new_keys', c_vp), ('new_cnt', c_vp),
+                ('status', c_vp)]
 
 
 class CentralArgs(ctypes.Structure):
@@ -110,7 +111,7 @@ class MainProgArgs(ctypes.Structure):
 ID_KIND = {np.dtype('int64'): 0, np.dtype('uint64'): 1, np.dtype('int32'): 2, np.dtype('uint32'): 3}
 COLLATE_CHUNK = 4096
 CENTRAL_MAX_N = 4096
-POST_MISSING, POST_SENTINEL, POST_OVERFLOW = 1, 2, 4
+POST_MISSING, POST_SENTINEL, POST_OVERFLOW, POST_BOUNDS = 1, 2, 4, 8
 
 # every symbol include/orbit_hip.h and include/orbit_post.h declare: name -> (restype, argtypes)
 SYMBOLS = {
@@ -136,6 +137,11 @@ SYMBOLS = {
     'oa_compare_pairs': (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,
                                         c_vp, c_vp, c_vp]),
     'oa_angle_add': (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    'oa_host_register': (ctypes.c_int, [c_vp, c_i64, ctypes.POINTER(c_vp)]),
+    'oa_host_unregister': (ctypes.c_int, [c_vp]),
+    'oa_stream_set_flag': (ctypes.c_int, [c_vp, c_vp, c_i64]),
+    'oa_place_records': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_vp,
+                                        c_vp]),
     # orbit_post.h
     'oa_post_struct_size': (c_i64, [c_i32]),
     'oa_collate_step': (ctypes.c_int, [ctypes.POINTER(CollateArgs), c_vp]),

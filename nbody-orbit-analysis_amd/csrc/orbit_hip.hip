@@ -118,6 +118,11 @@ template <typename T> __device__ __forceinline__ T lds_nt(const T *p) {
 #ifndef OA_STAMPS
 #define OA_STAMPS 0
 #endif
+#if OA_STAMPS && OA_TU != 0
+// every unit of the split build would hold its own copy of the stamp buffers, and
+// oa_debug_stamps (unit -1) would read an empty one: stamps builds are one unit
+#error "OA_STAMPS needs the single-unit build (OA_TU=0, tools/variants.sh)"
+#endif
 #if OA_STAMPS
 // diagnostic build only: per-work-group s_memrealtime (100 MHz) at the 8 phase
 // boundaries plus, per wave, the ends of its phase-1, 2a and 2b loops (WSTAMP 0/1/2)
@@ -2662,6 +2667,40 @@ int oa_step_plan_f64(const oa_step_args &a, hipStream_t st) { return launch_step
 #endif
 
 #if OA_TU <= 0
+// ------------------------------------------------------------------ sharded output
+// One rank's apsis records to their final positions in the output every rank maps
+// (sharding.ShardedEngine.fetch_async).  The destination is page-locked host memory:
+// a rank's records of one halo are one run of consecutive positions, so a wave's stores
+// cover consecutive bytes and cross PCIe as full lines.  Four records per thread, every
+// load issued before the stores.
+template <typename ID>
+__global__ __launch_bounds__(256) void k_place_records(const ID *ids, const uint16_t *ang,
+                                                       const int64_t *dst, int64_t n,
+                                                       ID *out_ids, uint16_t *out_ang,
+                                                       int64_t cap, int32_t *status) {
+    constexpr int U = 4;
+    const int64_t i0 = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
+    ID v[U];
+    uint16_t g[U];
+    int64_t d[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + u * 256, ic = i < n ? i : n - 1;
+        v[u] = __builtin_nontemporal_load(ids + ic);
+        g[u] = __builtin_nontemporal_load(ang + ic);
+        d[u] = __builtin_nontemporal_load(dst + ic);
+    }
+    bool bad = false;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (i0 + u * 256 >= n) break;
+        if (d[u] < 0 || d[u] >= cap) { bad = true; continue; }
+        out_ids[d[u]] = v[u];
+        out_ang[d[u]] = g[u];
+    }
+    if (bad && status) atomicAdd(status, 1);
+}
+
 // Error channel shared with the other units (orbit_post.hip, the step-plan units):
 // nullptr clears the message, anything else becomes oa_last_error().
 void oa_internal_error(const char *msg) {
@@ -2756,6 +2795,68 @@ int64_t oa_plan_items(const int64_t *cur_off, const int64_t *cur_cnt, const int6
     }
     *scratch = sc;
     return n;
+}
+
+int oa_host_register(void *host, int64_t bytes, void **device_ptr) {
+    g_err[0] = 0;
+    if (!host || bytes <= 0 || !device_ptr) return fail(OA_E_ARG, "oa_host_register: bad arguments");
+    hipError_t e = hipHostRegister(host, (size_t)bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+    if (e != hipSuccess) return fail(OA_E_DEVICE, "hipHostRegister: %s", hipGetErrorString(e));
+    e = hipHostGetDevicePointer(device_ptr, host, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(host);
+        return fail(OA_E_DEVICE, "hipHostGetDevicePointer: %s", hipGetErrorString(e));
+    }
+    return OA_OK;
+}
+
+int oa_host_unregister(void *host) {
+    g_err[0] = 0;
+    if (!host) return fail(OA_E_ARG, "oa_host_unregister: null");
+    const hipError_t e = hipHostUnregister(host);
+    if (e != hipSuccess) return fail(OA_E_DEVICE, "hipHostUnregister: %s", hipGetErrorString(e));
+    return OA_OK;
+}
+
+namespace {
+struct HostFlag { int64_t *addr; int64_t value; };
+void host_flag_cb(void *p) {
+    HostFlag *f = static_cast<HostFlag *>(p);
+    __atomic_store_n(f->addr, f->value, __ATOMIC_RELEASE);
+    delete f;
+}
+}  // namespace
+
+int oa_stream_set_flag(void *stream, int64_t *host_addr, int64_t value) {
+    g_err[0] = 0;
+    if (!host_addr) return fail(OA_E_ARG, "oa_stream_set_flag: null address");
+    HostFlag *f = new HostFlag{host_addr, value};
+    const hipError_t e = hipLaunchHostFunc(reinterpret_cast<hipStream_t>(stream), host_flag_cb, f);
+    if (e != hipSuccess) {
+        delete f;
+        return fail(OA_E_LAUNCH, "hipLaunchHostFunc: %s", hipGetErrorString(e));
+    }
+    return OA_OK;
+}
+
+int oa_place_records(const void *ids, const uint16_t *ang, const int64_t *dst, int64_t n,
+                     int32_t id_bytes, void *out_ids, uint16_t *out_ang, int64_t cap,
+                     int32_t *status, void *stream) {
+    g_err[0] = 0;
+    if (n <= 0) return OA_OK;
+    if (!ids || !ang || !dst || !out_ids || !out_ang || cap < 0 || (id_bytes != 4 && id_bytes != 8))
+        return fail(OA_E_ARG, "oa_place_records: bad arguments");
+    const unsigned grid = (unsigned)((n + 1023) / 1024);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (id_bytes == 8)
+        hipLaunchKernelGGL(k_place_records<uint64_t>, dim3(grid), dim3(256), 0, st,
+                           static_cast<const uint64_t *>(ids), ang, dst, n,
+                           static_cast<uint64_t *>(out_ids), out_ang, cap, status);
+    else
+        hipLaunchKernelGGL(k_place_records<uint32_t>, dim3(grid), dim3(256), 0, st,
+                           static_cast<const uint32_t *>(ids), ang, dst, n,
+                           static_cast<uint32_t *>(out_ids), out_ang, cap, status);
+    return check_launch("k_place_records");
 }
 
 int oa_build_halos(const int64_t *cur_off, const int64_t *cur_cnt, const int64_t *prev_off,

@@ -277,8 +277,15 @@ __global__ __launch_bounds__(CT) void k_collate_rank(const oa_collate_args a) {
     const int64_t ob = a.old_off[j], on = a.old_off[j + 1] - ob;
     const int64_t rem = a.src_cnt[j] - a.chunk_start;
     const int nraw = rem <= 0 ? 0 : (rem < CH ? (int)rem : CH);
-    if (nraw == 0) {                                         // nothing new: the list is kept
-        if (threadIdx.x == 0) { a.w_ulen[j] = 0; a.w_found[j] = 0; }
+    const int64_t base = a.new_base[j];
+    // the halo's workspace rows [base, base + nraw) must lie in [0, n_new_cap): the w_*
+    // stores below are then in bounds (u <= m <= nraw); otherwise report, store nothing
+    const bool bad = nraw > 0 && (base < 0 || base + nraw > a.n_new_cap || nraw > a.lds_keys);
+    if (nraw == 0 || bad) {                                  // nothing new: the list is kept
+        if (threadIdx.x == 0) {
+            a.w_ulen[j] = 0; a.w_found[j] = 0;
+            if (bad && a.status) atomicOr(a.status, (int32_t)OA_POST_BOUNDS);
+        }
         return;
     }
     // the first old-key tile: loads issued now, staged after the sort
@@ -345,7 +352,6 @@ __global__ __launch_bounds__(CT) void k_collate_rank(const oa_collate_args a) {
     }
     RSTAMP(2);
     int u;
-    const int64_t base = a.new_base[j];
     {   // run heads: thread t owns positions [t*E, t*E + E)
         const int E = (m + CT - 1) / CT;
         const int lo = threadIdx.x * E, hi = min(lo + E, m);
@@ -456,7 +462,16 @@ __global__ __launch_bounds__(CT) void k_collate_place(const oa_collate_args a) {
     const int u = a.w_ulen[j];
     const int64_t base = a.new_base[j];
     const int64_t ob = a.old_off[j], on = a.old_off[j + 1] - ob;
-    const int64_t no = a.new_off[j];
+    const int64_t no = a.new_off[j], ne = a.new_off[j + 1];
+    // every store below goes to [no, ne) of the merged state (and the workspace rows read
+    // to [base, base + u) of [0, n_new_cap)): a position outside it -- an inconsistent
+    // workspace -- raises OA_POST_BOUNDS and is dropped
+    if (u < 0 || u > a.lds_keys || (u > 0 && (base < 0 || base + u > a.n_new_cap)) ||
+        ne - no < on || ne > a.n_old + a.n_new_cap) {
+        if (threadIdx.x == 0 && a.status) atomicOr(a.status, (int32_t)OA_POST_BOUNDS);
+        return;
+    }
+    bool oob = false;
     for (int q0 = 0; q0 < u; q0 += CL_U * CT) {
         uint64_t k[CL_U];
         int f[CL_U], c[CL_U];
@@ -492,6 +507,7 @@ __global__ __launch_bounds__(CT) void k_collate_place(const oa_collate_args a) {
             const int L = lower_rank(nk, u, key[e]);
             const bool eq = L < u && nk[L] == key[e];
             const int64_t pos = no + i + L - fp[L];
+            if (pos < no || pos >= ne) { oob = true; continue; }
             // plain stores: the positions shift by one at every inserted key, so a wave's
             // stores straddle lines, which L2 merges (non-temporal: 1.6x the time)
             a.new_keys[pos] = key[e];
@@ -501,9 +517,11 @@ __global__ __launch_bounds__(CT) void k_collate_place(const oa_collate_args a) {
     for (int q = threadIdx.x; q < u; q += CT) {
         if (fp[q + 1] != fp[q]) continue;                    // already in the old list
         const int64_t pos = no + a.w_lb[base + q] + (q - fp[q]);
+        if (pos < no || pos >= ne) { oob = true; continue; }
         a.new_keys[pos] = nk[q];
         a.new_cnt[pos] = nc[q];
     }
+    if (oob && a.status) atomicOr(a.status, (int32_t)OA_POST_BOUNDS);
 }
 
 template <int KIND>
@@ -1210,8 +1228,13 @@ int oa_collate_step(const oa_collate_args *args, void *stream) {
         hipFuncSetAttribute(reinterpret_cast<const void *>(k_collate_place),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds3) != hipSuccess)
         return fail(OA_E_LAUNCH, "oa_collate_step: hipFuncSetAttribute");
-    hipLaunchKernelGGL(krank, dim3(a.n_halos), dim3(CT), (size_t)lds1, st, a);
-    if (int rc = check_launch("k_collate_rank")) return rc;
+    if (a.phases < 0 || a.phases > 3) return fail(OA_E_ARG, "oa_collate_step: phases must be 0-3");
+    const int ph = a.phases == 0 ? 3 : a.phases;
+    if (ph & 1) {
+        hipLaunchKernelGGL(krank, dim3(a.n_halos), dim3(CT), (size_t)lds1, st, a);
+        if (int rc = check_launch("k_collate_rank")) return rc;
+    }
+    if (!(ph & 2)) return OA_OK;
     hipLaunchKernelGGL(k_collate_offsets, dim3(1), dim3(1024), 0, st, a);
     if (int rc = check_launch("k_collate_offsets")) return rc;
     if (a.n_old + a.n_new_cap > 0) {

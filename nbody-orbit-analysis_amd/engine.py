@@ -1191,8 +1191,9 @@ class OrbitEngine:
         return a ``PendingFetch`` whose ``wait()`` gives (offsets, ids, angles) as
         ``fetch`` does.  The copies overlap whatever the compute stream runs next (the
         next snapshots' kernels write the other workspaces), so the records' transfer is
-        off the per-snapshot critical path.  The result's workspace must not be reused
-        before ``wait()``: ``step`` alternates two."""
+        off the per-snapshot critical path.  The workspaces rotate through ``N_WS``, so a
+        result's workspace is reused ``N_WS`` steps later, and that launch waits on the
+        GPU for this copy (``copy_done``)."""
         self.settle(res)
         res.check_fresh()
         dev = self.device

@@ -1,0 +1,334 @@
+"""Multi-GPU output stage: every rank stores its own apsis records straight into one
+page-locked host buffer that all ranks map (the reference's single
+writer is track_orbits.py:189-227 with save_to_file :366-397).
+
+Before this stage, each rank's records were gathered to rank 0's GPU and crossed PCIe
+over rank 0's link alone: at configs[3] on 8 GPUs, ~65 MB per snapshot through one
+link (~1.2 ms) against ~0.2 ms of kernel per rank.  Here:
+
+1. the (world, halo slot) record-count matrix is all-gathered (8 B per slot per rank);
+2. every rank computes its own records' final positions: with a presharded reader a
+   halo's records from rank r follow those of ranks < r (a count scan); with stripes,
+   the ranks' records of a halo interleave by global previous row, so each rank marks
+   its rows in a bitmap of the previous snapshot, one all-reduce (disjoint bits, so a
+   byte sum is an OR) gives every rank every row's rank among the records;
+3. each rank's placement kernel (``oa_place_records``) stores its records at those
+   positions through the device address of the shared mapping (zero-copy, over its own
+   PCIe link), and a host callback on the rank's stream publishes the fetch's epoch in
+   the buffer's header when the stores are done (``oa_stream_set_flag``);
+4. rank 0 waits for every rank's epoch and hands the buffer to the savefile writer.
+
+Buffers are POSIX shared-memory files (``/dev/shm``) in a small pool of slots chosen by
+rank 0 (a slot stays busy while the arrays it handed out are alive; a new or larger one
+is created when none fits) and announced with one broadcast per fetch.  Each slot is
+unlinked once every rank has mapped it.  CPU ranks (gloo tests) run the same protocol
+with numpy stores.
+"""
+import atexit
+import mmap
+import os
+import secrets
+import time
+import weakref
+
+import numpy as np
+import torch
+
+HDR = 64                          # header bytes per rank (one cache line each)
+_POP8 = np.array([bin(i).count('1') for i in range(256)], dtype=np.int64)
+
+
+def _shm_dir():
+    return '/dev/shm' if os.path.isdir('/dev/shm') else os.environ.get('TMPDIR', '/tmp')
+
+
+def _pow2(n, lo=1 << 20):
+    n = max(int(n), lo)
+    return 1 << (n - 1).bit_length()
+
+
+class _Slot:
+    """One shared-memory segment: [world x HDR header][cap IDs][cap f16 angles]."""
+
+    def __init__(self, path, world, cap, ib, create):
+        self.path, self.cap, self.ib = path, int(cap), int(ib)
+        self.hdr_bytes = -(-world * HDR // 4096) * 4096
+        ids_bytes = -(-self.cap * self.ib // 4096) * 4096
+        self.nbytes = self.hdr_bytes + ids_bytes + -(-self.cap * 2 // 4096) * 4096
+        flags = os.O_RDWR | (os.O_CREAT | os.O_EXCL if create else 0)
+        fd = os.open(path, flags, 0o600)
+        try:
+            if create:
+                os.ftruncate(fd, self.nbytes)
+            self.mm = mmap.mmap(fd, self.nbytes, mmap.MAP_SHARED,
+                                mmap.PROT_READ | mmap.PROT_WRITE)
+        finally:
+            os.close(fd)
+        self.linked = create              # rank 0 unlinks it once every rank mapped it
+        buf = np.frombuffer(self.mm, dtype=np.uint8)
+        self.base = buf.ctypes.data
+        self.hdr = buf[:self.hdr_bytes].view(np.int64)
+        o = self.hdr_bytes
+        self.ids = buf[o:o + self.cap * self.ib].view(np.int64 if self.ib == 8 else np.int32)
+        self.ang_off = o + ids_bytes
+        self.ang = buf[self.ang_off:self.ang_off + 2 * self.cap].view(np.int16)
+        self.ids_off = o
+        self.dev = None                   # device address of the mapping (registered)
+        self.busy = 0                     # rank 0: arrays handed out and still alive
+
+    def flag(self, rank):
+        return self.hdr[rank * (HDR // 8):rank * (HDR // 8) + 1]
+
+    def register(self, lib):
+        if self.dev is None:
+            import ctypes
+            from . import _native as N
+            p = ctypes.c_void_p()
+            N.check(lib.oa_host_register(ctypes.c_void_p(self.base), self.nbytes,
+                                         ctypes.byref(p)), 'oa_host_register')
+            self.dev = p.value
+        return self.dev
+
+    def release(self, lib):
+        if self.dev is not None and lib is not None:
+            import ctypes
+            lib.oa_host_unregister(ctypes.c_void_p(self.base))
+            self.dev = None
+        if self.linked:
+            try:
+                os.unlink(self.path)
+            except OSError:
+                pass
+            self.linked = False
+
+
+class StageFetch:
+    """One fetch's records on their way into the shared buffer (``ShardedEngine``'s
+    fetch_async result).  ``done.query()`` (the error path's poll) is true once this
+    rank's stores are done and, on rank 0, every rank's epoch is in the header."""
+
+    def __init__(self, stage, slot, epoch, event, off, total, ids_dtype, root, moved):
+        self.stage, self.slot, self.epoch, self.event = stage, slot, epoch, event
+        self.off, self.total, self.ids_dtype, self.root = off, total, ids_dtype, root
+        self.moved = moved                # bytes this rank stored into the buffer
+        self.done = self
+
+    def _mine(self):
+        return self.event is None or self.event.query()
+
+    def query(self):
+        if not self._mine():
+            return False
+        if not self.root:
+            return True
+        return all(int(self.slot.flag(r)[0]) == self.epoch for r in range(self.stage.world))
+
+    def wait(self):
+        from .engine import ids_as
+        dt = np.dtype(self.ids_dtype)
+        if self.event is not None:
+            self.event.synchronize()
+        if self.stage.status is not None and int(self.stage.status.item()):
+            raise RuntimeError('oa_place_records: %d records fell outside the output'
+                               % int(self.stage.status.item()))
+        if not self.root:
+            return np.zeros(len(self.off), np.int64), np.zeros(0, dt), np.zeros(0, np.float16)
+        t_end = time.time() + self.stage.timeout
+        while not self.query():
+            if time.time() > t_end:
+                raise RuntimeError('sharded records: a rank did not store its records within '
+                                   '%.0f s' % self.stage.timeout)
+            time.sleep(2e-5)
+        slot = self.slot
+        if slot.linked:                   # every rank has it mapped now
+            self.stage._unlink(slot)
+        n = self.total
+        slot.busy -= 1                    # in flight since _choose
+        if n == 0:
+            return self.off, np.zeros(0, dt), np.zeros(0, np.float16)
+        # the arrays are exported by two ctypes holders over the mapping: every array or
+        # view derived from them keeps its holder alive, and the slot is reused only once
+        # both holders are gone (the savefile has dropped the records)
+        import ctypes
+        hi = (ctypes.c_char * (n * slot.ib)).from_buffer(slot.mm, slot.ids_off)
+        ha = (ctypes.c_char * (2 * n)).from_buffer(slot.mm, slot.ang_off)
+        slot.busy += 2
+        for h in (hi, ha):
+            weakref.finalize(h, self.stage._free, slot)
+        ids_v = np.frombuffer(hi, dtype=slot.ids.dtype)
+        ang_v = np.frombuffer(ha, dtype=np.float16)
+        return self.off, ids_as(ids_v, dt), ang_v
+
+
+class SharedRecordStage:
+    """The shared output buffers of one ``ShardedEngine`` (see module docstring)."""
+
+    def __init__(self, group, rank, world, root=0, timeout=None):
+        self.group, self.rank, self.world, self.root = group, rank, world, root
+        self.slots = {}                   # slot index -> _Slot (this rank's mappings)
+        self.gens = {}                    # slot index -> generation mapped here
+        self.epoch = 0
+        self.name = None                  # (pid, nonce) of rank 0's files
+        self.status = None                # device word: records outside the output
+        self.timeout = float(timeout if timeout is not None else
+                             os.environ.get('ORBIT_FETCH_TIMEOUT', 600))
+        self.lib = None
+        atexit.register(self.close)
+
+    # ------------------------------------------------------------ slots (rank 0 decides)
+    def _path(self, slot, gen):
+        pid, nonce = self.name
+        return os.path.join(_shm_dir(), 'oa_rec_%d_%d_%d_%d' % (pid, nonce, slot, gen))
+
+    def _free(self, slot):
+        slot.busy -= 1
+
+    def _unlink(self, slot):
+        try:
+            os.unlink(slot.path)
+        except OSError:
+            pass
+        slot.linked = False
+
+    def _choose(self, total, ib):
+        """Rank 0: (slot, generation, capacity) for this fetch; creates the file.  The
+        slot is busy from here until this fetch's arrays are dropped (a fetch in flight
+        counts once, each handed-out array once)."""
+        fit = [k for k, s in self.slots.items() if s.busy == 0 and s.ib == ib and s.cap >= total]
+        if fit:
+            k = min(fit, key=lambda k: self.slots[k].cap)
+        else:
+            free = [k for k, s in self.slots.items() if s.busy == 0]
+            k = free[0] if free else len(self.slots)
+            self._map(k, self.gens.get(k, -1) + 1, _pow2(total), ib, create=True)
+        self.slots[k].busy += 1
+        return k, self.gens[k], self.slots[k].cap
+
+    def _map(self, k, gen, cap, ib, create):
+        old = self.slots.get(k)
+        if old is not None:
+            old.release(self.lib)
+        self.slots[k] = _Slot(self._path(k, gen), self.world, cap, ib, create)
+        self.gens[k] = gen
+
+    def _agree(self, total, ib, comm_dev):
+        """One broadcast from rank 0: the slot this fetch stores into (opened here)."""
+        import torch.distributed as dist
+        if self.rank == self.root:
+            if self.name is None:
+                self.name = (os.getpid(), secrets.randbits(31))
+            k, gen, cap = self._choose(total, ib)
+            msg = [k, gen, cap, ib, self.name[0], self.name[1]]
+        else:
+            msg = [0] * 6
+        t = torch.tensor(msg, dtype=torch.int64).to(comm_dev)
+        src = dist.get_global_rank(self.group, self.root) if self.group is not None else self.root
+        dist.broadcast(t, src=src, group=self.group)
+        k, gen, cap, ib, pid, nonce = (int(x) for x in t.cpu())
+        if self.rank != self.root:
+            self.name = (pid, nonce)
+            if self.gens.get(k) != gen:
+                self._map(k, gen, cap, ib, create=False)
+        return self.slots[k]
+
+    # ------------------------------------------------------------ one fetch
+    def fetch(self, lib, side, done, offs, a_ids, a_ang, total_local, C_local, n_slots,
+              ids_dtype, rows=None, n_rows=None, comm_dev=None, profile=None):
+        """Place this rank's ``total_local`` records (device tensors ``a_ids``,
+        ``a_ang``; per-slot counts ``C_local``) into the shared buffer.  ``rows``: the
+        records' global previous rows (stripe layout), else presharded.  Returns a
+        ``StageFetch``."""
+        import torch.distributed as dist
+        self.lib = lib
+        self.epoch += 1
+        epoch = self.epoch
+        dev = a_ids.device
+        S = n_slots
+        on_gpu = dev.type == 'cuda'
+        # 1. the count matrix on every rank (one all-gather)
+        cl = C_local.to(torch.int64).reshape(S).to(comm_dev)
+        allc = torch.empty(self.world * S, dtype=torch.int64, device=comm_dev)
+        dist.all_gather_into_tensor(allc, cl.contiguous(), group=self.group)
+        C = allc.view(self.world, S)
+        Ch = C.cpu().numpy()
+        tot_slot = Ch.sum(0)
+        total = int(tot_slot.sum())
+        off = np.zeros(S + 1, np.int64)
+        np.cumsum(tot_slot, out=off[1:])
+        ib = a_ids.element_size()
+        # 2. the slot (rank 0 chooses, one broadcast)
+        slot = self._agree(total, ib, comm_dev)
+        n = int(total_local)
+        t0 = time.perf_counter() if profile is not None else 0.0
+        # 3. this rank's records' positions
+        if rows is None:
+            Cd = C.to(dev)
+            before = (torch.cumsum(Cd, 0) - Cd)[self.rank]
+            loc = Cd[self.rank]
+            D = torch.from_numpy(off[:S]).to(dev) + before - (torch.cumsum(loc, 0) - loc)
+            dst = torch.arange(n, dtype=torch.int64, device=dev) + \
+                torch.repeat_interleave(D, loc, output_size=n) if n else \
+                torch.zeros(0, dtype=torch.int64, device=dev)
+        else:
+            dst = self._rank_by_row(rows[:n].to(torch.int64), int(n_rows), comm_dev).to(dev)
+        # 4. the stores, and this rank's epoch in the header when they are done
+        if on_gpu:
+            import ctypes
+            if self.status is None:
+                self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+            base = slot.register(lib)
+            st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            from . import _native as N
+            N.check(lib.oa_place_records(
+                ctypes.c_void_p(a_ids.data_ptr()), ctypes.c_void_p(a_ang.data_ptr()),
+                ctypes.c_void_p(dst.data_ptr()), n, ib,
+                ctypes.c_void_p(base + slot.ids_off), ctypes.c_void_p(base + slot.ang_off),
+                slot.cap, ctypes.c_void_p(self.status.data_ptr()), st), 'oa_place_records')
+            flag = slot.flag(self.rank)
+            N.check(lib.oa_stream_set_flag(st, ctypes.c_void_p(flag.ctypes.data), epoch),
+                    'oa_stream_set_flag')
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+        else:
+            if n:
+                d = dst.numpy()
+                if d.min() < 0 or d.max() >= slot.cap:
+                    raise RuntimeError('sharded records: positions outside the output')
+                slot.ids[d] = a_ids[:n].numpy().view(slot.ids.dtype)
+                slot.ang[d] = a_ang[:n].numpy().view(np.int16)
+            slot.flag(self.rank)[0] = epoch
+            ev = None
+        if profile is not None:
+            if on_gpu:
+                torch.cuda.current_stream(dev).synchronize()
+            profile.update(records=total, own_records=n, place_ms=(time.perf_counter() - t0) * 1e3,
+                           bytes_moved=n * (ib + 2), layout='stripes' if rows is not None
+                           else 'presharded')
+        return StageFetch(self, slot, epoch, ev, off, total, ids_dtype,
+                          self.rank == self.root, n * (ib + 2))
+
+    def _rank_by_row(self, rows, n_rows, comm_dev):
+        """Every record's position among all ranks' records ordered by global previous
+        row: bits of the rows each rank holds, OR-ed over the ranks by one all-reduce
+        (the ranks' rows are disjoint: a byte sum is the OR), then prefix popcounts."""
+        import torch.distributed as dist
+        nb = max((n_rows + 7) // 8, 1)
+        cpu = torch.device(comm_dev).type == 'cpu'
+        r = rows.to(comm_dev)
+        bits = torch.zeros(nb, dtype=torch.int32, device=comm_dev)
+        bits.index_add_(0, r >> 3, (1 << (r & 7)).to(torch.int32))
+        b = bits if cpu else bits.to(torch.uint8)
+        dist.all_reduce(b, op=dist.ReduceOp.SUM, group=self.group)
+        lut = torch.from_numpy(_POP8).to(comm_dev)
+        bl = b.long()
+        pc = lut[bl]
+        pre = torch.cumsum(pc, 0) - pc
+        byte = r >> 3
+        return pre[byte] + lut[bl[byte] & ((1 << (r & 7)) - 1)]
+
+    def close(self):
+        for s in self.slots.values():
+            try:
+                s.release(self.lib)
+            except Exception:
+                pass

@@ -195,6 +195,7 @@ class _CollateState:
         src_off_d = _dev(src_off, dev)
         src_cnt_d = _dev(src_cnt, dev)
         st = torch.cuda.current_stream(dev).cuda_stream
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
         for r in range(rounds):
             chunk = np.clip(src_cnt - r * ch, 0, ch).astype(np.int64)
             # LDS sized to this round's largest chunk (several work-groups share a CU)
@@ -221,7 +222,7 @@ class _CollateState:
                 old_off=_ptr(self.off), n_old=self.total, n_new_cap=cap, w_keys=_ptr(w_keys),
                 w_cnt=_ptr(w_cnt), w_lb=_ptr(w_lb), w_fp=_ptr(w_fp), w_ulen=_ptr(w_ulen),
                 w_found=_ptr(w_found), new_off=_ptr(new_off), new_keys=_ptr(new_keys),
-                new_cnt=_ptr(new_cnt))
+                new_cnt=_ptr(new_cnt), status=_ptr(status))
             if events is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -232,6 +233,9 @@ class _CollateState:
             self.off, self.keys, self.cnt = new_off, new_keys, new_cnt
             self.off_h = new_off.cpu().numpy()
             self.total = int(self.off_h[-1])
+        if rounds and int(status.item()) & N.POST_BOUNDS:
+            raise N.NativeError('oa_collate_step: a merged position fell outside its halo '
+                                '(OA_POST_BOUNDS): inconsistent collation workspace')
 
     def lengths(self):
         return np.diff(self.off_h)

@@ -216,6 +216,29 @@ def _comm_device():
 
 # gloo moves neither 16-bit integers nor bool: they travel widened
 _WIDEN = {torch.int16: torch.int32, torch.bool: torch.uint8, torch.float16: torch.float32}
+# the dtypes torch's NCCL backend maps to an RCCL type (ProcessGroupNCCL's ncclDataType
+# table: no int16 / uint16 / uint32 / uint64); any other dtype travels as its bytes
+NCCL_WIRE = frozenset({torch.uint8, torch.int8, torch.int32, torch.int64, torch.float16,
+                       torch.bfloat16, torch.float32, torch.float64, torch.bool})
+
+
+def to_wire(x, cpu_comm):
+    """``x`` (rows along dim 0) in a dtype the backend moves: widened for gloo
+    (``cpu_comm``), bit-viewed as (rows, bytes) uint8 for RCCL when torch's NCCL table
+    has no type for it.  Returns (wire tensor, bit-viewed); ``from_wire`` undoes it."""
+    dt = x.dtype
+    if cpu_comm:
+        return x.to(_WIDEN.get(dt, dt)), False
+    if dt in NCCL_WIRE:
+        return x, False
+    return x.contiguous().reshape(x.shape[0], -1).view(torch.uint8), True
+
+
+def from_wire(y, dt, tail, bitview):
+    """The rows ``to_wire`` sent, from the received wire rows ``y`` (row shape ``tail``)."""
+    if bitview:
+        return y.view(dt).reshape((y.shape[0],) + tuple(tail))
+    return y.to(dt)
 
 
 class RowExchange:
@@ -249,12 +272,11 @@ class RowExchange:
             return t
         home = t.device
         x = t.contiguous()
-        dt = x.dtype
-        wire = _WIDEN.get(dt, dt) if self.dev.type == 'cpu' else dt
-        x = x.to(self.dev).to(wire)
-        out = torch.empty((self.n_recv,) + tuple(x.shape[1:]), dtype=wire, device=self.dev)
+        dt, tail = x.dtype, tuple(x.shape[1:])
+        x, bv = to_wire(x.to(self.dev), self.dev.type == 'cpu')
+        out = torch.empty((self.n_recv,) + tuple(x.shape[1:]), dtype=x.dtype, device=self.dev)
         dist.all_to_all_single(out, x, self.recv, self.send, group=self.group)
-        return out.to(dt).to(home)
+        return from_wire(out, dt, tail, bv).to(home)
 
 
 def _exchange_rows(t, group=None):
@@ -601,6 +623,7 @@ class ShardedEngine:
         self.prev: Optional[ShardedPrep] = None
         self._pending: Optional[ShardedResult] = None   # a deferred step not yet settled
         self._side = None                               # stream of the records' gathers
+        self._stage = None                              # shared host output (world > 1)
         # rank 0's record placement timed (synchronised) into fetch_stats (rehearsals)
         self.profile_fetch = False
         self.fetch_stats = None
@@ -786,16 +809,19 @@ class ShardedEngine:
 
     # ---------------------------------------------------------------- outputs
     def fetch_async(self, res, ids_dtype):
-        """Start gathering a step's records to rank 0 (the only writer) and their D2H
-        there; ``wait()`` returns (offsets, IDs, f16 angles) in the reference's order
-        (track_orbits.py:199-227, 315-316).  A record travels as its ID and f16 angle
-        (10 B with int64 IDs) plus, in the stripe layout, its 4-byte global previous row;
-        rank 0 places the rank-ordered runs by a per-(rank, slot) count scan (presharded)
-        or a counting pass over the previous rows (stripes), never a sort.  The gather
-        runs on a side stream behind the step's own kernels only, so it overlaps whatever
-        the compute stream runs next (the next snapshot's step); the workspace holding
-        the records is not reused before it.  Ranks other than 0 (which write nothing)
-        get zero offsets and no records."""
+        """Start moving a step's records to the host for rank 0 (the only writer);
+        ``wait()`` returns (offsets, IDs, f16 angles) in the reference's order
+        (track_orbits.py:199-227, 315-316) on rank 0 and zero offsets elsewhere.
+
+        World > 1 (``host_share.SharedRecordStage``): every rank computes its own
+        records' final positions from the all-gathered (rank, halo slot) counts --
+        a count scan (presharded) or a bitmap rank over the global previous rows
+        (stripes) -- and stores them into one page-locked host buffer that every rank
+        maps, over its own PCIe link; rank 0 moves only its own records and waits for the
+        others' epochs.  World 1: one D2H into reused page-locked blocks.  Both run on a
+        side stream behind the step's own kernels only, so they overlap whatever the
+        compute stream runs next (the next snapshot's step); the workspace holding the
+        records is not reused before them."""
         self.settle(res)
         offs, a_ids, a_ang, a_pos = res.records
         lp = res.lp
@@ -811,6 +837,34 @@ class ShardedEngine:
         S = res.n_slots
         root = self.rank == self.ROOT
         prof = self.profile_fetch
+        if self.world > 1:
+            from .host_share import SharedRecordStage
+            if self._stage is None:
+                self._stage = SharedRecordStage(self.group, self.rank, self.world, self.ROOT)
+            with ctx:
+                if side is not None and done is not None:
+                    side.wait_event(done)
+                total = self.local.total(lp) if hasattr(self.local, 'total') else int(offs[-1])
+                cnt = (offs[1:S + 1] - offs[:S]).to(torch.int64)
+                rows = n_rows = None
+                if not self.presharded:
+                    pp = res.prev_prep
+                    rows = pp.sel[a_pos[:total].to(pp.sel.device).long()]
+                    n_rows = int(pp.n_global)
+                stats = {} if prof else None
+                lib = getattr(getattr(self.local, 'engine', None), 'lib', None)
+                f = self._stage.fetch(lib, side, done, offs, a_ids, a_ang, total, cnt, S,
+                                      ids_dtype, rows=rows, n_rows=n_rows,
+                                      comm_dev=_comm_device(), profile=stats)
+                if prof:
+                    stats['bytes_per_record'] = a_ids.element_size() + 2
+                    self.fetch_stats = stats
+                if side is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    if hasattr(self.local, 'records_consumed'):
+                        self.local.records_consumed(lp, ev)
+            return f
         with ctx:
             if side is not None and done is not None:
                 side.wait_event(done)
@@ -845,9 +899,16 @@ class ShardedEngine:
                     out_ids, out_ang = ids_r, ang_r
                 t1 = _sync_time(prof)
                 pin = out_ids.device.type == 'cuda'
-                h_off = torch.empty(S + 1, dtype=torch.int64, pin_memory=pin)
-                h_ids = torch.empty(n, dtype=out_ids.dtype, pin_memory=pin)
-                h_ang = torch.empty(n, dtype=torch.int16, pin_memory=pin)
+                if pin:
+                    # power-of-two page-locked blocks reused across snapshots (engine)
+                    from .engine import _pinned
+                    h_off = _pinned(S + 1, torch.int64)
+                    h_ids = _pinned(n, out_ids.dtype)
+                    h_ang = _pinned(n, torch.int16)
+                else:
+                    h_off = torch.empty(S + 1, dtype=torch.int64)
+                    h_ids = torch.empty(n, dtype=out_ids.dtype)
+                    h_ang = torch.empty(n, dtype=torch.int16)
                 h_off.copy_(off, non_blocking=pin)
                 h_ids.copy_(out_ids, non_blocking=pin)
                 h_ang.copy_(out_ang, non_blocking=pin)

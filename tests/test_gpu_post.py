@@ -99,9 +99,10 @@ def test_collate_random_vs_oracle(id_dtype, id_hi, per_halo):
                 assert_same(got[g][d], want[g][d], '%s/%s' % (g, d))
 
 
-def test_collate_many_halos_lookback():
-    """k_collate places every halo's merged list behind a look-back over the halos
-    before it: 3000 halos (47 windows of 64) over 5 snapshots, all outputs vs the oracle."""
+def test_collate_many_halos_several_snapshots():
+    """Many halos through k_collate_rank / k_collate_offsets / k_collate_place: 3000
+    halos over 5 snapshots (each halo's list merged into a growing state), all outputs
+    vs the oracle."""
     rng = np.random.default_rng(11)
     groups, attrs = _random_track_file(rng, 3000, 5, 60, np.int64, 2 ** 40)
     want = PO.collate_apsides(groups, attrs)
@@ -136,6 +137,82 @@ def test_collate_extreme_ids_vs_oracle(id_dtype):
     for g in want:
         for d in want[g]:
             assert_same(got[g][d], want[g][d], '%s/%s' % (g, d))
+
+
+def test_collate_inconsistent_workspace_raises_bounds_status():
+    """k_collate_place / k_collate_rank check every store against its halo's range: a
+    corrupted workspace (w_found off by a few, a new_base past the workspace) sets
+    OA_POST_BOUNDS and stores nothing out of range, instead of faulting.  The round runs
+    as its two phases (rank, then offsets + place) with the corruption in between."""
+    import ctypes
+    import torch
+    from orbitanalysis_amd import _native as N
+    lib = N.load(require_device=True)
+    dev = torch.device('cuda', 0)
+    rng = np.random.default_rng(5)
+    nh, per = 4, 300
+    old_k = [np.unique(rng.choice(10 ** 6, per)) for _ in range(nh)]
+    new_ids = [rng.choice(np.concatenate([old_k[h][:100], rng.choice(10 ** 6, 100)]), 150)
+               for h in range(nh)]
+    src_cnt = np.array([len(x) for x in new_ids], np.int64)
+    src_off = np.concatenate([[0], np.cumsum(src_cnt)[:-1]]).astype(np.int64)
+    ids = torch.from_numpy(np.concatenate(new_ids).astype(np.int64)).to(dev)
+    ang = torch.full((ids.numel(),), 0x4000, dtype=torch.int16, device=dev)    # 2.0
+    lut = torch.ones(65536, dtype=torch.uint8, device=dev)
+    okeys = torch.from_numpy(np.concatenate(old_k).astype(np.int64) ^ np.int64(-2 ** 63)).to(dev)
+    ooff = torch.from_numpy(np.concatenate([[0], np.cumsum([len(k) for k in old_k])])).to(dev)
+    ocnt = torch.ones_like(okeys)
+    cap, n_old = int(src_cnt.sum()), int(okeys.numel())
+    src_off_d, src_cnt_d = torch.from_numpy(src_off).to(dev), torch.from_numpy(src_cnt).to(dev)
+
+    def run(corrupt):
+        i32 = dict(dtype=torch.int32, device=dev)
+        w = dict(keys=torch.empty(cap, dtype=torch.int64, device=dev),
+                 cnt=torch.empty(cap, **i32), lb=torch.empty(cap, **i32),
+                 fp=torch.empty(cap, **i32), ulen=torch.empty(nh, **i32),
+                 found=torch.empty(nh, **i32))
+        base = torch.from_numpy(src_off.copy()).to(dev)
+        new_off = torch.empty(nh + 1, dtype=torch.int64, device=dev)
+        sentinel = -7
+        new_keys = torch.full((n_old + cap,), sentinel, dtype=torch.int64, device=dev)
+        new_cnt = torch.full((n_old + cap,), sentinel, dtype=torch.int64, device=dev)
+        status = torch.zeros(1, **i32)
+        p = lambda t: ctypes.c_void_p(t.data_ptr())             # noqa: E731
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+        def args(phases):
+            return N.CollateArgs(
+                n_halos=nh, in_kind=0, key_signed=1, chunk_start=0, lds_keys=256,
+                phases=phases, apsis_ids=p(ids), angles=p(ang), keep_lut=p(lut),
+                src_off=p(src_off_d), src_cnt=p(src_cnt_d), new_base=p(base),
+                old_keys=p(okeys), old_cnt=p(ocnt), old_off=p(ooff), n_old=n_old,
+                n_new_cap=cap, w_keys=p(w['keys']), w_cnt=p(w['cnt']), w_lb=p(w['lb']),
+                w_fp=p(w['fp']), w_ulen=p(w['ulen']), w_found=p(w['found']),
+                new_off=p(new_off), new_keys=p(new_keys), new_cnt=p(new_cnt),
+                status=p(status))
+        if corrupt == 'base':
+            base[2] = cap - 10                       # its 150 rows would run past the end
+        a1 = args(1)
+        N.check(lib.oa_collate_step(ctypes.byref(a1), st), 'oa_collate_step rank')
+        if corrupt == 'found':
+            w['found'][1] += 3                        # merged length 3 short
+        a2 = args(2)
+        N.check(lib.oa_collate_step(ctypes.byref(a2), st), 'oa_collate_step merge')
+        torch.cuda.synchronize()
+        off = new_off.cpu().numpy()
+        return int(status.item()), off, new_keys.cpu().numpy(), new_cnt.cpu().numpy()
+
+    s0, off0, k0, c0 = run(None)
+    assert s0 == 0
+    want = [np.unique(np.concatenate([old_k[h], new_ids[h]])) for h in range(nh)]
+    got = [(k0[off0[h]:off0[h + 1]] ^ np.int64(-2 ** 63)) for h in range(nh)]
+    for h in range(nh):
+        assert np.array_equal(got[h], want[h])
+    for corrupt in ('found', 'base'):
+        s, off, k, c = run(corrupt)
+        assert s & N.POST_BOUNDS, (corrupt, s)
+        # nothing was stored past the merged state's end
+        assert np.all(k[int(off0[-1]):] == -7) and np.all(c[int(off0[-1]):] == -7), corrupt
 
 
 def test_retro_counts_missing_id_raises():

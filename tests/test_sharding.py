@@ -401,3 +401,100 @@ def test_record_placement_equals_sorted_merge(seed):
     want = np.empty(len(rows), np.int64)
     want[np.argsort(rows, kind='stable')] = np.arange(len(rows))
     assert np.array_equal(dst, want)
+
+
+def test_nccl_wire_dtypes():
+    """every tensor the sharded paths move travels in a dtype torch's NCCL
+    backend maps to an RCCL type (int16 angle bits, uint dtypes as bytes), and comes
+    back bit-identical."""
+    import torch
+    from orbitanalysis_amd.sharding import to_wire, from_wire, NCCL_WIRE
+    rng = np.random.default_rng(0)
+    cases = [torch.from_numpy(rng.integers(-2 ** 15, 2 ** 15, 37).astype(np.int16)),
+             torch.from_numpy(rng.integers(0, 2 ** 16, (37, 3)).astype(np.uint16)),
+             torch.from_numpy(rng.integers(0, 2 ** 32, 37).astype(np.uint32)),
+             torch.from_numpy(rng.integers(0, 2 ** 63, 37).astype(np.uint64)),
+             torch.from_numpy(rng.normal(size=37).astype(np.float16)),
+             torch.from_numpy(rng.integers(-2 ** 62, 2 ** 62, (37, 2))),
+             torch.from_numpy(rng.normal(size=(37, 3))),
+             torch.from_numpy(rng.uniform(size=37) < 0.5)]
+    for x in cases:
+        for cpu in (False, True):
+            w, bv = to_wire(x, cpu)
+            if not cpu:
+                assert w.dtype in NCCL_WIRE, x.dtype
+            assert w.shape[0] == x.shape[0]              # rows stay rows (uneven splits)
+            y = from_wire(w.clone(), x.dtype, tuple(x.shape[1:]), bv)
+            assert y.dtype == x.dtype and y.shape == x.shape
+            assert torch.equal(y.view(torch.uint8) if x.dtype == torch.bool else y, x) or \
+                np.array_equal(y.numpy().view(np.uint8), x.numpy().view(np.uint8))
+
+
+def _stage_worker(rank, world, port, outdir, presharded):
+    """Records of random per-rank runs through host_share.SharedRecordStage: rank 0's
+    result must equal the sorted merge, and each rank stores only its own records."""
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from orbitanalysis_amd.host_share import SharedRecordStage
+        rng = np.random.default_rng(123)                  # the same universe on every rank
+        S = 23
+        blk = rng.integers(0, 50, size=(world, S))        # rank r's rows of prev block h
+        gstart = np.concatenate([[0], np.cumsum(blk.sum(0))])[:-1]
+        before = np.cumsum(blk, 0) - blk
+        n_rows = int(blk.sum())
+        perm = rng.permutation(n_rows)
+        stage = SharedRecordStage(None, rank, world)
+        for it in range(3):
+            ids_all, key_all, cnt = [], [], np.zeros((world, S), np.int64)
+            mine_rows = []
+            for r in range(world):
+                for h in range(S):
+                    if presharded:
+                        pos = np.sort(rng.choice(blk[r, h], size=rng.integers(0, blk[r, h] + 1),
+                                                 replace=False)) if blk[r, h] else np.zeros(0, np.int64)
+                        key = gstart[h] + before[r, h] + pos
+                    else:
+                        # stripes: any rows of block h, owned by rank r if perm % W == r
+                        rows_h = gstart[h] + np.arange(blk[:, h].sum())
+                        own = rows_h[perm[rows_h] % world == r]
+                        key = np.sort(own[rng.uniform(size=len(own)) < 0.4])
+                    cnt[r, h] = len(key)
+                    key_all.append(key)
+                    ids_all.append(key * 7 + 3)
+                    if r == rank:
+                        mine_rows.append(key)
+            mk = np.concatenate(mine_rows).astype(np.int64) if mine_rows else np.zeros(0, np.int64)
+            offs = torch.from_numpy(np.concatenate([[0], np.cumsum(cnt[rank])]).astype(np.int64))
+            a_ids = torch.from_numpy(mk * 7 + 3)
+            a_ang = torch.from_numpy((mk % 30000).astype(np.int16))
+            prof = {}
+            f = stage.fetch(None, None, None, offs, a_ids, a_ang, len(mk),
+                            torch.from_numpy(cnt[rank]), S, np.int64,
+                            rows=None if presharded else torch.from_numpy(mk), n_rows=n_rows,
+                            comm_dev=torch.device('cpu'), profile=prof)
+            assert prof['own_records'] == len(mk) and prof['bytes_moved'] == 10 * len(mk)
+            off, ids, ang = f.wait()
+            if rank == 0:
+                key = np.concatenate(key_all).astype(np.int64)
+                order = np.argsort(key, kind='stable')
+                assert np.array_equal(off, np.concatenate([[0], np.cumsum(cnt.sum(0))]))
+                assert np.array_equal(ids, (key * 7 + 3)[order])
+                assert np.array_equal(ang.view(np.int16), (key % 30000).astype(np.int16)[order])
+            else:
+                assert len(ids) == 0
+        stage.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,presharded', [(2, True), (3, True), (3, False)])
+def test_shared_record_stage_places_every_rank(world, presharded):
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_stage_worker, args=(world, _free_port(), d, presharded),
+                           nprocs=world, join=True, start_method='spawn')
+    left = [f for f in os.listdir('/dev/shm') if f.startswith('oa_rec_')] \
+        if os.path.isdir('/dev/shm') else []
+    assert not left, left                               # every slot file was unlinked

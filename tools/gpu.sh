@@ -147,6 +147,14 @@ pprof)   # per-kernel stats of tools/bench_post.py for each library variant in $
     rc=$?; echo "== $v $(grep -o '"ms_per_[a-z]*": [0-9.]*' "$O/pprof_${T}_$v.jsonl")"
     python3 tools/kstats.py "$O/pprof_${T}_$v" | head -6; ok $rc "pprof $v"
   done ;;
+cal)
+  # FETCH_SIZE / WRITE_SIZE per access width (tools/ubench/fetch_cal, built on the CPU host)
+  for c in FETCH_SIZE WRITE_SIZE; do
+    ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 60 rocprofv3 --pmc $c --output-format csv \
+        -d "$O/cal_$T/$c" -o run -- "$R/tools/ubench/fetch_cal" ) > "$O/cal_${T}_$c.out" 2>&1
+    rc=$?; tail -1 "$O/cal_${T}_$c.out"; ok $rc "cal $c"
+  done
+  python3 tools/fetch_cal.py "$O/cal_$T" "$O/cal_${T}_FETCH_SIZE.out" > "$O/fetch_cal_$T.json"; ok $? cal_summary ;;
 *) echo "unknown step $step"; exit 2 ;;
 esac
 done
