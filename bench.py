@@ -37,16 +37,19 @@ def log(*a):
     print('[bench]', *a, file=sys.stderr, flush=True)
 
 
-def step_bytes(pr, n_prev, n_apsis):
+def step_bytes(pr, n_prev, n_apsis, reads_only=False):
     """Algorithmic HBM bytes of one oa_step launch: every
     current particle reads id + x + v and writes its record; every previous
-    particle reads id + record; every apsis writes id + f16 angle."""
+    particle reads id + record; every apsis writes id + f16 angle.  ``reads_only``:
+    the bytes read."""
     p = pr.plan
-    cur = p.ids.itemsize + 3 * p.coord.itemsize + 3 * p.vel.itemsize + p.state_bytes
+    cur = p.ids.itemsize + 3 * p.coord.itemsize + 3 * p.vel.itemsize
     if p.mass is not None:
         cur += p.mass.itemsize
     prev = p.ids.itemsize + p.state_bytes
-    return pr.n * cur + n_prev * prev + n_apsis * (p.ids.itemsize + 2)
+    if reads_only:
+        return pr.n * cur + n_prev * prev
+    return pr.n * (cur + p.state_bytes) + n_prev * prev + n_apsis * (p.ids.itemsize + 2)
 
 
 def kernel_label(pr):
@@ -117,15 +120,25 @@ def main():
                     help='processes of the P-core CPU baseline (0: min(16, cpu_count): the '
                          'GPU box gives one GPU 16 host cores)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--scaling', default='weak', choices=['weak', 'strong'],
-                    help='weak: --particles per GPU (configs[2] per rank); strong: --particles '
-                         'in total over the ranks (configs[3])')
+    ap.add_argument('--scaling', default=None, choices=['weak', 'strong'],
+                    help='strong (default for N > 1): --particles in total over the ranks, '
+                         'BASELINE configs[3]; weak: --particles per GPU (configs[2] on every '
+                         'rank).  N = 1: both are configs[2]')
+    ap.add_argument('--ramp-steps', type=int, default=-1,
+                    help='back-to-back launches of the warm-up steps before the W warm-up '
+                         'steps proper, so the timed steps run at the steady GPU clock (-1: '
+                         '30 per GPU-equivalent of work, i.e. 30 x N under strong scaling)')
+    ap.add_argument('--no-output-stage', action='store_true',
+                    help='N > 1: skip the second timed pass that includes the records\' '
+                         'output stage (host_share.SharedRecordStage)')
     ap.add_argument('--backend', default='nccl',
                     help="collective backend for N > 1 ('gloo': rehearsal with several "
                          "ranks on one GPU; collectives go through host memory)")
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    if args.scaling is None:
+        args.scaling = 'strong' if world > 1 else 'weak'
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     import torch
@@ -224,6 +237,15 @@ def main():
         return eng.launch(pr, ws, SnapshotState.of(prev_pr, exists, ids=snaps[ps]['ids']),
                           step_events=events)
 
+    # Clock ramp: after the host-side setup the GPU runs its first ~15 launches 5-25 %
+    # slower (rocprof trace of this bench, profiles/r06/: 1.60 -> 1.40 ms per k_step over
+    # 15 launches, then flat), longer than W = 5 warm-up steps cover.  The warm-up steps
+    # are launched back to back first (each re-run writes the same outputs); the count is
+    # fixed, so every rank issues the same collectives.
+    ramp = args.ramp_steps if args.ramp_steps >= 0 else \
+        30 * (world if args.scaling == 'strong' else 1)
+    for i in range(ramp):
+        run(i % max(args.warmup, 1))
     for k in range(args.warmup):
         run(k)
     torch.cuda.synchronize()
@@ -274,21 +296,71 @@ def main():
         fetch_ms = float(t.item())
 
     # each timed step's own apsis count (its records' bytes): the steps are re-run
-    # once, untimed, in order (each reads the state its predecessor wrote)
+    # once, untimed, in order (each reads the state its predecessor wrote); N > 1: this
+    # rank's own count (the roofline is rank 0's kernel)
     n_aps = []
-    if world == 1:
+    for i in range(args.steps):
+        r_i = run(args.warmup + i)
+        torch.cuda.synchronize()
+        n_aps.append(int(ws.total.item()) if world == 1 else int(r_i.lp.res.total.item()))
+
+    # N > 1: the same K steps again with the output stage of the drop-in driver
+    # (track_orbits' pipelined order: step s launched, then the records of s - 1 start
+    # towards the host, then those of s - 2 are waited for), every rank storing its own
+    # records into the shared host buffer (host_share.SharedRecordStage); timed as the
+    # compute pass.  value stays the compute pass (as at N = 1, where the records' D2H is
+    # outside the timed region too); this pass is reported beside it.
+    stage = None
+    if world > 1 and not args.no_output_stage:
+        seng.profile_fetch = False
+        pend, moved = [], []
+        for i in range(2):                        # warm: maps and registers the slots
+            seng.fetch_async(run(i), fdt).wait()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        prev_res = None
         for i in range(args.steps):
-            run(args.warmup + i)
-            n_aps.append(int(ws.total.item()))
-    else:
-        n_aps = [n_apsis] * args.steps
+            r_i = run(args.warmup + i)
+            if prev_res is not None:
+                pend.append(seng.fetch_async(prev_res, fdt))
+            if len(pend) > 1:
+                got = pend.pop(0)
+                got.wait()
+                moved.append(got.moved)
+            prev_res = r_i
+        pend.append(seng.fetch_async(prev_res, fdt))
+        for f in pend:
+            f.wait()
+            moved.append(f.moved)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        e2e = time.perf_counter() - t1
+        t = torch.tensor([e2e], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        e2e = float(t.item())
+        mv = torch.tensor([float(np.mean(moved))], dtype=torch.float64, device=cdev)
+        allmv = [torch.zeros_like(mv) for _ in range(world)]
+        dist.all_gather(allmv, mv)
+        stage = {'e2e_value': units / e2e, 'e2e_ms_per_step': e2e / args.steps * 1e3,
+                 'bytes_stored_per_step_by_rank': [float(x.item()) for x in allmv],
+                 'note': 'the K compare steps again, each followed (pipelined as track_orbits '
+                         'does) by its records\' move to the host: every rank stores its own '
+                         'records at their final positions in one page-locked host buffer all '
+                         'ranks map (host_share.SharedRecordStage), rank 0 moves only its own '
+                         'and waits for the others; max over ranks'}
+        log('output stage: %.3f ms per step (compute only %.3f); bytes stored per rank %s'
+            % (stage['e2e_ms_per_step'], elapsed / args.steps * 1e3,
+               stage['bytes_stored_per_step_by_rank']))
     bytes_launch = float(np.mean([step_bytes(preps[args.warmup + i], preps[args.warmup + i].n_prev,
                                              n_aps[i]) for i in range(args.steps)]))
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     log('elapsed %.4f s for %d steps; k_step %.3f ms; %.1f GB/s; apsis %d'
         % (elapsed, args.steps, kern_ms, achieved, n_apsis))
 
-    traffic = None
+    traffic, counters = None, None
     for name in ('pmc_k_step.json', 'pmc_part.json'):
         pmc = os.path.join(ROOT, 'profiles', name)
         if traffic is not None or not os.path.exists(pmc):
@@ -299,6 +371,14 @@ def main():
         if (pj.get('particles'), pj.get('halos'), pj.get('n_gpus', 1)) == \
                 (per_rank, args.halos, 1):
             traffic = pj.get('hbm_bytes_per_launch')
+            counters = {'source': 'profiles/' + name,
+                        'fetch_size_bytes': pj.get('fetch_size_bytes'),
+                        'write_size_bytes': pj.get('write_size_bytes'),
+                        'width_calibration': pj.get('width_calibration'),
+                        'traffic_over_algorithmic': traffic / bytes_launch if traffic else None}
+    # §8(d): read-only bytes against the peak (the reads alone, per launch)
+    read_launch = float(np.mean([step_bytes(preps[args.warmup + i], preps[args.warmup + i].n_prev,
+                                            0, reads_only=True) for i in range(args.steps)]))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -337,6 +417,9 @@ def main():
         out = {
             'metric': METRIC, 'value': units / elapsed, 'unit': 'particle-snapshots/s',
             'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'warmup_note': 'the W warm-up steps are preceded by %d back-to-back launches of '
+                           'the same warm-up steps (GPU clock ramp after the host-side '
+                           'setup); the timed region is exactly the K steps' % ramp,
             'ms_per_step': elapsed / args.steps * 1e3, 'higher_is_better': True,
             'scaling': args.scaling, 'vs_baseline': None,
             'dtype': last.plan.coord.name.replace('float', 'f'),
@@ -364,14 +447,23 @@ def main():
                                        'timed region and is excluded, see host_prepare_ms',
                        'host_prepare_ms': float(np.median(prep_s)) * 1e3,
                        'fetch_ms': fetch_ms,
-                       'fetch_note': 'records of one step gathered to rank 0 (ShardedEngine: '
-                                     '10-B records, count-scan placement) and copied to '
-                                     'host, outside the timed region (the driver overlaps '
-                                     'it with the next step); max over ranks'},
+                       'fetch_note': 'records of one step moved to the host for rank 0 '
+                                     '(N = 1: one D2H; N > 1: every rank stores its own '
+                                     'records into the shared host buffer), outside the '
+                                     'timed region (the driver overlaps it with the next '
+                                     'step); max over ranks',
+                       'output_stage': stage,
+                       'weak_scaling_config': 'bench.py --scaling weak: configs[2] (1e8 '
+                                              'particles) on every rank'
+                                              if world > 1 else None},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
                          'traffic': traffic, 'kernel': kernel_label(last), 'kernel_ms': kern_ms,
-                         'alg_bytes_per_launch': bytes_launch},
+                         'alg_bytes_per_launch': bytes_launch,
+                         'alg_read_bytes_per_launch': read_launch,
+                         'read_only_achieved': read_launch / (kern_ms * 1e-3) / 1e9,
+                         'read_only_frac': read_launch / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         'counters': counters},
             'cpu_baseline': cpu,
         }
         print(json.dumps(out), flush=True)

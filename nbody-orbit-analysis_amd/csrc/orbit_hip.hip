@@ -55,7 +55,7 @@ namespace {
 #define OA_UNR1 1           // phase 1: rows per wave trip (2: dynamic trips; A/B r02 wg: 1 is 0.7 % faster)
 #endif
 #ifndef OA_KROWS
-#define OA_KROWS 12         // phase 2: progenitor rows held per wave (n_pv <= KROWS * WG)
+#define OA_KROWS (12 * 1024 / OA_WG)   // phase 2: progenitor rows held per wave (n_pv <= KROWS * WG)
 #endif
 #ifndef OA_PF2
 #define OA_PF2 5            // phase 2b: rows of previous r̂ loads in flight ahead (A/B r02: 2 +3.5 %, 4 = 3, 5 -0.4 %)
@@ -65,7 +65,7 @@ namespace {
 #endif
 // phase 2b stages an item's current r̂ through registers, STAGE_* rows per thread:
 // lds_entries <= STAGE_* * WG (11776 float32 / 6144 float64 entries fill the LDS)
-constexpr int STAGE_F32 = 12, STAGE_F64 = 6;
+constexpr int STAGE_F32 = 12 * 1024 / OA_WG, STAGE_F64 = 6 * 1024 / OA_WG;
 constexpr int WG = OA_WG;           // k_step work-group
 constexpr int NWAVE = WG / 64;
 constexpr int HMAX = OA_HMAX;       // halos per item

@@ -844,6 +844,7 @@ class ShardedEngine:
             with ctx:
                 if side is not None and done is not None:
                     side.wait_event(done)
+                    done.synchronize()            # the record count's host copy (launch)
                 total = self.local.total(lp) if hasattr(self.local, 'total') else int(offs[-1])
                 cnt = (offs[1:S + 1] - offs[:S]).to(torch.int64)
                 rows = n_rows = None
@@ -868,6 +869,7 @@ class ShardedEngine:
         with ctx:
             if side is not None and done is not None:
                 side.wait_event(done)
+                done.synchronize()                # the record count's host copy (launch)
             total = self.local.total(lp) if hasattr(self.local, 'total') else int(offs[-1])
             cnt = (offs[1:S + 1] - offs[:S]).to(torch.int64).reshape(1, S)
             send = [a_ids[:total], a_ang[:total].to(torch.int16)]

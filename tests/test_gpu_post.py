@@ -141,7 +141,8 @@ def test_collate_extreme_ids_vs_oracle(id_dtype):
 
 def test_collate_inconsistent_workspace_raises_bounds_status():
     """k_collate_place / k_collate_rank check every store against its halo's range: a
-    corrupted workspace (w_found off by a few, a new_base past the workspace) sets
+    corrupted workspace (lower bounds past a halo's merged range, a new_base past the
+    workspace) sets
     OA_POST_BOUNDS and stores nothing out of range, instead of faulting.  The round runs
     as its two phases (rank, then offsets + place) with the corruption in between."""
     import ctypes
@@ -194,8 +195,9 @@ def test_collate_inconsistent_workspace_raises_bounds_status():
             base[2] = cap - 10                       # its 150 rows would run past the end
         a1 = args(1)
         N.check(lib.oa_collate_step(ctypes.byref(a1), st), 'oa_collate_step rank')
-        if corrupt == 'found':
-            w['found'][1] += 3                        # merged length 3 short
+        if corrupt == 'lb':
+            # halo 1's absent keys placed past its merged range
+            w['lb'][int(src_off[1]):int(src_off[2])] = 10 ** 6
         a2 = args(2)
         N.check(lib.oa_collate_step(ctypes.byref(a2), st), 'oa_collate_step merge')
         torch.cuda.synchronize()
@@ -208,7 +210,7 @@ def test_collate_inconsistent_workspace_raises_bounds_status():
     got = [(k0[off0[h]:off0[h + 1]] ^ np.int64(-2 ** 63)) for h in range(nh)]
     for h in range(nh):
         assert np.array_equal(got[h], want[h])
-    for corrupt in ('found', 'base'):
+    for corrupt in ('lb', 'base'):
         s, off, k, c = run(corrupt)
         assert s & N.POST_BOUNDS, (corrupt, s)
         # nothing was stored past the merged state's end

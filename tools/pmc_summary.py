@@ -2,21 +2,22 @@
 """Reduce the rocprofv3 --pmc passes of tools/pmc.sh to profiles/pmc_k_step.json.
 
 HBM bytes per k_step launch, following MI355X_MICROARCH.md §HBM: FETCH_SIZE and
-WRITE_SIZE come from the L2's fabric requests (TCC_EA0_RDREQ x 64 B, WRREQ x 64 B);
-WRITE_SIZE is exact for streaming stores, FETCH_SIZE under-counts wide reads and
-"other access widths are uncalibrated: calibrate on a known byte count in your own
-access pattern".  The bench's first launch IS such a calibration: snapshot 0 runs
-k_step frame-only (compare = 0), which streams exactly n0 x (id 8 + x 12 + v 12) B
-with the same load instructions the compared launches use for both the current and
-the previous blocks.  So
+WRITE_SIZE come from the L2's fabric requests.  The guide calibrates 16-B-per-lane
+streams (FETCH_SIZE = 1/2 of the bytes read, WRITE_SIZE exact) and leaves other widths
+to the user; tools/ubench/fetch_cal.hip measured every width k_step uses (buffer loads
+of 4, 8, 12 and 16 B per lane, stores of 4, 12 and 16 B, nt bit, 2 GiB each:
+profiles/fetch_cal.json): FETCH_SIZE reads 1/2 of the bytes at every load width
+(factors 1.9999-2.0000) and WRITE_SIZE reads the bytes at every store width
+(0.998-0.999).  So
 
-    k              = n0 * 32 / FETCH_SIZE(frame-only launch)
-    hbm_bytes      = k * FETCH_SIZE(compared launch) + WRITE_SIZE(compared launch)
+    hbm_bytes_per_launch = f_load * FETCH_SIZE + f_store * WRITE_SIZE
 
-k also scales the r̂ gathers' requests (12-B random reads, served mostly by the
-Infinity Cache: the rows were written by the same work-group ~30 us earlier), so
-`hbm_bytes_per_launch` is an upper bound on true HBM traffic; `guide_rule_bytes`
-(2 x FETCH + WRITE, the guide's rule for 16-B/lane streams) is given beside it.
+with the calibrated factors (2 and 1: the guide's rule, now measured for these widths).
+
+Round 1-5 scaled FETCH_SIZE by the frame-only launch's ratio (k = 2.57), which is not
+a clean calibration: snapshot 0's arrays were written by the generator just before
+that launch, so part of its reads came from the Infinity Cache and fewer requests
+reached the counters.  `frame_calibrated_bytes` keeps that figure for comparison.
 
 usage: pmc_summary.py PMC_DIR N_FRAME_ONLY [OUT_JSON]
 """
@@ -54,6 +55,10 @@ def main():
     k = n0 * 32.0 / fetch0
     fetch = mean['FETCH_SIZE'] * 1024.0
     write = mean['WRITE_SIZE'] * 1024.0
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cal = json.load(open(os.path.join(root, 'profiles', 'fetch_cal.json')))
+    f_load = sum(v['factor'] for v in cal['load'].values()) / len(cal['load'])
+    f_store = sum(v['factor'] for v in cal['store'].values()) / len(cal['store'])
     res = {
         'kernel': 'k_step<float,float,float,8,compare>',
         'workload': 'bench.py defaults (1e8 particles, 1e4 halos, f32)',
@@ -64,8 +69,12 @@ def main():
                         'frame_only_write_size_bytes': frame['WRITE_SIZE'] * 1024.0,
                         'frame_only_write_expected': n0 * 16},
         'fetch_size_bytes': fetch, 'write_size_bytes': write,
-        'hbm_bytes_per_launch': k * fetch + write,
+        'width_calibration': {'source': 'profiles/fetch_cal.json', 'load_factor': f_load,
+                              'store_factor': f_store},
+        'hbm_bytes_per_launch': f_load * fetch + f_store * write,
+        'hbm_read_bytes_per_launch': f_load * fetch,
         'guide_rule_bytes': 2.0 * fetch + write,
+        'frame_calibrated_bytes': k * fetch + write,
         'counters_mean_compared': mean,
         'counters_frame_only': frame,
     }
