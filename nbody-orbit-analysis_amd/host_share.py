@@ -260,14 +260,21 @@ class SharedRecordStage:
         slot = self._agree(total, ib, comm_dev)
         n = int(total_local)
         t0 = time.perf_counter() if profile is not None else 0.0
-        # 3. this rank's records' positions
+        # 3. this rank's records' positions (the counts are checked on the host first: a
+        # count matrix that disagrees with the record total would place records outside
+        # their runs)
+        loc_h = Ch[self.rank]
+        if (Ch < 0).any() or int(loc_h.sum()) != n or n > slot.cap or total > slot.cap:
+            raise RuntimeError('sharded records: rank %d holds %d records but its per-halo '
+                               'counts sum to %d (min count %d, output capacity %d)'
+                               % (self.rank, n, int(loc_h.sum()), int(Ch.min(initial=0)),
+                                  slot.cap))
         if rows is None:
-            Cd = C.to(dev)
-            before = (torch.cumsum(Cd, 0) - Cd)[self.rank]
-            loc = Cd[self.rank]
-            D = torch.from_numpy(off[:S]).to(dev) + before - (torch.cumsum(loc, 0) - loc)
+            before_h = Ch[:self.rank].sum(0)
+            D_h = off[:S] + before_h - (np.cumsum(loc_h) - loc_h)
             dst = torch.arange(n, dtype=torch.int64, device=dev) + \
-                torch.repeat_interleave(D, loc, output_size=n) if n else \
+                torch.repeat_interleave(torch.from_numpy(D_h).to(dev),
+                                        torch.from_numpy(loc_h).to(dev), output_size=n) if n else \
                 torch.zeros(0, dtype=torch.int64, device=dev)
         else:
             dst = self._rank_by_row(rows[:n].to(torch.int64), int(n_rows), comm_dev).to(dev)

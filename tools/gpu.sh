@@ -45,7 +45,8 @@ bench)
 prof)
   prof "$O/prof_$T" 400 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} \
     > "$O/bench_prof_$T.json" 2> "$O/bench_prof_$T.err"
-  rc=$?; find "$O/prof_$T" -name '*kernel_stats.csv' -exec cut -c1-150 {} \; | head -8; ok $rc prof ;;
+  rc=$?; python3 tools/kstats.py "$O/prof_$T" | head -8
+  python3 tools/trace_window.py "$O/prof_$T" ${RAMP:-30} ${WARM:-5} ${STEPS_T:-20} "$O/trace_window_$T.json"; ok $rc prof ;;
 pmc)
   TAG=$T PMC_FILE=$R/tools/pmc_bytes.txt bash tools/pmc.sh > "$O/pmc_$T.out" 2>&1
   rc=$?; tail -3 "$O/pmc_$T.out"; ok $rc pmc
