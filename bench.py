@@ -229,11 +229,13 @@ def main():
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
 
-    def run(k, events=None):
+    def run(k, events=None, defer=False):
         pr, s = chain[k + 1]
         prev_pr, ps = chain[k]
         if world > 1:
-            return seng.launch(pr, prev=prev_pr, step_events=events, check=False)
+            # defer: the drop-in driver's order -- the step's status is read (and the step
+            # re-run on a re-plan or look-back timeout) by the fetch that settles it
+            return seng.launch(pr, prev=prev_pr, step_events=events, check=defer, defer=defer)
         return eng.launch(pr, ws, SnapshotState.of(prev_pr, exists, ids=snaps[ps]['ids']),
                           step_events=events)
 
@@ -315,14 +317,14 @@ def main():
         seng.profile_fetch = False
         pend, moved = [], []
         for i in range(2):                        # warm: maps and registers the slots
-            seng.fetch_async(run(i), fdt).wait()
+            seng.fetch_async(run(i, defer=True), fdt).wait()
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         prev_res = None
         for i in range(args.steps):
-            r_i = run(args.warmup + i)
+            r_i = run(args.warmup + i, defer=True)
             if prev_res is not None:
                 pend.append(seng.fetch_async(prev_res, fdt))
             if len(pend) > 1:

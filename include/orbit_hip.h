@@ -261,7 +261,7 @@ typedef struct oa_step_args {
                                    oa_compact_args.out_pos of a scratch_pos step)     */
     int64_t *total_out;         /* device scalar: number of records                    */
     uint32_t lb_spin_max;       /* direct records: polls of an unpublished look-back word
-                                   before OA_STATUS_LOOKBACK (0: the default, 2^20; a
+                                   before OA_STATUS_LOOKBACK (0: the default, 2^14; a
                                    test sets 1 to exercise the re-run without direct)  */
     int32_t reserved_abi16;
 } oa_step_args;

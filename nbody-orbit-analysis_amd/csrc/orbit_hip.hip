@@ -297,7 +297,9 @@ constexpr int64_t HDR_BYTES = (sizeof(ItemHdr) + 255) & ~int64_t(255);
 // waiting on anyone, so the chain always resolves; the spin is still bounded (a
 // status bit asks the host for a re-run without direct records).
 constexpr uint64_t LB_AGG = 1ull << 46, LB_INC = 2ull << 46, LB_VAL = (1ull << 46) - 1ull;
-constexpr uint32_t LB_SPIN_MAX = 1u << 20;
+// a poll is one L2 round trip (~1 us): 2^14 polls bound a wait at ~16 ms, ~400x the
+// time an item takes; past it the step is re-run without direct records (the engine)
+constexpr uint32_t LB_SPIN_MAX = 1u << 14;
 
 __device__ __forceinline__ void lb_publish(uint64_t *w, uint64_t v) {
     __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

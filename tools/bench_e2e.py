@@ -269,16 +269,20 @@ def main():
         'total_wall_s': t_end - t_start,
     }
     if args.sharded and fstats:
-        res['records_gather'] = {
+        def med(k):
+            v = [f[k] for f in fstats[W:] if k in f] or [f[k] for f in fstats if k in f]
+            return float(np.median(v)) if v else None
+        res['records_output'] = {
             'layout': fstats[-1]['layout'],
             'bytes_per_record': fstats[-1]['bytes_per_record'],
-            'records_per_snapshot_median': float(np.median([f['records'] for f in fstats[W:]]
-                                                           or [f['records'] for f in fstats])),
-            'root_merge_ms_median': float(np.median([f['merge_ms'] for f in fstats[W:]]
-                                                    or [f['merge_ms'] for f in fstats])),
-            'note': 'rank 0 places the gathered records by a per-(rank, slot) count scan '
-                    '(presharded) or a counting pass over previous rows (stripes); '
-                    'synchronised timing of the placement alone'}
+            'records_per_snapshot_median': med('records'),
+            'own_records_per_snapshot_median': med('own_records'),
+            'bytes_stored_by_this_rank_median': med('bytes_moved'),
+            'place_ms_median': med('place_ms'),
+            'note': 'every rank computes its records\' final positions (count scan: '
+                    'presharded; bitmap rank over global previous rows: stripes) and stores '
+                    'them into the shared page-locked host buffer (host_share); place_ms: '
+                    'this rank\'s position computation + stores, synchronised'}
     if args.timeline and kern_ev:
         # GPU timeline relative to the first timed compare step's start: each step's
         # kernel window, the gap before it, and each records D2H window and its rate

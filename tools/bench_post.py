@@ -34,10 +34,21 @@ def log(*a):
     print('[bench_post]', *a, file=sys.stderr, flush=True)
 
 
-def roof(bytes_, ms):
+def _pmc(which):
+    """HBM bytes per call of a workload's kernels from profiles/pmc_post.json
+    (tools/pmc_post.sh over this bench at scale 1), or None."""
+    p = os.path.join(ROOT, 'profiles', 'pmc_post.json')
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f).get('per_call', {}).get(which)
+
+
+def roof(bytes_, ms, which=None, scale=1.0):
     gbs = bytes_ / (ms * 1e-3) / 1e9
+    t = _pmc(which) if which and scale == 1.0 else None
     return {'bound': 'hbm', 'achieved': gbs, 'peak': PEAK, 'unit': 'GB/s', 'frac': gbs / PEAK,
-            'traffic': None}
+            'traffic': t, 'traffic_over_algorithmic': t / bytes_ if t else None}
 
 
 def make_track_groups(rng, n_halos, n_snap, rec_per_halo, pool):
@@ -114,7 +125,8 @@ def bench_collate(scale, cpu_halos):
             'unit': 'records/s', 'ms_per_snapshot': tot_ms / (ns - 1), 'dtype': 'int64',
             'config': {'workload': 'f3 collate: %d halos, ~%d records/snapshot, %d snapshots, '
                        'pi/4 cut' % (nh, recs // (ns - 1), ns), 'state_final': n_new[-1]},
-            'roofline': dict(roof(bytes_ / (ns - 1), tot_ms / (ns - 1)), kernel='oa_collate_step'),
+            'roofline': dict(roof(bytes_ / (ns - 1), tot_ms / (ns - 1), 'collate', scale),
+                             kernel='oa_collate_step'),
             'cpu_baseline': {'value': crec / cdt, 'unit': 'records/s', 'cores': 1, 'kind': 'port',
                              'sample': '%d of %d halos, all %d snapshots, %.1f s; final particle '
                                        'IDs identical to the GPU: %s' % (cpu_halos, nh, ns, cdt, ok)}}
@@ -152,7 +164,7 @@ def bench_central(scale, cpu_halos, reps=5):
             'unit': 'particles/s', 'ms_per_call': ms, 'dtype': 'f32',
             'config': {'workload': 'f4 central IDs: %d particles f32 in %d blocks, n=100, box'
                        % (n, nh)},
-            'roofline': dict(roof(12.0 * n, ms), kernel='k_central'),
+            'roofline': dict(roof(12.0 * n, ms, 'central', scale), kernel='k_central'),
             'cpu_baseline': {'value': cpu_halos * per / cdt, 'unit': 'particles/s', 'cores': 1,
                              'kind': 'port', 'sample': '%d of %d blocks, %.1f s; IDs identical '
                              'to the GPU: %s' % (cpu_halos, nh, cdt, ok)}}
@@ -196,7 +208,8 @@ def bench_mainprog(scale, cpu_blocks, reps=5):
             'unit': 'members/s', 'ms_per_call': ms, 'dtype': 'int64',
             'config': {'workload': 'f4 main progenitors: %d int64 members in %d halos, %d tracked '
                        'blocks of 100' % (n, nh, nb)},
-            'roofline': dict(roof(8.0 * n + 8.0 * len(tp), ms), kernel='k_mp_probe'),
+            'roofline': dict(roof(8.0 * n + 8.0 * len(tp), ms, 'mainprog', scale),
+                             kernel='k_mp_probe'),
             'cpu_baseline': {'value': n / cdt, 'unit': 'members/s', 'cores': 1, 'kind': 'port',
                              'sample': 'all %d members, first %d tracked blocks, %.1f s; results '
                              'identical to the GPU: %s' % (n, cpu_blocks, cdt, ok)}}

@@ -97,7 +97,7 @@ e2e)
 e2es)
   # the sharded driver end to end: world-2 gloo rehearsal on this one GPU
   for c in presharded whole; do
-    timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    ORBIT_DIRECT=${B2_DIRECT:-0} timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
       --master-addr 127.0.0.1 --master-port ${E2E_PORT:-29521} tools/bench_e2e.py --sharded \
       --backend gloo --contract $c --scaling ${E2E_SCALING:-strong} --snapshots ${E2E_SNAPS:-12} \
       > "$O/e2es_${c}_$T.json" 2> "$O/e2es_${c}_$T.err"
@@ -113,7 +113,10 @@ post)
   rc=$?; python3 tools/kstats.py "$O/prof_post_$T"; ok $rc post_prof ;;
 b2)
   sc=${B2_SCALING:-strong}
-  timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+  # ORBIT_DIRECT=0: two processes share this one GPU, whose time slicing can hold a
+  # k_step item's predecessor off the CUs past the direct records' look-back bound (a
+  # production run has one process per GPU); the rehearsal checks the plumbing
+  ORBIT_DIRECT=${B2_DIRECT:-0} timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
     --master-addr 127.0.0.1 --master-port ${B2_PORT:-29517} bench.py --gpus 2 --steps 5 --warmup 2 \
     --backend gloo --scaling "$sc" --no-cpu-baseline ${B2_ARGS:-} > "$O/b2_${sc}_$T.json" 2> "$O/b2_${sc}_$T.err"
   rc=$?; grep -v Warning "$O/b2_${sc}_$T.err" | tail -3; cat "$O/b2_${sc}_$T.json"; ok $rc b2 ;;
@@ -156,6 +159,9 @@ cal)
     rc=$?; tail -1 "$O/cal_${T}_$c.out"; ok $rc "cal $c"
   done
   python3 tools/fetch_cal.py "$O/cal_$T" "$O/cal_${T}_FETCH_SIZE.out" > "$O/fetch_cal_$T.json"; ok $? cal_summary ;;
+pmcpost)
+  TAG=$T bash tools/pmc_post.sh > "$O/pmcpost_$T.out" 2>&1
+  rc=$?; tail -12 "$O/pmcpost_$T.out"; ok $rc pmcpost ;;
 *) echo "unknown step $step"; exit 2 ;;
 esac
 done
