@@ -50,7 +50,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--particles', type=float, default=1.25e8)
     ap.add_argument('--per-halo', type=int, default=10000)
-    ap.add_argument('--steps', type=int, default=6)
+    ap.add_argument('--steps', type=int, default=12,
+                    help='timed snapshots; the window also holds the last compare, which no '
+                         'later H2D hides, so ms_per_step overstates the steady period by '
+                         'about one compare / steps')
     ap.add_argument('--snapshots', type=int, default=3, help='distinct host snapshots (cycled)')
     ap.add_argument('--cpu-halos', type=int, default=150)
     ap.add_argument('--mode', default='pericentric')
