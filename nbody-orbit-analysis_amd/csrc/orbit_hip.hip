@@ -34,7 +34,6 @@
 #include <stdarg.h>
 #include <math.h>
 #include <type_traits>
-#include <algorithm>
 
 #include "orbit_hip.h"
 
@@ -77,9 +76,6 @@ constexpr int BULK_CHUNK = 8192;    // numpy pairwise-sum buffer chunk
 constexpr int STASH = 64;           // cuckoo stash entries per item
 #ifndef OA_MAXEV
 #define OA_MAXEV 48
-#endif
-#ifndef OA_PERSIST
-#define OA_PERSIST 0        // one-halo compare steps: persistent k_step
 #endif
 #ifndef OA_PU
 #define OA_PU 4             // k_part_join: previous entries per thread loaded up front
@@ -721,12 +717,7 @@ constexpr uint32_t PK_HIT = 1u << 14, PK_FLAG = 1u << 15;
 
 // SINGLE: every item holds one halo (oa_step_args.items_single): the packed-item paths
 // (per-row halo and segment lookups) are compiled out
-// PERSIST (OA_PERSIST builds, one-halo compare steps): one work-group per CU walks the
-// items b = blockIdx.x, + gridDim.x, ...; item b + gridDim.x's descriptor, halo row and
-// first phase-1 trip are loaded at the start of item b's phase 3, so its phase 0 waits
-// on no global load and the next item starts without a dispatch.
-template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF, bool SINGLE = false,
-          bool PERSIST = false>
+template <typename TX, typename TV, typename TD, int IDB, bool COMPARE, bool OTF, bool SINGLE = false>
 __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK fk) {
     typedef typename IdT<IDB>::T ID;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -741,27 +732,9 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         smem + HDR_BYTES + region_a_bytes((int)E, (int)nslots_max, (int)sizeof(TD)));
     uint16_t *prow = reinterpret_cast<uint16_t *>(
         smem + HDR_BYTES + prow_offset((int)E, (int)nslots_max, (int)sizeof(TD)));
-    // Phase-1 rows go in trips of U1 consecutive rows; a wave takes at most NTRIP trips
-    // (<= SU rows) and keeps each row's r̂ in registers (rr) until phase 2b writes it
-    // into the LDS the table held -- no read-back of the rows it stored.
-    constexpr int SU = sizeof(TD) == 4 ? STAGE_F32 : STAGE_F64;
-    // float64 r̂ keeps its phase-1 stores (register budget)
-    constexpr bool RD = COMPARE && sizeof(TD) == 4;
-    // float64 inputs: one row per trip (register budget of 1024-thread work-groups)
-    constexpr int U1 = (sizeof(TX) == 8 || sizeof(TV) == 8) ? 1 : UNR1;
-    constexpr int NTRIP = SU / U1;
-    static_assert(SU % U1 == 0, "rows per wave must be whole trips");
-    // the next item's prefetched loads (PERSIST)
-    bool pf_ok = false;
-    oa_item pf_it;
-    oa_halo pf_hrow;
-    uint32_t pf_hi0 = 0u;
-    typename IdT<IDB>::T pf_id[U1];
-    V3<TX> pf_x[U1];
-    V3<TV> pf_v[U1];
-    auto item = [&](const uint32_t b) __attribute__((always_inline)) {
+
     // the item (host-planned, oa_plan_items): scalar loads, uniform values
-    const oa_item it = (PERSIST && pf_ok) ? pf_it : a.items[b];
+    const oa_item it = a.items[blockIdx.x];
     const int nh = SINGLE ? 1 : it.h1 - it.h0;
     const uint32_t nhu = (uint32_t)nh;
     const int64_t base = it.cur_off;
@@ -783,19 +756,26 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // rows leaves them in flight), clears its share of the table, and the only barrier
     // waits for LDS traffic alone.
     oa_halo hrow;
-    if (PERSIST && pf_ok) hrow = pf_hrow;
-    else if (SINGLE) hrow = a.halos[it.h0];          // uniform: scalar loads
-    else if (wave == 0 && lane < nh) hrow = a.halos[it.h0 + lane];
+    if (wave == 0 && lane < nh) hrow = a.halos[it.h0 + lane];
     // reference high word for the 32-bit LDS keys: the item's first particle
     uint32_t hi0 = 0u;
-    if (PERSIST && pf_ok) hi0 = pf_hi0;
-    else if (IDB == 8 && COMPARE && n_span > 0) hi0 = uni((uint32_t)((uint64_t)ids[base] >> 32));
+    if (IDB == 8 && COMPARE && n_span > 0) hi0 = uni((uint32_t)((uint64_t)ids[base] >> 32));
     __builtin_amdgcn_sched_barrier(0);
     const Rsrc r_id = make_rsrc(ids + base, n_span * IDB);
     const Rsrc r_x = make_rsrc(reinterpret_cast<const TX *>(a.coords) + 3 * base, n_span * SX);
     const Rsrc r_v = make_rsrc(reinterpret_cast<const TV *>(a.vels) + 3 * base, n_span * SV);
     const Rsrc r_rh = make_rsrc(rhat_out + 3 * base, n_span * SD);
     const Rsrc r_mt = make_rsrc(a.meta_out + base, n_span * 4u);
+    // Phase-1 rows go in trips of U1 consecutive rows; a wave takes at most NTRIP trips
+    // (<= SU rows) and keeps each row's r̂ in registers (rr) until phase 2b writes it
+    // into the LDS the table held -- no read-back of the rows it stored.
+    constexpr int SU = sizeof(TD) == 4 ? STAGE_F32 : STAGE_F64;
+    // float64 r̂ keeps its phase-1 stores (register budget)
+    constexpr bool RD = COMPARE && sizeof(TD) == 4;
+    // float64 inputs: one row per trip (register budget of 1024-thread work-groups)
+    constexpr int U1 = (sizeof(TX) == 8 || sizeof(TV) == 8) ? 1 : UNR1;
+    constexpr int NTRIP = SU / U1;
+    static_assert(SU % U1 == 0, "rows per wave must be whole trips");
     const uint32_t nrow1 = (n_span + 63) / 64;
     const uint32_t ntr1 = (nrow1 + U1 - 1) / U1;     // trips of U1 consecutive rows
     // the wave's k-th trip: wave, wave + NWAVE, then trips from an LDS counter (read a
@@ -818,12 +798,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     V3<TX> xv[U1], xn[U1];
     V3<TV> vv[U1], vn[U1];
     V3<TD> rr[SU];
-    if (PERSIST && pf_ok) {
-#pragma unroll
-        for (int u = 0; u < U1; ++u) { idv[u] = pf_id[u]; xv[u] = pf_x[u]; vv[u] = pf_v[u]; }
-    } else {
-        OA_LOAD1(idv, xv, vv, tp[0])
-    }
+    OA_LOAD1(idv, xv, vv, tp[0])
     __builtin_amdgcn_sched_barrier(0);
     if (COMPARE) {
         for (uint32_t w = tid; w < nslots; w += WG) slots[w] = 0ull;
@@ -1021,7 +996,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         }
         const uint32_t os = lane < nh ? H.hslot[lane] >> 1 : 0u;
         if (os) a.offsets_out[os - 1u] = P + (incl - c);
-        if (lane == 0 && b == (uint32_t)a.n_items - 1) {
+        if (lane == 0 && blockIdx.x == gridDim.x - 1) {
             a.offsets_out[a.n_slots] = P + total;
             *a.total_out = P + total;
         }
@@ -1031,8 +1006,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         __syncthreads();
         for (uint32_t li = tid; li < n_span; li += WG)
             bst32<AUX_NT>(r_mt, li * 4u, (uint32_t)(sgn8[li] & 3u) << 16);
-        if (tid == 0) a.item_count[b] = 0;
-        if (a.direct && wave == 0) direct_tail(item_lookback(a, b, 0u), 0u);
+        if (tid == 0) a.item_count[blockIdx.x] = 0;
+        if (a.direct && wave == 0) direct_tail(item_lookback(a, blockIdx.x, 0u), 0u);
         return;
     }
     const uint32_t cnt0 = uni(H.seg_cnt[0]), hal0 = uni((uint32_t)H.seg_halo[0]);
@@ -1148,10 +1123,10 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         // records from this item
         if (tid == 0) {
             atomicOr(a.status, H.overflow ? OA_STATUS_TABLE_OVERFLOW : OA_STATUS_PLAN);
-            a.item_count[b] = 0;
+            a.item_count[blockIdx.x] = 0;
         }
         // the later items' look-backs must still resolve (the step is re-run anyway)
-        if (a.direct && wave == 0) item_lookback(a, b, 0u);
+        if (a.direct && wave == 0) item_lookback(a, blockIdx.x, 0u);
         return;
     }
     const bool nonuniform = IDB == 8 && uni(H.nonuniform) != 0;
@@ -1256,7 +1231,7 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         // direct records: the item's count is published now; its prefix is resolved
         // after phase 2b, beside phase 3, and the records are stored after that
         if (a.direct && lane == 0)
-            lb_publish(&a.lookback[b],
+            lb_publish(&a.lookback[blockIdx.x],
                        ((uint64_t)(uint32_t)a.lb_epoch << 48) | LB_AGG | carry);
     }
     // the item's current r̂, from the registers phase 1 left it in
@@ -1343,33 +1318,8 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
     // (four consecutive positions per thread: one 16-byte store)
     // direct records: wave 0 resolves the item's prefix meanwhile (the look-back's
     // round trips overlap the other waves' stores)
-    if constexpr (PERSIST) {
-        // the next item's descriptor, halo row, first key and first trip: their latency
-        // runs under this item's phase 3
-        const uint32_t nb = b + gridDim.x;
-        pf_ok = nb < (uint32_t)a.n_items;
-        if (pf_ok) {
-            pf_it = a.items[nb];
-            // one halo: a uniform row (scalar loads, no VGPRs held across phase 3)
-            if (SINGLE) pf_hrow = a.halos[pf_it.h0];
-            else if (wave == 0 && lane < pf_it.h1 - pf_it.h0) pf_hrow = a.halos[pf_it.h0 + lane];
-            const int64_t b2 = pf_it.cur_off;
-            const uint32_t n2 = (uint32_t)pf_it.n_span;
-            if (IDB == 8 && n2 > 0) pf_hi0 = uni((uint32_t)((uint64_t)ids[b2] >> 32));
-            const Rsrc q_id = make_rsrc(ids + b2, n2 * IDB);
-            const Rsrc q_x = make_rsrc(reinterpret_cast<const TX *>(a.coords) + 3 * b2, n2 * SX);
-            const Rsrc q_v = make_rsrc(reinterpret_cast<const TV *>(a.vels) + 3 * b2, n2 * SV);
-#pragma unroll
-            for (int u = 0; u < U1; ++u) {
-                const uint32_t li_ = ((uint32_t)wave * U1 + u) * 64 + lane;
-                pf_id[u] = bld<ID, AUX_NT>(q_id, li_ * IDB);
-                pf_x[u] = bld3<TX, AUX_NT>(q_x, li_ * SX);
-                pf_v[u] = bld3<TV, AUX_NT>(q_v, li_ * SV);
-            }
-        }
-    }
     if (direct && wave == 0) {
-        const int64_t P = item_lookback(a, b, uni(H.chunk_total), false);
+        const int64_t P = item_lookback(a, blockIdx.x, uni(H.chunk_total), false);
         if (lane == 0) H.prefix = P;
     }
     const uint32_t t3 = direct ? (uint32_t)tid - 64u : (uint32_t)tid;
@@ -1419,22 +1369,9 @@ __global__ __launch_bounds__(WG) void k_step(const oa_step_args a, const FrameK 
         const uint32_t os = H.hslot[tid] >> 1;
         if (os) a.halo_count[os - 1u] = H.halo_cnt[tid];
     }
-    if (tid == 0) a.item_count[b] = (int32_t)H.chunk_total;
+    if (tid == 0) a.item_count[blockIdx.x] = (int32_t)H.chunk_total;
     STAMP(7);
-    };
-    if constexpr (PERSIST) {
-        for (uint32_t b = blockIdx.x; b < (uint32_t)a.n_items; b += gridDim.x) {
-            item(b);
-            // the next item's phase 0 rewrites the LDS this item's phase 3 reads
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    } else {
-        item(blockIdx.x);
-    }
 }
-
 
 // ------------------------------------------------------------------ compaction
 // previous-block positions per record chunk of a partitioned halo (k_part_join's RCHUNK)
@@ -1789,25 +1726,10 @@ int launch_step_c(const oa_step_args &a, hipStream_t st) {
         // a frame-only launch needs no table: several work-groups share a CU
         const int64_t lds = COMPARE ? step_lds_bytes(a.lds_entries, a.lds_slots, (int)sizeof(TD))
                                     : HDR_BYTES;
-        const bool single = COMPARE && !OTF && a.items_single;
-        auto k = single ? k_step<TX, TV, TD, IDB, COMPARE, OTF, true>
-                        : k_step<TX, TV, TD, IDB, COMPARE, OTF, false>;
-        unsigned grid = (unsigned)a.n_items;
-        if constexpr (OA_PERSIST != 0) if (single) {
-            // persistent: as many work-groups as are resident at once (each item's
-            // look-back waits only on lower items, which resident work-groups own)
-            k = k_step<TX, TV, TD, IDB, COMPARE, OTF, true, true>;
-            if (int rc = set_lds(k, lds)) return rc;
-            int dev = 0, ncu = 0, per = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void *>(k), WG,
-                                                             (size_t)lds) != hipSuccess || per < 1)
-                return fail(OA_E_LAUNCH, "k_step: occupancy query");
-            grid = (unsigned)std::min<int64_t>((int64_t)a.n_items, (int64_t)ncu * per);
-        }
+        auto k = (COMPARE && !OTF && a.items_single) ? k_step<TX, TV, TD, IDB, COMPARE, OTF, true>
+                                                     : k_step<TX, TV, TD, IDB, COMPARE, OTF, false>;
         if (int rc = set_lds(k, lds)) return rc;
-        hipLaunchKernelGGL(k, dim3(grid), dim3(WG), (size_t)lds, st, a, make_frame_k(a));
+        hipLaunchKernelGGL(k, dim3(a.n_items), dim3(WG), (size_t)lds, st, a, make_frame_k(a));
         if (int rc = check_launch("k_step")) return rc;
     }
     return launch_big<TX, TV, TD, IDB, COMPARE, OTF>(a, st);
