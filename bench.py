@@ -314,6 +314,11 @@ def main():
     # outside the timed region too); this pass is reported beside it.
     stage = None
     if world > 1 and not args.no_output_stage:
+        from orbitanalysis_amd.host_share import SharedRecordStage
+        seng._stage = SharedRecordStage(seng.group, seng.rank, seng.world, seng.ROOT, timeout=120)
+        if not seng._stage.probe(eng.lib, cdev, True):
+            stage = {'skipped': 'a rank could not page-lock a shared-memory segment'}
+    if world > 1 and not args.no_output_stage and stage is None:
         seng.profile_fetch = False
         pend, moved = [], []
         for i in range(2):                        # warm: maps and registers the slots

@@ -314,6 +314,33 @@ class SharedRecordStage:
         return StageFetch(self, slot, epoch, ev, off, total, ids_dtype,
                           self.rank == self.root, n * (ib + 2))
 
+    def probe(self, lib, comm_dev, on_gpu):
+        """Whether every rank can map a shared segment and page-lock it for device
+        stores (one 1-element all-reduce): a caller that cannot rely on the stage (a
+        benchmark pass) checks this first, so no rank is left in a collective alone."""
+        import ctypes
+        import tempfile
+        import torch.distributed as dist
+        ok = 1
+        try:
+            fd, path = tempfile.mkstemp(prefix='oa_probe_', dir=_shm_dir())
+            os.ftruncate(fd, 1 << 16)
+            mm = mmap.mmap(fd, 1 << 16, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+            os.close(fd)
+            os.unlink(path)
+            if on_gpu:
+                base = np.frombuffer(mm, dtype=np.uint8).ctypes.data
+                p = ctypes.c_void_p()
+                if lib.oa_host_register(ctypes.c_void_p(base), 1 << 16, ctypes.byref(p)) != 0:
+                    ok = 0
+                else:
+                    lib.oa_host_unregister(ctypes.c_void_p(base))
+        except Exception:
+            ok = 0
+        t = torch.tensor([ok], dtype=torch.int32).to(comm_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(int(t.item()))
+
     def _rank_by_row(self, rows, n_rows, comm_dev):
         """Every record's position among all ranks' records ordered by global previous
         row: bits of the rows each rank holds, OR-ed over the ranks by one all-reduce

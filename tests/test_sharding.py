@@ -447,6 +447,7 @@ def _stage_worker(rank, world, port, outdir, presharded):
         n_rows = int(blk.sum())
         perm = rng.permutation(n_rows)
         stage = SharedRecordStage(None, rank, world)
+        assert stage.probe(None, torch.device('cpu'), False)
         for it in range(3):
             ids_all, key_all, cnt = [], [], np.zeros((world, S), np.int64)
             mine_rows = []
