@@ -48,7 +48,7 @@ prof)
   rc=$?; python3 tools/kstats.py "$O/prof_$T" | head -8
   python3 tools/trace_window.py "$O/prof_$T" ${RAMP:-30} ${WARM:-5} ${STEPS_T:-20} "$O/trace_window_$T.json"; ok $rc prof ;;
 pmc)
-  TAG=$T PMC_FILE=$R/tools/pmc_bytes.txt bash tools/pmc.sh > "$O/pmc_$T.out" 2>&1
+  TAG=$T PMC_FILE=${PMC_FILE:-$R/tools/pmc_bytes.txt} bash tools/pmc.sh > "$O/pmc_$T.out" 2>&1
   rc=$?; tail -3 "$O/pmc_$T.out"; ok $rc pmc
   N0=$(grep -o 'particles_per_step_per_gpu": [0-9]*' "$O/bench_prof_$T.json" 2>/dev/null | grep -o '[0-9]*$' || true)
   python3 tools/pmc_summary.py "$O/pmc_$T" "${N0:-99998874}" "$O/pmc_k_step_$T.json"; ok $? pmc_summary ;;
