@@ -37,6 +37,16 @@ def main():
     if len(sys.argv) > 5:
         with open(sys.argv[5], 'w') as fo:
             json.dump(res, fo, indent=1)
+        # the timed window in rocprofv3's kernel_stats.csv columns (one row)
+        if timed:
+            ns = [int(round(x * 1e6)) for x in timed]
+            with open(os.path.splitext(sys.argv[5])[0] + '_kernel_stats_timed.csv', 'w') as fo:
+                w = csv.writer(fo, quoting=csv.QUOTE_NONNUMERIC)
+                w.writerow(['Name', 'Calls', 'TotalDurationNs', 'AverageNs', 'MinNs', 'MaxNs',
+                            'Window'])
+                w.writerow([res['kernel'], len(ns), sum(ns), sum(ns) / len(ns), min(ns), max(ns),
+                            'dispatches %d..%d of %d (after %d ramp + warm-up launches)'
+                            % (a, a + len(ns) - 1, len(d), a)])
     print(json.dumps({k: v for k, v in res.items() if k != 'durations_ms'}))
 
 
