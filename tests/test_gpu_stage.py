@@ -1,0 +1,69 @@
+"""The multi-GPU output stage's device pieces on one GPU (host_share.py): a shared-memory
+segment page-locked for device stores, ``oa_place_records`` storing records at their
+positions through the mapping's device address (positions outside the buffer dropped
+and counted), and ``oa_stream_set_flag`` publishing an epoch once the stream's work is
+done.  The collective protocol around them is covered at world 2 / 3 on CPU
+(tests/test_sharding.py) and through ``track_orbits`` at world 2 on this GPU
+(tests/test_gpu_multi_configs.py)."""
+import ctypes
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize('ib', [8, 4])
+def test_place_records_into_shared_host_buffer(ib, tmp_path):
+    import torch
+    from orbitanalysis_amd import _native as N
+    from orbitanalysis_amd.host_share import _Slot
+    lib = N.load(require_device=True)
+    dev = torch.device('cuda', 0)
+    rng = np.random.default_rng(ib)
+    cap, n = 1 << 16, 40000
+    import os
+    from orbitanalysis_amd.host_share import _shm_dir
+    slot = _Slot(os.path.join(_shm_dir(), 'oa_test_%d_%d' % (os.getpid(), ib)), 2, cap, ib,
+                 create=True)
+    base = slot.register(lib)
+    try:
+        idt = np.int64 if ib == 8 else np.int32
+        ids = rng.integers(-2 ** 30, 2 ** 30, n).astype(idt)
+        ang = rng.integers(-2 ** 15, 2 ** 15, n).astype(np.int16)
+        dst = rng.permutation(cap)[:n].astype(np.int64)
+        bad = rng.choice(n, 37, replace=False)
+        dst[bad[:20]] = cap + rng.integers(0, 100, 20)      # past the buffer
+        dst[bad[20:]] = -1 - rng.integers(0, 100, 17)       # before it
+        slot.ids[:] = 0
+        slot.ang[:] = 0
+        t_ids, t_ang, t_dst = (torch.from_numpy(x).to(dev) for x in (ids, ang, dst))
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        N.check(lib.oa_place_records(ctypes.c_void_p(t_ids.data_ptr()),
+                                     ctypes.c_void_p(t_ang.data_ptr()),
+                                     ctypes.c_void_p(t_dst.data_ptr()), n, ib,
+                                     ctypes.c_void_p(base + slot.ids_off),
+                                     ctypes.c_void_p(base + slot.ang_off), cap,
+                                     ctypes.c_void_p(status.data_ptr()), st),
+                'oa_place_records')
+        flag = slot.flag(1)
+        flag[0] = 0
+        N.check(lib.oa_stream_set_flag(st, ctypes.c_void_p(flag.ctypes.data), 12345),
+                'oa_stream_set_flag')
+        t_end = time.time() + 30
+        while int(flag[0]) != 12345:                   # the host callback, not a sync
+            assert time.time() < t_end, 'the stream flag was never set'
+            time.sleep(1e-4)
+        torch.cuda.synchronize()
+        assert int(status.item()) > 0                  # out-of-range records counted
+        good = np.ones(n, bool)
+        good[bad] = False
+        assert np.array_equal(slot.ids[dst[good]], ids[good])
+        assert np.array_equal(slot.ang[dst[good]], ang[good])
+        untouched = np.ones(cap, bool)
+        untouched[dst[good]] = False
+        assert not slot.ids[untouched].any() and not slot.ang[untouched].any()
+    finally:
+        slot.release(lib)
