@@ -429,7 +429,9 @@ int oa_stream_set_flag(void *stream, int64_t *host_addr, int64_t value);
 
 /* out_ids[dst[i]] = ids[i] (id_bytes 4 or 8 each), out_ang[dst[i]] = ang[i] for
  * i < n; dst values must lie in [0, cap) (a record outside is dropped and counted in
- * *status).  The outputs may be host memory from oa_host_register (zero-copy stores). */
+ * *status).  The outputs may be host memory from oa_host_register (zero-copy stores).
+ * ids and out_ids may both be NULL: the 16-bit values alone (checkpoint angles at their
+ * global snapshot rows, track_orbits.py:390-394). */
 int oa_place_records(const void *ids, const uint16_t *ang, const int64_t *dst, int64_t n,
                      int32_t id_bytes, void *out_ids, uint16_t *out_ang, int64_t cap,
                      int32_t *status, void *stream);

@@ -2688,7 +2688,7 @@ __global__ __launch_bounds__(256) void k_place_records(const ID *ids, const uint
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int64_t i = i0 + u * 256, ic = i < n ? i : n - 1;
-        v[u] = __builtin_nontemporal_load(ids + ic);
+        v[u] = ids ? __builtin_nontemporal_load(ids + ic) : (ID)0;
         g[u] = __builtin_nontemporal_load(ang + ic);
         d[u] = __builtin_nontemporal_load(dst + ic);
     }
@@ -2697,7 +2697,7 @@ __global__ __launch_bounds__(256) void k_place_records(const ID *ids, const uint
     for (int u = 0; u < U; ++u) {
         if (i0 + u * 256 >= n) break;
         if (d[u] < 0 || d[u] >= cap) { bad = true; continue; }
-        out_ids[d[u]] = v[u];
+        if (out_ids) out_ids[d[u]] = v[u];
         out_ang[d[u]] = g[u];
     }
     if (bad && status) atomicAdd(status, 1);
@@ -2846,7 +2846,8 @@ int oa_place_records(const void *ids, const uint16_t *ang, const int64_t *dst, i
                      int32_t *status, void *stream) {
     g_err[0] = 0;
     if (n <= 0) return OA_OK;
-    if (!ids || !ang || !dst || !out_ids || !out_ang || cap < 0 || (id_bytes != 4 && id_bytes != 8))
+    if (!ang || !dst || !out_ang || cap < 0 || (id_bytes != 4 && id_bytes != 8) ||
+        (!ids != !out_ids))
         return fail(OA_E_ARG, "oa_place_records: bad arguments");
     const unsigned grid = (unsigned)((n + 1023) / 1024);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);

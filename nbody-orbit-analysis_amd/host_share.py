@@ -69,6 +69,7 @@ class _Slot:
         self.base = buf.ctypes.data
         self.hdr = buf[:self.hdr_bytes].view(np.int64)
         o = self.hdr_bytes
+        # ib = 0: a slot of 16-bit values alone (checkpoint angles)
         self.ids = buf[o:o + self.cap * self.ib].view(np.int64 if self.ib == 8 else np.int32)
         self.ang_off = o + ids_bytes
         self.ang = buf[self.ang_off:self.ang_off + 2 * self.cap].view(np.int16)
@@ -313,6 +314,60 @@ class SharedRecordStage:
                            else 'presharded')
         return StageFetch(self, slot, epoch, ev, off, total, ids_dtype,
                           self.rank == self.root, n * (ib + 2))
+
+    def place_rows(self, lib, vals, rows, n_total, comm_dev):
+        """Checkpoint angles (track_orbits.py:390-394): this rank's f16 bits ``vals`` at
+        their global snapshot rows ``rows`` (every row held by exactly one rank) into a
+        shared buffer of ``n_total`` angles (a slot without an ID region); returns the
+        float16 array on rank 0 (a view of the buffer, the slot busy while it lives),
+        None elsewhere.  Synchronous: each rank's stores are done before its epoch is
+        published."""
+        import ctypes
+        self.lib = lib
+        self.epoch += 1
+        epoch = self.epoch
+        dev = vals.device
+        slot = self._agree(int(n_total), 0, comm_dev)
+        n = int(vals.shape[0])
+        if dev.type == 'cuda':
+            from . import _native as N
+            if self.status is None:
+                self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+            base = slot.register(lib)
+            v16 = vals.to(torch.int16).contiguous()
+            r64 = rows.to(dev).to(torch.int64).contiguous()
+            st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            N.check(lib.oa_place_records(None, ctypes.c_void_p(v16.data_ptr()),
+                                         ctypes.c_void_p(r64.data_ptr()), n, 8, None,
+                                         ctypes.c_void_p(base + slot.ang_off), slot.cap,
+                                         ctypes.c_void_p(self.status.data_ptr()), st),
+                    'oa_place_records')
+            torch.cuda.current_stream(dev).synchronize()
+            if int(self.status.item()):
+                raise RuntimeError('checkpoint angles: rows outside the snapshot')
+        elif n:
+            r = rows.numpy().astype(np.int64)
+            if r.min() < 0 or r.max() >= slot.cap:
+                raise RuntimeError('checkpoint angles: rows outside the snapshot')
+            slot.ang[r] = vals.numpy().astype(np.int64).astype(np.uint16).view(np.int16)
+        slot.flag(self.rank)[0] = epoch
+        if self.rank != self.root:
+            return None
+        t_end = time.time() + self.timeout
+        while not all(int(slot.flag(q)[0]) == epoch for q in range(self.world)):
+            if time.time() > t_end:
+                raise RuntimeError('checkpoint angles: a rank did not store its angles within '
+                                   '%.0f s' % self.timeout)
+            time.sleep(2e-5)
+        if slot.linked:
+            self._unlink(slot)
+        slot.busy -= 1                    # in flight since _choose
+        if not n_total:
+            return np.zeros(0, np.float16)
+        h = (ctypes.c_char * (2 * int(n_total))).from_buffer(slot.mm, slot.ang_off)
+        slot.busy += 1
+        weakref.finalize(h, self._free, slot)
+        return np.frombuffer(h, dtype=np.float16)
 
     def probe(self, lib, comm_dev, on_gpu):
         """Whether every rank can map a shared segment and page-lock it for device

@@ -21,16 +21,18 @@ particle's current and previous rows -- including its copies in overlapping regi
 * **step**: the rank's ``OrbitEngine`` on its shard; the kernel also emits each apsis
   record's previous-state row, which maps to its global previous-block position
   through the previous snapshot's gpos (a device gather).
-* **records** stay on the device as (halo slot << 32 | gpos, ID, f16 angle) until the
-  savefile needs them: ``fetch`` gathers them to rank 0 -- the only writer -- and
-  sorts them there by key, which is exactly the reference's order (previous-block
-  order within each halo, halos in ``halo_exists`` order, track_orbits.py:199-227,
-  315-316).
+* **records** stay on the device until the savefile needs them: ``fetch_async``
+  has every rank store its own records at their final positions in one page-locked
+  host buffer that all ranks map (``host_share.SharedRecordStage``), which is exactly
+  the reference's order (previous-block order within each halo, halos in
+  ``halo_exists`` order, track_orbits.py:199-227, 315-316); rank 0, the only writer,
+  hands that buffer to the savefile.
 
 Collectives per snapshot: the shard's all-to-all (not with presharded loaders), one
 all-gather of the halo catalogue rows (centre, bulk velocity), an all-gather of the
-computed bulk velocities when the catalogue gives none, and the records' gather to
-rank 0.  None of them exchanges per-particle data with every rank.
+computed bulk velocities when the catalogue gives none, and the output stage's count
+all-gather and slot broadcast (with stripes, one all-reduce of a previous-row bitmap).
+None of them exchanges per-particle data with every rank.
 
 ``ShardedEngine`` exposes the ``OrbitEngine`` interface the driver uses, so
 ``track_orbits(..., engine=ShardedEngine(EngineLocal(OrbitEngine())))`` is the
@@ -341,16 +343,6 @@ def _f64_bits(x):
     return np.ascontiguousarray(x, dtype=np.float64).view(np.int64)
 
 
-def _sync_time(on):
-    """A synchronised timestamp (profiling only; 0 when off)."""
-    if not on:
-        return 0.0
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
-    import time
-    return time.perf_counter()
-
-
 def _to_tensor(x, device):
     """A row range of a loader array -> tensor on ``device`` (uint dtypes bit-cast)."""
     if isinstance(x, torch.Tensor):
@@ -507,33 +499,6 @@ class ShardedFetch:
             self.done.synchronize()
         return (self.h_off.numpy().astype(np.int64), ids_as(self.h_ids.numpy(), dt),
                 self.h_ang.numpy().view(np.float16))
-
-
-def place_presharded(C, off, n):
-    """Output positions of the records gathered from the ranks of a presharded run.
-    ``C`` (W, S): rank r's records per halo slot, received rank-major and slot-major
-    within a rank; ``off`` (S + 1): the merged offsets.  A halo's global previous block
-    is the rank-major concatenation of the ranks' blocks, so its records from rank r
-    follow those from ranks < r, each rank's in its own (previous-block) order: a
-    per-(rank, slot) count scan places them, no sort."""
-    W, S = C.shape
-    flat = C.reshape(-1)
-    seg0 = torch.cumsum(flat, 0) - flat                         # (r, h) run start, received
-    before = torch.cumsum(C, 0) - C                             # ranks < r in slot h
-    D = (off[:S].unsqueeze(0) + before).reshape(-1) - seg0
-    return torch.arange(n, dtype=torch.int64, device=C.device) + \
-        torch.repeat_interleave(D, flat, output_size=n)
-
-
-def place_by_row(rows, n_rows):
-    """Output positions of records keyed by their global previous-snapshot row (the
-    stripe layout: a halo's records from different ranks interleave).  The reference's
-    order is increasing previous row (slots follow the previous blocks' order, and each
-    slot's records its block's order), so a record's position is the number of keyed rows
-    before it: a counting pass over the previous snapshot's rows (O(rows), no sort)."""
-    flags = torch.zeros(max(int(n_rows), 1), dtype=torch.int8, device=rows.device)
-    flags[rows.long()] = 1
-    return (torch.cumsum(flags, 0, dtype=torch.int32)[rows.long()] - 1).long()
 
 
 @dataclass
@@ -866,59 +831,34 @@ class ShardedEngine:
                     if hasattr(self.local, 'records_consumed'):
                         self.local.records_consumed(lp, ev)
             return f
+        # world 1: this rank's records are the whole output and already in the
+        # reference's order (its shard is the snapshot): one D2H into reused page-locked
+        # blocks, no placement
         with ctx:
             if side is not None and done is not None:
                 side.wait_event(done)
                 done.synchronize()                # the record count's host copy (launch)
             total = self.local.total(lp) if hasattr(self.local, 'total') else int(offs[-1])
-            cnt = (offs[1:S + 1] - offs[:S]).to(torch.int64).reshape(1, S)
-            send = [a_ids[:total], a_ang[:total].to(torch.int16)]
-            rows = None
-            if not self.presharded:
-                pp = res.prev_prep
-                rows = pp.sel[a_pos[:total].to(pp.sel.device).long()]
-                n_rows = int(pp.n_global)
-                send.append(rows.to(torch.int32 if n_rows < 2 ** 31 else torch.int64).to(dev))
-            C, = gather_rows(self.group, self.ROOT, cnt)
-            got = gather_rows(self.group, self.ROOT, *send)
             ev = None
-            h_off = h_ids = h_ang = None
-            if root:
-                t0 = _sync_time(prof)
-                ids_r, ang_r = got[0], got[1]
-                n = int(ids_r.shape[0])
-                C = C.to(ids_r.device)
-                off = torch.zeros(S + 1, dtype=torch.int64, device=ids_r.device)
-                off[1:] = torch.cumsum(C.sum(0), 0)
-                if n:
-                    dst = place_presharded(C, off, n) if self.presharded else \
-                        place_by_row(got[2], n_rows)
-                    out_ids = torch.empty_like(ids_r)
-                    out_ang = torch.empty_like(ang_r)
-                    out_ids[dst] = ids_r
-                    out_ang[dst] = ang_r
-                else:
-                    out_ids, out_ang = ids_r, ang_r
-                t1 = _sync_time(prof)
-                pin = out_ids.device.type == 'cuda'
-                if pin:
-                    # power-of-two page-locked blocks reused across snapshots (engine)
-                    from .engine import _pinned
-                    h_off = _pinned(S + 1, torch.int64)
-                    h_ids = _pinned(n, out_ids.dtype)
-                    h_ang = _pinned(n, torch.int16)
-                else:
-                    h_off = torch.empty(S + 1, dtype=torch.int64)
-                    h_ids = torch.empty(n, dtype=out_ids.dtype)
-                    h_ang = torch.empty(n, dtype=torch.int16)
-                h_off.copy_(off, non_blocking=pin)
-                h_ids.copy_(out_ids, non_blocking=pin)
-                h_ang.copy_(out_ang, non_blocking=pin)
-                if prof:
-                    self.fetch_stats = dict(
-                        records=n, merge_ms=(t1 - t0) * 1e3,
-                        bytes_per_record=sum(t.element_size() for t in send),
-                        layout='presharded' if self.presharded else 'stripes')
+            pin = offs.device.type == 'cuda'
+            if pin:
+                from .engine import _pinned
+                h_off = _pinned(S + 1, torch.int64)
+                h_ids = _pinned(total, a_ids.dtype)
+                h_ang = _pinned(total, torch.int16)
+            else:
+                h_off = torch.empty(S + 1, dtype=torch.int64)
+                h_ids = torch.empty(total, dtype=a_ids.dtype)
+                h_ang = torch.empty(total, dtype=torch.int16)
+            h_off.copy_(offs[:S + 1].to(torch.int64), non_blocking=pin)
+            h_ids.copy_(a_ids[:total], non_blocking=pin)
+            h_ang.copy_(a_ang[:total].view(torch.int16) if a_ang.dtype != torch.int16
+                        else a_ang[:total], non_blocking=pin)
+            if prof:
+                self.fetch_stats = dict(records=total, own_records=total, place_ms=0.0,
+                                        bytes_moved=total * (a_ids.element_size() + 2),
+                                        bytes_per_record=a_ids.element_size() + 2,
+                                        layout='presharded' if self.presharded else 'stripes')
             if side is not None:
                 ev = torch.cuda.Event()
                 ev.record(side)
@@ -934,10 +874,19 @@ class ShardedEngine:
         return res.bulk
 
     def angles(self):
-        """Global float16 angle state in current-snapshot order (checkpoint payload),
-        gathered to rank 0; None on the other ranks."""
+        """Global float16 angle state in current-snapshot order (checkpoint payload) on
+        rank 0, None on the other ranks.  World > 1: every rank stores its angles at
+        their global rows in one shared page-locked buffer (``host_share``), so no rank's
+        angles cross another rank's link."""
         self.settle()
         p = self.prev
+        if self.world > 1:
+            from .host_share import SharedRecordStage
+            if self._stage is None:
+                self._stage = SharedRecordStage(self.group, self.rank, self.world, self.ROOT)
+            vals = self.local.angles_tensor()
+            lib = getattr(getattr(self.local, 'engine', None), 'lib', None)
+            return self._stage.place_rows(lib, vals, p.sel, p.n_global, _comm_device())
         loc = self.local.angles_tensor().to(torch.int64)
         rows = torch.stack([p.sel.to(loc.device), loc], dim=1) if loc.numel() else \
             torch.zeros((0, 2), dtype=torch.int64, device=loc.device)

@@ -364,45 +364,6 @@ def test_salvage_starts_no_collective_fetch():
     assert sorted(out.groups) == ['snapshot_004'] and len(groups) == 1
 
 
-@pytest.mark.parametrize('seed', [0, 1, 2])
-def test_record_placement_equals_sorted_merge(seed):
-    """Rank 0's placement of the gathered records (sharding.place_presharded /
-    place_by_row) equals the sort of the records by (slot, global previous row), the
-    round-4 merge, for random per-rank runs."""
-    import torch
-    from orbitanalysis_amd.sharding import place_presharded, place_by_row
-    rng = np.random.default_rng(seed)
-    W, S = int(rng.integers(1, 5)), int(rng.integers(1, 40))
-    blk = rng.integers(0, 60, size=(W, S))                 # rank r's rows of prev block h
-    gstart = np.concatenate([[0], np.cumsum(blk.sum(0))])[:-1]
-    before = np.cumsum(blk, 0) - blk
-    keys, C = [], np.zeros((W, S), np.int64)
-    for r in range(W):                                      # presharded: rank-major blocks
-        for h in range(S):
-            pos = np.sort(rng.choice(blk[r, h], size=rng.integers(0, blk[r, h] + 1),
-                                     replace=False)) if blk[r, h] else np.zeros(0, np.int64)
-            C[r, h] = len(pos)
-            keys.append(gstart[h] + before[r, h] + pos)
-    key = np.concatenate(keys).astype(np.int64)
-    n = len(key)
-    off = torch.zeros(S + 1, dtype=torch.int64)
-    off[1:] = torch.cumsum(torch.from_numpy(C).sum(0), 0)
-    dst = place_presharded(torch.from_numpy(C), off, n).numpy()
-    want = np.empty(n, np.int64)
-    want[np.argsort(key, kind='stable')] = np.arange(n)
-    assert np.array_equal(dst, want)
-    # stripes: each rank's rows of a block are any subset, runs sorted within a rank
-    perm = rng.permutation(int(blk.sum()))
-    own = perm % W
-    keys = [np.flatnonzero(own == r) for r in range(W)]
-    keep = [k[rng.uniform(size=len(k)) < 0.4] for k in keys]
-    rows = np.concatenate(keep).astype(np.int32)
-    dst = place_by_row(torch.from_numpy(rows), int(blk.sum())).numpy()
-    want = np.empty(len(rows), np.int64)
-    want[np.argsort(rows, kind='stable')] = np.arange(len(rows))
-    assert np.array_equal(dst, want)
-
-
 def test_nccl_wire_dtypes():
     """every tensor the sharded paths move travels in a dtype torch's NCCL
     backend maps to an RCCL type (int16 angle bits, uint dtypes as bytes), and comes
