@@ -2220,6 +2220,9 @@ __device__ __forceinline__ void part_scatter(const oa_step_args &a, const FrameK
                 __builtin_nontemporal_store(skey[s], &bkey[o]);
                 __builtin_nontemporal_store(spw[s], &bpos[o]);
                 if (!CUR) __builtin_nontemporal_store(smeta[s], &bmeta[o]);
+#ifdef OA_DIAG_PART_NORH
+                if (!CUR)   // diagnostic: no current r̂ in the bucket (wrong angles)
+#endif
                 d[0] = srh[3 * s]; d[1] = srh[3 * s + 1]; d[2] = srh[3 * s + 2];
             }
         }
@@ -2463,36 +2466,43 @@ __global__ __launch_bounds__(PART_WG) void k_part_join(const oa_step_args a) {
         for (uint32_t j0 = 0; j0 < np; j0 += (uint32_t)PART_WG * PU) {
             if (j0 || q) load_prev(q, np, j0);
             uint32_t hit[PU];
+            V3<TD> crh[PU];                             // a miss reads past the buffer: 0
 #pragma unroll
             for (int u = 0; u < PU; ++u) {
                 hit[u] = 0xFFFFFFFFu;
-                const uint32_t j = j0 + (uint32_t)u * PART_WG + tid;
-                const uint64_t key = (uint64_t)qkey[u] | hiw;
-                const uint32_t lo = (uint32_t)key;
-                if (j >= np || (KB == 8 && !nonuniform && (uint32_t)(key >> 32) != hi0)) continue;
-                if (filt && part_of(key, K) != (uint32_t)pp) continue;
-                uint32_t cs[NCAND];
-                cuckoo_slots(lo, nsl, cs);
-                uint64_t m = 0ull;
+                do {
+                    const uint32_t j = j0 + (uint32_t)u * PART_WG + tid;
+                    const uint64_t key = (uint64_t)qkey[u] | hiw;
+                    const uint32_t lo = (uint32_t)key;
+                    if (j >= np || (KB == 8 && !nonuniform && (uint32_t)(key >> 32) != hi0)) break;
+                    if (filt && part_of(key, K) != (uint32_t)pp) break;
+                    uint32_t cs[NCAND];
+                    cuckoo_slots(lo, nsl, cs);
+                    uint64_t m = 0ull;
 #pragma unroll
-                for (int c = 0; c < NCAND; ++c) {
-                    const uint64_t v = slots[cs[c]];
-                    if (!m && v && (uint32_t)v == lo && slot_pos(v) < nc &&
-                        (!nonuniform || (uint64_t)ck[slot_pos(v)] == key))
-                        m = v;
-                }
-                for (uint32_t e = 0; !m && e < nstash; ++e) {
-                    const uint64_t v = stash[e];
-                    if ((uint32_t)v == lo && (!nonuniform || (uint64_t)ck[slot_pos(v)] == key)) m = v;
-                }
-                if (m) hit[u] = slot_pos(m) | ((slot_meta(m) >> 16) << 30);
-            }
-            V3<TD> crh[PU];                             // a miss reads past the buffer: 0
-#pragma unroll
-            for (int u = 0; u < PU; ++u)
+                    for (int c = 0; c < NCAND; ++c) {
+                        const uint64_t v = slots[cs[c]];
+                        if (!m && v && (uint32_t)v == lo && slot_pos(v) < nc &&
+                            (!nonuniform || (uint64_t)ck[slot_pos(v)] == key))
+                            m = v;
+                    }
+                    for (uint32_t e = 0; !m && e < nstash; ++e) {
+                        const uint64_t v = stash[e];
+                        if ((uint32_t)v == lo && (!nonuniform || (uint64_t)ck[slot_pos(v)] == key)) m = v;
+                    }
+                    if (m) hit[u] = slot_pos(m) | ((slot_meta(m) >> 16) << 30);
+                } while (0);
+                // the gather of the matched current r̂ issued right after its lookup, so
+                // it is in flight through the next entries' lookups (1 % on configs[1])
                 crh[u] = bld3<TD, 0>(rcr, hit[u] != 0xFFFFFFFFu
                                               ? (hit[u] & 0x3FFFFFFFu) * 3 * (uint32_t)sizeof(TD)
                                               : 0x7FFFFFF0u);
+            }
+#ifdef OA_DIAG_PART_NOGATHER
+            // diagnostic: the matched current r̂ not used (wrong angles), as if no gather
+#pragma unroll
+            for (int u = 0; u < PU; ++u) crh[u] = qrh[u];
+#endif
             uint16_t rang[PU];
             uint32_t rslot[PU];
 #pragma unroll
