@@ -431,7 +431,9 @@ int oa_stream_set_flag(void *stream, int64_t *host_addr, int64_t value);
  * i < n; dst values must lie in [0, cap) (a record outside is dropped and counted in
  * *status).  The outputs may be host memory from oa_host_register (zero-copy stores).
  * ids and out_ids may both be NULL: the 16-bit values alone (checkpoint angles at their
- * global snapshot rows, track_orbits.py:390-394). */
+ * global snapshot rows, track_orbits.py:390-394).  ang and out_ang may both be NULL: the
+ * 4- or 8-byte values alone (the on-the-fly driver's IDs, or its angle changes in the
+ * coordinate dtype, track_orbits_onthefly.py:154-174). */
 int oa_place_records(const void *ids, const uint16_t *ang, const int64_t *dst, int64_t n,
                      int32_t id_bytes, void *out_ids, uint16_t *out_ang, int64_t cap,
                      int32_t *status, void *stream);

@@ -2699,7 +2699,7 @@ __global__ __launch_bounds__(256) void k_place_records(const ID *ids, const uint
     for (int u = 0; u < U; ++u) {
         const int64_t i = i0 + u * 256, ic = i < n ? i : n - 1;
         v[u] = ids ? __builtin_nontemporal_load(ids + ic) : (ID)0;
-        g[u] = __builtin_nontemporal_load(ang + ic);
+        g[u] = ang ? __builtin_nontemporal_load(ang + ic) : (uint16_t)0;
         d[u] = __builtin_nontemporal_load(dst + ic);
     }
     bool bad = false;
@@ -2708,7 +2708,7 @@ __global__ __launch_bounds__(256) void k_place_records(const ID *ids, const uint
         if (i0 + u * 256 >= n) break;
         if (d[u] < 0 || d[u] >= cap) { bad = true; continue; }
         if (out_ids) out_ids[d[u]] = v[u];
-        out_ang[d[u]] = g[u];
+        if (out_ang) out_ang[d[u]] = g[u];
     }
     if (bad && status) atomicAdd(status, 1);
 }
@@ -2856,8 +2856,8 @@ int oa_place_records(const void *ids, const uint16_t *ang, const int64_t *dst, i
                      int32_t *status, void *stream) {
     g_err[0] = 0;
     if (n <= 0) return OA_OK;
-    if (!ang || !dst || !out_ang || cap < 0 || (id_bytes != 4 && id_bytes != 8) ||
-        (!ids != !out_ids))
+    if (!dst || cap < 0 || (id_bytes != 4 && id_bytes != 8) || (!ids != !out_ids) ||
+        (!ang != !out_ang) || (!ids && !ang))
         return fail(OA_E_ARG, "oa_place_records: bad arguments");
     const unsigned grid = (unsigned)((n + 1023) / 1024);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);

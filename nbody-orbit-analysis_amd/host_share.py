@@ -236,9 +236,9 @@ class SharedRecordStage:
     def fetch(self, lib, side, done, offs, a_ids, a_ang, total_local, C_local, n_slots,
               ids_dtype, rows=None, n_rows=None, comm_dev=None, profile=None):
         """Place this rank's ``total_local`` records (device tensors ``a_ids``,
-        ``a_ang``; per-slot counts ``C_local``) into the shared buffer.  ``rows``: the
-        records' global previous rows (stripe layout), else presharded.  Returns a
-        ``StageFetch``."""
+        ``a_ang``, which may be None: IDs alone; per-slot counts ``C_local``) into the
+        shared buffer.  ``rows``: the records' global previous rows (stripe layout), else
+        presharded.  Returns a ``StageFetch``."""
         import torch.distributed as dist
         self.lib = lib
         self.epoch += 1
@@ -278,7 +278,7 @@ class SharedRecordStage:
                                         torch.from_numpy(loc_h).to(dev), output_size=n) if n else \
                 torch.zeros(0, dtype=torch.int64, device=dev)
         else:
-            dst = self._rank_by_row(rows[:n].to(torch.int64), int(n_rows), comm_dev).to(dev)
+            dst = self._rank_by_row(rows[:n].to(dev).to(torch.int64), int(n_rows), comm_dev)
         # 4. the stores, and this rank's epoch in the header when they are done
         if on_gpu:
             import ctypes
@@ -287,10 +287,13 @@ class SharedRecordStage:
             base = slot.register(lib)
             st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
             from . import _native as N
+            has_ang = a_ang is not None
             N.check(lib.oa_place_records(
-                ctypes.c_void_p(a_ids.data_ptr()), ctypes.c_void_p(a_ang.data_ptr()),
+                ctypes.c_void_p(a_ids.data_ptr()),
+                ctypes.c_void_p(a_ang.data_ptr()) if has_ang else None,
                 ctypes.c_void_p(dst.data_ptr()), n, ib,
-                ctypes.c_void_p(base + slot.ids_off), ctypes.c_void_p(base + slot.ang_off),
+                ctypes.c_void_p(base + slot.ids_off),
+                ctypes.c_void_p(base + slot.ang_off) if has_ang else None,
                 slot.cap, ctypes.c_void_p(self.status.data_ptr()), st), 'oa_place_records')
             flag = slot.flag(self.rank)
             N.check(lib.oa_stream_set_flag(st, ctypes.c_void_p(flag.ctypes.data), epoch),
@@ -303,17 +306,19 @@ class SharedRecordStage:
                 if d.min() < 0 or d.max() >= slot.cap:
                     raise RuntimeError('sharded records: positions outside the output')
                 slot.ids[d] = a_ids[:n].numpy().view(slot.ids.dtype)
-                slot.ang[d] = a_ang[:n].numpy().view(np.int16)
+                if a_ang is not None:
+                    slot.ang[d] = a_ang[:n].numpy().view(np.int16)
             slot.flag(self.rank)[0] = epoch
             ev = None
         if profile is not None:
             if on_gpu:
                 torch.cuda.current_stream(dev).synchronize()
             profile.update(records=total, own_records=n, place_ms=(time.perf_counter() - t0) * 1e3,
-                           bytes_moved=n * (ib + 2), layout='stripes' if rows is not None
+                           bytes_moved=n * (ib + (2 if a_ang is not None else 0)),
+                           layout='stripes' if rows is not None
                            else 'presharded')
         return StageFetch(self, slot, epoch, ev, off, total, ids_dtype,
-                          self.rank == self.root, n * (ib + 2))
+                          self.rank == self.root, n * (ib + (2 if a_ang is not None else 0)))
 
     def place_rows(self, lib, vals, rows, n_total, comm_dev):
         """Checkpoint angles (track_orbits.py:390-394): this rank's f16 bits ``vals`` at
@@ -351,23 +356,80 @@ class SharedRecordStage:
                 raise RuntimeError('checkpoint angles: rows outside the snapshot')
             slot.ang[r] = vals.numpy().astype(np.int64).astype(np.uint16).view(np.int16)
         slot.flag(self.rank)[0] = epoch
+        return self._collect(slot, epoch, slot.ang_off, int(n_total), np.float16,
+                             'checkpoint angles')
+
+    def place_ranked(self, lib, vals, rows, n_rows, comm_dev):
+        """The on-the-fly angle changes (track_orbits_onthefly.py:154-174): this rank's
+        values ``vals`` (4- or 8-byte elements, device or CPU) among every rank's,
+        ordered by their global previous rows ``rows`` (disjoint over the ranks, in
+        [0, n_rows)).  A bitmap rank gives each value its position and every rank the
+        total; each rank stores its values there, over its own link.  Returns the values
+        (``vals``' dtype) on rank 0, a view of the buffer (the slot busy while it lives);
+        None elsewhere.  Synchronous."""
+        import ctypes
+        self.lib = lib
+        self.epoch += 1
+        epoch = self.epoch
+        dev = vals.device
+        n = int(vals.shape[0])
+        dst, total = self._rank_by_row(rows[:n].to(dev).to(torch.int64), int(n_rows), comm_dev,
+                                       with_total=True)
+        ib = vals.element_size()
+        if ib not in (4, 8):
+            raise ValueError('place_ranked: 4- or 8-byte values, got %d bytes' % ib)
+        slot = self._agree(total, ib, comm_dev)
+        if total > slot.cap:
+            raise RuntimeError('sharded outputs: %d values, output capacity %d'
+                               % (total, slot.cap))
+        if dev.type == 'cuda':
+            from . import _native as N
+            if self.status is None:
+                self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+            base = slot.register(lib)
+            v = vals.contiguous()
+            d = dst.contiguous()
+            st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            N.check(lib.oa_place_records(ctypes.c_void_p(v.data_ptr()), None,
+                                         ctypes.c_void_p(d.data_ptr()), n, ib,
+                                         ctypes.c_void_p(base + slot.ids_off), None, slot.cap,
+                                         ctypes.c_void_p(self.status.data_ptr()), st),
+                    'oa_place_records')
+            torch.cuda.current_stream(dev).synchronize()
+            if int(self.status.item()):
+                raise RuntimeError('sharded outputs: values outside the output')
+        elif n:
+            d = dst.numpy()
+            if d.min() < 0 or d.max() >= slot.cap:
+                raise RuntimeError('sharded outputs: values outside the output')
+            slot.ids[d] = vals.numpy().view(slot.ids.dtype)
+        slot.flag(self.rank)[0] = epoch
+        return self._collect(slot, epoch, slot.ids_off, total,
+                             torch.empty(0, dtype=vals.dtype).numpy().dtype, 'sharded outputs')
+
+    def _collect(self, slot, epoch, off, n, dtype, what):
+        """Rank 0 of a synchronous placement: wait for every rank's epoch, then the first
+        ``n`` values of ``dtype`` at byte ``off`` of the slot as an array backed by a ctypes
+        holder (the slot stays busy while it lives); None on the other ranks."""
+        import ctypes
         if self.rank != self.root:
             return None
         t_end = time.time() + self.timeout
         while not all(int(slot.flag(q)[0]) == epoch for q in range(self.world)):
             if time.time() > t_end:
-                raise RuntimeError('checkpoint angles: a rank did not store its angles within '
-                                   '%.0f s' % self.timeout)
+                raise RuntimeError('%s: a rank did not store its values within %.0f s'
+                                   % (what, self.timeout))
             time.sleep(2e-5)
         if slot.linked:
             self._unlink(slot)
         slot.busy -= 1                    # in flight since _choose
-        if not n_total:
-            return np.zeros(0, np.float16)
-        h = (ctypes.c_char * (2 * int(n_total))).from_buffer(slot.mm, slot.ang_off)
+        dt = np.dtype(dtype)
+        if not n:
+            return np.zeros(0, dt)
+        h = (ctypes.c_char * (int(n) * dt.itemsize)).from_buffer(slot.mm, off)
         slot.busy += 1
         weakref.finalize(h, self._free, slot)
-        return np.frombuffer(h, dtype=np.float16)
+        return np.frombuffer(h, dtype=dt)
 
     def probe(self, lib, comm_dev, on_gpu):
         """Whether every rank can map a shared segment and page-lock it for device
@@ -396,24 +458,30 @@ class SharedRecordStage:
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
         return bool(int(t.item()))
 
-    def _rank_by_row(self, rows, n_rows, comm_dev):
+    def _rank_by_row(self, rows, n_rows, comm_dev, with_total=False):
         """Every record's position among all ranks' records ordered by global previous
         row: bits of the rows each rank holds, OR-ed over the ranks by one all-reduce
-        (the ranks' rows are disjoint: a byte sum is the OR), then prefix popcounts."""
+        (the ranks' rows are disjoint: a byte sum is the OR), then prefix popcounts.
+        The bitmap is built and ranked on the rows' device; only its bytes travel
+        through ``comm_dev``.  ``with_total``: also the number of records over all
+        ranks."""
         import torch.distributed as dist
         nb = max((n_rows + 7) // 8, 1)
-        cpu = torch.device(comm_dev).type == 'cpu'
-        r = rows.to(comm_dev)
-        bits = torch.zeros(nb, dtype=torch.int32, device=comm_dev)
+        dev = rows.device
+        r = rows.to(torch.int64)
+        bits = torch.zeros(nb, dtype=torch.int32, device=dev)
         bits.index_add_(0, r >> 3, (1 << (r & 7)).to(torch.int32))
-        b = bits if cpu else bits.to(torch.uint8)
+        b = bits.to(torch.uint8).to(comm_dev)
         dist.all_reduce(b, op=dist.ReduceOp.SUM, group=self.group)
-        lut = torch.from_numpy(_POP8).to(comm_dev)
-        bl = b.long()
+        bl = b.to(dev).long()
+        lut = torch.from_numpy(_POP8).to(dev)
         pc = lut[bl]
         pre = torch.cumsum(pc, 0) - pc
         byte = r >> 3
-        return pre[byte] + lut[bl[byte] & ((1 << (r & 7)) - 1)]
+        pos = pre[byte] + lut[bl[byte] & ((1 << (r & 7)) - 1)]
+        if with_total:
+            return pos, int((pre[-1] + pc[-1]).item())
+        return pos
 
     def close(self):
         for s in self.slots.values():

@@ -478,12 +478,12 @@ class ShardedOnTheFly:
     rank's stripe on the device (``stripes``: a double-buffered reader, as
     ``tools/bench_onthefly.py --sharded``) skips the upload.
 
-    The outputs stay on the devices: every rank's records -- apsis (global previous
-    row, ID), angle changes (global previous row, value), departed (halo, ID), entered
-    (halo, ID, global current row) -- are gathered to rank 0, the only writer, and
-    merged there with device sorts (``merge_onthefly``) into exactly the
-    single-process file.  Ranks other than 0 return the per-halo tables with empty
-    record arrays.
+    Outputs, into exactly the single-process file on rank 0, the only writer: apsis IDs
+    and angle changes (by global previous row) are stored by every rank straight into
+    shared page-locked host buffers (``_stage_outputs``, ``host_share``; world > 1);
+    departed (halo, ID) and entered (halo, ID, global current row) rows are gathered to
+    rank 0 and merged there with device sorts (``merge_onthefly``).  Ranks other than 0
+    return the per-halo tables with empty record arrays.
 
     ``track_orbits(..., engine=ShardedOnTheFly(OrbitEngine(mode=...)))``."""
 
@@ -495,6 +495,10 @@ class ShardedOnTheFly:
         self.mode = engine.mode
         self.group = group
         self.owner = owner if owner is not None else IdRangeOwner()
+        # world > 1: apsis IDs and angle changes go into the shared host buffer
+        # (host_share.SharedRecordStage); ORBIT_OTF_STAGE=0 gathers them to rank 0
+        self.use_stage = os.environ.get('ORBIT_OTF_STAGE', '1') != '0'
+        self._stage = None
         engine.emit_positions = True
         self.otf = OnTheFly(engine)
         self.carry = None
@@ -621,22 +625,30 @@ class ShardedOnTheFly:
         entered = torch.stack([_halo_of(erow, pc.starts, eng.device),
                                _i64(pc.snap['ids'][erow]), sel_c[erow]], dim=1)
         self._mark('records')
+        sl1 = np.asarray(slices[1], dtype=np.int64).reshape(-1, 2)
+        p_has = (sl1[:, 1] - sl1[:, 0]) > 0            # the reference's np.diff(sl_prev) > 0
+        adt = _angles_dtype(pc.plan.coord, ids_dtype, p_has)
+        n_prev = max(int(np.max(sl1[:, 1])) if len(sl1) else 0, 0)
+        staged = None
+        if self.world > 1 and self.use_stage:
+            staged = self._stage_outputs(apsis, a_ids, angle_g, angle_v, nh,
+                                         _block_starts(sl1, n_prev), n_prev, ids_dtype)
+            apsis = apsis[:0]
+            angle_g, angle_v = angle_g[:0], angle_v[:0]
         apsis, = gather_rows(self.group, self.ROOT, apsis)
         if self.world > 1:
             angle_g, angle_v = gather_rows(self.group, self.ROOT, angle_g, angle_v)
         departed, = gather_rows(self.group, self.ROOT, departed)
         entered, = gather_rows(self.group, self.ROOT, entered)
         self._mark('gather')
-        sl1 = np.asarray(slices[1], dtype=np.int64).reshape(-1, 2)
-        p_has = (sl1[:, 1] - sl1[:, 0]) > 0            # the reference's np.diff(sl_prev) > 0
-        adt = _angles_dtype(pc.plan.coord, ids_dtype, p_has)
         if self.rank == self.ROOT:
-            n_prev = int(np.max(sl1[:, 1])) if len(sl1) else 0
             merged = merge_onthefly(dict(apsis=apsis, angle_g=angle_g if self.world > 1 else None,
                                          angle_v=angle_v, departed=departed, entered=entered),
-                                    nh, _block_starts(sl1, max(n_prev, 0)), p_has, ids_dtype,
-                                    n_prev=max(n_prev, 0), ordered=self.world == 1,
+                                    nh, _block_starts(sl1, n_prev), p_has, ids_dtype,
+                                    n_prev=n_prev, ordered=self.world == 1,
                                     lib=eng.lib)
+            if staged is not None:
+                merged['apsis_offsets'], merged['apsis_ids'], merged['angles'] = staged
             merged['angles'] = merged['angles'].astype(adt, copy=False)
         else:
             z = np.zeros(nh + 1, np.int64)
@@ -648,6 +660,45 @@ class ShardedOnTheFly:
         self._mark('merge+d2h')
         self._close_marks()
         return merged
+
+    def _stage_outputs(self, apsis, a_ids, angle_g, angle_v, nh, prev_starts, n_prev, ids_dtype):
+        """World > 1: this rank's apsis IDs and angle changes stored straight into one
+        shared page-locked host buffer each (``host_share.SharedRecordStage``), at their
+        positions among every rank's, ordered by global previous row as the reference emits
+        them (previous-block order, halos in order, :154-174): the per-halo apsis counts
+        are all-gathered, the positions come from one bitmap all-reduce per list.  Each rank
+        moves its own outputs over its own link; nothing crosses to rank 0's GPU.  Returns
+        (apsis offsets, apsis IDs, angle changes) on rank 0 (views of the buffers), None
+        elsewhere."""
+        import torch.distributed as dist
+        from .host_share import SharedRecordStage
+        from .sharding import _comm_device
+        if self._stage is None:
+            self._stage = SharedRecordStage(self.group, self.rank, self.world, self.ROOT)
+        cdev = _comm_device()
+        dev = apsis.device
+        a_rows = apsis[:, 0]
+        # a bound on every rank's global previous rows (rows after the last block included)
+        hi = max(n_prev, int(a_rows.max()) + 1 if a_rows.numel() else 0,
+                 int(angle_g.max()) + 1 if angle_g.numel() else 0)
+        m = torch.tensor([hi], dtype=torch.int64).to(cdev)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)
+        n_rows = int(m.item())
+        st = _h2d(np.asarray(prev_starts, dtype=np.int64), dev)
+        n = int(a_rows.numel())
+        if n and len(st):
+            halo = torch.searchsorted(st, a_rows.contiguous(), right=True) - 1
+            cnt = torch.bincount(halo.clamp_(min=0), minlength=nh)[:nh]
+        else:
+            cnt = torch.zeros(nh, dtype=torch.int64, device=dev)
+        lib = self.eng.lib
+        f = self._stage.fetch(lib, None, None, None, _to_loader_width(a_ids, ids_dtype), None, n,
+                              cnt, nh, ids_dtype, rows=a_rows, n_rows=n_rows, comm_dev=cdev)
+        off, ids, _ = f.wait()
+        ang = self._stage.place_ranked(lib, angle_v.contiguous(), angle_g, n_rows, cdev)
+        if self.rank != self.ROOT:
+            return None
+        return off, ids, ang
 
 
 def _i64(t):

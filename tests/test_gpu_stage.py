@@ -14,8 +14,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize('ib', [8, 4])
-def test_place_records_into_shared_host_buffer(ib, tmp_path):
+@pytest.mark.parametrize('ib,with_ang', [(8, True), (4, True), (8, False), (4, False)])
+def test_place_records_into_shared_host_buffer(ib, with_ang, tmp_path):
     import torch
     from orbitanalysis_amd import _native as N
     from orbitanalysis_amd.host_share import _Slot
@@ -25,8 +25,8 @@ def test_place_records_into_shared_host_buffer(ib, tmp_path):
     cap, n = 1 << 16, 40000
     import os
     from orbitanalysis_amd.host_share import _shm_dir
-    slot = _Slot(os.path.join(_shm_dir(), 'oa_test_%d_%d' % (os.getpid(), ib)), 2, cap, ib,
-                 create=True)
+    slot = _Slot(os.path.join(_shm_dir(), 'oa_test_%d_%d_%d' % (os.getpid(), ib, with_ang)), 2,
+                 cap, ib, create=True)
     base = slot.register(lib)
     try:
         idt = np.int64 if ib == 8 else np.int32
@@ -41,11 +41,12 @@ def test_place_records_into_shared_host_buffer(ib, tmp_path):
         t_ids, t_ang, t_dst = (torch.from_numpy(x).to(dev) for x in (ids, ang, dst))
         status = torch.zeros(1, dtype=torch.int32, device=dev)
         st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        # without angles: the 4- / 8-byte values alone (the on-the-fly driver's lists)
         N.check(lib.oa_place_records(ctypes.c_void_p(t_ids.data_ptr()),
-                                     ctypes.c_void_p(t_ang.data_ptr()),
+                                     ctypes.c_void_p(t_ang.data_ptr()) if with_ang else None,
                                      ctypes.c_void_p(t_dst.data_ptr()), n, ib,
                                      ctypes.c_void_p(base + slot.ids_off),
-                                     ctypes.c_void_p(base + slot.ang_off), cap,
+                                     ctypes.c_void_p(base + slot.ang_off) if with_ang else None, cap,
                                      ctypes.c_void_p(status.data_ptr()), st),
                 'oa_place_records')
         flag = slot.flag(1)
@@ -61,7 +62,10 @@ def test_place_records_into_shared_host_buffer(ib, tmp_path):
         good = np.ones(n, bool)
         good[bad] = False
         assert np.array_equal(slot.ids[dst[good]], ids[good])
-        assert np.array_equal(slot.ang[dst[good]], ang[good])
+        if with_ang:
+            assert np.array_equal(slot.ang[dst[good]], ang[good])
+        else:
+            assert not slot.ang.any()
         untouched = np.ones(cap, bool)
         untouched[dst[good]] = False
         assert not slot.ids[untouched].any() and not slot.ang[untouched].any()

@@ -447,6 +447,21 @@ def _stage_worker(rank, world, port, outdir, presharded):
                 assert np.array_equal(ang.view(np.int16), (key % 30000).astype(np.int16)[order])
             else:
                 assert len(ids) == 0
+            # the on-the-fly driver's lists: 4-byte IDs alone, and 4/8-byte values ranked
+            # by their global rows (ShardedOnTheFly._stage_outputs)
+            f = stage.fetch(None, None, None, offs, torch.from_numpy((mk * 5 + 1).astype(np.int32)),
+                            None, len(mk), torch.from_numpy(cnt[rank]), S, np.uint32,
+                            rows=torch.from_numpy(mk), n_rows=n_rows, comm_dev=torch.device('cpu'))
+            off2, ids2, _ = f.wait()
+            vdt = np.float32 if it % 2 else np.float64
+            vals = stage.place_ranked(None, torch.from_numpy((mk * 0.5 + 0.25).astype(vdt)),
+                                      torch.from_numpy(mk), n_rows, torch.device('cpu'))
+            if rank == 0:
+                assert np.array_equal(off2, off) and ids2.dtype == np.uint32
+                assert np.array_equal(ids2, (key * 5 + 1).astype(np.uint32)[order])
+                assert vals.dtype == vdt and np.array_equal(vals, (key * 0.5 + 0.25).astype(vdt)[order])
+            else:
+                assert vals is None and len(ids2) == 0
         stage.close()
     finally:
         dist.destroy_process_group()

@@ -25,8 +25,8 @@ torch.distributed run (``python -m torch.distributed.run ... tools/bench_onthefl
 --sharded``; without a launcher, world 1).  Each rank holds only its block-aligned
 stripe of every snapshot in pinned host memory (a striped reader's view of the
 whole-snapshot contract), double-buffers that stripe's H2D on a copy stream, and runs
-the sharded pipeline on it: owner all-to-all, join, records gathered to rank 0 and
-merged there.  --particles is then the global snapshot size (configs[4]: 1e9 over 8
+the sharded pipeline on it: owner all-to-all, join, apsis IDs and angle changes stored
+by every rank into the shared host buffer, departed / entered rows merged on rank 0.  --particles is then the global snapshot size (configs[4]: 1e9 over 8
 GPUs; the default 1.25e8 is one GPU's share).
 """
 import argparse
@@ -273,7 +273,7 @@ def main():
     res = {
         'metric': 'particle-snapshots/s (track_orbits_onthefly stream, H2D inclusive)',
         'value': units / wall, 'unit': 'particle-snapshots/s', 'n_gpus': world,
-        'driver': 'ShardedOnTheFly (stripe H2D + owner all-to-all + gather to rank 0)'
+        'driver': 'ShardedOnTheFly (stripe H2D + owner all-to-all + shared-buffer output stage)'
                   if args.sharded else 'OnTheFly (single GPU)',
         'steps': args.steps, 'warmup': 1, 'ms_per_step': wall / args.steps * 1e3,
         'timed_window': 'from before the H2D of the first timed snapshot (2) is issued to '
