@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OA_ABI_VERSION 18
+#define OA_ABI_VERSION 19
 
 #define OA_OK 0
 #define OA_E_ARG (-1)       /* invalid argument / unsupported dtype plan */
@@ -426,6 +426,14 @@ int oa_host_unregister(void *host);
  * word `*host_addr` (a HIP host callback, release order): a rank tells the writing rank
  * that its records are in place without its host waiting for them. */
 int oa_stream_set_flag(void *stream, int64_t *host_addr, int64_t value);
+
+/* *host_status = *status and *host_total = *total, stored by a kernel on `stream`
+ * (host_* are device addresses of page-locked host words, oa_host_register): a step's
+ * status word and record count reach the host behind the step's kernels without a copy
+ * engine, which may still be moving an earlier step's records (track_orbits.py:189-227's
+ * pipelined form, OrbitEngine.settle).  ABI 19. */
+int oa_post_status(const int32_t *status, const int64_t *total, int32_t *host_status,
+                   int64_t *host_total, void *stream);
 
 /* out_ids[dst[i]] = ids[i] (id_bytes 4 or 8 each), out_ang[dst[i]] = ang[i] for
  * i < n; dst values must lie in [0, cap) (a record outside is dropped and counted in

@@ -13,7 +13,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.abspath(__file__))
 # ORBIT_HIP_LIB selects an alternative build (kernel variants for tuning sweeps)
 LIB_PATH = os.environ.get('ORBIT_HIP_LIB') or os.path.join(PKG, 'liborbit_hip.so')
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -140,6 +140,7 @@ SYMBOLS = {
     'oa_host_register': (ctypes.c_int, [c_vp, c_i64, ctypes.POINTER(c_vp)]),
     'oa_host_unregister': (ctypes.c_int, [c_vp]),
     'oa_stream_set_flag': (ctypes.c_int, [c_vp, c_vp, c_i64]),
+    'oa_post_status': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     'oa_place_records': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_vp,
                                         c_vp]),
     # orbit_post.h

@@ -2713,6 +2713,18 @@ __global__ __launch_bounds__(256) void k_place_records(const ID *ids, const uint
     if (bad && status) atomicAdd(status, 1);
 }
 
+// A step's status word and record count into page-locked host words (oa_post_status):
+// the host's settle then waits only for this stream, not for a copy engine that may be
+// busy with an earlier step's records.  Two lanes, two vector stores, then a
+// system-scope fence.
+__global__ __launch_bounds__(64) void k_post_status(const int32_t *status, const int64_t *total,
+                                                    int32_t *h_status, int64_t *h_total) {
+    const int t = threadIdx.x;
+    if (t == 0) h_status[0] = status[0];
+    else if (t == 1) h_total[0] = total[0];
+    __threadfence_system();
+}
+
 // Error channel shared with the other units (orbit_post.hip, the step-plan units):
 // nullptr clears the message, anything else becomes oa_last_error().
 void oa_internal_error(const char *msg) {
@@ -2849,6 +2861,16 @@ int oa_stream_set_flag(void *stream, int64_t *host_addr, int64_t value) {
         return fail(OA_E_LAUNCH, "hipLaunchHostFunc: %s", hipGetErrorString(e));
     }
     return OA_OK;
+}
+
+int oa_post_status(const int32_t *status, const int64_t *total, int32_t *host_status,
+                   int64_t *host_total, void *stream) {
+    g_err[0] = 0;
+    if (!status || !total || !host_status || !host_total)
+        return fail(OA_E_ARG, "oa_post_status: null pointer");
+    hipLaunchKernelGGL(k_post_status, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                       status, total, host_status, host_total);
+    return check_launch("k_post_status");
 }
 
 int oa_place_records(const void *ids, const uint16_t *ang, const int64_t *dst, int64_t n,

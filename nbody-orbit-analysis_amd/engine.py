@@ -573,6 +573,29 @@ class PreparedStep:
         return len(self.items) - self.n_small
 
 
+class _HostWords:
+    """Page-locked host words the device stores into (``oa_post_status``): registered
+    pages of 16-byte slots (status int32 at +0, record count int64 at +8), one slot per
+    workspace, returned to the page's free list when the workspace goes."""
+    PAGE = 4096
+    pages = []
+
+    @classmethod
+    def take(cls, lib):
+        for pg in cls.pages:
+            if pg['free']:
+                return pg, pg['free'].pop()
+        import mmap
+        mm = mmap.mmap(-1, cls.PAGE)
+        arr = np.frombuffer(mm, dtype=np.uint8)
+        dev = ctypes.c_void_p()
+        N.check(lib.oa_host_register(ctypes.c_void_p(arr.ctypes.data), cls.PAGE,
+                                     ctypes.byref(dev)), 'oa_host_register')
+        pg = dict(mm=mm, arr=arr, dev=dev.value, free=list(range(cls.PAGE // 16 - 1, -1, -1)))
+        cls.pages.append(pg)
+        return pg, pg['free'].pop()
+
+
 class Workspace:
     """Scratch of compare steps, kept by the engine and grown on demand (capacities are
     high-water marks, so a steady stream of snapshots allocates nothing)."""
@@ -601,13 +624,33 @@ class Workspace:
         self.scratch_pos = e(scratch, torch.int32) if positions else None
         self.out_pos = e(n_prev, torch.int32) if positions else None
         self.status.zero_()
-        # the status word and record count of the last launch, copied to the host
-        # behind the step's event (OrbitEngine.settle reads them without a stream sync)
-        self.h_status = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-        self.h_total = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+        # the status word and record count of the last launch, stored into page-locked
+        # host words by a kernel behind the step (post_status): OrbitEngine.settle reads
+        # them after the step's event, with no stream sync and no copy engine in between
+        self.h_status = np.zeros(1, np.int32)
+        self.h_total = np.zeros(1, np.int64)
+        self._hw = None
         self.copy_done = None               # event after the last D2H of its records
         self.scratch_rk = None              # partitioned halos' record positions (rk())
         self.lookback, self.lb_epoch = None, 0  # direct records' item words (lookback())
+
+    def post_status(self, lib, stream):
+        """Queue the status word and record count to the host words on ``stream``
+        (``oa_post_status``).  A D2H copy there would wait for the copy engine, which
+        may still be moving an earlier step's records (track_orbits' pipeline), and
+        hold the host's settle, and so the next launch, behind it."""
+        if self._hw is None:
+            import weakref
+            pg, k = _HostWords.take(lib)
+            self._hw = (pg['dev'] + 16 * k, pg['arr'])
+            self.h_status = pg['arr'][16 * k:16 * k + 4].view(np.int32)
+            self.h_total = pg['arr'][16 * k + 8:16 * k + 16].view(np.int64)
+            weakref.finalize(self, pg['free'].append, k)
+        dev = self._hw[0]
+        N.check(lib.oa_post_status(ctypes.c_void_p(self.status.data_ptr()),
+                                   ctypes.c_void_p(self.total.data_ptr()),
+                                   ctypes.c_void_p(dev), ctypes.c_void_p(dev + 8),
+                                   ctypes.c_void_p(stream.cuda_stream)), 'oa_post_status')
 
     @staticmethod
     def need(pr):
@@ -876,8 +919,7 @@ class OrbitEngine:
             ws.copy_done = None
         res = self.launch(prep, ws, prev=ctx['prev'])
         res.ws_idx = idx
-        ws.h_status.copy_(ws.status, non_blocking=True)
-        ws.h_total.copy_(ws.total, non_blocking=True)
+        ws.post_status(self.lib, torch.cuda.current_stream(self.device))
         res.done = torch.cuda.Event()
         res.done.record(torch.cuda.current_stream(self.device))
         return res

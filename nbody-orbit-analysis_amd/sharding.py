@@ -986,8 +986,7 @@ class EngineLocal:
             res = eng.launch(lp, ws, prev=self._prev_state(lp, prev_lp), step_events=step_events)
             lp.res = res
             if ws is not None:
-                ws.h_status.copy_(ws.status, non_blocking=True)
-                ws.h_total.copy_(ws.total, non_blocking=True)
+                ws.post_status(eng.lib, torch.cuda.current_stream(eng.device))
                 res.done = torch.cuda.Event()
                 res.done.record(torch.cuda.current_stream(eng.device))
             if ws is None or not check:
