@@ -427,6 +427,13 @@ int oa_host_unregister(void *host);
  * that its records are in place without its host waiting for them. */
 int oa_stream_set_flag(void *stream, int64_t *host_addr, int64_t value);
 
+/* dst[0, bytes) = src[0, bytes) by a kernel on `stream`: src any device-accessible
+ * address (a page-locked host block from oa_host_register), dst device memory, both
+ * 16-byte aligned.  The engines' per-step host tables (halo table, item plan, partition
+ * rows) go up this way, not by a copy-engine DMA queued behind an earlier step's
+ * records D2H (track_orbits.py:189-227's pipelined form).  ABI 19. */
+int oa_copy_bytes(const void *src, void *dst, int64_t bytes, void *stream);
+
 /* *host_status = *status and *host_total = *total, stored by a kernel on `stream`
  * (host_* are device addresses of page-locked host words, oa_host_register): a step's
  * status word and record count reach the host behind the step's kernels without a copy

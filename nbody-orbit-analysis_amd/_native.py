@@ -141,6 +141,7 @@ SYMBOLS = {
     'oa_host_unregister': (ctypes.c_int, [c_vp]),
     'oa_stream_set_flag': (ctypes.c_int, [c_vp, c_vp, c_i64]),
     'oa_post_status': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    'oa_copy_bytes': (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp]),
     'oa_place_records': (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_vp,
                                         c_vp]),
     # orbit_post.h

@@ -2725,6 +2725,19 @@ __global__ __launch_bounds__(64) void k_post_status(const int32_t *status, const
     __threadfence_system();
 }
 
+// Bytes from a device-accessible address (a page-locked staging block, oa_host_register)
+// into device memory by a kernel on `stream` (oa_copy_bytes): a step's host tables reach
+// the device without a copy engine, whose queue may hold an earlier step's records D2H
+// for milliseconds.  16-byte lanes, grid-stride; block 0 copies the tail bytes.
+__global__ __launch_bounds__(256) void k_copy_bytes(const uint8_t *src, uint8_t *dst, int64_t n) {
+    const int64_t n16 = n >> 4, stride = (int64_t)gridDim.x * 256;
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+    uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) d4[i] = s4[i];
+    if (blockIdx.x == 0)
+        for (int64_t i = (n16 << 4) + threadIdx.x; i < n; i += 256) dst[i] = src[i];
+}
+
 // Error channel shared with the other units (orbit_post.hip, the step-plan units):
 // nullptr clears the message, anything else becomes oa_last_error().
 void oa_internal_error(const char *msg) {
@@ -2861,6 +2874,19 @@ int oa_stream_set_flag(void *stream, int64_t *host_addr, int64_t value) {
         return fail(OA_E_LAUNCH, "hipLaunchHostFunc: %s", hipGetErrorString(e));
     }
     return OA_OK;
+}
+
+int oa_copy_bytes(const void *src, void *dst, int64_t bytes, void *stream) {
+    g_err[0] = 0;
+    if (bytes < 0 || (bytes > 0 && (!src || !dst)) ||
+        (((uintptr_t)src | (uintptr_t)dst) & 15u))
+        return fail(OA_E_ARG, "oa_copy_bytes: bad arguments (16-byte aligned pointers)");
+    if (bytes == 0) return OA_OK;
+    const int64_t n16 = bytes >> 4;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n16 + 255) / 256, 512));
+    hipLaunchKernelGGL(k_copy_bytes, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       static_cast<const uint8_t *>(src), static_cast<uint8_t *>(dst), bytes);
+    return check_launch("k_copy_bytes");
 }
 
 int oa_post_status(const int32_t *status, const int64_t *total, int32_t *host_status,

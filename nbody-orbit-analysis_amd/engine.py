@@ -393,13 +393,46 @@ def to_device(x, device, dtype=None):
     return t.to(device, non_blocking=False).contiguous()
 
 
+class _Staging:
+    """Page-locked staging blocks for the host tables of a step (halo table, item plan,
+    partition rows): the host fills a block and a kernel on the current stream pulls it
+    into device memory (``oa_copy_bytes``).  A copy-engine DMA would queue behind the
+    records D2H of an earlier step (track_orbits' pipeline: ~2.3 ms on a heavy pair) and
+    hold this step's launch behind it (``profiles/r06/e2e_timeline_*``).  A block is
+    reused once the event recorded after its pull has completed."""
+    blocks = []
+
+    @classmethod
+    def upload(cls, a, device):
+        import mmap
+        lib = N.load(require_device=True)
+        n = int(a.nbytes)
+        stream = torch.cuda.current_stream(device)
+        blk = next((b for b in cls.blocks
+                    if b['cap'] >= n and (b['ev'] is None or b['ev'].query())), None)
+        if blk is None:
+            cap = max(1 << 20, 1 << max(n - 1, 1).bit_length())
+            mm = mmap.mmap(-1, cap)
+            arr = np.frombuffer(mm, dtype=np.uint8)
+            dev = ctypes.c_void_p()
+            N.check(lib.oa_host_register(ctypes.c_void_p(arr.ctypes.data), cap,
+                                         ctypes.byref(dev)), 'oa_host_register')
+            blk = dict(mm=mm, arr=arr, cap=cap, dev=dev.value, ev=None)
+            cls.blocks.append(blk)
+        blk['arr'][:n] = a.reshape(-1).view(np.uint8)
+        out = torch.empty(n, dtype=torch.uint8, device=device)
+        N.check(lib.oa_copy_bytes(ctypes.c_void_p(blk['dev']), ctypes.c_void_p(out.data_ptr()),
+                                  n, ctypes.c_void_p(stream.cuda_stream)), 'oa_copy_bytes')
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        blk['ev'] = ev
+        return out
+
+
 def _upload(a, device):
-    """Host table -> device through a page-locked staging block (asynchronous DMA on
-    the current stream; torch's caching host allocator keeps the block until the copy
-    has run)."""
-    h = torch.empty(a.nbytes, dtype=torch.uint8, pin_memory=True)
-    h.numpy()[:] = a.reshape(-1).view(np.uint8)
-    return h.to(device, non_blocking=True)
+    """Host table -> device tensor of bytes, asynchronous on the current stream
+    (``_Staging``: a page-locked block pulled by a kernel, no copy-engine DMA)."""
+    return _Staging.upload(np.ascontiguousarray(a), device)
 
 
 def _up(a, device):

@@ -71,3 +71,23 @@ def test_place_records_into_shared_host_buffer(ib, with_ang, tmp_path):
         assert not slot.ids[untouched].any() and not slot.ang[untouched].any()
     finally:
         slot.release(lib)
+
+
+@pytest.mark.parametrize('n', [0, 1, 15, 16, 4097, (1 << 20) + 3, (3 << 20) + 16])
+def test_table_upload_by_kernel_pull(n):
+    """engine._upload: a host table reaches the device through a page-locked staging
+    block pulled by oa_copy_bytes (16-byte lanes, tail bytes by block 0); blocks are reused
+    only after their pull has run, so back-to-back uploads keep their own bytes."""
+    import torch
+    from orbitanalysis_amd.engine import _upload
+    dev = torch.device('cuda', 0)
+    rng = np.random.default_rng(n)
+    a = rng.integers(0, 256, n).astype(np.uint8)
+    b = rng.integers(0, 256, n).astype(np.uint8)
+    want_a = a.copy()
+    ta, tb = _upload(a, dev), _upload(b, dev)          # the second may not reuse a's block
+    a[:] = 0                                           # the staging block holds its own copy
+    torch.cuda.synchronize()
+    assert ta.dtype == torch.uint8 and ta.numel() == n
+    assert np.array_equal(ta.cpu().numpy(), want_a)
+    assert np.array_equal(tb.cpu().numpy(), b)
