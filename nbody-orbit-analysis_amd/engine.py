@@ -429,10 +429,26 @@ class _Staging:
         return out
 
 
+# set while an engine with ``table_pull`` prepares a step (OrbitEngine.prepare)
+_TABLE_PULL = [False]
+
+
 def _upload(a, device):
-    """Host table -> device tensor of bytes, asynchronous on the current stream
-    (``_Staging``: a page-locked block pulled by a kernel, no copy-engine DMA)."""
-    return _Staging.upload(np.ascontiguousarray(a), device)
+    """Host table -> device tensor of bytes, asynchronous on the current stream.
+
+    Two routes.  A DMA from a page-locked block of torch's caching host allocator (the
+    allocator keeps the block until the copy has run) -- the default.  Or, while an
+    engine with ``table_pull`` prepares (the pipelined batch driver), ``_Staging``: a
+    page-locked block pulled by a kernel.  The batch driver keeps the copy engine busy
+    with records D2H, behind which a DMA upload would wait; the on-the-fly stream keeps
+    the link's host-to-device direction busy with snapshots, which a kernel's reads
+    would have to share."""
+    a = np.ascontiguousarray(a)
+    if _TABLE_PULL[0]:
+        return _Staging.upload(a, device)
+    h = torch.empty(a.nbytes, dtype=torch.uint8, pin_memory=True)
+    h.numpy()[:] = a.reshape(-1).view(np.uint8)
+    return h.to(device, non_blocking=True)
 
 
 def _up(a, device):
@@ -777,6 +793,9 @@ class OrbitEngine:
         # direct records' look-back poll bound (0: the library default); tests set 1 to
         # force OA_STATUS_LOOKBACK and the re-run through oa_compact
         self.lb_spin_max = 0
+        # per-step tables pulled by a kernel instead of a DMA (_upload); the pipelined
+        # batch driver sets it for its run
+        self.table_pull = False
         # diagnostics (tools/bench_e2e.py --timeline): a list collecting (start, end) timing
         # events of each fetch_async's copies on the copy stream; None: off
         self.copy_events = None
@@ -1010,8 +1029,18 @@ class OrbitEngine:
         self._set_prev(ctx, prep)
         return True
 
-    def prepare(self, snap, centres, bulk_cat, H, z, exists, compare, angles_in=None,
-                plan_src=None, prev_layout=None, entries=None, part=True):
+    def prepare(self, *args, **kw):
+        """Host half of a step (``_prepare``), its table uploads routed by ``table_pull``
+        (``_upload``)."""
+        old = _TABLE_PULL[0]
+        _TABLE_PULL[0] = bool(self.table_pull)
+        try:
+            return self._prepare(*args, **kw)
+        finally:
+            _TABLE_PULL[0] = old
+
+    def _prepare(self, snap, centres, bulk_cat, H, z, exists, compare, angles_in=None,
+                 plan_src=None, prev_layout=None, entries=None, part=True):
         """Host half of a step: dtype plan, halo/item tables, device uploads.
 
         ``snap`` holds device tensors for ids/coordinates/velocities(/masses);

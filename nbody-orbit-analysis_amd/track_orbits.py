@@ -77,6 +77,13 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
     pipelined = hasattr(eng, 'fetch_async')
     defer = pipelined and not verbose and 'defer' in inspect.signature(eng.step).parameters
     groups = []                     # [res, ids dtype, fetched or None, save args, kw]
+    # the pipelined run keeps the copy engine busy with records D2H: the engines pull
+    # their per-step tables with a kernel instead (engine._upload), restored on exit
+    pulls = [e for e in (eng, getattr(getattr(eng, 'local', None), 'engine', None))
+             if pipelined and e is not None and hasattr(e, 'table_pull')]
+    saved_pull = [e.table_pull for e in pulls]
+    for e in pulls:
+        e.table_pull = True
 
     def flush(keep=0):
         """Write the groups oldest first, leaving the newest ``keep`` in flight."""
@@ -203,6 +210,9 @@ def track_orbits(snapshot_numbers, main_branches, regions, load_snapshot_data,
         _salvage(groups, eng, out, new_fetches=not (collective or interrupted),
                  timeout=0.0 if interrupted else 10.0)
         raise
+    finally:
+        for e, v in zip(pulls, saved_pull):
+            e.table_pull = v
     flush()
 
     if verbose:

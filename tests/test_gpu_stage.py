@@ -73,13 +73,17 @@ def test_place_records_into_shared_host_buffer(ib, with_ang, tmp_path):
         slot.release(lib)
 
 
+@pytest.mark.parametrize('pull', [True, False])
 @pytest.mark.parametrize('n', [0, 1, 15, 16, 4097, (1 << 20) + 3, (3 << 20) + 16])
-def test_table_upload_by_kernel_pull(n):
-    """engine._upload: a host table reaches the device through a page-locked staging
-    block pulled by oa_copy_bytes (16-byte lanes, tail bytes by block 0); blocks are reused
-    only after their pull has run, so back-to-back uploads keep their own bytes."""
+def test_table_upload_by_kernel_pull(n, pull, monkeypatch):
+    """engine._upload: with table pulls (the pipelined batch driver) a host table
+    reaches the device through a page-locked staging block pulled by oa_copy_bytes
+    (16-byte lanes, tail bytes by block 0), blocks reused only after their pull has run,
+    so back-to-back uploads keep their own bytes; without, by a DMA."""
     import torch
+    from orbitanalysis_amd import engine as E
     from orbitanalysis_amd.engine import _upload
+    monkeypatch.setattr(E, '_TABLE_PULL', [pull])
     dev = torch.device('cuda', 0)
     rng = np.random.default_rng(n)
     a = rng.integers(0, 256, n).astype(np.uint8)
