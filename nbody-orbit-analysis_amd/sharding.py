@@ -589,6 +589,7 @@ class ShardedEngine:
         self._pending: Optional[ShardedResult] = None   # a deferred step not yet settled
         self._side = None                               # stream of the records' gathers
         self._stage = None                              # shared host output (world > 1)
+        self._xstream = None                            # catalogue all-gather (RCCL)
         # rank 0's record placement timed (synchronised) into fetch_stats (rehearsals)
         self.profile_fetch = False
         self.fetch_stats = None
@@ -602,7 +603,12 @@ class ShardedEngine:
     # ---------------------------------------------------------------- collectives
     def _exchange(self, rows, nh):
         """The one per-snapshot all-gather of catalogue rows: rank r contributes halos
-        [r * nl, (r + 1) * nl) of its (nh, 6) float64 rows; every rank gets all nh."""
+        [r * nl, (r + 1) * nl) of its (nh, 6) float64 rows; every rank gets all nh.
+
+        On the device (RCCL) the all-gather is issued from a side stream: it depends on
+        nothing the previous step computes, so it runs while that step's kernels do,
+        and only the next launch waits for it (the current stream waits on the side
+        stream; the result is recorded as used there)."""
         import torch.distributed as dist
         nl = -(-nh // self.world)
         mine = np.zeros((nl, 6), dtype=np.float64)
@@ -610,8 +616,18 @@ class ShardedEngine:
         if hi > lo:
             mine[:hi - lo] = rows[lo:hi]
         dev = _comm_device()
-        out = torch.empty((nl * self.world, 6), dtype=torch.float64, device=dev)
-        dist.all_gather_into_tensor(out, _h2d(mine, dev), group=self.group)
+        if dev.type != 'cuda':
+            out = torch.empty((nl * self.world, 6), dtype=torch.float64, device=dev)
+            dist.all_gather_into_tensor(out, _h2d(mine, dev), group=self.group)
+            return out[:nh]
+        if self._xstream is None:
+            self._xstream = torch.cuda.Stream(device=dev)
+        cur = torch.cuda.current_stream(dev)
+        with torch.cuda.stream(self._xstream):
+            out = torch.empty((nl * self.world, 6), dtype=torch.float64, device=dev)
+            dist.all_gather_into_tensor(out, _h2d(mine, dev), group=self.group)
+        cur.wait_stream(self._xstream)
+        out.record_stream(cur)
         return out[:nh]
 
     # ---------------------------------------------------------------- shard

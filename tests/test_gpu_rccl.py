@@ -10,7 +10,9 @@ devices the sharded paths hand it:
 * the output stage (``host_share.SharedRecordStage``) with a CUDA comm device: the
   probe's int32 MIN all-reduce, the int64 count all-gather, the slot broadcast, the
   uint8 bitmap all-reduce of the row ranks; records (with and without angles), ranked
-  f32 / f64 values and checkpoint angles stored through the registered mapping.
+  f32 / f64 values and checkpoint angles stored through the registered mapping;
+* ``ShardedEngine`` through ``track_orbits`` with its catalogue all-gather on RCCL
+  (issued from a side stream, overlapping the previous step), equal to ``OrbitEngine``.
 """
 import json
 import os
@@ -107,6 +109,30 @@ def _worker(rank, port, outdir):
         del got
         stage.close()
         done.append('stage')
+        # 3. ShardedEngine through track_orbits over RCCL: the catalogue all-gather from
+        # its side stream, overlapping the previous step; the savefile equals a plain
+        # OrbitEngine run's bit for bit
+        from orbitanalysis_amd.engine import OrbitEngine
+        from orbitanalysis_amd.savefile import MemorySavefile
+        from orbitanalysis_amd.sharding import ShardedEngine, EngineLocal
+        from orbitanalysis_amd.synthetic import PlummerSnapshots
+        from orbitanalysis_amd.track_orbits import track_orbits
+        kw = dict(n_halos=30, n_per_halo=[3000, 800, 12000] * 10, n_snapshots=5, seed=17,
+                  dtype=np.float32, centre_dtype=np.float32, bulk='catalogue', box_size=300.0)
+        outs = []
+        for eng in (ShardedEngine(EngineLocal(OrbitEngine(mode='pericentric'))),
+                    OrbitEngine(mode='pericentric')):
+            u = PlummerSnapshots(**kw)
+            out = MemorySavefile()
+            track_orbits(u.snapshot_numbers, u.main_branches(), u.regions, u.load_snapshot_data,
+                         out, mode='pericentric', verbose=False, engine=eng)
+            outs.append(out)
+        assert sorted(outs[0].groups) == sorted(outs[1].groups) and outs[0].groups
+        for g in outs[1].groups:
+            for k, w in outs[1].groups[g].items():
+                assert np.array_equal(np.asarray(outs[0].groups[g][k]).view(np.uint8),
+                                      np.asarray(w).view(np.uint8)), (g, k)
+        done.append('sharded')
         with open(os.path.join(outdir, 'ok.json'), 'w') as fo:
             json.dump(done, fo)
     finally:
@@ -118,4 +144,4 @@ def test_rccl_collectives_and_output_stage_world1():
         mp.start_processes(_worker, args=(_free_port(), d), nprocs=1, join=True,
                            start_method='spawn')
         done = json.load(open(os.path.join(d, 'ok.json')))
-    assert 'stage' in done and len(done) == 9, done
+    assert 'stage' in done and 'sharded' in done and len(done) == 10, done
