@@ -257,6 +257,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         last_res = run(args.warmup + i, evs[i])
+    t_issue = time.perf_counter() - t0          # the host's launch calls of the K steps
     torch.cuda.synchronize()
     if dist:
         barrier()
@@ -453,6 +454,7 @@ def main():
                                        'table, item plan, partition plan) runs before the '
                                        'timed region and is excluded, see host_prepare_ms',
                        'host_prepare_ms': float(np.median(prep_s)) * 1e3,
+                       'host_launch_ms': t_issue / args.steps * 1e3,
                        'fetch_ms': fetch_ms,
                        'fetch_note': 'records of one step moved to the host for rank 0 '
                                      '(N = 1: one D2H; N > 1: every rank stores its own '
