@@ -719,6 +719,8 @@ class ShardedEngine:
                          layout_=layout, h2d_bytes=h2d)
         sp.local_args = (shard, centres, bulk, H, z, exists, compare, a_in, bulk_cat is not None)
         sp.lp = self._local_prepare(sp, None if (prev is None or p is None) else p.lp)
+        # the halos with a progenitor block, planned here (host work off the launch)
+        sp.has_prog_for = (p, np.isin(exists, p.exists)) if compare and p is not None else None
         return sp
 
     def _local_prepare(self, sp, prev_lp):
@@ -743,7 +745,8 @@ class ShardedEngine:
         res = ShardedResult(n_slots=0, has_prog=np.zeros(nh, dtype=bool), bulk=sp.bulk_out,
                             lp=sp.lp)
         if sp.compare:
-            has_prog = np.isin(sp.exists, p.exists)
+            pre = getattr(sp, 'has_prog_for', None)
+            has_prog = pre[1] if pre is not None and pre[0] is p else np.isin(sp.exists, p.exists)
             res.has_prog, res.n_slots = has_prog, int(has_prog.sum())
             res.records, res.prev_prep = out, p
         return res
