@@ -131,6 +131,10 @@ def main():
     ap.add_argument('--no-output-stage', action='store_true',
                     help='N > 1: skip the second timed pass that includes the records\' '
                          'output stage (host_share.SharedRecordStage)')
+    ap.add_argument('--sharded', action='store_true',
+                    help='N = 1: drive the multi-GPU path (ShardedEngine, its per-snapshot '
+                         'collectives at world 1) instead of OrbitEngine -- a probe of that '
+                         'path\'s per-step overhead, not the headline')
     ap.add_argument('--backend', default='nccl',
                     help="collective backend for N > 1 ('gloo': rehearsal with several "
                          "ranks on one GPU; collectives go through host memory)")
@@ -148,8 +152,14 @@ def main():
     dist = None
     gloo = args.backend == 'gloo'
     cdev = torch.device('cpu') if gloo else dev           # where collective tensors live
-    if world > 1:
+    shard = world > 1 or args.sharded         # the ShardedEngine path
+    if shard:
         import torch.distributed as dist
+        if world == 1:
+            os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+            os.environ.setdefault('MASTER_PORT', '29571')
+            os.environ.setdefault('RANK', '0')
+            os.environ.setdefault('WORLD_SIZE', '1')
         if gloo:
             dist.init_process_group('gloo')
         else:
@@ -190,7 +200,7 @@ def main():
     eng = OrbitEngine(mode=args.mode, device=dev)
 
     prep_s = []                               # host planning per compare step (untimed)
-    if world == 1:
+    if not shard:
         # snapshot 0: frame only (the reference's i == istart), outside the timing
         prep0 = eng.prepare(snaps[0], cats[0][0], cats[0][2], H, z, exists, False)
         eng.launch(prep0, None)
@@ -232,7 +242,7 @@ def main():
     def run(k, events=None, defer=False):
         pr, s = chain[k + 1]
         prev_pr, ps = chain[k]
-        if world > 1:
+        if shard:
             # defer: the drop-in driver's order -- the step's status is read (and the step
             # re-run on a re-plan or look-back timeout) by the fetch that settles it
             return seng.launch(pr, prev=prev_pr, step_events=events, check=defer, defer=defer)
@@ -288,7 +298,7 @@ def main():
             barrier()
         torch.cuda.synchronize()
         tf = time.perf_counter()
-        (seng if world > 1 else eng).fetch_async(last_res, fdt).wait()
+        (seng if shard else eng).fetch_async(last_res, fdt).wait()
         if dist:
             barrier()
         fetch.append(time.perf_counter() - tf)
@@ -305,7 +315,7 @@ def main():
     for i in range(args.steps):
         r_i = run(args.warmup + i)
         torch.cuda.synchronize()
-        n_aps.append(int(ws.total.item()) if world == 1 else int(r_i.lp.res.total.item()))
+        n_aps.append(int(ws.total.item()) if not shard else int(r_i.lp.res.total.item()))
 
     # N > 1: the same K steps again with the output stage of the drop-in driver
     # (track_orbits' pipelined order: step s launched, then the records of s - 1 start
@@ -447,7 +457,7 @@ def main():
                        'large_halos': int(last.n_global),
                        'parallelism': 'id-range shards x%d (ShardedEngine, presharded; one '
                                       'catalogue all-gather per snapshot)' % world
-                                      if world > 1 else 'single GPU',
+                                      if shard else 'single GPU',
                        'timed_region': 'the device launches of K compare steps (frame, join, '
                                        'sign test, angles, compaction) on inputs resident in '
                                        'HBM; the host planning of each step (prepare: halo '
